@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Headline benchmark: input events/s through the pattern NFA path on MI355X (BASELINE.json metric).
+
+Workload (the 1-GPU config the metric is quoted on):
+    partition with (symbol of StockStream) begin
+      from every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec
+      select e1.id as e1id, e2.id as e2id insert into M; end;
+    100,000,000 events per GPU per step, 10,000 keys per GPU, ts = T0 + floor(i/100) (splitmix64, synthetic).
+A step = one flush of one 100M-event batch, inputs already resident in HBM (sdg_push_device); consecutive steps
+are consecutive batches of one stream (timestamps continue), so partials crossing a batch boundary are carried.
+
+Multi-GPU (torchrun, one process per GPU): key-hash sharding, rank r owns keys k*N + r; no data-path
+collective — only the batch-boundary all-gather of per-rank match counts (RCCL over xGMI). scaling = weak.
+
+Roofline: algorithmic bytes per step B = N_in*28 + N_match*28 (ts 8 + key 4 + price 8 + id 8 in,
+ts 8 + key 4 + two ids out); achieved = B / duration of the dominant kernel (HIP events on the engine stream).
+CPU baseline: the oracle (C++ restatement of the reference engine, one core) on a bounded sample of the same
+workload.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+B_IN = 28
+B_OUT = 28
+HBM_PEAK_GBS = 8000.0
+
+
+def gen_shard(n, keys, rank, world, seed=7):
+    """C2 columns of this rank's shard (numpy, chunked to bound host memory)."""
+    from siddhi_amd import workloads as w
+    out = {k: [] for k in ("ts", "id", "key", "price", "volume")}
+    chunk = 10_000_000
+    for off in range(0, n, chunk):
+        m = min(chunk, n - off)
+        c = w.c2_columns(m, keys=keys, seed=seed + 1000 * rank, offset=off)
+        for k in out:
+            out[k].append(c[k])
+    return {k: np.concatenate(v) for k, v in out.items()}
+
+
+def cpu_baseline(cols, syms, sample):
+    """Oracle (reference-semantics C++ restatement, single thread) on the first `sample` events."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from oracle_rt import Oracle, lib
+    from siddhi_amd import workloads as w
+    o = Oracle(w.C2_APP)
+    L = lib()
+    L.orc_count_only(o.h, 1)
+    ids = np.array([L.orc_intern(o.h, s.encode()) for s in syms], dtype=np.int64)
+    si = o.stream("StockStream")
+    n = sample
+    slots = np.empty((n, 4), dtype=np.int64)
+    slots[:, 0] = cols["id"][:n]
+    slots[:, 1] = ids[cols["key"][:n]]
+    slots[:, 2] = cols["price"][:n].view(np.int64)
+    slots[:, 3] = cols["volume"][:n]
+    offs = np.arange(n, dtype=np.int64) * 4
+    strm = np.full(n, si, dtype=np.int32)
+    ts = np.ascontiguousarray(cols["ts"][:n])
+    t = time.perf_counter()
+    rc = L.orc_send_batch(o.h, n, strm.ctypes.data, ts.ctypes.data, offs.ctypes.data, slots.ctypes.data, None)
+    dt = time.perf_counter() - t
+    matches = L.orc_output_count(o.h)
+    o.close()
+    if rc != 0:
+        raise RuntimeError("oracle failed")
+    return n / dt, matches, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--events", type=int, default=100_000_000, help="events per GPU per step")
+    ap.add_argument("--keys", type=int, default=10_000, help="keys per GPU")
+    ap.add_argument("--cpu-sample", type=int, default=3_000_000)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import siddhi_amd as sa
+    from siddhi_amd import workloads as w
+
+    n, keys = args.events, args.keys
+    cols = gen_shard(n, keys, rank, world)
+    syms = ["S%07d" % (k * world + rank) for k in range(keys)]
+    rt = sa.SiddhiAppRuntime(w.C2_APP, device=local)
+    sym_ids = np.array([rt.intern(s) for s in syms], dtype=np.uint32)
+    dev = torch.device("cuda", local)
+    d_id = torch.from_numpy(cols["id"]).to(dev)
+    d_sym = torch.from_numpy(sym_ids[cols["key"]].view(np.int32)).to(dev)
+    d_price = torch.from_numpy(cols["price"]).to(dev)
+    d_vol = torch.from_numpy(cols["volume"]).to(dev)
+    d_ts0 = torch.from_numpy(cols["ts"]).to(dev)
+    span = int(cols["ts"][-1] - cols["ts"][0]) + 1
+    nsteps = args.warmup + args.steps
+    ts_steps = [d_ts0 + s * span for s in range(nsteps)]  # consecutive batches of one stream
+    torch.cuda.synchronize()
+
+    def step(s):
+        rt.push_device("StockStream", n, ts_steps[s].data_ptr(),
+                       [d_id.data_ptr(), d_sym.data_ptr(), d_price.data_ptr(), d_vol.data_ptr()])
+        rt.flush(deliver=False)
+        st = rt.stats()
+        if dist is not None:  # batch-boundary match-count all-gather (global output offsets)
+            cnt = torch.tensor([st.matches], dtype=torch.int64, device=dev)
+            allc = [torch.empty_like(cnt) for _ in range(world)]
+            dist.all_gather(allc, cnt)
+        return st
+
+    for s in range(args.warmup):
+        step(s)
+    keys_k = ["ms_kg_hist", "ms_kg_prefix", "ms_kg_scatter", "ms_chain_carry", "ms_chain_match"]
+    acc = {k: 0.0 for k in keys_k}
+    matches = 0
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.warmup, nsteps):
+        st = step(s)
+        matches += st.matches
+        for k in keys_k:
+            acc[k] += getattr(st, k)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        m = torch.tensor([matches], dtype=torch.int64, device=dev)
+        dist.all_reduce(m)
+        total_matches = int(m.item())
+    else:
+        total_matches = matches
+    K = args.steps
+    ms_per_step = elapsed * 1000.0 / K
+    value = n * world * K / elapsed
+
+    per_kernel = {k: acc[k] / K for k in keys_k}
+    dom = max(per_kernel, key=per_kernel.get)
+    step_bytes = n * B_IN + (matches / K) * B_OUT
+    achieved = step_bytes / (per_kernel[dom] / 1000.0) / 1e9
+    out = {
+        "metric": "input events/sec matched (node) at 1/2/4/8 MI355X; % HBM roofline",
+        "value": value,
+        "unit": "events/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (splitmix64 C2 generator, BASELINE.md), device-resident",
+        "config": {"workload": "C2: partition with (symbol of StockStream) every e1=StockStream[price>20] -> "
+                               "e2=StockStream[price>e1.price] within 1 sec",
+                   "events_per_gpu_per_step": n, "keys_per_gpu": keys, "parallelism": "key-hash shards x%d" % world,
+                   "matches_per_step": total_matches / K},
+        "roofline": {"bound": "hbm", "kernel": dom.replace("ms_", ""), "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "step_frac": step_bytes / (ms_per_step / 1000.0) / 1e9 / HBM_PEAK_GBS,
+                     "kernel_ms": per_kernel},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        rate, cm, dt = cpu_baseline(cols, syms, min(args.cpu_sample, n))
+        out["cpu_baseline"] = {"value": rate, "unit": "events/s", "cores": 1, "kind": "port",
+                               "sample": "first %d events of the C2 stream (%.1f s, %d matches), oracle restatement"
+                                         % (min(args.cpu_sample, n), dt, cm)}
+    else:
+        out["cpu_baseline"] = None
+    rt.shutdown()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

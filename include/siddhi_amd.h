@@ -1,0 +1,119 @@
+/* siddhi_amd — MI355X engine for Siddhi's pattern/sequence NFA path: the drop-in C-ABI.
+ *
+ * Everything behind this header runs on the GPU (gfx950 HIP kernels); there is no CPU fallback. The ABI is
+ * what a JNI / Panama FFM binding of the reference's API would call (INTEGRATION.md shows the bindings):
+ *
+ *   sdg_compile          <- SiddhiManager.createSiddhiAppRuntime(String)
+ *                           (modules/siddhi-core/src/main/java/io/siddhi/core/SiddhiManager.java:93-96)
+ *   sdg_stream_index /   <- SiddhiAppRuntime.getInputHandler(String) + the stream definition
+ *   sdg_stream_schema       (core/SiddhiAppRuntimeImpl.java:414)
+ *   sdg_push             <- InputHandler.send(long, Object[]) / send(Event[]) for one stream, columnar
+ *                           (core/stream/input/InputHandler.java:59-95); events keep their call order
+ *   sdg_push_device      <- the same for event columns already resident in HBM (device pointers)
+ *   sdg_advance_time     <- TimestampGeneratorImpl.setCurrentTimestamp (playback clock, util/timestamp/
+ *                           TimestampGeneratorImpl.java:105-122)
+ *   sdg_flush            <- the receivers' per-event processing of everything pushed so far
+ *                           (core/query/input/ProcessStreamReceiver.java:98-179 -> state processors)
+ *   sdg_poll             <- QueryCallback.receive(long, Event[], Event[]) / StreamCallback.receive(Event[])
+ *                           (core/query/output/callback/QueryCallback.java:60-105,
+ *                            core/stream/output/StreamCallback.java:93-129), columnar
+ *   sdg_destroy          <- SiddhiAppRuntime.shutdown()
+ *
+ * Conventions (mirroring the reference): compile errors are returned as status codes with a thread-local
+ * message (SiddhiAppCreationException / SiddhiAppValidationException / OperationNotSupportedException); one
+ * handle is single-threaded (the reference serialises a query under patternSyncObject); the engine owns the
+ * copies it makes of pushed data; poll results are valid until the next sdg_flush / sdg_poll / sdg_destroy.
+ *
+ * Value encoding of columns: INT int32, LONG int64, FLOAT float, DOUBLE double, BOOL uint8, STRING uint32
+ * (ids from sdg_intern: equal strings <=> equal ids). Nulls: optional per-column uint8 arrays (1 = null).
+ */
+#ifndef SIDDHI_AMD_H
+#define SIDDHI_AMD_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum sdg_status {
+    SDG_OK = 0,
+    SDG_ERR_PARSE = 1,        /* SiddhiParserException */
+    SDG_ERR_VALIDATION = 2,   /* SiddhiAppValidationException / SiddhiAppCreationException */
+    SDG_ERR_UNSUPPORTED = 3,  /* OperationNotSupportedException (outside the accelerated subset) */
+    SDG_ERR_ARG = 4,
+    SDG_ERR_DEVICE = 5,       /* HIP error or no gfx950 device */
+    SDG_ERR_CAPACITY = 6      /* a bounded device structure overflowed (reported, never silently dropped) */
+};
+
+enum sdg_type { SDG_INT = 0, SDG_LONG = 1, SDG_FLOAT = 2, SDG_DOUBLE = 3, SDG_BOOL = 4, SDG_STRING = 5 };
+
+typedef struct sdg_engine sdg_engine;
+
+typedef struct sdg_opts {
+    int32_t device;            /* HIP device ordinal (one engine per GPU) */
+    int64_t batch_capacity;    /* max events buffered between flushes (0 = default 1<<24) */
+    int32_t max_partials;      /* per-key bounded partial-match slots for the generic NFA (0 = default) */
+    int32_t flags;             /* SDG_COMPILE_ONLY: parse + lower only, no device (introspection on hosts
+                                  without a GPU; push/flush then fail with SDG_ERR_DEVICE) */
+} sdg_opts;
+#define SDG_COMPILE_ONLY 1
+
+typedef struct sdg_out {
+    int64_t n;                 /* output events */
+    const int64_t* ts;         /* [n] event timestamps (StateEvent timestamp) */
+    const uint8_t* expired;    /* [n] 1 = removeEvents / expired */
+    int32_t n_attrs;           /* output attributes (select list order) */
+    const int32_t* types;      /* [n_attrs] sdg_type */
+    const int64_t* const* values; /* [n_attrs][n] 64-bit payload (float/double as bit patterns) */
+    const uint8_t* const* nulls;  /* [n_attrs][n] 1 = null */
+} sdg_out;
+
+int sdg_compile(const char* siddhi_app, const sdg_opts* opts, sdg_engine** out);
+void sdg_destroy(sdg_engine* e);
+const char* sdg_last_error(void);
+
+int sdg_stream_index(sdg_engine* e, const char* stream_id);
+int sdg_stream_schema(sdg_engine* e, int stream, int32_t* n_attrs, const int32_t** types);
+int sdg_num_queries(sdg_engine* e);
+/* device path chosen for a query: 0 = chain kernel (independent partials), 1 = generic keyed NFA */
+int sdg_query_path(sdg_engine* e, int query);
+const char* sdg_query_name(sdg_engine* e, int query);
+const char* sdg_query_target(sdg_engine* e, int query);
+int sdg_query_output_schema(sdg_engine* e, int query, int32_t* n_attrs, const int32_t** types,
+                            const char* const** names);
+uint32_t sdg_intern(sdg_engine* e, const char* s, size_t len);
+const char* sdg_string(sdg_engine* e, uint32_t id);
+
+/* columnar host batch for ONE stream: ts[n], cols[a] (typed as above), nulls[a] may be NULL */
+int sdg_push(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const void* const* cols,
+             const uint8_t* const* nulls);
+/* the same with device-resident columns (no copy; the caller keeps them alive until sdg_flush returns) */
+int sdg_push_device(sdg_engine* e, int stream, int64_t n, const int64_t* d_ts, const void* const* d_cols,
+                    const uint8_t* const* d_nulls);
+int sdg_advance_time(sdg_engine* e, int64_t ts);
+int sdg_flush(sdg_engine* e);
+int sdg_sync(sdg_engine* e);
+int sdg_poll(sdg_engine* e, int query, sdg_out* out);
+
+/* introspection for measurement: device time of the last flush per kernel family, algorithmic bytes,
+ * match count, and which kernel path each query took (0 = chain, 1 = generic). */
+typedef struct sdg_stats {
+    int64_t events;            /* events processed by the last flush (all queries) */
+    int64_t matches;           /* output events produced by the last flush */
+    double ms_keygroup;        /* device ms: key grouping (histogram + scan + scatter) */
+    double ms_match;           /* device ms: NFA / match kernels */
+    double ms_total;           /* device ms: whole flush */
+    int64_t keygroup_launches;
+    int64_t match_launches;
+    int32_t path;              /* 0 chain (independent partials), 1 generic keyed NFA */
+    int32_t overflow;          /* capacity overflows detected (0 on a valid run) */
+    /* device ms per kernel (HIP events on the engine's stream), summed over the flush's queries */
+    double ms_kg_hist, ms_kg_prefix, ms_kg_scatter, ms_chain_carry, ms_chain_match;
+} sdg_stats;
+int sdg_last_stats(sdg_engine* e, sdg_stats* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

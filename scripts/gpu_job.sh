@@ -1,0 +1,34 @@
+#!/bin/bash
+# One gpurun job: each GPU step under its own timeout; stop at the first crash / fault / timeout.
+# usage: scripts/gpu_job.sh <tag> [steps...]   steps: smoke tests bench benchsmall prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-run}; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export PYTHONUNBUFFERED=1
+run() {  # name timeout cmd...
+    local name=$1 to=$2; shift 2
+    echo "== $name: $*" | tee -a "$OUT/steps.log"
+    timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc" | tee -a "$OUT/steps.log"
+    tail -5 "$OUT/$name.log"
+    if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+        echo "fatal rc=$rc in $name: stopping" | tee -a "$OUT/steps.log"; exit $rc
+    fi
+    return 0
+}
+for s in "$@"; do
+    case $s in
+        smoke) run smoke 180 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+        tests) run tests 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+        testsall) run testsall 900 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+        benchsmall) run benchsmall 300 python3 bench.py --events 10000000 --steps 3 --warmup 1 --no-cpu ;;
+        bench) run bench 600 python3 bench.py ;;
+        prof) (cd /tmp && export TMPDIR=/tmp; true); run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu ;;
+        pmc) for c in "FETCH_SIZE" "WRITE_SIZE"; do run pmc_$c 300 rocprofv3 --pmc $c --kernel-trace -d "$OUT/pmc_$c" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu; done ;;
+        *) echo "unknown step $s" ;;
+    esac
+done
+echo "job done"

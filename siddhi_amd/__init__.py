@@ -1,0 +1,381 @@
+"""siddhi_amd — MI355X-native engine for Siddhi's pattern/sequence NFA path.
+
+Host-side mirror of the reference API the path sits behind (modules/siddhi-core/src/main/java/io/siddhi/core/):
+
+    SiddhiManager.createSiddhiAppRuntime(String)           SiddhiManager.java:93-96
+    SiddhiAppRuntime.getInputHandler / addCallback / start / shutdown   SiddhiAppRuntimeImpl.java:260-440
+    InputHandler.send(Object[]) / send(long, Object[]) / send(Event) / send(Event[])   stream/input/InputHandler.java:50-95
+    QueryCallback.receive(long, Event[], Event[])            query/output/callback/QueryCallback.java:106
+    StreamCallback.receive(Event[])                          stream/output/StreamCallback.java:129
+
+Every call goes through the C-ABI in include/siddhi_amd.h (siddhi_amd/_lib/libsiddhi_amd.so). There is no CPU
+fallback: importing works anywhere, but creating a runtime needs the gfx950 library and a GPU, and fails loudly
+otherwise. Events are processed in batches on the GPU: callbacks fire when a batch is flushed
+(SiddhiAppRuntime.flush(), shutdown(), or when the ingestion buffer fills), in the reference's delivery order.
+"""
+import ctypes
+import os
+import struct
+import time
+
+__all__ = ["SiddhiManager", "SiddhiAppRuntime", "InputHandler", "Event", "QueryCallback", "StreamCallback",
+           "SiddhiAppCreationException", "OperationNotSupportedException", "SiddhiParserException",
+           "DeviceError", "library_path", "load_library"]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libsiddhi_amd.so")
+
+INT, LONG, FLOAT, DOUBLE, BOOL, STRING = range(6)
+_CT = {INT: ctypes.c_int32, LONG: ctypes.c_int64, FLOAT: ctypes.c_float, DOUBLE: ctypes.c_double,
+       BOOL: ctypes.c_uint8, STRING: ctypes.c_uint32}
+
+
+class SiddhiAppCreationException(Exception):
+    pass
+
+
+class SiddhiParserException(SiddhiAppCreationException):
+    pass
+
+
+class OperationNotSupportedException(SiddhiAppCreationException):
+    pass
+
+
+class DeviceError(RuntimeError):
+    pass
+
+
+class CapacityError(RuntimeError):
+    pass
+
+
+_ERRS = {1: SiddhiParserException, 2: SiddhiAppCreationException, 3: OperationNotSupportedException,
+         4: ValueError, 5: DeviceError, 6: CapacityError}
+
+
+class _Opts(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("batch_capacity", ctypes.c_int64), ("max_partials", ctypes.c_int32),
+                ("flags", ctypes.c_int32)]
+
+
+class _Out(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int64), ("ts", ctypes.POINTER(ctypes.c_int64)),
+                ("expired", ctypes.POINTER(ctypes.c_uint8)), ("n_attrs", ctypes.c_int32),
+                ("types", ctypes.POINTER(ctypes.c_int32)),
+                ("values", ctypes.POINTER(ctypes.POINTER(ctypes.c_int64))),
+                ("nulls", ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)))]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("events", ctypes.c_int64), ("matches", ctypes.c_int64), ("ms_keygroup", ctypes.c_double),
+                ("ms_match", ctypes.c_double), ("ms_total", ctypes.c_double),
+                ("keygroup_launches", ctypes.c_int64), ("match_launches", ctypes.c_int64),
+                ("path", ctypes.c_int32), ("overflow", ctypes.c_int32),
+                ("ms_kg_hist", ctypes.c_double), ("ms_kg_prefix", ctypes.c_double),
+                ("ms_kg_scatter", ctypes.c_double), ("ms_chain_carry", ctypes.c_double),
+                ("ms_chain_match", ctypes.c_double)]
+
+
+_lib = None
+
+
+def library_path():
+    return LIB_PATH
+
+
+def load_library():
+    """Load the gfx950 engine library (raises if it was not built: no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise DeviceError("siddhi_amd native library missing at %s — run __graft_entry__.build() "
+                          "(make -C siddhi_amd); there is no CPU fallback" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    P, I32, I64, U32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint32
+    L.sdg_compile.argtypes = [ctypes.c_char_p, ctypes.POINTER(_Opts), ctypes.POINTER(P)]
+    L.sdg_destroy.argtypes = [P]
+    L.sdg_last_error.restype = ctypes.c_char_p
+    L.sdg_stream_index.argtypes = [P, ctypes.c_char_p]
+    L.sdg_stream_schema.argtypes = [P, I32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.POINTER(ctypes.c_int32))]
+    L.sdg_num_queries.argtypes = [P]
+    L.sdg_query_path.argtypes = [P, I32]
+    L.sdg_query_name.restype = ctypes.c_char_p
+    L.sdg_query_name.argtypes = [P, I32]
+    L.sdg_query_target.restype = ctypes.c_char_p
+    L.sdg_query_target.argtypes = [P, I32]
+    L.sdg_query_output_schema.argtypes = [P, I32, ctypes.POINTER(ctypes.c_int32),
+                                          ctypes.POINTER(ctypes.POINTER(ctypes.c_int32)),
+                                          ctypes.POINTER(ctypes.POINTER(ctypes.c_char_p))]
+    L.sdg_intern.restype = U32
+    L.sdg_intern.argtypes = [P, ctypes.c_char_p, ctypes.c_size_t]
+    L.sdg_string.restype = ctypes.c_char_p
+    L.sdg_string.argtypes = [P, U32]
+    L.sdg_push.argtypes = [P, I32, I64, P, P, P]
+    L.sdg_push_device.argtypes = [P, I32, I64, P, P, P]
+    L.sdg_advance_time.argtypes = [P, I64]
+    L.sdg_flush.argtypes = [P]
+    L.sdg_sync.argtypes = [P]
+    L.sdg_poll.argtypes = [P, I32, ctypes.POINTER(_Out)]
+    L.sdg_last_stats.argtypes = [P, ctypes.POINTER(Stats)]
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        msg = load_library().sdg_last_error().decode()
+        raise _ERRS.get(rc, RuntimeError)(msg)
+
+
+class Event:
+    """io.siddhi.core.event.Event: (timestamp, data, isExpired)"""
+    __slots__ = ("timestamp", "data", "expired")
+
+    def __init__(self, timestamp=-1, data=None, expired=False):
+        self.timestamp = timestamp
+        self.data = list(data) if data is not None else []
+        self.expired = expired
+
+    def getData(self, i=None):
+        return self.data if i is None else self.data[i]
+
+    def getTimestamp(self):
+        return self.timestamp
+
+    def isExpired(self):
+        return self.expired
+
+    def __repr__(self):
+        return "Event{timestamp=%d, data=%r, isExpired=%s}" % (self.timestamp, self.data, self.expired)
+
+
+class QueryCallback:
+    def receive(self, timestamp, inEvents, removeEvents):  # noqa: N802 (reference API names)
+        raise NotImplementedError
+
+
+class StreamCallback:
+    def receive(self, events):
+        raise NotImplementedError
+
+
+class InputHandler:
+    def __init__(self, rt, stream_id, index, types):
+        self._rt = rt
+        self.stream_id = stream_id
+        self._idx = index
+        self._types = types
+
+    def getStreamId(self):  # noqa: N802
+        return self.stream_id
+
+    def send(self, *args):
+        """send(data) | send(timestamp, data) | send(Event) | send([Event, ...])"""
+        if len(args) == 2:
+            self._rt._send(self._idx, self._types, [(int(args[0]), list(args[1]))])
+        elif isinstance(args[0], Event):
+            self._rt._send(self._idx, self._types, [(args[0].timestamp, args[0].data)])
+        elif args and isinstance(args[0], (list, tuple)) and args[0] and isinstance(args[0][0], Event):
+            self._rt._send(self._idx, self._types, [(ev.timestamp, ev.data) for ev in args[0]])
+        else:
+            self._rt._send(self._idx, self._types, [(None, list(args[0]))])
+
+    def send_columns(self, ts, columns, nulls=None):
+        """Columnar fast path: ts int64[n], one array per attribute (numpy or ctypes-compatible)."""
+        self._rt._push_columns(self._idx, self._types, ts, columns, nulls)
+
+
+class SiddhiAppRuntime:
+    def __init__(self, app_text, device=0, batch_capacity=0, compile_only=False):
+        L = load_library()
+        self._L = L
+        h = ctypes.c_void_p()
+        opts = _Opts(device, batch_capacity, 0, 1 if compile_only else 0)
+        _check(L.sdg_compile(app_text.encode(), ctypes.byref(opts), ctypes.byref(h)))
+        self._h = h
+        self.playback = "@app:playback" in app_text.replace(" ", "").lower()
+        self._last_ts = 0
+        self._callbacks = {}  # name -> [callback]
+        self._queries = []
+        for q in range(L.sdg_num_queries(h)):
+            name = L.sdg_query_name(h, q).decode()
+            target = L.sdg_query_target(h, q).decode()
+            n = ctypes.c_int32()
+            types = ctypes.POINTER(ctypes.c_int32)()
+            names = ctypes.POINTER(ctypes.c_char_p)()
+            _check(L.sdg_query_output_schema(h, q, ctypes.byref(n), ctypes.byref(types), ctypes.byref(names)))
+            self._queries.append((name, target, [types[i] for i in range(n.value)],
+                                  [names[i].decode() for i in range(n.value)]))
+        self._started = False
+
+    # --- reference API ---------------------------------------------------------------------------------
+    def getInputHandler(self, stream_id):  # noqa: N802
+        idx = self._L.sdg_stream_index(self._h, stream_id.encode())
+        if idx < 0:
+            raise SiddhiAppCreationException("Stream with id '%s' is not defined" % stream_id)
+        n = ctypes.c_int32()
+        types = ctypes.POINTER(ctypes.c_int32)()
+        _check(self._L.sdg_stream_schema(self._h, idx, ctypes.byref(n), ctypes.byref(types)))
+        return InputHandler(self, stream_id, idx, [types[i] for i in range(n.value)])
+
+    def addCallback(self, name, callback):  # noqa: N802
+        self._callbacks.setdefault(name, []).append(callback)
+
+    def start(self):
+        self._started = True
+
+    def shutdown(self):
+        if self._h:
+            try:
+                self.flush()
+            finally:
+                self._L.sdg_destroy(self._h)
+                self._h = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None):
+                self._L.sdg_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    # --- engine ----------------------------------------------------------------------------------------
+    def query_paths(self):
+        """device path per query: 0 chain kernel, 1 generic keyed NFA"""
+        return [self._L.sdg_query_path(self._h, q) for q in range(len(self._queries))]
+
+    def intern(self, s):
+        b = s.encode()
+        return self._L.sdg_intern(self._h, b, len(b))
+
+    def string(self, i):
+        r = self._L.sdg_string(self._h, i)
+        return None if r is None else r.decode()
+
+    def _encode(self, t, v):
+        if v is None:
+            return 0
+        if t == STRING:
+            return self.intern(str(v))
+        if t == BOOL:
+            return 1 if v else 0
+        if t in (INT, LONG):
+            return int(v)
+        return float(v)
+
+    def _send(self, idx, types, rows):
+        n = len(rows)
+        ts = (ctypes.c_int64 * n)()
+        for i, (t, _) in enumerate(rows):
+            if t is None:
+                t = self._last_ts if self.playback else int(time.time() * 1000)
+            ts[i] = t
+            self._last_ts = max(self._last_ts, t)
+        cols = (ctypes.c_void_p * max(1, len(types)))()
+        nulls = (ctypes.c_void_p * max(1, len(types)))()
+        keep = []
+        for a, t in enumerate(types):
+            arr = (_CT[t] * n)(*[self._encode(t, r[1][a]) for r in rows])
+            nl = (ctypes.c_uint8 * n)(*[1 if r[1][a] is None else 0 for r in rows])
+            keep += [arr, nl]
+            cols[a] = ctypes.cast(arr, ctypes.c_void_p)
+            nulls[a] = ctypes.cast(nl, ctypes.c_void_p) if any(r[1][a] is None for r in rows) else None
+        _check(self._L.sdg_push(self._h, idx, n, ts, cols, nulls))
+
+    def _push_columns(self, idx, types, ts, columns, nulls=None):
+        import numpy as np
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        n = len(ts)
+        cols = (ctypes.c_void_p * max(1, len(types)))()
+        nl = (ctypes.c_void_p * max(1, len(types)))()
+        keep = [ts]
+        dt = {INT: np.int32, LONG: np.int64, FLOAT: np.float32, DOUBLE: np.float64, BOOL: np.uint8, STRING: np.uint32}
+        for a, t in enumerate(types):
+            c = np.ascontiguousarray(columns[a], dtype=dt[t])
+            keep.append(c)
+            cols[a] = c.ctypes.data
+            if nulls is not None and nulls[a] is not None:
+                m = np.ascontiguousarray(nulls[a], dtype=np.uint8)
+                keep.append(m)
+                nl[a] = m.ctypes.data
+        _check(self._L.sdg_push(self._h, idx, n, ts.ctypes.data, cols, nl))
+
+    def push_device(self, stream_id, n, ts_ptr, col_ptrs):
+        """Device-resident columns (e.g. torch CUDA tensors' data_ptr()); kept alive by the caller."""
+        idx = self._L.sdg_stream_index(self._h, stream_id.encode())
+        cols = (ctypes.c_void_p * len(col_ptrs))(*col_ptrs)
+        _check(self._L.sdg_push_device(self._h, idx, n, ctypes.c_void_p(ts_ptr), cols, None))
+
+    def advance_time(self, ts):
+        _check(self._L.sdg_advance_time(self._h, ts))
+
+    def flush(self, deliver=True):
+        _check(self._L.sdg_flush(self._h))
+        if deliver:
+            self._deliver()
+
+    def stats(self):
+        s = Stats()
+        _check(self._L.sdg_last_stats(self._h, ctypes.byref(s)))
+        return s
+
+    def poll(self, q):
+        out = _Out()
+        _check(self._L.sdg_poll(self._h, q, ctypes.byref(out)))
+        name, target, types, names = self._queries[q]
+        evs = []
+        for i in range(out.n):
+            data = []
+            for j, t in enumerate(types):
+                if out.nulls[j][i]:
+                    data.append(None)
+                    continue
+                v = out.values[j][i]
+                if t == INT:
+                    data.append(ctypes.c_int32(v).value)
+                elif t == LONG:
+                    data.append(v)
+                elif t == FLOAT:
+                    data.append(struct.unpack("<f", struct.pack("<I", v & 0xffffffff))[0])
+                elif t == DOUBLE:
+                    data.append(struct.unpack("<d", struct.pack("<q", v))[0])
+                elif t == BOOL:
+                    data.append(bool(v))
+                else:
+                    data.append(self.string(v))
+            evs.append(Event(out.ts[i], data, bool(out.expired[i])))
+        return evs
+
+    def _deliver(self):
+        for q, (name, target, types, names) in enumerate(self._queries):
+            evs = self.poll(q)
+            if not evs:
+                continue
+            for cb in self._callbacks.get(name, []):
+                cb.receive(evs[-1].timestamp, evs, None)
+            for cb in self._callbacks.get(target, []):
+                cb.receive(evs)
+
+    def raw_outputs(self, q):
+        """(types, ts[n], values[attr][n] payload ints, nulls[attr][n]) straight from sdg_poll"""
+        out = _Out()
+        _check(self._L.sdg_poll(self._h, q, ctypes.byref(out)))
+        n = out.n
+        types = self._queries[q][2]
+        return types, [out.ts[i] for i in range(n)], \
+            [[out.values[j][i] for i in range(n)] for j in range(len(types))], \
+            [[out.nulls[j][i] for i in range(n)] for j in range(len(types))]
+
+
+class SiddhiManager:
+    def __init__(self, device=0):
+        self.device = device
+
+    def createSiddhiAppRuntime(self, app, batch_capacity=0):  # noqa: N802
+        return SiddhiAppRuntime(app, device=self.device, batch_capacity=batch_capacity)
+
+    def shutdown(self):
+        pass

@@ -1,0 +1,528 @@
+// SiddhiQL AST -> NFA table + bytecode. An independent implementation of the reference's lowering:
+//   util/parser/StateInputStreamParser.java:76-408   (state ids, start flags, next / every / within wiring,
+//                                                     logical element 2 before element 1, count bounds)
+//   util/parser/ExpressionParser.java:224-667, 1254-1520 (variables, compare / math promotion and checks)
+//   util/parser/SelectorParser.java:212-218          (select expressions: UNKNOWN_STATE, default index 0)
+#include "compile.h"
+
+#include <algorithm>
+#include <cstring>
+#include <functional>
+#include <map>
+
+#include "../../../include/siddhi_amd.h"
+
+namespace sdg {
+
+namespace {
+
+struct Meta {
+    std::vector<const sql::StreamDefinition*> defs;
+    std::vector<std::string> refs;
+    std::vector<bool> multi;
+};
+
+class QC {
+   public:
+    QC(const sql::App& app, const sql::Query& q, Interner& s, HostQuery& out) : app_(app), q_(q), strings_(s), h_(out) {}
+
+    void run() {
+        h_.name = q_.name;
+        h_.target = q_.target;
+        h_.partition = q_.partition_index;
+        Plan& p = h_.plan;
+        p.seq = q_.state_type == sql::StateType::SEQUENCE;
+        // receivers: stream ids in first-appearance order (StateInputStreamParser :91-110 iterates getAllStreamIds)
+        std::function<void(const sql::StateP&)> walk = [&](const sql::StateP& e) {
+            if (e->kind == sql::StateKind::STREAM || e->kind == sql::StateKind::ABSENT) {
+                int si = app_.stream_index(e->stream_id);
+                if (si < 0)
+                    throw CompileError(SDG_ERR_VALIDATION, "Stream with id '" + e->stream_id + "' is not defined");
+                if (std::find(h_.streams.begin(), h_.streams.end(), si) == h_.streams.end()) h_.streams.push_back(si);
+            }
+            for (auto& k : e->kids) walk(k);
+        };
+        walk(q_.root);
+        if ((int)h_.streams.size() > MAX_STATES) throw CompileError(SDG_ERR_UNSUPPORTED, "too many streams");
+        std::vector<int> pre_list;
+        Sub root = parse(q_.root, -1, -1, false, pre_list, true);
+        p.n_states = (int)rows_.size();
+        if (p.n_states > MAX_STATES) throw CompileError(SDG_ERR_UNSUPPORTED, "too many states");
+        // within -> every processor, start ids = processors flagged start (:129-141)
+        p.has_within = q_.has_within;
+        p.within_ms = q_.within_ms;
+        rows_[root.first].last = root.last;  // the first processor's thisLastProcessor
+        set_selector(q_.root, root);
+        h_.expire_order = pre_list;
+        // selector
+        if (q_.select_all) throw CompileError(SDG_ERR_UNSUPPORTED, "select * on a pattern query is not supported");
+        if ((int)q_.select.size() > MAX_OUT) throw CompileError(SDG_ERR_UNSUPPORTED, "too many output attributes");
+        p.n_out = (int)q_.select.size();
+        for (size_t i = 0; i < q_.select.size(); ++i) {
+            const auto& oa = q_.select[i];
+            Prog pr;
+            pr.start = (int)h_.code.size();
+            bool multi = false;
+            uint8_t k = expr(oa.expr, -1, 0, &multi);
+            pr.len = (int)h_.code.size() - pr.start;
+            if (multi)
+                throw CompileError(SDG_ERR_UNSUPPORTED,
+                                   "multi-value selection of a count state (no [index]) is not supported on device");
+            p.out_prog[i] = pr;
+            p.out_kind[i] = k;
+            p.out_multi[i] = 0;
+            h_.out_names.push_back(oa.rename);
+            h_.out_types.push_back(k);
+        }
+        for (int s = 0; s < p.n_states; ++s) p.st[s] = rows_[s];
+        // physical columns
+        if ((int)h_.cols.size() > MAX_COLS) throw CompileError(SDG_ERR_UNSUPPORTED, "too many referenced attributes");
+        p.n_cols = (int)h_.cols.size();
+        for (size_t c = 0; c < h_.cols.size(); ++c) p.col_kind[c] = h_.cols[c].second;
+        p.n_streams = (int)h_.streams.size();
+        for (size_t i = 0; i < h_.streams.size(); ++i) p.streams[i] = h_.streams[i];
+        h_.col_attr.assign(h_.streams.size(), std::vector<int>(h_.cols.size(), -1));
+        for (size_t i = 0; i < h_.streams.size(); ++i) {
+            const auto& def = app_.streams[h_.streams[i]];
+            for (size_t c = 0; c < h_.cols.size(); ++c) {
+                int ai = def.index_of(h_.cols[c].first);
+                if (ai >= 0 && (uint8_t)def.attrs[ai].type == h_.cols[c].second) h_.col_attr[i][c] = ai;
+            }
+        }
+        partition_keys();
+        p.partitioned = q_.partition_index >= 0;
+        detect_chain(root);
+        p.n_code = (int)h_.code.size();
+        p.n_consts = (int)h_.consts.size();
+    }
+
+   private:
+    const sql::App& app_;
+    const sql::Query& q_;
+    Interner& strings_;
+    HostQuery& h_;
+    Meta meta_;
+    std::vector<StateRow> rows_;
+
+    struct Sub {
+        int first = -1, last = -1;
+    };
+
+    int col_id(const std::string& name, uint8_t kind) {
+        for (size_t i = 0; i < h_.cols.size(); ++i)
+            if (h_.cols[i].first == name && h_.cols[i].second == kind) return (int)i;
+        h_.cols.push_back({name, kind});
+        return (int)h_.cols.size() - 1;
+    }
+    void emit(uint8_t op, uint8_t k = 0, uint8_t a = 0, int32_t b = 0, int32_t c = 0, int32_t imm = 0) {
+        Instr in;
+        std::memset(&in, 0, sizeof in);
+        in.op = op;
+        in.k = k;
+        in.a = a;
+        in.b = b;
+        in.c = c;
+        in.imm = imm;
+        h_.code.push_back(in);
+    }
+    int konst(int64_t v) {
+        h_.consts.push_back(v);
+        return (int)h_.consts.size() - 1;
+    }
+    static int64_t f32b(float f) { uint32_t u; std::memcpy(&u, &f, 4); return (int64_t)u; }
+    static int64_t f64b(double d) { int64_t u; std::memcpy(&u, &d, 8); return u; }
+
+    void cvt(uint8_t from, uint8_t to) {
+        if (from != to) emit(OP_CVT, to, from);
+    }
+
+    // ExpressionParser.parseVariable (MetaStateEvent branch)
+    uint8_t var(const sql::ExprP& e, int cur, int defidx, bool* multi_out) {
+        int idx = defidx;
+        if (e->has_index) idx = e->index <= sql::IDX_LAST ? e->index + 1 : e->index;
+        int chain = -1;
+        sql::Type type = sql::Type::OBJECT;
+        bool multi = false;
+        if (e->stream_ref.empty()) {
+            if (cur == -1) {
+                bool found = false;
+                for (size_t i = 0; i < meta_.defs.size(); ++i) {
+                    int ai = meta_.defs[i]->index_of(e->attr);
+                    if (ai < 0) continue;
+                    if (found)
+                        throw CompileError(SDG_ERR_VALIDATION, "attribute '" + e->attr + "' is ambiguous");
+                    found = true;
+                    chain = (int)i;
+                    type = meta_.defs[i]->attrs[ai].type;
+                }
+            } else {
+                int ai = meta_.defs[cur]->index_of(e->attr);
+                if (ai < 0)
+                    throw CompileError(SDG_ERR_VALIDATION, "attribute '" + e->attr + "' does not exist in '" +
+                                                               meta_.defs[cur]->id + "'");
+                chain = cur;
+                type = meta_.defs[cur]->attrs[ai].type;
+            }
+        } else {
+            for (size_t i = 0; i < meta_.defs.size(); ++i) {
+                bool hit = meta_.refs[i].empty() ? meta_.defs[i]->id == e->stream_ref : meta_.refs[i] == e->stream_ref;
+                if (!hit) continue;
+                int ai = meta_.defs[i]->index_of(e->attr);
+                if (ai < 0)
+                    throw CompileError(SDG_ERR_VALIDATION, "attribute '" + e->attr + "' does not exist in '" +
+                                                               meta_.defs[i]->id + "'");
+                type = meta_.defs[i]->attrs[ai].type;
+                chain = (int)i;
+                if (!meta_.refs[i].empty()) {
+                    if (cur > -1 && !meta_.refs[cur].empty() && e->has_index && e->index <= sql::IDX_LAST) {
+                        if (e->stream_ref == meta_.refs[cur]) idx = e->index;  // e2[last] inside e2's own filter
+                    } else if (cur == -1 && !e->has_index) {
+                        multi = meta_.multi[i];
+                    }
+                }
+                break;
+            }
+        }
+        if (chain < 0) throw CompileError(SDG_ERR_VALIDATION, "no matching stream reference for '" + e->attr + "'");
+        if (type == sql::Type::OBJECT) throw CompileError(SDG_ERR_UNSUPPORTED, "object attributes are not supported");
+        if (multi_out) *multi_out = multi;
+        uint8_t k = (uint8_t)type;
+        emit(OP_LOAD, k, (uint8_t)chain, col_id(e->attr, k), idx);
+        return k;
+    }
+
+    uint8_t cond(const sql::ExprP& e, int cur, int defidx) {
+        uint8_t k = expr(e, cur, defidx, nullptr);
+        if (k != VK_BOOL) throw CompileError(SDG_ERR_VALIDATION, "condition is not a bool expression");
+        return k;
+    }
+
+    uint8_t expr(const sql::ExprP& e, int cur, int defidx, bool* multi_out) {
+        using sql::ExprKind;
+        if (multi_out) *multi_out = false;
+        switch (e->kind) {
+            case ExprKind::CONST: {
+                const auto& c = e->c;
+                int64_t v = 0;
+                switch (c.type) {
+                    case sql::Type::INT: v = (int32_t)c.i; break;
+                    case sql::Type::LONG: v = c.i; break;
+                    case sql::Type::FLOAT: v = f32b(c.f); break;
+                    case sql::Type::DOUBLE: v = f64b(c.d); break;
+                    case sql::Type::BOOL: v = c.i ? 1 : 0; break;
+                    case sql::Type::STRING: v = strings_.get(c.s); break;
+                    default: throw CompileError(SDG_ERR_UNSUPPORTED, "unsupported constant");
+                }
+                emit(OP_CONST, (uint8_t)c.type, 0, 0, 0, konst(v));
+                return (uint8_t)c.type;
+            }
+            case ExprKind::VAR: return var(e, cur, defidx, multi_out);
+            case ExprKind::AND:
+            case ExprKind::OR:
+                cond(e->kids[0], cur, defidx);
+                cond(e->kids[1], cur, defidx);
+                emit(e->kind == ExprKind::AND ? OP_AND : OP_OR, VK_BOOL);
+                return VK_BOOL;
+            case ExprKind::NOT:
+                cond(e->kids[0], cur, defidx);
+                emit(OP_NOT, VK_BOOL);
+                return VK_BOOL;
+            case ExprKind::CMP: {
+                size_t at_l = h_.code.size();
+                uint8_t lk = expr(e->kids[0], cur, defidx, nullptr);
+                size_t end_l = h_.code.size();
+                uint8_t rk = expr(e->kids[1], cur, defidx, nullptr);
+                bool eq = e->cmp == sql::CmpOp::EQ || e->cmp == sql::CmpOp::NE;
+                uint8_t t;
+                if (lk == VK_STR || rk == VK_STR) {
+                    if (lk != rk || !eq)
+                        throw CompileError(SDG_ERR_UNSUPPORTED, "string values support only == and !=");
+                    t = VK_STR;
+                } else if (lk == VK_BOOL || rk == VK_BOOL) {
+                    if (lk != rk || !eq) throw CompileError(SDG_ERR_UNSUPPORTED, "bool values support only == and !=");
+                    t = VK_BOOL;
+                } else if (lk == VK_F64 || rk == VK_F64) {
+                    t = VK_F64;
+                } else if (lk == VK_F32 || rk == VK_F32) {
+                    t = (eq && (lk == VK_I64 || rk == VK_I64)) ? VK_F64 : VK_F32;
+                } else if (lk == VK_I64 || rk == VK_I64) {
+                    t = VK_I64;
+                } else {
+                    t = VK_I32;
+                }
+                if (lk != t) {  // insert the left conversion right after the left operand's code
+                    Instr in;
+                    std::memset(&in, 0, sizeof in);
+                    in.op = OP_CVT;
+                    in.k = t;
+                    in.a = lk;
+                    h_.code.insert(h_.code.begin() + end_l, in);
+                }
+                (void)at_l;
+                cvt(rk, t);
+                static const uint8_t map[] = {CMP_EQ, CMP_NE, CMP_GT, CMP_GE, CMP_LT, CMP_LE};
+                emit(OP_CMP, t, map[(int)e->cmp]);
+                return VK_BOOL;
+            }
+            case ExprKind::ADD: case ExprKind::SUB: case ExprKind::MUL: case ExprKind::DIV: case ExprKind::MOD: {
+                uint8_t lk = expr(e->kids[0], cur, defidx, nullptr);
+                size_t end_l = h_.code.size();
+                uint8_t rk = expr(e->kids[1], cur, defidx, nullptr);
+                if (lk > VK_F64 || rk > VK_F64)
+                    throw CompileError(SDG_ERR_VALIDATION, "Arithmetic operation between non-numeric types");
+                uint8_t t = (lk == VK_F64 || rk == VK_F64) ? VK_F64
+                            : (lk == VK_F32 || rk == VK_F32) ? VK_F32
+                            : (lk == VK_I64 || rk == VK_I64) ? VK_I64 : VK_I32;
+                if (lk != t) {
+                    Instr in;
+                    std::memset(&in, 0, sizeof in);
+                    in.op = OP_CVT;
+                    in.k = t;
+                    in.a = lk;
+                    h_.code.insert(h_.code.begin() + end_l, in);
+                }
+                cvt(rk, t);
+                uint8_t op = e->kind == ExprKind::ADD ? AR_ADD : e->kind == ExprKind::SUB ? AR_SUB
+                             : e->kind == ExprKind::MUL ? AR_MUL : e->kind == ExprKind::DIV ? AR_DIV : AR_MOD;
+                emit(OP_ARITH, t, op);
+                return t;
+            }
+            case ExprKind::IS_NULL:
+                expr(e->kids[0], cur, defidx, nullptr);
+                emit(OP_ISNULL, VK_BOOL);
+                return VK_BOOL;
+            case ExprKind::IS_NULL_STREAM: {
+                int idx = defidx;
+                if (e->has_index) idx = e->index <= sql::IDX_LAST ? e->index + 1 : e->index;
+                int chain = -1;
+                for (size_t i = 0; i < meta_.refs.size(); ++i) {
+                    bool hit = meta_.refs[i].empty() ? meta_.defs[i]->id == e->stream_ref : meta_.refs[i] == e->stream_ref;
+                    if (!hit) continue;
+                    chain = (int)i;
+                    if (!meta_.refs[i].empty() && cur > -1 && !meta_.refs[cur].empty() && e->has_index &&
+                        e->index <= sql::IDX_LAST && e->stream_ref == meta_.refs[cur])
+                        idx = e->index;
+                    break;
+                }
+                if (chain < 0) throw CompileError(SDG_ERR_VALIDATION, "stream reference '" + e->stream_ref + "' not found");
+                emit(OP_SLOTNULL, VK_BOOL, (uint8_t)chain, 0, idx);
+                return VK_BOOL;
+            }
+            default:
+                throw CompileError(SDG_ERR_UNSUPPORTED, "function '" + e->fn_name + "' is not supported in pattern queries");
+        }
+    }
+
+    StateRow& newrow(uint8_t kind, const sql::StateElement& el, bool is_start) {
+        StateRow r;
+        std::memset(&r, 0, sizeof r);
+        r.kind = kind;
+        r.is_start = is_start;
+        r.seq = q_.state_type == sql::StateType::SEQUENCE;
+        r.stream = app_.stream_index(el.stream_id);
+        r.next = r.next_every = r.within_every = r.partner = r.callback = -1;
+        r.last = (int)rows_.size();
+        r.waiting_ms = el.has_waiting ? el.waiting_ms : -1;
+        rows_.push_back(r);
+        return rows_.back();
+    }
+
+    void set_next(int post_state, int next_first) {
+        StateRow& r = rows_[post_state];
+        r.next = next_first;
+        if (r.kind == PK_LOGICAL && r.partner >= 0) rows_[r.partner].next = next_first;
+        if (r.kind == PK_COUNT && r.is_start && r.seq && r.min_count == 0) rows_[next_first].callback = post_state;
+    }
+    void set_next_every(int post_state, int target) {
+        StateRow& r = rows_[post_state];
+        r.next_every = target;
+        if (r.kind == PK_LOGICAL && r.partner >= 0) rows_[r.partner].next_every = target;
+    }
+
+    // StateInputStreamParser.parse
+    Sub parse(const sql::StateP& el, int kind_override, int logical_or, bool multi, std::vector<int>& pre_list,
+              bool is_start) {
+        using sql::StateKind;
+        switch (el->kind) {
+            case StateKind::STREAM:
+            case StateKind::ABSENT: {
+                const sql::StreamDefinition* def = app_.stream(el->stream_id);
+                meta_.defs.push_back(def);
+                meta_.refs.push_back(el->ref);
+                meta_.multi.push_back(multi);
+                int sid = (int)meta_.defs.size() - 1;
+                uint8_t kind = el->kind == StateKind::ABSENT ? PK_ABSENT : PK_STREAM;
+                if (kind_override >= 0) kind = (uint8_t)kind_override;
+                if (el->kind == StateKind::ABSENT && kind_override >= 0)
+                    throw CompileError(SDG_ERR_UNSUPPORTED, "absent states inside logical/count are not supported on device");
+                StateRow& r = newrow(kind, *el, is_start);
+                r.logical_or = (uint8_t)(logical_or > 0);
+                // filters: FilterProcessor per [..], CURRENT default index
+                Prog pr;
+                pr.start = (int)h_.code.size();
+                for (size_t i = 0; i < el->filters.size(); ++i) {
+                    cond(el->filters[i], sid, sql::IDX_CURRENT);
+                    if (i > 0) emit(OP_AND, VK_BOOL);
+                }
+                pr.len = (int)h_.code.size() - pr.start;
+                rows_[sid].filter = pr;
+                pre_list.push_back(sid);
+                Sub s;
+                s.first = s.last = sid;
+                return s;
+            }
+            case StateKind::NEXT: {
+                Sub a = parse(el->kids[0], -1, -1, multi, pre_list, is_start);
+                Sub b = parse(el->kids[1], -1, -1, multi, pre_list, false);
+                set_next(a.last, b.first);
+                Sub s;
+                s.first = a.first;
+                s.last = b.last;
+                return s;
+            }
+            case StateKind::EVERY: {
+                std::vector<int> group;
+                Sub in = parse(el->kids[0], -1, -1, multi, group, is_start);
+                set_next_every(in.last, in.first);
+                for (int g : group) rows_[g].within_every = in.first;
+                pre_list.insert(pre_list.end(), group.begin(), group.end());
+                return in;
+            }
+            case StateKind::LOGICAL: {
+                bool orr = el->logical == sql::LogicalType::OR;
+                if (el->kids[0]->kind == StateKind::ABSENT || el->kids[1]->kind == StateKind::ABSENT)
+                    throw CompileError(SDG_ERR_UNSUPPORTED, "absent inside a logical state is not supported on device yet");
+                Sub s2 = parse(el->kids[1], PK_LOGICAL, orr, multi, pre_list, is_start);
+                Sub s1 = parse(el->kids[0], PK_LOGICAL, orr, multi, pre_list, is_start);
+                rows_[s1.first].partner = s2.first;
+                rows_[s2.first].partner = s1.first;
+                Sub s;
+                s.first = s1.first;
+                s.last = s2.last;
+                return s;
+            }
+            case StateKind::COUNT: {
+                int mn = el->min_count == sql::COUNT_ANY ? 0 : el->min_count;
+                int mx = el->max_count == sql::COUNT_ANY ? INT32_MAX : el->max_count;
+                if (el->seq_quantifier && q_.state_type != sql::StateType::SEQUENCE)
+                    throw CompileError(SDG_ERR_PARSE, "'*', '+' and '?' are only valid in sequences");
+                Sub s = parse(el->kids[0], PK_COUNT, -1, true, pre_list, is_start);
+                rows_[s.first].min_count = mn;
+                rows_[s.first].max_count = mx;
+                return s;
+            }
+        }
+        throw CompileError(SDG_ERR_UNSUPPORTED, "unsupported state element");
+    }
+
+    // StateInnerStateRuntime.setQuerySelector: which posts feed the selector
+    void set_selector(const sql::StateP& el, Sub s) {
+        std::function<int(const sql::StateP&, int&)> walk;  // returns nothing; marks via ids
+        // recompute by structure: Next -> right, Every -> inner, Logical -> both, leaf -> itself
+        std::function<void(const sql::StateP&, std::vector<int>&, int&)> ids = [&](const sql::StateP& e,
+                                                                                  std::vector<int>& out, int& ctr) {
+            // assign the same state ids as parse(): leaves in parse order (logical: kid 1 first)
+            switch (e->kind) {
+                case sql::StateKind::STREAM:
+                case sql::StateKind::ABSENT: out.push_back(ctr++); break;
+                case sql::StateKind::NEXT: ids(e->kids[0], out, ctr); ids(e->kids[1], out, ctr); break;
+                case sql::StateKind::EVERY:
+                case sql::StateKind::COUNT: ids(e->kids[0], out, ctr); break;
+                case sql::StateKind::LOGICAL: ids(e->kids[1], out, ctr); ids(e->kids[0], out, ctr); break;
+            }
+        };
+        std::function<void(const sql::StateP&, int)> mark;  // base = first state id of this subtree
+        mark = [&](const sql::StateP& e, int base) {
+            std::vector<int> tmp;
+            int ctr = base;
+            switch (e->kind) {
+                case sql::StateKind::STREAM:
+                case sql::StateKind::ABSENT:
+                case sql::StateKind::COUNT:
+                    rows_[base].selector_after = 1;
+                    break;
+                case sql::StateKind::EVERY:
+                    mark(e->kids[0], base);
+                    break;
+                case sql::StateKind::NEXT: {
+                    ids(e->kids[0], tmp, ctr);
+                    mark(e->kids[1], ctr);
+                    break;
+                }
+                case sql::StateKind::LOGICAL: {
+                    // element 2 got `base`, element 1 got base+1
+                    rows_[base].selector_after = 1;
+                    rows_[base + 1].selector_after = 1;
+                    break;
+                }
+            }
+        };
+        (void)s;
+        mark(el, 0);
+    }
+
+    void partition_keys() {
+        h_.key_attr.assign(h_.streams.size(), -1);
+        h_.key_kind.assign(h_.streams.size(), 0);
+        if (q_.partition_index < 0) return;
+        const sql::Partition& part = app_.partitions[q_.partition_index];
+        for (size_t i = 0; i < h_.streams.size(); ++i) {
+            const auto& def = app_.streams[h_.streams[i]];
+            bool found = false;
+            for (const auto& w : part.with) {
+                if (w.stream_id != def.id) continue;
+                if (found) throw CompileError(SDG_ERR_UNSUPPORTED, "a stream partitioned twice is not supported");
+                if (w.expr->kind != sql::ExprKind::VAR || !w.expr->stream_ref.empty() || w.expr->has_index)
+                    throw CompileError(SDG_ERR_UNSUPPORTED, "value partitions must be a plain attribute of the stream");
+                int ai = def.index_of(w.expr->attr);
+                if (ai < 0) throw CompileError(SDG_ERR_VALIDATION, "partition attribute '" + w.expr->attr + "' not found");
+                h_.key_attr[i] = ai;
+                h_.key_kind[i] = (uint8_t)def.attrs[ai].type;
+                found = true;
+            }
+            if (!found)
+                throw CompileError(SDG_ERR_UNSUPPORTED, "stream '" + def.id + "' used in a partition without a key");
+        }
+    }
+
+    // independent-partial fast path: PATTERN, every e1=S0[c0] -> e2=S1[c1] (or every e1=S0[c0] alone), plain
+    // stream states. See DESIGN.md "chain kernel" for the equivalence argument.
+    void detect_chain(Sub) {
+        Plan& p = h_.plan;
+        p.chain = 0;
+        if (q_.state_type != sql::StateType::PATTERN) { h_.chain_reason = "sequence"; return; }
+        const sql::StateP& r = q_.root;
+        auto plain = [](const sql::StateP& e) { return e->kind == sql::StateKind::STREAM; };
+        bool ok = false;
+        if (r->kind == sql::StateKind::EVERY && plain(r->kids[0])) ok = true;
+        if (r->kind == sql::StateKind::NEXT && r->kids[0]->kind == sql::StateKind::EVERY && plain(r->kids[0]->kids[0]) &&
+            plain(r->kids[1]))
+            ok = true;
+        if (!ok) { h_.chain_reason = "not `every e1 -> e2`"; return; }
+        p.chain = 1;
+        h_.chain_reason = "every e1 -> e2 (independent partials)";
+    }
+};
+
+}  // namespace
+
+std::vector<HostQuery> compile_app(const sql::App& app, Interner& strings) {
+    std::vector<HostQuery> out;
+    for (const auto& q : app.queries) {
+        if (q.target_inner) throw CompileError(SDG_ERR_UNSUPPORTED, "inner (#) streams are not supported");
+        if (q.out_type != sql::OutputEventType::CURRENT)
+            throw CompileError(SDG_ERR_UNSUPPORTED, "only 'insert [current events] into' is supported on device");
+        HostQuery h;
+        QC(app, q, strings, h).run();
+        out.push_back(std::move(h));
+    }
+    // a query output consumed by another query (query chaining) is not on the device path
+    for (const auto& h : out)
+        for (const auto& g : out)
+            for (int s : g.streams)
+                if (app.streams[s].id == h.target)
+                    throw CompileError(SDG_ERR_UNSUPPORTED, "query chaining (output '" + h.target + "' consumed) is not supported");
+    return out;
+}
+
+}  // namespace sdg

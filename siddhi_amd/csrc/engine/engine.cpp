@@ -1,0 +1,722 @@
+// Engine runtime behind include/siddhi_amd.h: ingestion buffers, device residency, flush orchestration,
+// output delivery. One engine == one HIP device + one stream; calls on a handle are serialised by the caller
+// (the reference serialises a query under patternSyncObject, MultiProcessStreamReceiver.java:97).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../../include/siddhi_amd.h"
+#include "../kernels/kernels.h"
+#include "../siddhiql/parser.h"
+#include "compile.h"
+
+namespace sdg {
+namespace {
+
+thread_local std::string g_err;
+
+struct DeviceError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+#define HIPCHECK(x)                                                                                   \
+    do {                                                                                              \
+        hipError_t e_ = (x);                                                                          \
+        if (e_ != hipSuccess) throw DeviceError(std::string(#x) + ": " + hipGetErrorString(e_));       \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    void* ensure(size_t bytes) {
+        if (bytes == 0) bytes = 8;
+        if (bytes > cap) {
+            if (p) HIPCHECK(hipFree(p));
+            p = nullptr;
+            size_t c = std::max(bytes, cap + cap / 2);
+            HIPCHECK(hipMalloc(&p, c));
+            cap = c;
+        }
+        return p;
+    }
+    template <class T>
+    T* as() const { return (T*)p; }
+};
+
+int width_of(uint8_t kind) {
+    switch (kind) {
+        case VK_I64: case VK_F64: return 8;
+        case VK_BOOL: return 1;
+        default: return 4;
+    }
+}
+
+// Java toString of a partition value (ValuePartitionExecutor.execute) -- Float/Double use the Java layout
+std::string java_real(double x, bool is_float) {
+    if (x != x) return "NaN";
+    if (std::isinf(x)) return x > 0 ? "Infinity" : "-Infinity";
+    if (x == 0) return std::signbit(x) ? "-0.0" : "0.0";
+    char buf[64];
+    for (int prec = 1; prec <= 17; ++prec) {
+        std::snprintf(buf, sizeof buf, "%.*e", prec - 1, x);
+        if (is_float ? (std::strtof(buf, nullptr) == (float)x) : (std::strtod(buf, nullptr) == x)) break;
+    }
+    std::string s(buf);
+    bool neg = s[0] == '-';
+    if (neg) s = s.substr(1);
+    size_t ep = s.find('e');
+    int e10 = std::atoi(s.c_str() + ep + 1);
+    std::string d;
+    for (size_t i = 0; i < ep; ++i) if (s[i] != '.') d += s[i];
+    while (d.size() > 1 && d.back() == '0') d.pop_back();
+    std::string o;
+    double ax = std::fabs(x);
+    if (ax >= 1e-3 && ax < 1e7) {
+        int pt = e10 + 1;
+        if (pt <= 0) o = "0." + std::string(-pt, '0') + d;
+        else if ((int)d.size() <= pt) o = d + std::string(pt - d.size(), '0') + ".0";
+        else o = d.substr(0, pt) + "." + d.substr(pt);
+    } else {
+        o = d.substr(0, 1) + "." + (d.size() > 1 ? d.substr(1) : "0") + "E" + std::to_string(e10);
+    }
+    return neg ? "-" + o : o;
+}
+
+struct PushChunk {
+    int stream;
+    int64_t n;
+    bool device;
+    std::vector<int64_t> ts;
+    std::vector<std::vector<uint8_t>> cols;
+    std::vector<std::vector<uint8_t>> nulls;
+    const int64_t* d_ts = nullptr;
+    std::vector<const void*> d_cols;
+    std::vector<const uint8_t*> d_nulls;
+};
+
+struct QueryRt {
+    HostQuery hq;
+    DevBuf d_plan, d_code, d_consts;
+    bool string_keys = true;                        // all partition keys are string attributes (ids used as keys)
+    std::unordered_map<std::string, uint32_t> keydict;
+    int64_t seq = 0;
+    // batch staging
+    DevBuf st_ts, st_qs, st_key, st_cols[MAX_COLS], st_nulls[MAX_COLS];
+    // sorted view
+    DevBuf so_ts, so_qs, so_key, so_orig, so_cols[MAX_COLS], so_nulls[MAX_COLS], seg, kg_counts, kg_gsum;
+    // carries (double buffered)
+    struct Carry {
+        DevBuf key, ts, seq, vals, nulls;
+        int64_t n = 0, cap = 0;
+    } carry[2];
+    int cur = 0;
+    // outputs
+    DevBuf o_ts, o_key, o_vals, o_nulls, o_emit, o_first, counters, flags;
+    int64_t out_n = 0, out_cap = 0;
+    bool polled = true;
+    // host copies for sdg_poll
+    std::vector<int64_t> h_ts;
+    std::vector<uint8_t> h_expired;
+    std::vector<std::vector<int64_t>> h_vals;
+    std::vector<std::vector<uint8_t>> h_nulls;
+    std::vector<const int64_t*> h_vptr;
+    std::vector<const uint8_t*> h_nptr;
+};
+
+}  // namespace
+}  // namespace sdg
+
+using namespace sdg;
+
+struct sdg_engine {
+    sql::App app;
+    Interner strings;
+    std::vector<std::unique_ptr<QueryRt>> qs;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[12] = {};
+    std::vector<PushChunk> pending;
+    int64_t capacity = 1 << 24;
+    int64_t pending_n = 0;
+    sdg_stats stats{};
+    std::vector<std::vector<int32_t>> stream_types;
+    std::vector<std::vector<int32_t>> out_types;
+    std::vector<std::vector<const char*>> out_names;
+    bool compile_only = false;
+};
+
+namespace {
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+void upload_plan(sdg_engine* e, QueryRt& q) {
+    HostQuery& h = q.hq;
+    void* dp = q.d_plan.ensure(sizeof(Plan));
+    HIPCHECK(hipMemcpyAsync(dp, &h.plan, sizeof(Plan), hipMemcpyHostToDevice, e->stream));
+    if (!h.code.empty()) {
+        void* dc = q.d_code.ensure(h.code.size() * sizeof(Instr));
+        HIPCHECK(hipMemcpyAsync(dc, h.code.data(), h.code.size() * sizeof(Instr), hipMemcpyHostToDevice, e->stream));
+    } else {
+        q.d_code.ensure(sizeof(Instr));
+    }
+    if (!h.consts.empty()) {
+        void* dk = q.d_consts.ensure(h.consts.size() * 8);
+        HIPCHECK(hipMemcpyAsync(dk, h.consts.data(), h.consts.size() * 8, hipMemcpyHostToDevice, e->stream));
+    } else {
+        q.d_consts.ensure(8);
+    }
+    HIPCHECK(hipStreamSynchronize(e->stream));
+}
+
+// key of one host row (ValuePartitionExecutor: toString, null -> dropped)
+bool host_key(sdg_engine* e, QueryRt& q, int qpos, const PushChunk& c, int64_t row, uint32_t* key) {
+    int ai = q.hq.key_attr[qpos];
+    if (!c.nulls[ai].empty() && c.nulls[ai][row]) return false;
+    const uint8_t* col = c.cols[ai].data();
+    uint8_t kind = q.hq.key_kind[qpos];
+    if (q.string_keys) {
+        *key = ((const uint32_t*)col)[row];
+        return true;
+    }
+    std::string s;
+    switch (kind) {
+        case VK_I32: s = std::to_string(((const int32_t*)col)[row]); break;
+        case VK_I64: s = std::to_string(((const int64_t*)col)[row]); break;
+        case VK_F32: s = java_real(((const float*)col)[row], true); break;
+        case VK_F64: s = java_real(((const double*)col)[row], false); break;
+        case VK_BOOL: s = col[row] ? "true" : "false"; break;
+        default: s = e->strings.strs[((const uint32_t*)col)[row]]; break;
+    }
+    auto it = q.keydict.find(s);
+    if (it == q.keydict.end()) it = q.keydict.emplace(s, (uint32_t)q.keydict.size()).first;
+    *key = it->second;
+    return true;
+}
+
+void flush_query(sdg_engine* e, QueryRt& q) {
+    HostQuery& h = q.hq;
+    Plan& P = h.plan;
+    hipStream_t st = e->stream;
+    if (!P.chain)
+        throw CompileError(SDG_ERR_UNSUPPORTED, "query '" + h.name + "': only the chain fast path is on device in this build (" +
+                                                    h.chain_reason + ")");
+    const int nc = P.n_cols;
+    // ---- 1. batch view -------------------------------------------------------------------------------
+    std::vector<const PushChunk*> parts;
+    int64_t n = 0;
+    for (auto& c : e->pending)
+        if (h.stream_pos(c.stream) >= 0) { parts.push_back(&c); n += c.n; }
+    const bool partitioned = P.partitioned;
+    const bool multi_stream = h.streams.size() > 1;
+    const int64_t* d_ts = nullptr;
+    const uint8_t* d_qs = nullptr;
+    const uint32_t* d_key = nullptr;
+    const void* d_cols[MAX_COLS] = {};
+    const uint8_t* d_nulls[MAX_COLS] = {};
+    int64_t nrows = 0;
+    bool zero_copy = parts.size() == 1 && parts[0]->device && !multi_stream;
+    if (zero_copy) {
+        const PushChunk& c = *parts[0];
+        int qpos = h.stream_pos(c.stream);
+        d_ts = c.d_ts;
+        for (int k = 0; k < nc; ++k) {
+            int ai = h.col_attr[qpos][k];
+            d_cols[k] = ai >= 0 ? c.d_cols[ai] : nullptr;
+            d_nulls[k] = ai >= 0 ? c.d_nulls[ai] : nullptr;
+            if (!d_cols[k]) d_cols[k] = q.st_cols[k].ensure((size_t)std::max<int64_t>(n, 1) * width_of(P.col_kind[k]));
+        }
+        if (partitioned) {
+            if (!q.string_keys) throw CompileError(SDG_ERR_UNSUPPORTED, "device-resident batches need string partition keys");
+            int ai = h.key_attr[qpos];
+            if (c.d_nulls[ai]) throw CompileError(SDG_ERR_UNSUPPORTED, "null partition keys in device-resident batches");
+            d_key = (const uint32_t*)c.d_cols[ai];
+        }
+        nrows = n;
+    } else {
+        // assemble on the host (host chunks) / device-to-device (device chunks)
+        std::vector<int64_t> ts;
+        std::vector<uint8_t> qs;
+        std::vector<uint32_t> keys;
+        std::vector<std::vector<uint8_t>> cols(nc), nulls(nc);
+        std::vector<bool> any_null(nc, false);
+        ts.reserve(n);
+        for (int k = 0; k < nc; ++k) cols[k].reserve((size_t)n * width_of(P.col_kind[k]));
+        for (const PushChunk* c : parts) {
+            if (c->device) throw CompileError(SDG_ERR_UNSUPPORTED, "mixed / multi-stream device-resident batches");
+            int qpos = h.stream_pos(c->stream);
+            for (int64_t r = 0; r < c->n; ++r) {
+                uint32_t key = 0;
+                if (partitioned && !host_key(e, q, qpos, *c, r, &key)) continue;  // null key: dropped
+                ts.push_back(c->ts[r]);
+                qs.push_back((uint8_t)qpos);
+                if (partitioned) keys.push_back(key);
+                for (int k = 0; k < nc; ++k) {
+                    int w = width_of(P.col_kind[k]);
+                    int ai = h.col_attr[qpos][k];
+                    size_t off = cols[k].size();
+                    cols[k].resize(off + w, 0);
+                    bool isnull = false;
+                    if (ai >= 0) {
+                        std::memcpy(&cols[k][off], c->cols[ai].data() + r * w, w);
+                        isnull = !c->nulls[ai].empty() && c->nulls[ai][r];
+                    }
+                    nulls[k].push_back(isnull);
+                    if (isnull) any_null[k] = true;
+                }
+            }
+        }
+        nrows = (int64_t)ts.size();
+        size_t cnt = (size_t)std::max<int64_t>(nrows, 1);
+        d_ts = (const int64_t*)q.st_ts.ensure(cnt * 8);
+        if (nrows) HIPCHECK(hipMemcpyAsync((void*)d_ts, ts.data(), nrows * 8, hipMemcpyHostToDevice, st));
+        if (multi_stream) {
+            d_qs = (const uint8_t*)q.st_qs.ensure(cnt);
+            if (nrows) HIPCHECK(hipMemcpyAsync((void*)d_qs, qs.data(), nrows, hipMemcpyHostToDevice, st));
+        }
+        if (partitioned) {
+            d_key = (const uint32_t*)q.st_key.ensure(cnt * 4);
+            if (nrows) HIPCHECK(hipMemcpyAsync((void*)d_key, keys.data(), nrows * 4, hipMemcpyHostToDevice, st));
+        }
+        for (int k = 0; k < nc; ++k) {
+            int w = width_of(P.col_kind[k]);
+            d_cols[k] = q.st_cols[k].ensure(cnt * w);
+            if (nrows) HIPCHECK(hipMemcpyAsync((void*)d_cols[k], cols[k].data(), nrows * w, hipMemcpyHostToDevice, st));
+            if (any_null[k]) {
+                d_nulls[k] = (const uint8_t*)q.st_nulls[k].ensure(cnt);
+                HIPCHECK(hipMemcpyAsync((void*)d_nulls[k], nulls[k].data(), nrows, hipMemcpyHostToDevice, st));
+            }
+        }
+        // hipMemcpyAsync from pageable memory: keep the host vectors alive until the copies land
+        HIPCHECK(hipStreamSynchronize(st));
+    }
+    // ---- 2. key grouping ---------------------------------------------------------------------------------
+    uint32_t K = 1;
+    if (partitioned) K = q.string_keys ? (uint32_t)std::max<size_t>(e->strings.strs.size(), 1) : (uint32_t)std::max<size_t>(q.keydict.size(), 1);
+    const int64_t* v_ts = d_ts;
+    const uint8_t* v_qs = d_qs;
+    const uint32_t* v_key = nullptr;
+    const uint32_t* v_seg = nullptr;
+    const uint32_t* v_orig = nullptr;
+    const void* v_cols[MAX_COLS];
+    const uint8_t* v_nulls[MAX_COLS];
+    for (int k = 0; k < nc; ++k) { v_cols[k] = d_cols[k]; v_nulls[k] = d_nulls[k]; }
+    HIPCHECK(hipEventRecord(e->ev[0], st));
+    if (partitioned && nrows > 0) {
+        if ((int)K > KG_MAXK)
+            throw CompileError(SDG_ERR_CAPACITY, "key space " + std::to_string(K) + " exceeds the LDS key-grouping path (" +
+                                                     std::to_string(KG_MAXK) + ")");
+        KeyGroupArgs a;
+        std::memset(&a, 0, sizeof a);
+        size_t cb, gb;
+        keygroup_workspace(nrows, (int32_t)K, &a.nchunks, &cb, &gb);
+        a.n = nrows;
+        a.K = (int32_t)K;
+        a.keys = d_key;
+        a.counts = (uint32_t*)q.kg_counts.ensure(cb);
+        a.gsum = (uint32_t*)q.kg_gsum.ensure(gb);
+        a.seg_start = (uint32_t*)q.seg.ensure((K + 1) * 4);
+        a.keys_sorted = (uint32_t*)q.so_key.ensure(nrows * 4);
+        a.orig_sorted = (uint32_t*)q.so_orig.ensure(nrows * 4);
+        int c = 0;
+        a.src[c] = d_ts; a.dst[c] = q.so_ts.ensure(nrows * 8); a.width[c] = 8; v_ts = (const int64_t*)a.dst[c]; ++c;
+        if (d_qs) { a.src[c] = d_qs; a.dst[c] = q.so_qs.ensure(nrows); a.width[c] = 1; v_qs = (const uint8_t*)a.dst[c]; ++c; }
+        for (int k = 0; k < nc; ++k) {
+            if (c >= MAX_COLS + 2) throw CompileError(SDG_ERR_UNSUPPORTED, "too many columns");
+            int w = width_of(P.col_kind[k]);
+            a.src[c] = d_cols[k]; a.dst[c] = q.so_cols[k].ensure(nrows * w); a.width[c] = (uint8_t)w;
+            v_cols[k] = a.dst[c];
+            ++c;
+            if (d_nulls[k]) {
+                a.src[c] = d_nulls[k]; a.dst[c] = q.so_nulls[k].ensure(nrows); a.width[c] = 1;
+                v_nulls[k] = (const uint8_t*)a.dst[c];
+                ++c;
+            }
+        }
+        a.ncols = c;
+        keygroup(a, st, &e->ev[4]);
+        v_key = a.keys_sorted;
+        v_seg = a.seg_start;
+        v_orig = a.orig_sorted;
+        e->stats.keygroup_launches += 6;
+    } else if (partitioned) {
+        // empty batch: segments all empty
+        std::vector<uint32_t> z(K + 1, 0);
+        v_seg = (const uint32_t*)q.seg.ensure((K + 1) * 4);
+        HIPCHECK(hipMemcpyAsync((void*)v_seg, z.data(), (K + 1) * 4, hipMemcpyHostToDevice, st));
+        HIPCHECK(hipStreamSynchronize(st));
+    }
+    HIPCHECK(hipEventRecord(e->ev[1], st));
+    // ---- 3. chain matcher -------------------------------------------------------------------------------
+    QueryRt::Carry& cin = q.carry[q.cur];
+    QueryRt::Carry& cout = q.carry[q.cur ^ 1];
+    int64_t cap = nrows + cin.n + 1;
+    q.out_cap = cap;
+    ChainArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.plan = q.d_plan.as<Plan>();
+    a.code = q.d_code.as<Instr>();
+    a.consts = q.d_consts.as<int64_t>();
+    a.n = nrows;
+    a.ts = v_ts;
+    a.qstream = multi_stream ? v_qs : nullptr;
+    a.key = partitioned ? v_key : nullptr;
+    a.seg_start = partitioned ? v_seg : nullptr;
+    a.orig = v_orig;
+    for (int k = 0; k < nc; ++k) { a.cols[k] = v_cols[k]; a.nulls[k] = v_nulls[k]; }
+    a.seq_base = q.seq;
+    a.s0 = h.stream_pos(P.st[0].stream);
+    a.s1 = P.n_states > 1 ? h.stream_pos(P.st[1].stream) : a.s0;
+    a.out_cap = cap;
+    unsigned long long* counters = (unsigned long long*)q.counters.ensure(16);
+    int* flags = (int*)q.flags.ensure(16);
+    HIPCHECK(hipMemsetAsync(counters, 0, 16, st));
+    HIPCHECK(hipMemsetAsync(flags, 0, 16, st));
+    a.out_count = counters;
+    a.carry_count = counters + 1;
+    a.flags = flags;
+    a.out_ts = (int64_t*)q.o_ts.ensure(cap * 8);
+    a.out_key = (uint32_t*)q.o_key.ensure(cap * 4);
+    a.out_vals = (int64_t*)q.o_vals.ensure((size_t)std::max(P.n_out, 1) * cap * 8);
+    a.out_nulls = (uint32_t*)q.o_nulls.ensure(cap * 4);
+    a.out_emit_seq = (int64_t*)q.o_emit.ensure(cap * 8);
+    a.out_first_seq = (int64_t*)q.o_first.ensure(cap * 8);
+    cout.cap = cap;
+    a.carry_cap = cap;
+    a.carry_key = (uint32_t*)cout.key.ensure(cap * 4);
+    a.carry_ts = (int64_t*)cout.ts.ensure(cap * 8);
+    a.carry_seq = (int64_t*)cout.seq.ensure(cap * 8);
+    a.carry_vals = (int64_t*)cout.vals.ensure((size_t)std::max(nc, 1) * cap * 8);
+    a.carry_nulls = (uint32_t*)cout.nulls.ensure(cap * 4);
+    a.cin_n = cin.n;
+    a.cin_key = cin.key.as<uint32_t>();
+    a.cin_ts = cin.ts.as<int64_t>();
+    a.cin_seq = cin.seq.as<int64_t>();
+    a.cin_vals = cin.vals.as<int64_t>();
+    a.cin_nulls = cin.nulls.as<uint32_t>();
+    a.cin_cap = cin.cap;
+    chain_carry(a, st);
+    HIPCHECK(hipEventRecord(e->ev[8], st));
+    chain_match(a, st);
+    e->stats.match_launches += (cin.n > 0) + (nrows > 0);
+    HIPCHECK(hipEventRecord(e->ev[2], st));
+    unsigned long long hc[2];
+    int hf[4];
+    HIPCHECK(hipMemcpyAsync(hc, counters, 16, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(hf, flags, 16, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    float ms_kg = 0, ms_m = 0;
+    HIPCHECK(hipEventElapsedTime(&ms_kg, e->ev[0], e->ev[1]));
+    HIPCHECK(hipEventElapsedTime(&ms_m, e->ev[1], e->ev[2]));
+    e->stats.ms_keygroup += ms_kg;
+    e->stats.ms_match += ms_m;
+    float t;
+    if (partitioned && nrows > 0) {
+        HIPCHECK(hipEventElapsedTime(&t, e->ev[4], e->ev[5]));
+        e->stats.ms_kg_hist += t;
+        HIPCHECK(hipEventElapsedTime(&t, e->ev[5], e->ev[6]));
+        e->stats.ms_kg_prefix += t;
+        HIPCHECK(hipEventElapsedTime(&t, e->ev[6], e->ev[7]));
+        e->stats.ms_kg_scatter += t;
+    }
+    HIPCHECK(hipEventElapsedTime(&t, e->ev[1], e->ev[8]));
+    e->stats.ms_chain_carry += t;
+    HIPCHECK(hipEventElapsedTime(&t, e->ev[8], e->ev[2]));
+    e->stats.ms_chain_match += t;
+    e->stats.events += nrows;
+    if (hf[0]) {
+        e->stats.overflow += 1;
+        throw CompileError(SDG_ERR_CAPACITY, "match/carry buffer overflow in query '" + h.name + "'");
+    }
+    if (hf[1])
+        throw CompileError(SDG_ERR_UNSUPPORTED, "query '" + h.name +
+                                                    "': timestamps decrease within a partition key; the chain path needs "
+                                                    "per-key non-decreasing timestamps (generic path not in this build)");
+    cout.n = (int64_t)hc[1];
+    cin.n = 0;
+    q.cur ^= 1;
+    q.out_n = (int64_t)hc[0];
+    q.polled = false;
+    e->stats.matches += q.out_n;
+    e->stats.path = 0;
+    q.seq += nrows;
+}
+
+int do_flush(sdg_engine* e) {
+    if (e->compile_only) throw DeviceError("engine was compiled with SDG_COMPILE_ONLY");
+    HIPCHECK(hipSetDevice(e->device));
+    e->stats.events = e->stats.matches = 0;
+    e->stats.ms_keygroup = e->stats.ms_match = e->stats.ms_total = 0;
+    e->stats.keygroup_launches = e->stats.match_launches = 0;
+    e->stats.overflow = 0;
+    e->stats.ms_kg_hist = e->stats.ms_kg_prefix = e->stats.ms_kg_scatter = 0;
+    e->stats.ms_chain_carry = e->stats.ms_chain_match = 0;
+    for (auto& q : e->qs) flush_query(e, *q);
+    e->stats.ms_total = e->stats.ms_keygroup + e->stats.ms_match;
+    e->pending.clear();
+    e->pending_n = 0;
+    return SDG_OK;
+}
+
+template <class F>
+int guarded(F f) {
+    try {
+        return f();
+    } catch (const CompileError& ex) {
+        return fail(ex.code, ex.what());
+    } catch (const sql::Unsupported& ex) {
+        return fail(SDG_ERR_UNSUPPORTED, ex.what());
+    } catch (const sql::ParseError& ex) {
+        return fail(SDG_ERR_PARSE, ex.what());
+    } catch (const DeviceError& ex) {
+        return fail(SDG_ERR_DEVICE, ex.what());
+    } catch (const std::exception& ex) {
+        return fail(SDG_ERR_ARG, ex.what());
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* sdg_last_error(void) { return g_err.c_str(); }
+
+int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
+    if (!text || !out) return fail(SDG_ERR_ARG, "null argument");
+    *out = nullptr;
+    return guarded([&]() {
+        auto e = std::make_unique<sdg_engine>();
+        e->app = sql::parse_app(text);
+        if (opts) {
+            e->device = opts->device;
+            if (opts->batch_capacity > 0) e->capacity = opts->batch_capacity;
+            e->compile_only = (opts->flags & SDG_COMPILE_ONLY) != 0;
+        }
+        auto hqs = compile_app(e->app, e->strings);
+        for (auto& h : hqs)
+            if (!h.plan.chain)
+                throw CompileError(SDG_ERR_UNSUPPORTED, "query '" + h.name + "' (" + h.chain_reason +
+                                                            ") needs the generic keyed-NFA kernel, not in this build");
+        if (!e->compile_only) {
+            int ndev = 0;
+            if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+                throw DeviceError("no HIP device visible (the engine has no CPU fallback)");
+            HIPCHECK(hipSetDevice(e->device));
+            hipDeviceProp_t prop;
+            HIPCHECK(hipGetDeviceProperties(&prop, e->device));
+            if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+                throw DeviceError(std::string("device is ") + prop.gcnArchName + ", this build targets gfx950");
+            HIPCHECK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+            for (auto& ev : e->ev) HIPCHECK(hipEventCreate(&ev));
+        }
+        for (auto& h : hqs) {
+            auto q = std::make_unique<QueryRt>();
+            q->hq = std::move(h);
+            for (size_t i = 0; i < q->hq.key_kind.size(); ++i)
+                if (q->hq.key_attr[i] >= 0 && q->hq.key_kind[i] != VK_STR) q->string_keys = false;
+            if (!e->compile_only) upload_plan(e.get(), *q);
+            e->qs.push_back(std::move(q));
+        }
+        for (auto& s : e->app.streams) {
+            std::vector<int32_t> t;
+            for (auto& a : s.attrs) t.push_back((int32_t)a.type);
+            e->stream_types.push_back(t);
+        }
+        for (auto& q : e->qs) {
+            e->out_types.push_back(q->hq.out_types);
+            std::vector<const char*> nm;
+            for (auto& s : q->hq.out_names) nm.push_back(s.c_str());
+            e->out_names.push_back(nm);
+        }
+        *out = e.release();
+        return SDG_OK;
+    });
+}
+
+void sdg_destroy(sdg_engine* e) {
+    if (!e) return;
+    if (e->compile_only) {
+        delete e;
+        return;
+    }
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    e->qs.clear();
+    for (auto& ev : e->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+int sdg_stream_index(sdg_engine* e, const char* sid) { return e && sid ? e->app.stream_index(sid) : -1; }
+
+int sdg_stream_schema(sdg_engine* e, int s, int32_t* n, const int32_t** types) {
+    if (!e || s < 0 || s >= (int)e->stream_types.size()) return fail(SDG_ERR_ARG, "bad stream index");
+    *n = (int32_t)e->stream_types[s].size();
+    *types = e->stream_types[s].data();
+    return SDG_OK;
+}
+
+int sdg_num_queries(sdg_engine* e) { return e ? (int)e->qs.size() : 0; }
+int sdg_query_path(sdg_engine* e, int q) {
+    if (!e || q < 0 || q >= (int)e->qs.size()) return -1;
+    return e->qs[q]->hq.plan.chain ? 0 : 1;
+}
+const char* sdg_query_name(sdg_engine* e, int q) { return e->qs[q]->hq.name.c_str(); }
+const char* sdg_query_target(sdg_engine* e, int q) { return e->qs[q]->hq.target.c_str(); }
+int sdg_query_output_schema(sdg_engine* e, int q, int32_t* n, const int32_t** types, const char* const** names) {
+    if (!e || q < 0 || q >= (int)e->qs.size()) return fail(SDG_ERR_ARG, "bad query index");
+    *n = (int32_t)e->out_types[q].size();
+    *types = e->out_types[q].data();
+    *names = e->out_names[q].data();
+    return SDG_OK;
+}
+
+uint32_t sdg_intern(sdg_engine* e, const char* s, size_t len) { return e->strings.get(std::string(s, len)); }
+const char* sdg_string(sdg_engine* e, uint32_t id) {
+    return id < e->strings.strs.size() ? e->strings.strs[id].c_str() : nullptr;
+}
+
+int sdg_push(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const void* const* cols,
+             const uint8_t* const* nulls) {
+    if (!e || stream < 0 || stream >= (int)e->stream_types.size() || n < 0 || (n > 0 && !ts))
+        return fail(SDG_ERR_ARG, "bad push arguments");
+    return guarded([&]() {
+        PushChunk c;
+        c.stream = stream;
+        c.n = n;
+        c.device = false;
+        c.ts.assign(ts, ts + n);
+        const auto& types = e->stream_types[stream];
+        c.cols.resize(types.size());
+        c.nulls.resize(types.size());
+        for (size_t a = 0; a < types.size(); ++a) {
+            int w = width_of((uint8_t)types[a]);
+            if (n > 0 && !cols[a]) throw std::invalid_argument("missing column");
+            c.cols[a].assign((const uint8_t*)cols[a], (const uint8_t*)cols[a] + n * w);
+            if (nulls && nulls[a]) c.nulls[a].assign(nulls[a], nulls[a] + n);
+        }
+        e->pending_n += n;
+        e->pending.push_back(std::move(c));
+        if (e->pending_n >= e->capacity) return do_flush(e);
+        return (int)SDG_OK;
+    });
+}
+
+int sdg_push_device(sdg_engine* e, int stream, int64_t n, const int64_t* d_ts, const void* const* d_cols,
+                    const uint8_t* const* d_nulls) {
+    if (!e || stream < 0 || stream >= (int)e->stream_types.size() || n < 0)
+        return fail(SDG_ERR_ARG, "bad push arguments");
+    return guarded([&]() {
+        if (e->compile_only) throw DeviceError("engine was compiled with SDG_COMPILE_ONLY");
+        PushChunk c;
+        c.stream = stream;
+        c.n = n;
+        c.device = true;
+        c.d_ts = d_ts;
+        size_t na = e->stream_types[stream].size();
+        c.d_cols.assign(d_cols, d_cols + na);
+        c.d_nulls.assign(na, nullptr);
+        if (d_nulls)
+            for (size_t a = 0; a < na; ++a) c.d_nulls[a] = d_nulls[a];
+        e->pending_n += n;
+        e->pending.push_back(std::move(c));
+        return (int)SDG_OK;
+    });
+}
+
+int sdg_advance_time(sdg_engine* e, int64_t) {
+    if (!e) return fail(SDG_ERR_ARG, "null engine");
+    return SDG_OK;  // no scheduler-driven states on the device path in this build
+}
+
+int sdg_flush(sdg_engine* e) {
+    if (!e) return fail(SDG_ERR_ARG, "null engine");
+    return guarded([&]() { return do_flush(e); });
+}
+
+int sdg_sync(sdg_engine* e) {
+    if (!e) return fail(SDG_ERR_ARG, "null engine");
+    return guarded([&]() {
+        HIPCHECK(hipStreamSynchronize(e->stream));
+        return (int)SDG_OK;
+    });
+}
+
+int sdg_poll(sdg_engine* e, int qi, sdg_out* out) {
+    if (!e || qi < 0 || qi >= (int)e->qs.size() || !out) return fail(SDG_ERR_ARG, "bad poll arguments");
+    return guarded([&]() {
+        QueryRt& q = *e->qs[qi];
+        const Plan& P = q.hq.plan;
+        int64_t n = q.polled ? 0 : q.out_n;
+        int na = P.n_out;
+        q.h_ts.resize(n);
+        q.h_expired.assign(n, 0);
+        q.h_vals.assign(na, std::vector<int64_t>(n));
+        q.h_nulls.assign(na, std::vector<uint8_t>(n));
+        if (n > 0) {
+            std::vector<int64_t> ts(n), emit(n), first(n), vals((size_t)na * q.out_cap);
+            std::vector<uint32_t> nulls(n);
+            hipStream_t st = e->stream;
+            HIPCHECK(hipMemcpyAsync(ts.data(), q.o_ts.p, n * 8, hipMemcpyDeviceToHost, st));
+            HIPCHECK(hipMemcpyAsync(emit.data(), q.o_emit.p, n * 8, hipMemcpyDeviceToHost, st));
+            HIPCHECK(hipMemcpyAsync(first.data(), q.o_first.p, n * 8, hipMemcpyDeviceToHost, st));
+            HIPCHECK(hipMemcpyAsync(nulls.data(), q.o_nulls.p, n * 4, hipMemcpyDeviceToHost, st));
+            for (int j = 0; j < na; ++j)
+                HIPCHECK(hipMemcpyAsync(vals.data() + (size_t)j * q.out_cap, (int64_t*)q.o_vals.p + (size_t)j * q.out_cap,
+                                        n * 8, hipMemcpyDeviceToHost, st));
+            HIPCHECK(hipStreamSynchronize(st));
+            // reference delivery order: by completing event, then by the partial's start (pending-list order)
+            std::vector<int64_t> ord(n);
+            std::iota(ord.begin(), ord.end(), 0);
+            std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
+                return emit[x] != emit[y] ? emit[x] < emit[y] : first[x] < first[y];
+            });
+            for (int64_t i = 0; i < n; ++i) {
+                int64_t s = ord[i];
+                q.h_ts[i] = ts[s];
+                for (int j = 0; j < na; ++j) {
+                    q.h_vals[j][i] = vals[(size_t)j * q.out_cap + s];
+                    q.h_nulls[j][i] = (nulls[s] >> j) & 1u;
+                }
+            }
+        }
+        q.polled = true;
+        q.h_vptr.resize(na);
+        q.h_nptr.resize(na);
+        for (int j = 0; j < na; ++j) {
+            q.h_vptr[j] = q.h_vals[j].data();
+            q.h_nptr[j] = q.h_nulls[j].data();
+        }
+        out->n = n;
+        out->ts = q.h_ts.data();
+        out->expired = q.h_expired.data();
+        out->n_attrs = na;
+        out->types = e->out_types[qi].data();
+        out->values = q.h_vptr.data();
+        out->nulls = q.h_nptr.data();
+        return (int)SDG_OK;
+    });
+}
+
+int sdg_last_stats(sdg_engine* e, sdg_stats* out) {
+    if (!e || !out) return fail(SDG_ERR_ARG, "null argument");
+    *out = e->stats;
+    return SDG_OK;
+}
+
+}  // extern "C"

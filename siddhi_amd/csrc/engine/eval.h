@@ -1,0 +1,243 @@
+// Device interpreter for the condition/selector bytecode (plan.h). Java semantics, bit-exact:
+//   null handling       CompareConditionExpressionExecutor.java:38-42 (null -> false),
+//                       And/Or/NotConditionExpressionExecutor.java (null -> false / not null -> TRUE)
+//   numeric promotion   executor/condition/compare/** (e.g. GreaterThanCompareConditionExpressionExecutorFloatLong:
+//                       float compare; EqualCompareConditionExpressionExecutorFloatLong: double compare)
+//   arithmetic          executor/math/** (int/long wrap, /,% by zero -> null, double % = fmod)
+// The program is wave-uniform (one query per launch), so instruction fetch is scalar and the op switch never
+// diverges; the evaluation stack lives in LDS, one column of STACK entries per lane (conflict-free stride).
+// Build with -ffp-contract=off: a fused multiply-add would change float/double results vs the JVM.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "plan.h"
+
+namespace sdg {
+
+__device__ __forceinline__ float bits_f32(int64_t v) { return __int_as_float((int)(uint32_t)v); }
+__device__ __forceinline__ double bits_f64(int64_t v) { return __longlong_as_double(v); }
+__device__ __forceinline__ int64_t f32_bits(float f) { return (int64_t)(uint32_t)__float_as_int(f); }
+__device__ __forceinline__ int64_t f64_bits(double d) { return __double_as_longlong(d); }
+
+// typed column load -> 64-bit payload (same encoding as sdg_out)
+__device__ __forceinline__ int64_t load_col(const void* col, uint8_t kind, int64_t row) {
+    switch (kind) {
+        case VK_I32: return (int64_t)((const int32_t*)col)[row];
+        case VK_I64: return ((const int64_t*)col)[row];
+        case VK_F32: return (int64_t)((const uint32_t*)col)[row];
+        case VK_F64: return ((const int64_t*)col)[row];
+        case VK_BOOL: return (int64_t)((const uint8_t*)col)[row];
+        default: return (int64_t)((const uint32_t*)col)[row];
+    }
+}
+
+__device__ __forceinline__ int64_t cvt(int64_t v, uint8_t from, uint8_t to) {
+    if (from == to) return v;
+    switch (to) {
+        case VK_I64: return (int64_t)(int32_t)v;  // only int -> long widens
+        case VK_F32: return from == VK_I32 ? f32_bits((float)(int32_t)v) : f32_bits((float)v);
+        case VK_F64:
+            if (from == VK_I32) return f64_bits((double)(int32_t)v);
+            if (from == VK_I64) return f64_bits((double)v);
+            return f64_bits((double)bits_f32(v));
+        default: return v;
+    }
+}
+
+template <class T>
+__device__ __forceinline__ bool cmpT(uint8_t op, T a, T b) {
+    switch (op) {
+        case CMP_EQ: return a == b;
+        case CMP_NE: return a != b;
+        case CMP_GT: return a > b;
+        case CMP_GE: return a >= b;
+        case CMP_LT: return a < b;
+        default: return a <= b;
+    }
+}
+
+__device__ __forceinline__ bool cmp(uint8_t op, uint8_t k, int64_t a, int64_t b) {
+    switch (k) {
+        case VK_I32: return cmpT<int32_t>(op, (int32_t)a, (int32_t)b);
+        case VK_I64: return cmpT<int64_t>(op, a, b);
+        case VK_F32: return cmpT<float>(op, bits_f32(a), bits_f32(b));
+        case VK_F64: return cmpT<double>(op, bits_f64(a), bits_f64(b));
+        case VK_BOOL: return cmpT<int>(op, (int)(a != 0), (int)(b != 0));
+        default: return cmpT<uint32_t>(op, (uint32_t)a, (uint32_t)b);  // string ids: == / != only
+    }
+}
+
+// returns false (and *null = true) when Java would produce null
+__device__ __forceinline__ int64_t arith(uint8_t op, uint8_t k, int64_t a, int64_t b, bool* null) {
+    *null = false;
+    switch (k) {
+        case VK_I32: {
+            int32_t x = (int32_t)a, y = (int32_t)b;
+            uint32_t ux = (uint32_t)x, uy = (uint32_t)y;
+            switch (op) {
+                case AR_ADD: return (int64_t)(int32_t)(ux + uy);
+                case AR_SUB: return (int64_t)(int32_t)(ux - uy);
+                case AR_MUL: return (int64_t)(int32_t)(ux * uy);
+                case AR_DIV:
+                    if (y == 0) { *null = true; return 0; }
+                    if (x == INT32_MIN && y == -1) return x;
+                    return (int64_t)(x / y);
+                default:
+                    if (y == 0) { *null = true; return 0; }
+                    if (y == -1) return 0;
+                    return (int64_t)(x % y);
+            }
+        }
+        case VK_I64: {
+            uint64_t ux = (uint64_t)a, uy = (uint64_t)b;
+            switch (op) {
+                case AR_ADD: return (int64_t)(ux + uy);
+                case AR_SUB: return (int64_t)(ux - uy);
+                case AR_MUL: return (int64_t)(ux * uy);
+                case AR_DIV:
+                    if (b == 0) { *null = true; return 0; }
+                    if (a == INT64_MIN && b == -1) return a;
+                    return a / b;
+                default:
+                    if (b == 0) { *null = true; return 0; }
+                    if (b == -1) return 0;
+                    return a % b;
+            }
+        }
+        case VK_F32: {
+            float x = bits_f32(a), y = bits_f32(b);
+            switch (op) {
+                case AR_ADD: return f32_bits(__fadd_rn(x, y));
+                case AR_SUB: return f32_bits(__fsub_rn(x, y));
+                case AR_MUL: return f32_bits(__fmul_rn(x, y));
+                case AR_DIV:
+                    if (y == 0.0f) { *null = true; return 0; }
+                    return f32_bits(__fdiv_rn(x, y));
+                default:
+                    if (y == 0.0f) { *null = true; return 0; }
+                    return f32_bits(fmodf(x, y));
+            }
+        }
+        default: {
+            double x = bits_f64(a), y = bits_f64(b);
+            switch (op) {
+                case AR_ADD: return f64_bits(__dadd_rn(x, y));
+                case AR_SUB: return f64_bits(__dsub_rn(x, y));
+                case AR_MUL: return f64_bits(__dmul_rn(x, y));
+                case AR_DIV:
+                    if (y == 0.0) { *null = true; return 0; }
+                    return f64_bits(__ddiv_rn(x, y));
+                default:
+                    if (y == 0.0) { *null = true; return 0; }
+                    return f64_bits(fmod(x, y));
+            }
+        }
+    }
+}
+
+// Acc must provide:
+//   __device__ void load(int slot, int col, int chain, uint8_t kind, int64_t* v, bool* null);
+//   __device__ bool slot_empty(int slot, int chain);
+// stk: this lane's LDS stack base, entries at stk[i * stride]
+template <class Acc>
+__device__ __forceinline__ void run(const Instr* __restrict__ code, Prog p, const int64_t* __restrict__ consts,
+                                    Acc& acc, int64_t* stk, int stride, int64_t* out, bool* out_null) {
+    uint32_t nulls = 0;
+    int sp = 0;
+    for (int pc = p.start; pc < p.start + p.len; ++pc) {
+        const Instr in = code[pc];
+        switch (in.op) {
+            case OP_LOAD: {
+                int64_t v;
+                bool n;
+                acc.load(in.a, in.b, in.c, in.k, &v, &n);
+                stk[sp * stride] = v;
+                nulls = n ? (nulls | (1u << sp)) : (nulls & ~(1u << sp));
+                ++sp;
+                break;
+            }
+            case OP_CONST:
+                stk[sp * stride] = consts[in.imm];
+                nulls &= ~(1u << sp);
+                ++sp;
+                break;
+            case OP_CVT:
+                if (!(nulls & (1u << (sp - 1)))) stk[(sp - 1) * stride] = cvt(stk[(sp - 1) * stride], in.a, in.k);
+                break;
+            case OP_CMP: {
+                bool na = nulls & (1u << (sp - 2)), nb = nulls & (1u << (sp - 1));
+                int64_t a = stk[(sp - 2) * stride], b = stk[(sp - 1) * stride];
+                bool r = !(na || nb) && cmp(in.a, in.k, a, b);
+                --sp;
+                stk[(sp - 1) * stride] = r;
+                nulls &= ~(3u << (sp - 1));
+                break;
+            }
+            case OP_ARITH: {
+                bool na = nulls & (1u << (sp - 2)), nb = nulls & (1u << (sp - 1));
+                int64_t a = stk[(sp - 2) * stride], b = stk[(sp - 1) * stride];
+                --sp;
+                nulls &= ~(3u << (sp - 1));
+                if (na || nb) {
+                    nulls |= 1u << (sp - 1);
+                } else {
+                    bool n;
+                    int64_t r = arith(in.a, in.k, a, b, &n);
+                    stk[(sp - 1) * stride] = r;
+                    if (n) nulls |= 1u << (sp - 1);
+                }
+                break;
+            }
+            case OP_AND:
+            case OP_OR: {
+                bool ta = !(nulls & (1u << (sp - 2))) && stk[(sp - 2) * stride] != 0;
+                bool tb = !(nulls & (1u << (sp - 1))) && stk[(sp - 1) * stride] != 0;
+                --sp;
+                stk[(sp - 1) * stride] = in.op == OP_AND ? (ta && tb) : (ta || tb);
+                nulls &= ~(3u << (sp - 1));
+                break;
+            }
+            case OP_NOT: {
+                bool t = !(nulls & (1u << (sp - 1))) && stk[(sp - 1) * stride] != 0;
+                stk[(sp - 1) * stride] = !t;
+                nulls &= ~(1u << (sp - 1));
+                break;
+            }
+            case OP_ISNULL: {
+                bool n = nulls & (1u << (sp - 1));
+                stk[(sp - 1) * stride] = n;
+                nulls &= ~(1u << (sp - 1));
+                break;
+            }
+            case OP_SLOTNULL:
+                stk[sp * stride] = acc.slot_empty(in.a, in.c);
+                nulls &= ~(1u << sp);
+                ++sp;
+                break;
+            case OP_COND: {
+                bool n = nulls & (1u << (sp - 1));
+                if (n) stk[(sp - 1) * stride] = 0;
+                nulls &= ~(1u << (sp - 1));
+                break;
+            }
+            default:
+                break;
+        }
+    }
+    *out = stk[0];
+    *out_null = (nulls & 1u) != 0;
+}
+
+// a filter passes iff its result is non-null and true (FilterProcessor.java:48-60)
+template <class Acc>
+__device__ __forceinline__ bool pass(const Instr* code, Prog p, const int64_t* consts, Acc& acc, int64_t* stk,
+                                     int stride) {
+    if (p.len == 0) return true;
+    int64_t v;
+    bool n;
+    run(code, p, consts, acc, stk, stride, &v, &n);
+    return !n && v != 0;
+}
+
+}  // namespace sdg

@@ -1,0 +1,91 @@
+// Compiled query plan: the NFA table + condition bytecode a SiddhiQL pattern/sequence query lowers to.
+// POD only: the same structs are copied verbatim into device memory and read by the kernels.
+//
+// Lowering contract followed (reference, paths under modules/siddhi-core/src/main/java/io/siddhi/core/):
+//   state ids / start states / every / within      util/parser/StateInputStreamParser.java:76-408
+//   variable positions [slot, chain index, attr]    util/parser/ExpressionParser.java:1302-1438
+//   compare / arithmetic promotion, null rules      executor/condition/compare/**, executor/math/**,
+//                                                   util/parser/ExpressionParser.java:568-667, 1488-1520
+#pragma once
+#include <stdint.h>
+
+namespace sdg {
+
+// value kinds == sql::Type codes 0..5 == sdg_type
+enum VK : uint8_t { VK_I32 = 0, VK_I64 = 1, VK_F32 = 2, VK_F64 = 3, VK_BOOL = 4, VK_STR = 5 };
+
+enum OpCode : uint8_t {
+    OP_LOAD = 1,   // push attribute: a = state slot, b = column, c = chain index, k = kind
+    OP_CONST,      // push consts[imm] (kind k)
+    OP_CVT,        // convert top of stack: a = from kind, k = to kind (Number.xValue())
+    OP_CMP,        // a = CmpOp, k = operand kind; pop 2, push bool; null operand -> false
+    OP_ARITH,      // a = ArithOp, k = kind; pop 2, push; null propagates; int/long/float/double /,% by 0 -> null
+    OP_AND,        // pop 2 push bool  (AndConditionExpressionExecutor: null -> false)
+    OP_OR,         // pop 2 push bool
+    OP_NOT,        // pop 1 push bool  (null -> TRUE)
+    OP_ISNULL,     // pop 1 push bool
+    OP_SLOTNULL,   // push bool: state slot a, chain index c is empty (IsNullStreamConditionExpressionExecutor)
+    OP_COND,       // pop 1 push bool: null -> false (BoolConditionExpressionExecutor)
+};
+enum CmpOp : uint8_t { CMP_EQ = 0, CMP_NE, CMP_GT, CMP_GE, CMP_LT, CMP_LE };
+enum ArithOp : uint8_t { AR_ADD = 0, AR_SUB, AR_MUL, AR_DIV, AR_MOD };
+
+struct Instr {
+    uint8_t op, k, a, pad;
+    int32_t b;     // column
+    int32_t c;     // chain index (>= 0 nth; -1 CURRENT/last; -2 LAST/second to last; <= -3 from the end)
+    int32_t imm;   // constant index
+};
+
+struct Prog {
+    int32_t start = 0, len = 0;  // into Plan::code; len 0 == always true (no filter)
+};
+
+constexpr int MAX_STATES = 16;
+constexpr int MAX_OUT = 32;
+constexpr int MAX_COLS = 32;
+constexpr int STACK = 8;
+
+// processor kinds of the generic NFA (one per PreStateProcessor)
+enum ProcKind : uint8_t { PK_STREAM = 0, PK_COUNT = 1, PK_LOGICAL = 2, PK_ABSENT = 3 };
+
+struct StateRow {
+    uint8_t kind;            // ProcKind
+    uint8_t is_start;
+    uint8_t logical_or;      // LOGICAL: 1 = or, 0 = and
+    uint8_t seq;             // SEQUENCE
+    int32_t stream;          // app stream index of this state's events
+    Prog filter;             // conjunction of the state's [..] filters
+    int32_t next;            // nextStatePreProcessor (state id) or -1
+    int32_t next_every;      // nextEveryStatePreProcessor or -1
+    int32_t within_every;    // withinEveryPreStateProcessor or -1
+    int32_t partner;         // LOGICAL partner state or -1
+    int32_t callback;        // callbackPreStateProcessor (count) or -1
+    int32_t last;            // thisLastProcessor's state id (own, or the query's last for the first state)
+    int32_t min_count, max_count;
+    int64_t waiting_ms;      // ABSENT
+    uint8_t selector_after;  // post.nextProcessor == selector (last state / logical partners of it)
+    uint8_t pad[7];
+};
+
+struct Plan {
+    int32_t n_states = 0;
+    int32_t seq = 0;               // SEQUENCE (1) / PATTERN (0)
+    int32_t has_within = 0;
+    int64_t within_ms = 0;
+    int32_t partitioned = 0;
+    int32_t chain = 0;             // 1: the independent-partial fast path applies
+    int32_t n_out = 0;
+    uint8_t out_kind[MAX_OUT];
+    Prog out_prog[MAX_OUT];
+    uint8_t out_multi[MAX_OUT];    // multi-value (count state, no index) -> unsupported on device for now
+    int32_t n_cols = 0;            // physical columns of this query's batch view
+    uint8_t col_kind[MAX_COLS];
+    int32_t n_streams = 0;         // streams this query reads, in receiver order
+    int32_t streams[MAX_STATES];
+    StateRow st[MAX_STATES];
+    // expire order (allStateProcessors), setup order per stream etc. live on the host plan
+    int32_t n_code = 0, n_consts = 0;
+};
+
+}  // namespace sdg

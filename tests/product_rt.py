@@ -1,0 +1,74 @@
+"""Replays golden-fixture traces through the product (GPU engine via the C-ABI) in the oracle's output format."""
+import ctypes
+import struct
+
+import siddhi_amd as sa
+
+TAG = {sa.INT: "i", sa.LONG: "l", sa.FLOAT: "f", sa.DOUBLE: "d", sa.BOOL: "b", sa.STRING: "s"}
+
+
+class ProductAdapter:
+    def __init__(self, app):
+        self.rt = sa.SiddhiAppRuntime(app)
+        self.handlers = {}
+        self.records = []
+
+    def start(self, ts):
+        self.rt.start()
+
+    def handler(self, sid):
+        if sid not in self.handlers:
+            self.handlers[sid] = self.rt.getInputHandler(sid)
+        return self.handlers[sid]
+
+    def send(self, sid, ts, values, now=None, mode=0):
+        h = self.handler(sid)
+        if mode == 1 and self.rt.playback:
+            h.send(values)
+        else:
+            h.send(ts, values)
+
+    def advance(self, ts):
+        pass  # no scheduler-driven states on the device path in this build
+
+    def flush(self):
+        self.rt.flush(deliver=False)
+        for q, (name, target, types, names) in enumerate(self.rt._queries):
+            types, ts, vals, nulls = self.rt.raw_outputs(q)
+            for i in range(len(ts)):
+                row = []
+                for j, t in enumerate(types):
+                    if nulls[j][i]:
+                        row.append(None)
+                    elif t == sa.INT:
+                        row.append(("i", ctypes.c_int32(vals[j][i]).value))
+                    elif t == sa.FLOAT:
+                        row.append(("f", vals[j][i] & 0xffffffff))
+                    elif t == sa.BOOL:
+                        row.append(("b", bool(vals[j][i])))
+                    elif t == sa.STRING:
+                        row.append(("s", self.rt.string(vals[j][i])))
+                    else:
+                        row.append((TAG[t], vals[j][i]))
+                for kind, nm in (("query", name), ("stream", target)):
+                    self.records.append({"kind": kind, "name": nm, "ts": ts[i], "expired": False, "values": row})
+
+    def outputs(self):
+        return self.records
+
+    def close(self):
+        self.rt.shutdown()
+
+
+def run_product_fixture(fx):
+    from oracle_rt import Driver, callback_events
+    p = ProductAdapter(fx["app"])
+    try:
+        def count_fn(ci):
+            p.flush()
+            return len(callback_events(p.outputs(), fx["callbacks"][ci])[0])
+        Driver(fx, p).run(count_fn)
+        p.flush()
+        return p.outputs()
+    finally:
+        p.close()

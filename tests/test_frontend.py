@@ -1,0 +1,52 @@
+"""SiddhiQL front end + lowering checks through the compile-only C-ABI (no GPU needed)."""
+import pytest
+
+import siddhi_amd as sa
+from siddhi_amd import workloads as w
+
+
+def compile_only(app):
+    return sa.SiddhiAppRuntime(app, compile_only=True)
+
+
+def test_c1_c2_lower_to_chain_kernel():
+    for app in (w.C1_APP, w.C2_APP):
+        rt = compile_only(app)
+        assert rt.query_paths() == [0]
+        name, target, types, names = rt._queries[0]
+        assert (name, target, names) == ("query1", "M", ["e1id", "e2id"])
+        assert types == [sa.LONG, sa.LONG]
+
+
+def test_output_types_follow_java_promotion():
+    app = ("define stream S (a int, b long, f float, d double, s string); "
+           "from every e1=S[a > 1] -> e2=S[f > e1.b] select e1.a + e2.b as x, e1.f * 2 as y, e2.d / e1.a as z, "
+           "e1.a % 2 as m insert into O;")
+    rt = compile_only(app)
+    assert rt._queries[0][2] == [sa.LONG, sa.FLOAT, sa.DOUBLE, sa.INT]
+
+
+@pytest.mark.parametrize("app,exc", [
+    ("define stream S (a int); from every e1=S[a > 'x'] -> e2=S[a > 1] select e1.a as a insert into O;",
+     sa.OperationNotSupportedException),
+    ("define stream S (a int); from every e1=T[a > 1] -> e2=S[a > 1] select e1.a as a insert into O;",
+     sa.SiddhiAppCreationException),
+    ("define stream S (a int); from every e1=S[b > 1] -> e2=S[a > 1] select e1.a as a insert into O;",
+     sa.SiddhiAppCreationException),
+    ("define stream S (a int); from every e1=S[a > 1] -> e2=S[a > 1 select e1.a insert into O;",
+     sa.SiddhiParserException),
+])
+def test_errors_map_to_reference_exceptions(app, exc):
+    with pytest.raises(exc):
+        compile_only(app)
+
+
+def test_sequence_is_rejected_until_generic_kernel():
+    with pytest.raises(sa.OperationNotSupportedException):
+        compile_only(w.C3_APP)
+
+
+def test_push_needs_a_device():
+    rt = compile_only(w.C1_APP)
+    with pytest.raises(sa.DeviceError):
+        rt.flush()
