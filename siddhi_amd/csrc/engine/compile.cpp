@@ -74,7 +74,10 @@ class QC {
             h_.out_names.push_back(oa.rename);
             h_.out_types.push_back(k);
         }
-        for (int s = 0; s < p.n_states; ++s) p.st[s] = rows_[s];
+        for (int s = 0; s < p.n_states; ++s) {
+            p.st[s] = rows_[s];
+            p.fast[s] = fast_pred(rows_[s].filter);
+        }
         // physical columns
         if ((int)h_.cols.size() > MAX_COLS) throw CompileError(SDG_ERR_UNSUPPORTED, "too many referenced attributes");
         p.n_cols = (int)h_.cols.size();
@@ -459,6 +462,71 @@ class QC {
         };
         (void)s;
         mark(el, 0);
+    }
+
+    // host-side conversion identical to eval.h cvt()
+    static int64_t host_cvt(int64_t v, uint8_t from, uint8_t to) {
+        if (from == to) return v;
+        if (to == VK_I64) return (int64_t)(int32_t)v;
+        if (to == VK_F32) return from == VK_I32 ? f32b((float)(int32_t)v) : f32b((float)v);
+        if (to == VK_F64) {
+            if (from == VK_I32) return f64b((double)(int32_t)v);
+            if (from == VK_I64) return f64b((double)v);
+            float f;
+            uint32_t u = (uint32_t)v;
+            std::memcpy(&f, &u, 4);
+            return f64b((double)f);
+        }
+        return v;
+    }
+
+    // recognise `LOAD [CVT] (CONST|LOAD) [CVT] CMP` (either operand order)
+    FastPred fast_pred(Prog pr) {
+        FastPred f;
+        if (pr.len == 0) { f.kind = FP_TRUE; return f; }
+        const Instr* c = h_.code.data() + pr.start;
+        int i = 0, n = pr.len;
+        struct Opnd { bool is_const; int slot, col, chain; uint8_t k, t; int64_t v; };
+        auto operand = [&](Opnd& o) -> bool {
+            if (i >= n) return false;
+            if (c[i].op == OP_LOAD) {
+                o = {false, c[i].a, c[i].b, c[i].c, c[i].k, c[i].k, 0};
+            } else if (c[i].op == OP_CONST) {
+                o = {true, 0, 0, 0, c[i].k, c[i].k, h_.consts[c[i].imm]};
+            } else {
+                return false;
+            }
+            ++i;
+            if (i < n && c[i].op == OP_CVT) { o.t = c[i].k; ++i; }
+            return true;
+        };
+        Opnd a, b;
+        if (!operand(a) || !operand(b) || i != n - 1 || c[i].op != OP_CMP) return f;
+        uint8_t op = c[i].a, t = c[i].k;
+        if (a.is_const && b.is_const) return f;
+        if (a.is_const) {  // mirror so that the attribute is on the left
+            std::swap(a, b);
+            static const uint8_t mir[] = {CMP_EQ, CMP_NE, CMP_LT, CMP_LE, CMP_GT, CMP_GE};
+            op = mir[op];
+        }
+        if (a.chain != 0 && a.chain != -1) return f;
+        if (!b.is_const && b.chain != 0 && b.chain != -1) return f;
+        f.op = op;
+        f.t = t;
+        f.ka = a.k;
+        f.sa = (int8_t)a.slot;
+        f.ca = a.col;
+        if (b.is_const) {
+            f.kind = FP_CONST;
+            f.kb = b.k;
+            f.konst = host_cvt(b.v, b.k, t);
+        } else {
+            f.kind = FP_SLOT;
+            f.kb = b.k;
+            f.sb = (int8_t)b.slot;
+            f.cb = b.col;
+        }
+        return f;
     }
 
     void partition_keys() {

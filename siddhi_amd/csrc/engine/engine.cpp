@@ -316,22 +316,13 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     const uint8_t* v_nulls[MAX_COLS];
     for (int k = 0; k < nc; ++k) { v_cols[k] = d_cols[k]; v_nulls[k] = d_nulls[k]; }
     HIPCHECK(hipEventRecord(e->ev[0], st));
+    const uint32_t* v_segend = nullptr;
     if (partitioned && nrows > 0) {
-        if ((int)K > KG_MAXK)
-            throw CompileError(SDG_ERR_CAPACITY, "key space " + std::to_string(K) + " exceeds the LDS key-grouping path (" +
-                                                     std::to_string(KG_MAXK) + ")");
         KeyGroupArgs a;
         std::memset(&a, 0, sizeof a);
-        size_t cb, gb;
-        keygroup_workspace(nrows, (int32_t)K, &a.nchunks, &cb, &gb);
         a.n = nrows;
         a.K = (int32_t)K;
         a.keys = d_key;
-        a.counts = (uint32_t*)q.kg_counts.ensure(cb);
-        a.gsum = (uint32_t*)q.kg_gsum.ensure(gb);
-        a.seg_start = (uint32_t*)q.seg.ensure((K + 1) * 4);
-        a.keys_sorted = (uint32_t*)q.so_key.ensure(nrows * 4);
-        a.orig_sorted = (uint32_t*)q.so_orig.ensure(nrows * 4);
         int c = 0;
         a.src[c] = d_ts; a.dst[c] = q.so_ts.ensure(nrows * 8); a.width[c] = 8; v_ts = (const int64_t*)a.dst[c]; ++c;
         if (d_qs) { a.src[c] = d_qs; a.dst[c] = q.so_qs.ensure(nrows); a.width[c] = 1; v_qs = (const uint8_t*)a.dst[c]; ++c; }
@@ -348,17 +339,22 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             }
         }
         a.ncols = c;
+        keygroup_bind(a, q.kg_counts.ensure(keygroup_workspace(nrows, (int32_t)K, a.ncols, a.width)));
+        a.keys_sorted = (uint32_t*)q.so_key.ensure(nrows * 4);
+        a.orig_sorted = (uint32_t*)q.so_orig.ensure(nrows * 4);
+        a.seg_start = (uint32_t*)q.seg.ensure((size_t)K * 4);
+        a.seg_end = (uint32_t*)q.kg_gsum.ensure((size_t)K * 4);
         keygroup(a, st, &e->ev[4]);
         v_key = a.keys_sorted;
         v_seg = a.seg_start;
+        v_segend = a.seg_end;
         v_orig = a.orig_sorted;
-        e->stats.keygroup_launches += 6;
+        e->stats.keygroup_launches += 1;
     } else if (partitioned) {
-        // empty batch: segments all empty
-        std::vector<uint32_t> z(K + 1, 0);
-        v_seg = (const uint32_t*)q.seg.ensure((K + 1) * 4);
-        HIPCHECK(hipMemcpyAsync((void*)v_seg, z.data(), (K + 1) * 4, hipMemcpyHostToDevice, st));
-        HIPCHECK(hipStreamSynchronize(st));
+        v_seg = (const uint32_t*)q.seg.ensure((size_t)K * 4);
+        v_segend = (const uint32_t*)q.kg_gsum.ensure((size_t)K * 4);
+        HIPCHECK(hipMemsetAsync((void*)v_seg, 0, (size_t)K * 4, st));
+        HIPCHECK(hipMemsetAsync((void*)v_segend, 0, (size_t)K * 4, st));
     }
     HIPCHECK(hipEventRecord(e->ev[1], st));
     // ---- 3. chain matcher -------------------------------------------------------------------------------
@@ -376,6 +372,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     a.qstream = multi_stream ? v_qs : nullptr;
     a.key = partitioned ? v_key : nullptr;
     a.seg_start = partitioned ? v_seg : nullptr;
+    a.seg_end = partitioned ? v_segend : nullptr;
+    a.K = (int32_t)K;
     a.orig = v_orig;
     for (int k = 0; k < nc; ++k) { a.cols[k] = v_cols[k]; a.nulls[k] = v_nulls[k]; }
     a.seq_base = q.seq;
@@ -426,11 +424,12 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     e->stats.ms_match += ms_m;
     float t;
     if (partitioned && nrows > 0) {
+        // radix: [4]..[5] first hist+prefix, [5]..[6] scatter passes (+ later hist/prefix), [6]..[7] segments
         HIPCHECK(hipEventElapsedTime(&t, e->ev[4], e->ev[5]));
         e->stats.ms_kg_hist += t;
-        HIPCHECK(hipEventElapsedTime(&t, e->ev[5], e->ev[6]));
-        e->stats.ms_kg_prefix += t;
         HIPCHECK(hipEventElapsedTime(&t, e->ev[6], e->ev[7]));
+        e->stats.ms_kg_prefix += t;
+        HIPCHECK(hipEventElapsedTime(&t, e->ev[5], e->ev[6]));
         e->stats.ms_kg_scatter += t;
     }
     HIPCHECK(hipEventElapsedTime(&t, e->ev[1], e->ev[8]));

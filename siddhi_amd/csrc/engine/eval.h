@@ -229,6 +229,24 @@ __device__ __forceinline__ void run(const Instr* __restrict__ code, Prog p, cons
     *out_null = (nulls & 1u) != 0;
 }
 
+// FastPred evaluation (compile-time recognised `a OP b`): identical results to the bytecode
+template <class Acc>
+__device__ __forceinline__ bool fast_pass(const FastPred& f, Acc& acc) {
+    int64_t a, b;
+    bool na, nb;
+    acc.load(f.sa, f.ca, -1, f.ka, &a, &na);
+    if (na) return false;
+    a = cvt(a, f.ka, f.t);
+    if (f.kind == FP_CONST) {
+        b = f.konst;
+    } else {
+        acc.load(f.sb, f.cb, -1, f.kb, &b, &nb);
+        if (nb) return false;
+        b = cvt(b, f.kb, f.t);
+    }
+    return cmp(f.op, f.t, a, b);
+}
+
 // a filter passes iff its result is non-null and true (FilterProcessor.java:48-60)
 template <class Acc>
 __device__ __forceinline__ bool pass(const Instr* code, Prog p, const int64_t* consts, Acc& acc, int64_t* stk,

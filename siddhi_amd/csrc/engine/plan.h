@@ -41,6 +41,20 @@ struct Prog {
     int32_t start = 0, len = 0;  // into Plan::code; len 0 == always true (no filter)
 };
 
+// A filter of the shape `a OP b` with a = attribute of a state slot and b = constant or attribute of another
+// slot, recognised at compile time and evaluated natively (no interpreter); same semantics as the bytecode.
+enum FastKind : uint8_t { FP_NONE = 0, FP_TRUE = 1, FP_CONST = 2, FP_SLOT = 3 };
+struct FastPred {
+    uint8_t kind = FP_NONE;
+    uint8_t op = 0;      // CmpOp, oriented as a OP b
+    uint8_t t = 0;       // comparison kind after promotion
+    uint8_t ka = 0, kb = 0;
+    int8_t sa = 0, sb = 0;
+    uint8_t pad = 0;
+    int32_t ca = 0, cb = 0;
+    int64_t konst = 0;   // FP_CONST: b already converted to kind t
+};
+
 constexpr int MAX_STATES = 16;
 constexpr int MAX_OUT = 32;
 constexpr int MAX_COLS = 32;
@@ -84,6 +98,7 @@ struct Plan {
     int32_t n_streams = 0;         // streams this query reads, in receiver order
     int32_t streams[MAX_STATES];
     StateRow st[MAX_STATES];
+    FastPred fast[MAX_STATES];     // per state filter (FP_NONE: use the bytecode)
     // expire order (allStateProcessors), setup order per stream etc. live on the host plan
     int32_t n_code = 0, n_consts = 0;
 };

@@ -7,31 +7,42 @@
 
 namespace sdg {
 
-// ---- key grouping: stable counting sort of a batch by dense key id -------------------------------------
-// hist (one wave per chunk, LDS counters) -> per-key prefix over chunks -> stable scatter (one wave per chunk;
-// lanes with equal keys are ranked by a ballot match over the key bits, so order inside a key is the
-// arrival order). Columns are moved by the scatter (coalesced reads, per-key runs of writes).
-constexpr int KG_CHUNK = 65536;       // events per histogram/scatter wave
-constexpr int KG_MAXK = 16384;        // key space handled by the LDS-counter path
-constexpr int KG_GROUP = 64;          // chunks per prefix group
+// ---- key grouping: stable LSD radix sort of a batch by dense key id ------------------------------------
+// Each pass sorts by one digit of <= 8 bits (<= 256 buckets): per-tile digit histogram -> prefix over tiles ->
+// stable tile scatter. Inside a tile (4096 events, 256 threads) ranks are stable (wave ballot match over the
+// digit bits + per-wave prefix in LDS), the tile is staged in LDS in digit order and every column is written
+// out with consecutive lanes on consecutive addresses of one digit run (coalesced), one column at a time.
+constexpr int RX_TILE = 4096;
+constexpr int RX_THREADS = 256;
+constexpr int RX_MAXBITS = 8;
+constexpr int KG_GROUP = 64;          // tiles per prefix group
 
 struct KeyGroupArgs {
     int64_t n;
-    int32_t K;
-    int32_t nchunks;
-    const uint32_t* keys;             // [n] dense key ids (< K)
-    uint32_t* counts;                 // [nchunks * K] workspace (becomes per-chunk start offsets)
-    uint32_t* gsum;                   // [ngroups * K] workspace
-    uint32_t* seg_start;              // [K + 1] out: first sorted position of key k; seg_start[K] = n
-    uint32_t* keys_sorted;            // [n] out
-    uint32_t* orig_sorted;            // [n] out: original row of each sorted position
-    int32_t ncols;                    // columns moved with the keys
+    int32_t K;                        // keys are dense ids < K
+    const uint32_t* keys;             // [n] input keys (time order)
+    // workspace (keygroup_workspace)
+    uint32_t* counts;                 // [ntiles * 256]
+    uint32_t* gsum;                   // [ngroups * 256]
+    uint32_t* tot;                    // [257]
+    uint32_t* tmp_keys[2];            // [n] ping-pong key buffers
+    uint32_t* tmp_orig[2];            // [n] ping-pong original-row buffers
+    void* tmp_cols[2][MAX_COLS + 2];  // [n * width] ping-pong payload buffers
+    // outputs
+    uint32_t* keys_sorted;            // [n]
+    uint32_t* orig_sorted;            // [n] original row of each sorted position
+    uint32_t* seg_start;              // [K] first sorted position of key k (0 if absent)
+    uint32_t* seg_end;                // [K] one past the last (0 if absent)
+    int32_t ncols;                    // payload columns moved with the keys
     const void* src[MAX_COLS + 2];
     void* dst[MAX_COLS + 2];
     uint8_t width[MAX_COLS + 2];      // bytes per element (1, 4 or 8)
 };
-size_t keygroup_workspace(int64_t n, int32_t K, int32_t* nchunks, size_t* counts_bytes, size_t* gsum_bytes);
-// marks (optional, 4 events): recorded before hist, after hist, after the prefix kernels, after the scatter
+// bytes of workspace for n events; fills the workspace pointers of `a` from `base`
+size_t keygroup_workspace(int64_t n, int32_t K, int32_t ncols, const uint8_t* widths);
+void keygroup_bind(KeyGroupArgs& a, void* base);
+// marks (optional, 4 events): recorded before the histograms, after the prefix kernels of pass 1, after
+// the last scatter, after the segment kernel
 void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks = nullptr);
 
 // ---- chain matcher: `every e1=S0[c0] -> e2=S1[c1] within T` (independent partials) ---------------------
@@ -43,7 +54,9 @@ struct ChainArgs {
     const int64_t* ts;                // sorted view
     const uint8_t* qstream;           // [n] query-stream position of each row (nullptr: single stream 0)
     const uint32_t* key;              // [n] sorted keys (nullptr: unpartitioned, one segment)
-    const uint32_t* seg_start;        // [K + 1] (nullptr: unpartitioned)
+    const uint32_t* seg_start;        // [K] (nullptr: unpartitioned)
+    const uint32_t* seg_end;          // [K]
+    int32_t K;
     const uint32_t* orig;             // [n] sorted -> original row (nullptr: identity)
     const void* cols[MAX_COLS];
     const uint8_t* nulls[MAX_COLS];

@@ -4,6 +4,8 @@
 // atomic per wave. Everything is integer/byte work bound by HBM, so no MFMA.
 #include <hip/hip_runtime.h>
 
+#include <cstring>
+
 #include "../engine/eval.h"
 #include "kernels.h"
 
@@ -30,132 +32,205 @@ __device__ __forceinline__ int64_t wave_reserve(bool take, unsigned long long* c
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// key grouping
+// key grouping: LSD radix passes
 
-__global__ __launch_bounds__(256) void kg_hist(const uint32_t* __restrict__ keys, int64_t n, int K,
-                                               uint32_t* __restrict__ counts) {
-    extern __shared__ uint32_t h[];
-    for (int k = threadIdx.x; k < K; k += blockDim.x) h[k] = 0;
+__device__ __forceinline__ uint32_t digit_of(uint32_t k, int shift, uint32_t mask) { return (k >> shift) & mask; }
+
+// per-tile digit histogram: counts[tile * nb + d]
+__global__ __launch_bounds__(RX_THREADS) void rx_hist(const uint32_t* __restrict__ keys, int64_t n, int shift,
+                                                      uint32_t mask, int nb, uint32_t* __restrict__ counts) {
+    __shared__ uint32_t h[1 << RX_MAXBITS];
+    for (int d = threadIdx.x; d < nb; d += RX_THREADS) h[d] = 0;
     __syncthreads();
-    int64_t s = (int64_t)blockIdx.x * KG_CHUNK;
-    int64_t e = s + KG_CHUNK < n ? s + KG_CHUNK : n;
-    for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) atomicAdd(&h[keys[i]], 1u);
+    int64_t base = (int64_t)blockIdx.x * RX_TILE;
+#pragma unroll 4
+    for (int r = 0; r < RX_TILE / RX_THREADS; ++r) {
+        int64_t i = base + r * RX_THREADS + threadIdx.x;
+        if (i < n) atomicAdd(&h[digit_of(keys[i], shift, mask)], 1u);
+    }
     __syncthreads();
-    for (int k = threadIdx.x; k < K; k += blockDim.x) counts[(int64_t)blockIdx.x * K + k] = h[k];
+    for (int d = threadIdx.x; d < nb; d += RX_THREADS) counts[(int64_t)blockIdx.x * nb + d] = h[d];
 }
 
-// group sums over KG_GROUP chunks: thread (g, k)
-__global__ __launch_bounds__(256) void kg_p1(const uint32_t* __restrict__ counts, int nchunks, int K,
+// group sums over KG_GROUP tiles: thread (g, d)
+__global__ __launch_bounds__(256) void rx_p1(const uint32_t* __restrict__ counts, int ntiles, int nb,
                                              uint32_t* __restrict__ gsum) {
     int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    int ng = (nchunks + KG_GROUP - 1) / KG_GROUP;
-    if (idx >= (int64_t)ng * K) return;
-    int g = (int)(idx / K), k = (int)(idx % K);
-    int b0 = g * KG_GROUP, b1 = min(nchunks, b0 + KG_GROUP);
+    int ng = (ntiles + KG_GROUP - 1) / KG_GROUP;
+    if (idx >= (int64_t)ng * nb) return;
+    int g = (int)(idx / nb), d = (int)(idx % nb);
+    int b0 = g * KG_GROUP, b1 = min(ntiles, b0 + KG_GROUP);
     uint32_t s = 0;
-    for (int b = b0; b < b1; ++b) s += counts[(int64_t)b * K + k];
+    for (int b = b0; b < b1; ++b) s += counts[(int64_t)b * nb + d];
     gsum[idx] = s;
 }
 
-// per key: exclusive scan over groups (in place); totals to tot[k]
-__global__ __launch_bounds__(256) void kg_p2(uint32_t* __restrict__ gsum, int ng, int K, uint32_t* __restrict__ tot) {
-    int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= K) return;
+// one block: per digit, exclusive scan over groups (in place) + digit totals; then exclusive scan over digits
+__global__ __launch_bounds__(256) void rx_p2(uint32_t* __restrict__ gsum, int ng, int nb, uint32_t* __restrict__ tot) {
+    __shared__ uint32_t part[256];
+    int d = threadIdx.x;
     uint32_t run = 0;
-    for (int g = 0; g < ng; ++g) {
-        uint32_t c = gsum[(int64_t)g * K + k];
-        gsum[(int64_t)g * K + k] = run;
-        run += c;
+    if (d < nb) {
+        for (int g = 0; g < ng; ++g) {
+            uint32_t c = gsum[(int64_t)g * nb + d];
+            gsum[(int64_t)g * nb + d] = run;
+            run += c;
+        }
     }
-    tot[k] = run;
-}
-
-// exclusive scan of tot[0..K) in place (K <= KG_MAXK), one 1024-thread block; tot[K] = n
-__global__ __launch_bounds__(1024) void kg_kscan(uint32_t* __restrict__ tot, int K, int64_t n) {
-    __shared__ uint32_t part[1024];
-    constexpr int PER = KG_MAXK / 1024;
-    int t = threadIdx.x;
-    uint32_t v[PER];
-    uint32_t s = 0;
-    for (int j = 0; j < PER; ++j) {
-        int k = t * PER + j;
-        v[j] = k < K ? tot[k] : 0;
-        s += v[j];
-    }
-    part[t] = s;
+    part[d] = d < nb ? run : 0;
     __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-        uint32_t x = t >= off ? part[t - off] : 0;
+    for (int off = 1; off < 256; off <<= 1) {
+        uint32_t x = d >= off ? part[d - off] : 0;
         __syncthreads();
-        part[t] += x;
+        part[d] += x;
         __syncthreads();
     }
-    uint32_t run = part[t] - s;
-    for (int j = 0; j < PER; ++j) {
-        int k = t * PER + j;
-        if (k < K) tot[k] = run;
-        run += v[j];
-    }
-    if (t == 0) tot[K] = (uint32_t)n;
+    if (d < nb) tot[d] = part[d] - run;  // exclusive digit base
 }
 
-// per (group, key): rewrite the group's chunk counts as absolute start offsets
-__global__ __launch_bounds__(256) void kg_p3(uint32_t* __restrict__ counts, const uint32_t* __restrict__ gsum,
-                                             const uint32_t* __restrict__ seg_start, int nchunks, int K) {
+// per (group, digit): rewrite the group's tile counts as absolute start offsets
+__global__ __launch_bounds__(256) void rx_p3(uint32_t* __restrict__ counts, const uint32_t* __restrict__ gsum,
+                                             const uint32_t* __restrict__ tot, int ntiles, int nb) {
     int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    int ng = (nchunks + KG_GROUP - 1) / KG_GROUP;
-    if (idx >= (int64_t)ng * K) return;
-    int g = (int)(idx / K), k = (int)(idx % K);
-    uint32_t run = seg_start[k] + gsum[idx];
-    int b0 = g * KG_GROUP, b1 = min(nchunks, b0 + KG_GROUP);
+    int ng = (ntiles + KG_GROUP - 1) / KG_GROUP;
+    if (idx >= (int64_t)ng * nb) return;
+    int g = (int)(idx / nb), d = (int)(idx % nb);
+    uint32_t run = tot[d] + gsum[idx];
+    int b0 = g * KG_GROUP, b1 = min(ntiles, b0 + KG_GROUP);
     for (int b = b0; b < b1; ++b) {
-        uint32_t c = counts[(int64_t)b * K + k];
-        counts[(int64_t)b * K + k] = run;
+        uint32_t c = counts[(int64_t)b * nb + d];
+        counts[(int64_t)b * nb + d] = run;
         run += c;
     }
 }
 
-// stable scatter: one wave per chunk, LDS cursor per key; equal keys inside one wave step are ranked by a
-// ballot match over the key bits (lane order == arrival order).
-__global__ __launch_bounds__(64) void kg_scatter(KeyGroupArgs a, int kbits) {
-    extern __shared__ uint32_t cur[];
-    const int K = a.K;
-    const int lane = threadIdx.x;
-    for (int k = lane; k < K; k += 64) cur[k] = a.counts[(int64_t)blockIdx.x * K + k];
+struct RxPass {
+    const uint32_t* keys_in;
+    uint32_t* keys_out;
+    const uint32_t* orig_in;  // nullptr: identity (first pass)
+    uint32_t* orig_out;
+    int ncols;
+    const void* src[MAX_COLS + 2];
+    void* dst[MAX_COLS + 2];
+    uint8_t width[MAX_COLS + 2];
+    const uint32_t* offsets;  // counts rewritten by rx_p3: [tile * nb + d]
+    int64_t n;
+    int shift;
+    uint32_t mask;
+    int nb;
+    int bits;
+};
+
+// stable tile scatter
+__global__ __launch_bounds__(RX_THREADS) void rx_scatter(RxPass a) {
+    constexpr int R = RX_TILE / RX_THREADS;  // rounds (16): element r*256 + t of the tile
+    __shared__ uint32_t cnt[1 << RX_MAXBITS];
+    __shared__ uint32_t wavecnt[RX_THREADS / 64][1 << RX_MAXBITS];
+    __shared__ uint32_t tstart[1 << RX_MAXBITS];
+    __shared__ uint32_t gbase[1 << RX_MAXBITS];
+    __shared__ uint32_t dest[RX_TILE];
+    __shared__ uint64_t stage[RX_TILE];
+    const int t = threadIdx.x, w = t >> 6;
+    const int64_t base = (int64_t)blockIdx.x * RX_TILE;
+    const int64_t tile_n = min((int64_t)RX_TILE, a.n - base);
+    for (int d = t; d < a.nb; d += RX_THREADS) {
+        cnt[d] = 0;
+        gbase[d] = a.offsets[(int64_t)blockIdx.x * a.nb + d];
+        for (int v = 0; v < RX_THREADS / 64; ++v) wavecnt[v][d] = 0;
+    }
     __syncthreads();
-    int64_t s = (int64_t)blockIdx.x * KG_CHUNK;
-    int64_t e = s + KG_CHUNK < a.n ? s + KG_CHUNK : a.n;
     const uint64_t lt = lanemask_lt();
-    for (int64_t base = s; base < e; base += 64) {
-        int64_t i = base + lane;
-        bool valid = i < e;
-        uint32_t k = valid ? a.keys[i] : 0u;
+    uint32_t rank[R];
+    uint16_t dig[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        int64_t i = base + r * RX_THREADS + t;
+        bool valid = i < a.n;
+        uint32_t d = valid ? digit_of(a.keys_in[i], a.shift, a.mask) : 0u;
         uint64_t peers = __ballot(valid);
-        for (int bit = 0; bit < kbits; ++bit) {
-            bool on = (k >> bit) & 1u;
+        for (int bit = 0; bit < a.bits; ++bit) {
+            bool on = (d >> bit) & 1u;
             uint64_t b = __ballot(on);
             peers &= on ? b : ~b;
         }
-        int leader = peers ? __ffsll((unsigned long long)peers) - 1 : lane;
-        uint32_t kb = 0;
-        if (valid && lane == leader) {
-            kb = cur[k];
-            cur[k] = kb + (uint32_t)__popcll(peers);
-        }
-        kb = __shfl(kb, leader);
+        int leader = peers ? __ffsll((unsigned long long)peers) - 1 : 0;
+        if (valid && lane_id() == leader) wavecnt[w][d] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        uint32_t pre = 0;
         if (valid) {
-            uint32_t dest = kb + (uint32_t)__popcll(peers & lt);
-            a.keys_sorted[dest] = k;
-            a.orig_sorted[dest] = (uint32_t)i;
-            for (int c = 0; c < a.ncols; ++c) {
-                switch (a.width[c]) {
-                    case 8: ((int64_t*)a.dst[c])[dest] = ((const int64_t*)a.src[c])[i]; break;
-                    case 4: ((uint32_t*)a.dst[c])[dest] = ((const uint32_t*)a.src[c])[i]; break;
-                    default: ((uint8_t*)a.dst[c])[dest] = ((const uint8_t*)a.src[c])[i]; break;
-                }
+            pre = cnt[d];
+            for (int v = 0; v < w; ++v) pre += wavecnt[v][d];
+        }
+        rank[r] = pre + (uint32_t)__popcll(peers & lt);
+        dig[r] = (uint16_t)d;
+        __syncthreads();
+        for (int dd = t; dd < a.nb; dd += RX_THREADS) {
+            uint32_t s = 0;
+            for (int v = 0; v < RX_THREADS / 64; ++v) {
+                s += wavecnt[v][dd];
+                wavecnt[v][dd] = 0;
+            }
+            cnt[dd] += s;
+        }
+        __syncthreads();
+    }
+    // tile-local start of each digit run (exclusive scan of cnt over nb <= 256 digits)
+    if (t < 256) tstart[t] = t < a.nb ? cnt[t] : 0;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+        uint32_t x = (t < 256 && t >= off) ? tstart[t - off] : 0;
+        __syncthreads();
+        if (t < 256) tstart[t] += x;
+        __syncthreads();
+    }
+    if (t < 256) tstart[t] -= (t < a.nb ? cnt[t] : 0);
+    __syncthreads();
+    uint32_t sp[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        int64_t i = base + r * RX_THREADS + t;
+        sp[r] = tstart[dig[r]] + rank[r];
+        if (i < a.n) dest[sp[r]] = gbase[dig[r]] + rank[r];
+    }
+    __syncthreads();
+    // keys, original rows, then every payload column: stage in digit order, write runs out coalesced
+    for (int c = -2; c < a.ncols; ++c) {
+        int wd = c < 0 ? 4 : a.width[c];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            int64_t i = base + r * RX_THREADS + t;
+            if (i < a.n) {
+                uint64_t v;
+                if (c == -2) v = a.keys_in[i];
+                else if (c == -1) v = a.orig_in ? a.orig_in[i] : (uint32_t)i;
+                else if (wd == 8) v = ((const uint64_t*)a.src[c])[i];
+                else if (wd == 4) v = ((const uint32_t*)a.src[c])[i];
+                else v = ((const uint8_t*)a.src[c])[i];
+                stage[sp[r]] = v;
             }
         }
+        __syncthreads();
+        for (int j = t; j < tile_n; j += RX_THREADS) {
+            uint32_t o = dest[j];
+            uint64_t v = stage[j];
+            if (c == -2) a.keys_out[o] = (uint32_t)v;
+            else if (c == -1) a.orig_out[o] = (uint32_t)v;
+            else if (wd == 8) ((uint64_t*)a.dst[c])[o] = v;
+            else if (wd == 4) ((uint32_t*)a.dst[c])[o] = (uint32_t)v;
+            else ((uint8_t*)a.dst[c])[o] = (uint8_t)v;
+        }
+        __syncthreads();
     }
+}
+
+// key segments of the sorted keys
+__global__ __launch_bounds__(256) void rx_segments(const uint32_t* __restrict__ keys, int64_t n,
+                                                   uint32_t* __restrict__ seg_start, uint32_t* __restrict__ seg_end) {
+    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    uint32_t k = keys[p];
+    if (p == 0 || keys[p - 1] != k) seg_start[k] = (uint32_t)p;
+    if (p == n - 1 || keys[p + 1] != k) seg_end[k] = (uint32_t)(p + 1);
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -205,6 +280,7 @@ __device__ __forceinline__ int64_t chain_scan(const ChainArgs& a, ChainAcc& acc,
     const int32_t has_within = P->has_within;
     const int64_t within = P->within_ms;
     const Prog c1 = P->st[1].filter;
+    const FastPred f1 = P->fast[1];
     for (int64_t q = from; q < end; ++q) {
         int64_t tq = a.ts[q];
         // StreamPreStateProcessor.isExpired: |start.ts - now| > within, checked before the event is processed
@@ -215,7 +291,10 @@ __device__ __forceinline__ int64_t chain_scan(const ChainArgs& a, ChainAcc& acc,
         }
         if (qstream_of(a, q) == a.s1) {
             acc.r1 = q;
-            if (pass(a.code, c1, a.consts, acc, stk, stride)) return q;
+            bool ok = f1.kind == FP_TRUE ? true
+                      : f1.kind == FP_NONE ? pass(a.code, c1, a.consts, acc, stk, stride)
+                                           : fast_pass(f1, acc);
+            if (ok) return q;
             acc.r1 = -1;
         }
     }
@@ -255,12 +334,17 @@ __global__ __launch_bounds__(256) void chain_match_k(ChainArgs a) {
     if (active) {
         key = a.key ? a.key[p] : 0u;
         if (p > 0 && a.ts[p] < a.ts[p - 1] && (!a.key || a.key[p - 1] == key)) atomicOr(&a.flags[1], 1);
-        if (qstream_of(a, p) == a.s0 && pass(a.code, P->st[0].filter, a.consts, acc, stk, stride)) {
+        const FastPred f0 = P->fast[0];
+        bool c0 = false;
+        if (qstream_of(a, p) == a.s0)
+            c0 = f0.kind == FP_TRUE ? true
+                 : f0.kind == FP_NONE ? pass(a.code, P->st[0].filter, a.consts, acc, stk, stride) : fast_pass(f0, acc);
+        if (c0) {
             if (P->n_states == 1) {
                 has = true;
                 qhit = p;
             } else {
-                int64_t end = a.key ? (int64_t)a.seg_start[key + 1] : a.n;
+                int64_t end = a.key ? (int64_t)a.seg_end[key] : a.n;
                 int64_t r = chain_scan(a, acc, p + 1, end, a.ts[p], stk, stride);
                 if (r >= 0) { has = true; qhit = r; }
                 else if (r == -2) carry = true;
@@ -303,8 +387,11 @@ __global__ __launch_bounds__(256) void chain_carry_k(ChainArgs a) {
     uint32_t key = 0;
     if (active) {
         key = a.cin_key[c];
-        int64_t b = a.key ? (int64_t)a.seg_start[key] : 0;
-        int64_t e = a.key ? (int64_t)a.seg_start[key + 1] : a.n;
+        int64_t b = 0, e = a.n;
+        if (a.key) {
+            b = key < (uint32_t)a.K ? (int64_t)a.seg_start[key] : 0;
+            e = key < (uint32_t)a.K ? (int64_t)a.seg_end[key] : 0;
+        }
         int64_t r = chain_scan(a, acc, b, e, a.cin_ts[c], stk, stride);
         if (r >= 0) { has = true; qhit = r; }
         else if (r == -2) carry = true;
@@ -331,33 +418,84 @@ __global__ __launch_bounds__(256) void chain_carry_k(ChainArgs a) {
 
 }  // namespace
 
-size_t keygroup_workspace(int64_t n, int32_t K, int32_t* nchunks, size_t* counts_bytes, size_t* gsum_bytes) {
-    int32_t nc = (int32_t)((n + KG_CHUNK - 1) / KG_CHUNK);
-    if (nc < 1) nc = 1;
-    int32_t ng = (nc + KG_GROUP - 1) / KG_GROUP;
-    *nchunks = nc;
-    *counts_bytes = (size_t)nc * K * 4;
-    *gsum_bytes = (size_t)ng * K * 4;
-    return *counts_bytes + *gsum_bytes;
+static int64_t rx_ntiles(int64_t n) { return n <= 0 ? 1 : (n + RX_TILE - 1) / RX_TILE; }
+
+size_t keygroup_workspace(int64_t n, int32_t K, int32_t ncols, const uint8_t* widths) {
+    int64_t nt = rx_ntiles(n);
+    int64_t ng = (nt + KG_GROUP - 1) / KG_GROUP;
+    size_t b = (size_t)nt * 256 * 4 + (size_t)ng * 256 * 4 + 257 * 4 + 4 * (size_t)n * 4;
+    for (int c = 0; c < ncols; ++c) b += 2 * (size_t)n * widths[c] + 256;
+    return b + 4096;
+}
+
+void keygroup_bind(KeyGroupArgs& a, void* base) {
+    uint8_t* p = (uint8_t*)base;
+    auto take = [&](size_t bytes) {
+        uint8_t* r = p;
+        p += (bytes + 255) & ~size_t(255);
+        return (void*)r;
+    };
+    int64_t nt = rx_ntiles(a.n);
+    int64_t ng = (nt + KG_GROUP - 1) / KG_GROUP;
+    a.counts = (uint32_t*)take((size_t)nt * 256 * 4);
+    a.gsum = (uint32_t*)take((size_t)ng * 256 * 4);
+    a.tot = (uint32_t*)take(257 * 4);
+    for (int i = 0; i < 2; ++i) {
+        a.tmp_keys[i] = (uint32_t*)take((size_t)a.n * 4);
+        a.tmp_orig[i] = (uint32_t*)take((size_t)a.n * 4);
+    }
+    for (int i = 0; i < 2; ++i)
+        for (int c = 0; c < a.ncols; ++c) a.tmp_cols[i][c] = take((size_t)a.n * a.width[c]);
 }
 
 void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
-    const int K = a.K;
-    const int nc = a.nchunks;
-    const int ng = (nc + KG_GROUP - 1) / KG_GROUP;
     int kbits = 0;
-    while ((1 << kbits) < K) ++kbits;
+    while ((1ll << kbits) < (int64_t)a.K) ++kbits;
+    if (kbits == 0) kbits = 1;
+    int npass = (kbits + RX_MAXBITS - 1) / RX_MAXBITS;
+    int bits = (kbits + npass - 1) / npass;
+    int64_t nt = rx_ntiles(a.n);
+    int ng = (int)((nt + KG_GROUP - 1) / KG_GROUP);
     if (marks) (void)hipEventRecord(marks[0], stream);
-    hipLaunchKernelGGL(kg_hist, dim3(nc), dim3(256), K * 4, stream, a.keys, a.n, K, a.counts);
-    if (marks) (void)hipEventRecord(marks[1], stream);
-    int64_t gk = (int64_t)ng * K;
-    hipLaunchKernelGGL(kg_p1, dim3((unsigned)((gk + 255) / 256)), dim3(256), 0, stream, a.counts, nc, K, a.gsum);
-    hipLaunchKernelGGL(kg_p2, dim3((K + 255) / 256), dim3(256), 0, stream, a.gsum, ng, K, a.seg_start);
-    hipLaunchKernelGGL(kg_kscan, dim3(1), dim3(1024), 0, stream, a.seg_start, K, a.n);
-    hipLaunchKernelGGL(kg_p3, dim3((unsigned)((gk + 255) / 256)), dim3(256), 0, stream, a.counts, a.gsum,
-                       a.seg_start, nc, K);
+    for (int p = 0; p < npass; ++p) {
+        int shift = p * bits;
+        int b = min(bits, kbits - shift);
+        int nb = 1 << b;
+        uint32_t mask = (uint32_t)nb - 1;
+        const uint32_t* kin = p == 0 ? a.keys : a.tmp_keys[(p - 1) & 1];
+        bool last = p == npass - 1;
+        hipLaunchKernelGGL(rx_hist, dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, kin, a.n, shift, mask, nb, a.counts);
+        int64_t gk = (int64_t)ng * nb;
+        hipLaunchKernelGGL(rx_p1, dim3((unsigned)((gk + 255) / 256)), dim3(256), 0, stream, a.counts, (int)nt, nb, a.gsum);
+        hipLaunchKernelGGL(rx_p2, dim3(1), dim3(256), 0, stream, a.gsum, ng, nb, a.tot);
+        hipLaunchKernelGGL(rx_p3, dim3((unsigned)((gk + 255) / 256)), dim3(256), 0, stream, a.counts, a.gsum, a.tot,
+                           (int)nt, nb);
+        if (marks && p == 0) (void)hipEventRecord(marks[1], stream);
+        RxPass rp;
+        std::memset(&rp, 0, sizeof rp);
+        rp.keys_in = kin;
+        rp.keys_out = last ? a.keys_sorted : a.tmp_keys[p & 1];
+        rp.orig_in = p == 0 ? nullptr : a.tmp_orig[(p - 1) & 1];
+        rp.orig_out = last ? a.orig_sorted : a.tmp_orig[p & 1];
+        rp.ncols = a.ncols;
+        for (int c = 0; c < a.ncols; ++c) {
+            rp.src[c] = p == 0 ? a.src[c] : a.tmp_cols[(p - 1) & 1][c];
+            rp.dst[c] = last ? a.dst[c] : a.tmp_cols[p & 1][c];
+            rp.width[c] = a.width[c];
+        }
+        rp.offsets = a.counts;
+        rp.n = a.n;
+        rp.shift = shift;
+        rp.mask = mask;
+        rp.nb = nb;
+        rp.bits = b;
+        hipLaunchKernelGGL(rx_scatter, dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, rp);
+    }
     if (marks) (void)hipEventRecord(marks[2], stream);
-    hipLaunchKernelGGL(kg_scatter, dim3(nc), dim3(64), K * 4, stream, a, kbits);
+    (void)hipMemsetAsync(a.seg_start, 0, (size_t)a.K * 4, stream);
+    (void)hipMemsetAsync(a.seg_end, 0, (size_t)a.K * 4, stream);
+    hipLaunchKernelGGL(rx_segments, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, stream, a.keys_sorted, a.n,
+                       a.seg_start, a.seg_end);
     if (marks) (void)hipEventRecord(marks[3], stream);
 }
 

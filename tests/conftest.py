@@ -20,3 +20,15 @@ def oracle_built():
         import subprocess
         subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle")])
     return so
+
+
+def pytest_sessionstart(session):
+    # torch ships its own HIP runtime (ROCm 7.0) beside the engine's /opt/rocm one: when a GPU session uses
+    # both (device-resident inputs from torch tensors), torch's runtime must initialise first.
+    if "gpu" in (session.config.getoption("markexpr") or "") and "not gpu" not in session.config.getoption("markexpr"):
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except Exception:
+            pass
