@@ -110,6 +110,7 @@ typedef struct sdg_stats {
     int32_t overflow;          /* capacity overflows detected (0 on a valid run) */
     /* device ms per kernel (HIP events on the engine's stream), summed over the flush's queries */
     double ms_kg_hist, ms_kg_prefix, ms_kg_scatter, ms_chain_carry, ms_chain_match;
+    double ms_nfa;             /* generic keyed-NFA kernel */
 } sdg_stats;
 int sdg_last_stats(sdg_engine* e, sdg_stats* out);
 

@@ -74,7 +74,8 @@ class Stats(ctypes.Structure):
                 ("path", ctypes.c_int32), ("overflow", ctypes.c_int32),
                 ("ms_kg_hist", ctypes.c_double), ("ms_kg_prefix", ctypes.c_double),
                 ("ms_kg_scatter", ctypes.c_double), ("ms_chain_carry", ctypes.c_double),
-                ("ms_chain_match", ctypes.c_double)]
+                ("ms_chain_match", ctypes.c_double),
+                ("ms_nfa", ctypes.c_double)]
 
 
 _lib = None

@@ -95,6 +95,7 @@ class QC {
         partition_keys();
         p.partitioned = q_.partition_index >= 0;
         detect_chain(root);
+        runtime_tables(root.node);
         p.n_code = (int)h_.code.size();
         p.n_consts = (int)h_.consts.size();
     }
@@ -109,7 +110,84 @@ class QC {
 
     struct Sub {
         int first = -1, last = -1;
+        int node = -1;
     };
+    // inner runtime tree (runtime/*InnerStateRuntime.java)
+    struct Inner {
+        int kind;  // 0 stream/count leaf, 1 next, 2 every, 3 logical
+        int a = -1, b = -1;
+        int first = -1;
+    };
+    std::vector<Inner> inner_;
+    std::vector<int> startup_;
+    int mk_inner(int kind, int a, int b, int first) {
+        Inner in;
+        in.kind = kind;
+        in.a = a;
+        in.b = b;
+        in.first = first;
+        inner_.push_back(in);
+        return (int)inner_.size() - 1;
+    }
+    void tree_init(int n, std::vector<int>& out) {
+        const Inner& in = inner_[n];
+        if (in.kind == 1) { tree_init(in.a, out); tree_init(in.b, out); }
+        else if (in.kind == 2) tree_init(in.a, out);
+        else if (in.kind == 3) { tree_init(in.b, out); tree_init(in.a, out); }
+        else out.push_back(in.first);
+    }
+    void tree_reset(int n, std::vector<int>& out) {
+        const Inner& in = inner_[n];
+        if (in.kind == 1) { tree_reset(in.b, out); tree_reset(in.a, out); }
+        else if (in.kind == 3) tree_reset(in.b, out);
+        else out.push_back(in.first);  // leaf, count and every: firstProcessor.resetState()
+    }
+    void tree_update(int n, std::vector<int>& out) {
+        const Inner& in = inner_[n];
+        if (in.kind == 1) { tree_update(in.a, out); tree_update(in.b, out); }
+        else if (in.kind == 3) tree_update(in.b, out);
+        else out.push_back(in.first);
+    }
+    void tree_setup(int n, std::vector<std::vector<int>>& per_stream) {
+        const Inner& in = inner_[n];
+        if (in.kind == 1) { tree_setup(in.a, per_stream); tree_setup(in.b, per_stream); }
+        else if (in.kind == 2) tree_setup(in.a, per_stream);
+        else if (in.kind == 3) { tree_setup(in.b, per_stream); tree_setup(in.a, per_stream); }
+        else per_stream[h_.stream_pos(rows_[in.first].stream)].push_back(in.first);
+    }
+    void runtime_tables(int root) {
+        Plan& p = h_.plan;
+        auto put = [](int32_t* n, int32_t* arr, const std::vector<int>& v) {
+            *n = (int32_t)v.size();
+            for (size_t i = 0; i < v.size(); ++i) arr[i] = v[i];
+        };
+        std::vector<int> v;
+        tree_init(root, v);
+        put(&p.n_init, p.init_seq, v);
+        v.clear();
+        tree_reset(root, v);
+        put(&p.n_reset, p.reset_seq, v);
+        v.clear();
+        tree_update(root, v);
+        put(&p.n_update, p.update_seq, v);
+        put(&p.n_expire, p.expire_seq, h_.expire_order);
+        put(&p.n_startup, p.startup_seq, startup_);
+        std::vector<std::vector<int>> per(h_.streams.size());
+        tree_setup(root, per);
+        for (size_t i = 0; i < per.size(); ++i) {
+            RecvRow& r = p.recv[i];
+            std::memset(&r, 0, sizeof r);
+            r.n = (int32_t)per[i].size();
+            r.multi = r.n > 1;
+            for (int j = 0; j < r.n; ++j) {
+                r.procs[j] = per[i][j];
+                r.order[j] = r.multi ? r.n - 1 - j : j;
+            }
+            // querySelector: multi -> last setNext's own post; single -> next's thisLastProcessor
+            int probe = r.n == 0 ? -1 : (r.multi ? per[i][r.n - 1] : rows_[per[i][0]].last);
+            r.selector = probe >= 0 && rows_[probe].selector_after;
+        }
+    }
 
     int col_id(const std::string& name, uint8_t kind) {
         for (size_t i = 0; i < h_.cols.size(); ++i)
@@ -370,8 +448,10 @@ class QC {
                 pr.len = (int)h_.code.size() - pr.start;
                 rows_[sid].filter = pr;
                 pre_list.push_back(sid);
+                if (kind == PK_ABSENT) startup_.push_back(sid);
                 Sub s;
                 s.first = s.last = sid;
+                s.node = mk_inner(0, -1, -1, sid);
                 return s;
             }
             case StateKind::NEXT: {
@@ -381,6 +461,7 @@ class QC {
                 Sub s;
                 s.first = a.first;
                 s.last = b.last;
+                s.node = mk_inner(1, a.node, b.node, a.first);
                 return s;
             }
             case StateKind::EVERY: {
@@ -389,6 +470,7 @@ class QC {
                 set_next_every(in.last, in.first);
                 for (int g : group) rows_[g].within_every = in.first;
                 pre_list.insert(pre_list.end(), group.begin(), group.end());
+                in.node = mk_inner(2, in.node, -1, in.first);
                 return in;
             }
             case StateKind::LOGICAL: {
@@ -402,6 +484,7 @@ class QC {
                 Sub s;
                 s.first = s1.first;
                 s.last = s2.last;
+                s.node = mk_inner(3, s1.node, s2.node, s1.first);
                 return s;
             }
             case StateKind::COUNT: {
@@ -509,12 +592,12 @@ class QC {
             static const uint8_t mir[] = {CMP_EQ, CMP_NE, CMP_LT, CMP_LE, CMP_GT, CMP_GE};
             op = mir[op];
         }
-        if (a.chain != 0 && a.chain != -1) return f;
-        if (!b.is_const && b.chain != 0 && b.chain != -1) return f;
+        if (a.chain < -128 || a.chain > 127 || b.chain < -128 || b.chain > 127) return f;
         f.op = op;
         f.t = t;
         f.ka = a.k;
         f.sa = (int8_t)a.slot;
+        f.ia = (int8_t)a.chain;
         f.ca = a.col;
         if (b.is_const) {
             f.kind = FP_CONST;
@@ -524,6 +607,7 @@ class QC {
             f.kind = FP_SLOT;
             f.kb = b.k;
             f.sb = (int8_t)b.slot;
+            f.ib = (int8_t)b.chain;
             f.cb = b.col;
         }
         return f;

@@ -122,6 +122,10 @@ struct QueryRt {
         int64_t n = 0, cap = 0;
     } carry[2];
     int cur = 0;
+    // generic NFA: per-key partial-match arenas (persist across batches)
+    DevBuf arena;
+    int64_t arena_keys = 0;
+    nfa::Layout L{};
     // outputs
     DevBuf o_ts, o_key, o_vals, o_nulls, o_emit, o_first, counters, flags;
     int64_t out_n = 0, out_cap = 0;
@@ -149,6 +153,7 @@ struct sdg_engine {
     hipEvent_t ev[12] = {};
     std::vector<PushChunk> pending;
     int64_t capacity = 1 << 24;
+    int32_t max_partials = 64;
     int64_t pending_n = 0;
     sdg_stats stats{};
     std::vector<std::vector<int32_t>> stream_types;
@@ -212,9 +217,6 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     HostQuery& h = q.hq;
     Plan& P = h.plan;
     hipStream_t st = e->stream;
-    if (!P.chain)
-        throw CompileError(SDG_ERR_UNSUPPORTED, "query '" + h.name + "': only the chain fast path is on device in this build (" +
-                                                    h.chain_reason + ")");
     const int nc = P.n_cols;
     // ---- 1. batch view -------------------------------------------------------------------------------
     std::vector<const PushChunk*> parts;
@@ -357,6 +359,92 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         HIPCHECK(hipMemsetAsync((void*)v_segend, 0, (size_t)K * 4, st));
     }
     HIPCHECK(hipEventRecord(e->ev[1], st));
+    if (!P.chain) {
+        NfaArgs a;
+        std::memset(&a, 0, sizeof a);
+        a.plan = q.d_plan.as<Plan>();
+        a.code = q.d_code.as<Instr>();
+        a.consts = q.d_consts.as<int64_t>();
+        a.n = nrows;
+        a.ts = v_ts;
+        a.qstream = multi_stream ? v_qs : nullptr;
+        a.seg_start = partitioned ? v_seg : nullptr;
+        a.seg_end = partitioned ? v_segend : nullptr;
+        a.K = partitioned ? (int32_t)K : 1;
+        a.orig = v_orig;
+        for (int k = 0; k < nc; ++k) { a.cols[k] = v_cols[k]; a.nulls[k] = v_nulls[k]; }
+        a.seq_base = q.seq;
+        // arenas: grow to K keys keeping the existing keys' state, new keys zeroed (= not yet initialised)
+        const int64_t kb = q.L.bytes;
+        if (q.arena_keys < a.K) {
+            int64_t nk = std::max<int64_t>(a.K, q.arena_keys + q.arena_keys / 2);
+            DevBuf nb;
+            nb.ensure((size_t)(nk * kb));
+            HIPCHECK(hipMemsetAsync(nb.p, 0, (size_t)(nk * kb), st));
+            if (q.arena_keys) HIPCHECK(hipMemcpyAsync(nb.p, q.arena.p, (size_t)(q.arena_keys * kb), hipMemcpyDeviceToDevice, st));
+            HIPCHECK(hipStreamSynchronize(st));
+            std::swap(nb.p, q.arena.p);
+            std::swap(nb.cap, q.arena.cap);
+            q.arena_keys = nk;
+        }
+        a.arena = q.arena.as<uint8_t>();
+        a.L = q.L;
+        int64_t cap = 2 * nrows + 4096;
+        q.out_cap = cap;
+        unsigned long long* counters = (unsigned long long*)q.counters.ensure(16);
+        int* flags = (int*)q.flags.ensure(16);
+        HIPCHECK(hipMemsetAsync(counters, 0, 16, st));
+        HIPCHECK(hipMemsetAsync(flags, 0, 16, st));
+        a.out_cap = cap;
+        a.out_count = counters;
+        a.flags = flags;
+        a.out_ts = (int64_t*)q.o_ts.ensure(cap * 8);
+        a.out_key = (uint32_t*)q.o_key.ensure(cap * 4);
+        a.out_vals = (int64_t*)q.o_vals.ensure((size_t)std::max(P.n_out, 1) * cap * 8);
+        a.out_nulls = (uint32_t*)q.o_nulls.ensure(cap * 4);
+        a.out_emit_seq = (int64_t*)q.o_emit.ensure(cap * 8);
+        a.out_sub = (int64_t*)q.o_first.ensure(cap * 8);
+        HIPCHECK(hipEventRecord(e->ev[8], st));
+        nfa_run(a, st);
+        e->stats.match_launches += nrows > 0;
+        HIPCHECK(hipEventRecord(e->ev[2], st));
+        unsigned long long hc[2];
+        int hf[4];
+        HIPCHECK(hipMemcpyAsync(hc, counters, 16, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(hf, flags, 16, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        float ms_kg = 0, ms_m = 0, t;
+        HIPCHECK(hipEventElapsedTime(&ms_kg, e->ev[0], e->ev[1]));
+        HIPCHECK(hipEventElapsedTime(&ms_m, e->ev[1], e->ev[2]));
+        e->stats.ms_keygroup += ms_kg;
+        e->stats.ms_match += ms_m;
+        if (partitioned && nrows > 0) {
+            HIPCHECK(hipEventElapsedTime(&t, e->ev[4], e->ev[5]));
+            e->stats.ms_kg_hist += t;
+            HIPCHECK(hipEventElapsedTime(&t, e->ev[6], e->ev[7]));
+            e->stats.ms_kg_prefix += t;
+            HIPCHECK(hipEventElapsedTime(&t, e->ev[5], e->ev[6]));
+            e->stats.ms_kg_scatter += t;
+        }
+        HIPCHECK(hipEventElapsedTime(&t, e->ev[8], e->ev[2]));
+        e->stats.ms_nfa += t;
+        e->stats.events += nrows;
+        if (hf[0]) {
+            e->stats.overflow += 1;
+            throw CompileError(SDG_ERR_CAPACITY, "match buffer overflow in query '" + h.name + "'");
+        }
+        if (hf[2]) {
+            e->stats.overflow += 1;
+            throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': a partition key exceeded max_partials (" +
+                                                     std::to_string(q.L.ns) + " live partial matches); raise sdg_opts.max_partials");
+        }
+        q.out_n = (int64_t)hc[0];
+        q.polled = false;
+        e->stats.matches += q.out_n;
+        e->stats.path = 1;
+        q.seq += nrows;
+        return;
+    }
     // ---- 3. chain matcher -------------------------------------------------------------------------------
     QueryRt::Carry& cin = q.carry[q.cur];
     QueryRt::Carry& cout = q.carry[q.cur ^ 1];
@@ -464,6 +552,7 @@ int do_flush(sdg_engine* e) {
     e->stats.overflow = 0;
     e->stats.ms_kg_hist = e->stats.ms_kg_prefix = e->stats.ms_kg_scatter = 0;
     e->stats.ms_chain_carry = e->stats.ms_chain_match = 0;
+    e->stats.ms_nfa = 0;
     for (auto& q : e->qs) flush_query(e, *q);
     e->stats.ms_total = e->stats.ms_keygroup + e->stats.ms_match;
     e->pending.clear();
@@ -505,11 +594,16 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             if (opts->batch_capacity > 0) e->capacity = opts->batch_capacity;
             e->compile_only = (opts->flags & SDG_COMPILE_ONLY) != 0;
         }
+        if (opts && opts->max_partials > 0) {
+            if (opts->max_partials > 4096) throw CompileError(SDG_ERR_ARG, "max_partials must be <= 4096");
+            e->max_partials = opts->max_partials;
+        }
         auto hqs = compile_app(e->app, e->strings);
         for (auto& h : hqs)
-            if (!h.plan.chain)
-                throw CompileError(SDG_ERR_UNSUPPORTED, "query '" + h.name + "' (" + h.chain_reason +
-                                                            ") needs the generic keyed-NFA kernel, not in this build");
+            for (int i = 0; i < h.plan.n_states; ++i)
+                if (h.plan.st[i].kind == PK_ABSENT)
+                    throw CompileError(SDG_ERR_UNSUPPORTED, "query '" + h.name + "': absent states (not ... for) need "
+                                                                "the timer path, not in this build");
         if (!e->compile_only) {
             int ndev = 0;
             if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
@@ -525,6 +619,7 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
         for (auto& h : hqs) {
             auto q = std::make_unique<QueryRt>();
             q->hq = std::move(h);
+            q->L = nfa::make_layout(q->hq.plan.n_states, std::max(q->hq.plan.n_cols, 1), e->max_partials);
             for (size_t i = 0; i < q->hq.key_kind.size(); ++i)
                 if (q->hq.key_attr[i] >= 0 && q->hq.key_kind[i] != VK_STR) q->string_keys = false;
             if (!e->compile_only) upload_plan(e.get(), *q);

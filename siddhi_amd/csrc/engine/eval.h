@@ -6,22 +6,27 @@
 //   arithmetic          executor/math/** (int/long wrap, /,% by zero -> null, double % = fmod)
 // The program is wave-uniform (one query per launch), so instruction fetch is scalar and the op switch never
 // diverges; the evaluation stack lives in LDS, one column of STACK entries per lane (conflict-free stride).
-// Build with -ffp-contract=off: a fused multiply-add would change float/double results vs the JVM.
+// Build with -ffp-contract=off (a fused multiply-add would change float/double results vs the JVM) and
+// -fhip-fp32-correctly-rounded-divide-sqrt: then + - * / are the IEEE round-to-nearest operations Java uses.
+// The functions are host+device so the test-only host harness (tests/native) runs the same code.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
 
 #include "plan.h"
 
+#define SDG_FN __host__ __device__ __forceinline__
+
 namespace sdg {
 
-__device__ __forceinline__ float bits_f32(int64_t v) { return __int_as_float((int)(uint32_t)v); }
-__device__ __forceinline__ double bits_f64(int64_t v) { return __longlong_as_double(v); }
-__device__ __forceinline__ int64_t f32_bits(float f) { return (int64_t)(uint32_t)__float_as_int(f); }
-__device__ __forceinline__ int64_t f64_bits(double d) { return __double_as_longlong(d); }
+SDG_FN float bits_f32(int64_t v) { return __builtin_bit_cast(float, (uint32_t)v); }
+SDG_FN double bits_f64(int64_t v) { return __builtin_bit_cast(double, v); }
+SDG_FN int64_t f32_bits(float f) { return (int64_t)__builtin_bit_cast(uint32_t, f); }
+SDG_FN int64_t f64_bits(double d) { return __builtin_bit_cast(int64_t, d); }
 
 // typed column load -> 64-bit payload (same encoding as sdg_out)
-__device__ __forceinline__ int64_t load_col(const void* col, uint8_t kind, int64_t row) {
+SDG_FN int64_t load_col(const void* col, uint8_t kind, int64_t row) {
     switch (kind) {
         case VK_I32: return (int64_t)((const int32_t*)col)[row];
         case VK_I64: return ((const int64_t*)col)[row];
@@ -32,7 +37,7 @@ __device__ __forceinline__ int64_t load_col(const void* col, uint8_t kind, int64
     }
 }
 
-__device__ __forceinline__ int64_t cvt(int64_t v, uint8_t from, uint8_t to) {
+SDG_FN int64_t cvt(int64_t v, uint8_t from, uint8_t to) {
     if (from == to) return v;
     switch (to) {
         case VK_I64: return (int64_t)(int32_t)v;  // only int -> long widens
@@ -46,7 +51,7 @@ __device__ __forceinline__ int64_t cvt(int64_t v, uint8_t from, uint8_t to) {
 }
 
 template <class T>
-__device__ __forceinline__ bool cmpT(uint8_t op, T a, T b) {
+SDG_FN bool cmpT(uint8_t op, T a, T b) {
     switch (op) {
         case CMP_EQ: return a == b;
         case CMP_NE: return a != b;
@@ -57,7 +62,7 @@ __device__ __forceinline__ bool cmpT(uint8_t op, T a, T b) {
     }
 }
 
-__device__ __forceinline__ bool cmp(uint8_t op, uint8_t k, int64_t a, int64_t b) {
+SDG_FN bool cmp(uint8_t op, uint8_t k, int64_t a, int64_t b) {
     switch (k) {
         case VK_I32: return cmpT<int32_t>(op, (int32_t)a, (int32_t)b);
         case VK_I64: return cmpT<int64_t>(op, a, b);
@@ -69,7 +74,7 @@ __device__ __forceinline__ bool cmp(uint8_t op, uint8_t k, int64_t a, int64_t b)
 }
 
 // returns false (and *null = true) when Java would produce null
-__device__ __forceinline__ int64_t arith(uint8_t op, uint8_t k, int64_t a, int64_t b, bool* null) {
+SDG_FN int64_t arith(uint8_t op, uint8_t k, int64_t a, int64_t b, bool* null) {
     *null = false;
     switch (k) {
         case VK_I32: {
@@ -108,12 +113,12 @@ __device__ __forceinline__ int64_t arith(uint8_t op, uint8_t k, int64_t a, int64
         case VK_F32: {
             float x = bits_f32(a), y = bits_f32(b);
             switch (op) {
-                case AR_ADD: return f32_bits(__fadd_rn(x, y));
-                case AR_SUB: return f32_bits(__fsub_rn(x, y));
-                case AR_MUL: return f32_bits(__fmul_rn(x, y));
+                case AR_ADD: return f32_bits(x + y);
+                case AR_SUB: return f32_bits(x - y);
+                case AR_MUL: return f32_bits(x * y);
                 case AR_DIV:
                     if (y == 0.0f) { *null = true; return 0; }
-                    return f32_bits(__fdiv_rn(x, y));
+                    return f32_bits(x / y);
                 default:
                     if (y == 0.0f) { *null = true; return 0; }
                     return f32_bits(fmodf(x, y));
@@ -122,12 +127,12 @@ __device__ __forceinline__ int64_t arith(uint8_t op, uint8_t k, int64_t a, int64
         default: {
             double x = bits_f64(a), y = bits_f64(b);
             switch (op) {
-                case AR_ADD: return f64_bits(__dadd_rn(x, y));
-                case AR_SUB: return f64_bits(__dsub_rn(x, y));
-                case AR_MUL: return f64_bits(__dmul_rn(x, y));
+                case AR_ADD: return f64_bits(x + y);
+                case AR_SUB: return f64_bits(x - y);
+                case AR_MUL: return f64_bits(x * y);
                 case AR_DIV:
                     if (y == 0.0) { *null = true; return 0; }
-                    return f64_bits(__ddiv_rn(x, y));
+                    return f64_bits(x / y);
                 default:
                     if (y == 0.0) { *null = true; return 0; }
                     return f64_bits(fmod(x, y));
@@ -137,11 +142,11 @@ __device__ __forceinline__ int64_t arith(uint8_t op, uint8_t k, int64_t a, int64
 }
 
 // Acc must provide:
-//   __device__ void load(int slot, int col, int chain, uint8_t kind, int64_t* v, bool* null);
-//   __device__ bool slot_empty(int slot, int chain);
+//   void load(int slot, int col, int chain, uint8_t kind, int64_t* v, bool* null);
+//   bool slot_empty(int slot, int chain);
 // stk: this lane's LDS stack base, entries at stk[i * stride]
 template <class Acc>
-__device__ __forceinline__ void run(const Instr* __restrict__ code, Prog p, const int64_t* __restrict__ consts,
+SDG_FN void run(const Instr* __restrict__ code, Prog p, const int64_t* __restrict__ consts,
                                     Acc& acc, int64_t* stk, int stride, int64_t* out, bool* out_null) {
     uint32_t nulls = 0;
     int sp = 0;
@@ -231,16 +236,16 @@ __device__ __forceinline__ void run(const Instr* __restrict__ code, Prog p, cons
 
 // FastPred evaluation (compile-time recognised `a OP b`): identical results to the bytecode
 template <class Acc>
-__device__ __forceinline__ bool fast_pass(const FastPred& f, Acc& acc) {
+SDG_FN bool fast_pass(const FastPred& f, Acc& acc) {
     int64_t a, b;
     bool na, nb;
-    acc.load(f.sa, f.ca, -1, f.ka, &a, &na);
+    acc.load(f.sa, f.ca, f.ia, f.ka, &a, &na);
     if (na) return false;
     a = cvt(a, f.ka, f.t);
     if (f.kind == FP_CONST) {
         b = f.konst;
     } else {
-        acc.load(f.sb, f.cb, -1, f.kb, &b, &nb);
+        acc.load(f.sb, f.cb, f.ib, f.kb, &b, &nb);
         if (nb) return false;
         b = cvt(b, f.kb, f.t);
     }
@@ -249,7 +254,7 @@ __device__ __forceinline__ bool fast_pass(const FastPred& f, Acc& acc) {
 
 // a filter passes iff its result is non-null and true (FilterProcessor.java:48-60)
 template <class Acc>
-__device__ __forceinline__ bool pass(const Instr* code, Prog p, const int64_t* consts, Acc& acc, int64_t* stk,
+SDG_FN bool pass(const Instr* code, Prog p, const int64_t* consts, Acc& acc, int64_t* stk,
                                      int stride) {
     if (p.len == 0) return true;
     int64_t v;

@@ -49,9 +49,9 @@ struct FastPred {
     uint8_t op = 0;      // CmpOp, oriented as a OP b
     uint8_t t = 0;       // comparison kind after promotion
     uint8_t ka = 0, kb = 0;
-    int8_t sa = 0, sb = 0;
-    uint8_t pad = 0;
-    int32_t ca = 0, cb = 0;
+    int8_t sa = 0, sb = 0;   // state slots
+    int8_t ia = -1, ib = -1; // chain indexes (count states: e1[0], e1[last] ...)
+    int32_t ca = 0, cb = 0;  // columns
     int64_t konst = 0;   // FP_CONST: b already converted to kind t
 };
 
@@ -82,6 +82,17 @@ struct StateRow {
     uint8_t pad[7];
 };
 
+// per query stream: the receiver built by StateInputStreamParser (:91-110) and wired by the inner runtimes'
+// setup() (query/input/stream/state/runtime/*InnerStateRuntime.java)
+struct RecvRow {
+    int32_t n;                   // processors subscribed to this stream (setup order)
+    int32_t procs[MAX_STATES];   // nextProcessors / stateProcessorsForStream
+    int32_t order[MAX_STATES];   // eventSequence (reversed for Pattern/SequenceMultiProcessStreamReceiver)
+    uint8_t multi;
+    uint8_t selector;            // querySelector != null
+    uint8_t pad[2];
+};
+
 struct Plan {
     int32_t n_states = 0;
     int32_t seq = 0;               // SEQUENCE (1) / PATTERN (0)
@@ -99,6 +110,12 @@ struct Plan {
     int32_t streams[MAX_STATES];
     StateRow st[MAX_STATES];
     FastPred fast[MAX_STATES];     // per state filter (FP_NONE: use the bytecode)
+    RecvRow recv[MAX_STATES];      // indexed by query-stream position
+    int32_t n_expire, expire_seq[MAX_STATES];   // allStateProcessors (expireEvents order)
+    int32_t n_init, init_seq[MAX_STATES];       // innerStateRuntime.init()
+    int32_t n_reset, reset_seq[MAX_STATES];     // innerStateRuntime.reset()
+    int32_t n_update, update_seq[MAX_STATES];   // innerStateRuntime.update()
+    int32_t n_startup, startup_seq[MAX_STATES]; // startupPreStateProcessors (absent partitionCreated)
     // expire order (allStateProcessors), setup order per stream etc. live on the host plan
     int32_t n_code = 0, n_consts = 0;
 };

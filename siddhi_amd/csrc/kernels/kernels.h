@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../engine/nfa.h"
 #include "../engine/plan.h"
 
 namespace sdg {
@@ -91,5 +92,34 @@ struct ChainArgs {
 };
 void chain_match(const ChainArgs& a, hipStream_t stream);
 void chain_carry(const ChainArgs& a, hipStream_t stream);
+
+// ---- generic keyed NFA (nfa.h): one lane per partition key walks that key's events in order --------------
+struct NfaArgs {
+    const Plan* plan;
+    const Instr* code;
+    const int64_t* consts;
+    int64_t n;
+    const int64_t* ts;                // sorted view
+    const uint8_t* qstream;           // nullptr: single stream 0
+    const uint32_t* seg_start;        // [K] (nullptr: unpartitioned, K == 1, one segment [0, n))
+    const uint32_t* seg_end;
+    int32_t K;
+    const uint32_t* orig;             // sorted -> original row (nullptr: identity)
+    const void* cols[MAX_COLS];
+    const uint8_t* nulls[MAX_COLS];
+    int64_t seq_base;
+    uint8_t* arena;                   // [K][L.bytes], zero-initialised on allocation, persists across batches
+    nfa::Layout L;
+    int64_t out_cap;
+    unsigned long long* out_count;
+    int64_t* out_ts;
+    uint32_t* out_key;
+    int64_t* out_vals;                // [n_out][out_cap]
+    uint32_t* out_nulls;
+    int64_t* out_emit_seq;            // sequence number of the event whose processing emitted the match
+    int64_t* out_sub;                 // emission ordinal within that event
+    int* flags;                       // [0] output overflow, [2] arena overflow (some key ran out of partial slots)
+};
+void nfa_run(const NfaArgs& a, hipStream_t stream);
 
 }  // namespace sdg

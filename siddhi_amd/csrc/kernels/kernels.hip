@@ -416,6 +416,42 @@ __global__ __launch_bounds__(256) void chain_carry_k(ChainArgs a) {
     }
 }
 
+// one lane per key: the key's arena is private to the lane, so the state machine runs without atomics; only
+// the output slot reservation is shared
+__global__ __launch_bounds__(256) void nfa_k(NfaArgs a) {
+    __shared__ int64_t stack_mem[STACK * 256];
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= a.K) return;
+    int64_t b = 0, e = a.n;
+    if (a.seg_start) {
+        b = a.seg_start[k];
+        e = a.seg_end[k];
+    }
+    if (b >= e) return;  // initPartition happens at a key's first event
+    const Plan* P = a.plan;
+    nfa::Ctx c;
+    c.P = P;
+    c.code = a.code;
+    c.consts = a.consts;
+    c.L = a.L;
+    c.base = a.arena + k * a.L.bytes;
+    c.stk = stack_mem + threadIdx.x;
+    c.stride = 256;
+    c.emit_ts = a.out_ts;
+    c.emit_vals = a.out_vals;
+    c.emit_nulls = a.out_nulls;
+    c.emit_seq = a.out_emit_seq;
+    c.emit_sub = a.out_sub;
+    c.emit_key = a.out_key;
+    c.emit_count = a.out_count;
+    c.emit_cap = a.out_cap;
+    c.flags = &a.flags[0];
+    c.key = (uint32_t)k;
+    nfa::KeyEvents ev{a.ts, a.qstream, a.orig, a.cols, a.nulls, b, e, a.seq_base};
+    nfa::run_key(c, ev);
+    if (c.ovf()) atomicOr(&a.flags[2], 1);
+}
+
 }  // namespace
 
 static int64_t rx_ntiles(int64_t n) { return n <= 0 ? 1 : (n + RX_TILE - 1) / RX_TILE; }
@@ -507,6 +543,11 @@ void chain_match(const ChainArgs& a, hipStream_t stream) {
 void chain_carry(const ChainArgs& a, hipStream_t stream) {
     if (a.cin_n <= 0) return;
     hipLaunchKernelGGL(chain_carry_k, dim3((unsigned)((a.cin_n + 255) / 256)), dim3(256), 0, stream, a);
+}
+
+void nfa_run(const NfaArgs& a, hipStream_t stream) {
+    if (a.K <= 0 || a.n <= 0) return;
+    hipLaunchKernelGGL(nfa_k, dim3((unsigned)((a.K + 255) / 256)), dim3(256), 0, stream, a);
 }
 
 }  // namespace sdg

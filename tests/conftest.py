@@ -22,6 +22,15 @@ def oracle_built():
     return so
 
 
+@pytest.fixture(scope="session")
+def emu_built():
+    so = os.path.join(REPO, "tests", "native", "_build", "libnfa_emu.so")
+    if not os.path.exists(so):
+        import subprocess
+        subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "tests", "native")])
+    return so
+
+
 def pytest_sessionstart(session):
     # torch ships its own HIP runtime (ROCm 7.0) beside the engine's /opt/rocm one: when a GPU session uses
     # both (device-resident inputs from torch tensors), torch's runtime must initialise first.

@@ -1,0 +1,75 @@
+"""Seeded synthetic traces for the pattern shapes of SURVEY.md 8 (C1-C3 and the generic-NFA constructs:
+sequences, count quantifiers, logical and/or, non-every and >= 3-state chains, within), run through any adapter
+with send/flush/outputs (oracle, host NFA build, GPU engine)."""
+import numpy as np
+
+DEFS = ("define stream S (id long, key string, price double, volume int); "
+        "define stream T (id long, key string, price double, volume int); ")
+
+
+def part(q):
+    return "@app:playback " + DEFS + "partition with (key of S, key of T) begin " + q + " end;"
+
+
+def flat(q):
+    return "@app:playback " + DEFS + q
+
+
+APPS = {
+    "c3_sequence": part("@info(name='q') from every e1=S[price>20], e2=S[price>e1.price]<2:5>, "
+                        "e3=S[price<e2[last].price] select e1.id as a, e2[0].id as b, e2[last].id as c, e3.id as d "
+                        "insert into O;"),
+    "c3_sequence_min1": part("@info(name='q') from every e1=S[price>20], e2=S[price>e1.price]<1:5>, "
+                             "e3=S[price<e2[last].price] select e1.id as a, e2[0].id as b, e2[last].id as c, "
+                             "e3.id as d insert into O;"),
+    "three_state_within": part("@info(name='q') from every e1=S[price>30] -> e2=S[price>e1.price] -> "
+                               "e3=T[price<e2.price] within 40 milliseconds "
+                               "select e1.id as a, e2.id as b, e3.id as c insert into O;"),
+    "non_every": flat("@info(name='q') from e1=S[price>50] -> e2=T[price>e1.price] "
+                      "select e1.id as a, e2.id as b insert into O;"),
+    "every_group": part("@info(name='q') from every (e1=S[price>40] -> e2=T[price>e1.price]) -> e3=S[volume>50] "
+                        "select e1.id as a, e2.id as b, e3.id as c insert into O;"),
+    "count_pattern": part("@info(name='q') from every e1=S[price>20]<2:4> -> e2=T[price>e1[0].price] "
+                          "select e1[0].id as a, e1[1].id as b, e1[last].id as c, e2.id as d insert into O;"),
+    "count_zero_min": part("@info(name='q') from e1=S[price>60] -> e2=T[price>e1.price]<0:3> -> e3=S[volume<20] "
+                           "select e1.id as a, e2[0].id as b, e3.id as c insert into O;"),
+    "logical_and": part("@info(name='q') from every (e1=S[price>30] and e2=T[price>40]) -> e3=S[price>e1.price] "
+                        "select e1.id as a, e2.id as b, e3.id as c insert into O;"),
+    "logical_or": part("@info(name='q') from every e1=S[price>70] -> (e2=S[price>e1.price] or e3=T[volume>90]) "
+                       "select e1.id as a, e2.id as b, e3.id as c insert into O;"),
+    "sequence_plus": part("@info(name='q') from every e1=S[price>20], e2=T[price>e1.price]+, e3=S[price>e2[0].price] "
+                          "select e1.id as a, e2[0].id as b, e3.id as c insert into O;"),
+    "sequence_star_within": part("@info(name='q') from every e1=S[price>20], e2=S[volume>30]*, e3=T[price>e1.price] "
+                                 "within 30 milliseconds select e1.id as a, e2[last].id as b, e3.id as c "
+                                 "insert into O;"),
+    "arith_nulls": part("@info(name='q') from every e1=S[price>20] -> e2=T[(price - e1.price) / volume > 0.5 "
+                        "or e1.volume % volume == 0] select e1.id as a, e2.id as b, e1.price * e2.volume as c "
+                        "insert into O;"),
+}
+
+
+def trace(n, keys=5, seed=0, two_streams=True, null_rate=0.0):
+    """list of (stream, ts, [id, key, price, volume]) with non-decreasing ts (some equal)"""
+    rng = np.random.default_rng(seed)
+    ts = 1000 + np.cumsum(rng.integers(0, 4, size=n))
+    out = []
+    for i in range(n):
+        s = "T" if two_streams and rng.random() < 0.4 else "S"
+        price = float(np.round(rng.uniform(0, 100), 1))
+        vol = int(rng.integers(0, 100))
+        row = [i, "k%d" % rng.integers(0, keys), price, vol]
+        if null_rate and rng.random() < null_rate:
+            row[2 + int(rng.integers(0, 2))] = None
+        out.append((s, int(ts[i]), row))
+    return out
+
+
+def run(adapter, tr, batches=1):
+    bounds = np.linspace(0, len(tr), batches + 1).astype(int)
+    for b in range(batches):
+        for s, ts, row in tr[bounds[b]:bounds[b + 1]]:
+            adapter.send(s, ts, row)
+        if hasattr(adapter, "flush"):
+            adapter.flush()
+    return [(o["name"], o["ts"], tuple(o["values"])) for o in adapter.outputs()
+            if o["kind"] == "query" and not o["expired"]]

@@ -41,9 +41,16 @@ def test_errors_map_to_reference_exceptions(app, exc):
         compile_only(app)
 
 
-def test_sequence_is_rejected_until_generic_kernel():
+def test_sequence_lowers_to_generic_nfa():
+    rt = compile_only(w.C3_APP)
+    assert rt.query_paths() == [1]
+
+
+def test_absent_is_rejected_until_timer_path():
+    app = ("define stream S1 (symbol string, price float); define stream S2 (symbol string, price float); "
+           "from e1=S1[price>10] -> not S2[price>e1.price] for 1 sec select e1.symbol as s insert into O;")
     with pytest.raises(sa.OperationNotSupportedException):
-        compile_only(w.C3_APP)
+        compile_only(app)
 
 
 def test_push_needs_a_device():

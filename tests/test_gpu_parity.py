@@ -125,3 +125,48 @@ def test_c2_device_resident_input_properties():
         idx = by_key[k]
         after = idx[(idx > e1[i]) & (idx < e2[i])]
         assert not np.any(price[after] > price[e1[i]]), "e2 must be the first qualifying event"
+
+
+# ---- generic keyed-NFA kernel: every construct of tests/synth.py vs the oracle ----------------------------
+import zlib  # noqa: E402
+
+import synth  # noqa: E402
+from product_rt import ProductAdapter  # noqa: E402
+
+
+@pytest.mark.parametrize("name", sorted(synth.APPS))
+@pytest.mark.parametrize("batches", [1, 4])
+def test_generic_nfa_synthetic_on_gpu(name, batches, oracle_built):
+    app = synth.APPS[name]
+    tr = synth.trace(1500, keys=4, seed=zlib.crc32(name.encode()) % 1000,
+                     null_rate=0.05 if name == "arith_nulls" else 0.0)
+    o = Oracle(app)
+    try:
+        ref = synth.run(o, tr)
+    finally:
+        o.close()
+    p = ProductAdapter(app)
+    try:
+        assert p.rt.query_paths() == [1]
+        got = synth.run(p, tr, batches)
+    finally:
+        p.close()
+    assert got == ref
+
+
+def test_generic_nfa_many_keys_on_gpu(oracle_built):
+    """C3 (<1:5> form) over 3000 keys: thousands of lanes, arenas grown across batches as keys appear"""
+    app = synth.APPS["c3_sequence_min1"]
+    tr = synth.trace(40_000, keys=3000, seed=11, two_streams=False)
+    o = Oracle(app)
+    try:
+        ref = synth.run(o, tr)
+    finally:
+        o.close()
+    p = ProductAdapter(app)
+    try:
+        got = synth.run(p, tr, 3)
+    finally:
+        p.close()
+    assert len(ref) > 100
+    assert got == ref
