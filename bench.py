@@ -9,7 +9,8 @@ Workload (the 1-GPU config the metric is quoted on):
 A step = one flush of one 100M-event batch, inputs already resident in HBM (sdg_push_device); consecutive steps
 are consecutive batches of one stream (timestamps continue), so partials crossing a batch boundary are carried.
 
-Multi-GPU (torchrun, one process per GPU): key-hash sharding, rank r owns keys k*N + r; no data-path
+Multi-GPU (torchrun, one process per GPU): key-hash sharding (siddhi_amd/shard.py), each rank generates the events
+of the keys it owns; no data-path
 collective — only the batch-boundary all-gather of per-rank match counts (RCCL over xGMI). scaling = weak.
 
 Roofline: algorithmic bytes per step B = N_in*28 + N_match*28 (ts 8 + key 4 + price 8 + id 8 in,
@@ -102,7 +103,14 @@ def main():
 
     n, keys = args.events, args.keys
     cols = gen_shard(n, keys, rank, world)
-    syms = ["S%07d" % (k * world + rank) for k in range(keys)]
+    from siddhi_amd import shard
+    syms = []  # this rank's keys: the first `keys` global key names that hash to this rank (shard.py)
+    g = 0
+    while len(syms) < keys:
+        name = "S%07d" % g
+        if world == 1 or shard.owner(name, world) == rank:
+            syms.append(name)
+        g += 1
     rt = sa.SiddhiAppRuntime(w.C2_APP, device=local)
     sym_ids = np.array([rt.intern(s) for s in syms], dtype=np.uint32)
     dev = torch.device("cuda", local)

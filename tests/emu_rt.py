@@ -39,7 +39,7 @@ def lib():
         L.emu_query_chain.argtypes = [P, I32]
         L.emu_num_out.restype = I64
         L.emu_num_out.argtypes = [P, I32]
-        L.emu_out.argtypes = [P, I32, I64, ctypes.POINTER(I64), ctypes.POINTER(I64), ctypes.POINTER(U32)]
+        L.emu_out.argtypes = [P, I32, I64, ctypes.POINTER(I64), ctypes.POINTER(I64), ctypes.POINTER(U32), ctypes.POINTER(I64)]
         _lib = L
     return _lib
 
@@ -104,11 +104,12 @@ class EmuAdapter:
             raise EmuError(self.L.emu_error().decode())
         ts, nl = ctypes.c_int64(), ctypes.c_uint32()
         vals = (ctypes.c_int64 * 64)()
+        seq = (ctypes.c_int64 * 2)()
         for q in range(self.nq):
             name, target, types = self.meta[q]
             n = self.L.emu_num_out(self.h, q)
             for i in range(self.delivered[q], n):
-                self.L.emu_out(self.h, q, i, ctypes.byref(ts), vals, ctypes.byref(nl))
+                self.L.emu_out(self.h, q, i, ctypes.byref(ts), vals, ctypes.byref(nl), seq)
                 row = []
                 for j, t in enumerate(types):
                     v = vals[j]
@@ -129,7 +130,8 @@ class EmuAdapter:
                     else:
                         row.append(("?", v))
                 for kind, nm in (("query", name), ("stream", target)):
-                    self.records.append({"kind": kind, "name": nm, "ts": ts.value, "expired": False, "values": row})
+                    self.records.append({"kind": kind, "name": nm, "ts": ts.value, "expired": False, "values": row,
+                                         "seq": seq[0], "ordinal": seq[1]})
             self.delivered[q] = n
 
     def outputs(self):

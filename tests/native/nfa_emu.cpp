@@ -257,9 +257,10 @@ int emu_query_nout(void* h, int q) { return (int)((Emu*)h)->qs[q]->hq.out_types.
 int emu_query_out_type(void* h, int q, int j) { return ((Emu*)h)->qs[q]->hq.out_types[j]; }
 int emu_query_chain(void* h, int q) { return ((Emu*)h)->qs[q]->hq.plan.chain; }
 int64_t emu_num_out(void* h, int q) { return (int64_t)((Emu*)h)->qs[q]->outs.size(); }
-void emu_out(void* h, int q, int64_t i, int64_t* ts, int64_t* vals, uint32_t* nulls) {
+void emu_out(void* h, int q, int64_t i, int64_t* ts, int64_t* vals, uint32_t* nulls, int64_t* seq) {
     const Out& o = ((Emu*)h)->qs[q]->outs[i];
     *ts = o.ts;
+    if (seq) { seq[0] = o.seq; seq[1] = o.sub; }
     for (size_t j = 0; j < o.vals.size(); ++j) vals[j] = o.vals[j];
     *nulls = o.nulls;
 }

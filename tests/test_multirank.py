@@ -1,0 +1,86 @@
+"""N>1 path on CPU: world-size-2 gloo run of the key-hash sharding (siddhi_amd/shard.py). Each rank runs its shard
+of the trace through the generic keyed-NFA code (host build, tests/native) -- the GPU run of bench.py does the same
+with the device kernel -- then the ranks' match streams are gathered and merged in global delivery order, and the
+result must equal the oracle's single-process run of the whole trace. The batch-boundary match-count all-gather
+of bench.py is exercised too."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import synth
+from siddhi_amd import shard
+
+APPS = ["c3_sequence_min1", "logical_and", "three_state_within"]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from emu_rt import EmuAdapter
+        for name in APPS:
+            tr = synth.trace(3000, keys=40, seed=21)
+            owners = shard.route([row[1] for _, _, row in tr], world)
+            mine = [i for i in range(len(tr)) if owners[i] == rank]
+            e = EmuAdapter(synth.APPS[name], max_partials=256)
+            recs = []
+            try:
+                for b in range(3):  # three batches, partials carried across
+                    lo, hi = b * len(mine) // 3, (b + 1) * len(mine) // 3
+                    for i in mine[lo:hi]:
+                        s, ts, row = tr[i]
+                        e.send(s, ts, row)
+                    before = len(recs)
+                    e.flush()
+                    cur = [r for r in e.outputs() if r["kind"] == "query"]
+                    recs = cur
+                    cnt = torch.tensor([len(recs) - before], dtype=torch.int64)
+                    allc = [torch.empty_like(cnt) for _ in range(world)]
+                    dist.all_gather(allc, cnt)  # global output offsets of this batch
+            finally:
+                e.close()
+            # local sequence number (over the events of the query's streams) -> global position in the trace
+            streams = {"S", "T"} if "=T[" in synth.APPS[name] else {"S"}
+            mine_q = [i for i in mine if tr[i][0] in streams]
+            part = [(mine_q[r["seq"]], r["ordinal"], (r["name"], r["ts"], tuple(r["values"]))) for r in recs]
+            parts = [None] * world
+            dist.all_gather_object(parts, part)
+            if rank == 0:
+                merged = shard.merge(parts)
+                with open(os.path.join(out_dir, name + ".txt"), "w") as f:
+                    f.write(repr(merged))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_key_sharding_matches_single_process(tmp_path, oracle_built, emu_built):
+    from oracle_rt import Oracle
+    mp.spawn(_rank_main, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for name in APPS:
+        tr = synth.trace(3000, keys=40, seed=21)
+        o = Oracle(synth.APPS[name])
+        try:
+            ref = synth.run(o, tr)
+        finally:
+            o.close()
+        got = eval((tmp_path / (name + ".txt")).read_text())
+        assert len(ref) > 0
+        assert got == ref, name
+
+
+def test_route_is_balanced_and_stable():
+    keys = ["S%07d" % k for k in range(10_000)]
+    r = shard.route(keys, 8)
+    counts = [(r == i).sum() for i in range(8)]
+    assert min(counts) > 1100 and max(counts) < 1400
+    assert (shard.route(keys, 8) == r).all()
