@@ -58,6 +58,7 @@ typedef struct sdg_opts {
                                   without a GPU; push/flush then fail with SDG_ERR_DEVICE) */
 } sdg_opts;
 #define SDG_COMPILE_ONLY 1
+#define SDG_FORCE_GENERIC 2    /* run every query on the generic keyed-NFA kernel (testing: both kernels on one query) */
 
 typedef struct sdg_out {
     int64_t n;                 /* output events */

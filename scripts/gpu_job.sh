@@ -7,6 +7,7 @@ TAG=${1:-run}; shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export PYTHONUNBUFFERED=1
+export TMPDIR=/tmp
 run() {  # name timeout cmd...
     local name=$1 to=$2; shift 2
     echo "== $name: $*" | tee -a "$OUT/steps.log"
@@ -26,7 +27,7 @@ for s in "$@"; do
         testsall) run testsall 900 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -p no:cacheprovider ;;
         benchsmall) run benchsmall 300 python3 bench.py --events 10000000 --steps 3 --warmup 1 --no-cpu ;;
         bench) run bench 600 python3 bench.py ;;
-        prof) (cd /tmp && export TMPDIR=/tmp; true); run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu ;;
+        prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu ;;
         pmc) for c in "FETCH_SIZE" "WRITE_SIZE"; do run pmc_$c 300 rocprofv3 --pmc $c --kernel-trace -d "$OUT/pmc_$c" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu; done ;;
         *) echo "unknown step $s" ;;
     esac

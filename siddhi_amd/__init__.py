@@ -189,11 +189,11 @@ class InputHandler:
 
 
 class SiddhiAppRuntime:
-    def __init__(self, app_text, device=0, batch_capacity=0, compile_only=False):
+    def __init__(self, app_text, device=0, batch_capacity=0, compile_only=False, force_generic=False):
         L = load_library()
         self._L = L
         h = ctypes.c_void_p()
-        opts = _Opts(device, batch_capacity, 0, 1 if compile_only else 0)
+        opts = _Opts(device, batch_capacity, 0, (1 if compile_only else 0) | (2 if force_generic else 0))
         _check(L.sdg_compile(app_text.encode(), ctypes.byref(opts), ctypes.byref(h)))
         self._h = h
         self.playback = "@app:playback" in app_text.replace(" ", "").lower()

@@ -160,6 +160,7 @@ struct sdg_engine {
     std::vector<std::vector<int32_t>> out_types;
     std::vector<std::vector<const char*>> out_names;
     bool compile_only = false;
+    bool force_generic = false;
 };
 
 namespace {
@@ -306,6 +307,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         // hipMemcpyAsync from pageable memory: keep the host vectors alive until the copies land
         HIPCHECK(hipStreamSynchronize(st));
     }
+    // sorted positions and original rows are 32-bit on the device
+    if (nrows >= (int64_t)0xFFFFFFF0) throw CompileError(SDG_ERR_CAPACITY, "a flush holds more than 2^32 - 16 events");
     // ---- 2. key grouping ---------------------------------------------------------------------------------
     uint32_t K = 1;
     if (partitioned) K = q.string_keys ? (uint32_t)std::max<size_t>(e->strings.strs.size(), 1) : (uint32_t)std::max<size_t>(q.keydict.size(), 1);
@@ -593,6 +596,7 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             e->device = opts->device;
             if (opts->batch_capacity > 0) e->capacity = opts->batch_capacity;
             e->compile_only = (opts->flags & SDG_COMPILE_ONLY) != 0;
+            e->force_generic = (opts->flags & SDG_FORCE_GENERIC) != 0;
         }
         if (opts && opts->max_partials > 0) {
             if (opts->max_partials > 4096) throw CompileError(SDG_ERR_ARG, "max_partials must be <= 4096");
@@ -619,6 +623,7 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
         for (auto& h : hqs) {
             auto q = std::make_unique<QueryRt>();
             q->hq = std::move(h);
+            if (e->force_generic) q->hq.plan.chain = 0;
             q->L = nfa::make_layout(q->hq.plan.n_states, std::max(q->hq.plan.n_cols, 1), e->max_partials);
             for (size_t i = 0; i < q->hq.key_kind.size(); ++i)
                 if (q->hq.key_attr[i] >= 0 && q->hq.key_kind[i] != VK_STR) q->string_keys = false;

@@ -47,6 +47,9 @@ void keygroup_bind(KeyGroupArgs& a, void* base);
 void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks = nullptr);
 
 // ---- chain matcher: `every e1=S0[c0] -> e2=S1[c1] within T` (independent partials) ---------------------
+// One block per tile of CM_THREADS * CM_EPT sorted events; the block reserves its output range with one atomic.
+constexpr int CM_THREADS = 256;
+constexpr int CM_EPT = 8;
 struct ChainArgs {
     const Plan* plan;                 // device copy
     const Instr* code;

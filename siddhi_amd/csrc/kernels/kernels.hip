@@ -301,6 +301,17 @@ __device__ __forceinline__ int64_t chain_scan(const ChainArgs& a, ChainAcc& acc,
     return -2;
 }
 
+// select expressions: a plain attribute (`e1.id`) is loaded directly, anything else runs the bytecode
+__device__ __forceinline__ void eval_out(const ChainArgs& a, const Prog pr, ChainAcc& acc, int64_t* stk, int stride,
+                                         int64_t* v, bool* nl) {
+    if (pr.len == 1 && a.code[pr.start].op == OP_LOAD) {
+        const Instr in = a.code[pr.start];
+        acc.load(in.a, in.b, in.c, in.k, v, nl);
+    } else {
+        run(a.code, pr, a.consts, acc, stk, stride, v, nl);
+    }
+}
+
 __device__ __forceinline__ void emit_match(const ChainArgs& a, ChainAcc& acc, int64_t slot, int64_t q, uint32_t key,
                                            int64_t first_seq, int64_t* stk, int stride) {
     const Plan* P = a.plan;
@@ -313,63 +324,109 @@ __device__ __forceinline__ void emit_match(const ChainArgs& a, ChainAcc& acc, in
     for (int j = 0; j < P->n_out; ++j) {
         int64_t v;
         bool nl;
-        run(a.code, P->out_prog[j], a.consts, acc, stk, stride, &v, &nl);
+        eval_out(a, P->out_prog[j], acc, stk, stride, &v, &nl);
         a.out_vals[(int64_t)j * a.out_cap + slot] = v;
         if (nl) nm |= 1u << j;
     }
     a.out_nulls[slot] = nm;
 }
 
-__global__ __launch_bounds__(256) void chain_match_k(ChainArgs a) {
-    __shared__ int64_t stack_mem[STACK * 256];
+// block-wide exclusive scan of two per-thread counts; one atomic per block and counter reserves the block's
+// output range (per-wave reservations on one global counter serialise in L2 at ~10^8/s)
+__device__ __forceinline__ void block_reserve2(uint32_t c0, uint32_t c1, unsigned long long* ctr0,
+                                               unsigned long long* ctr1, int64_t* off0, int64_t* off1) {
+    __shared__ uint32_t wtot[2][CM_THREADS / 64];
+    __shared__ unsigned long long bbase[2];
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    uint32_t x0 = c0, x1 = c1;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y0 = __shfl_up(x0, d), y1 = __shfl_up(x1, d);
+        if (lane >= d) { x0 += y0; x1 += y1; }
+    }
+    if (lane == 63) { wtot[0][w] = x0; wtot[1][w] = x1; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t0 = 0, t1 = 0;
+        for (int v = 0; v < CM_THREADS / 64; ++v) {
+            uint32_t u0 = wtot[0][v], u1 = wtot[1][v];
+            wtot[0][v] = t0; wtot[1][v] = t1;
+            t0 += u0; t1 += u1;
+        }
+        bbase[0] = t0 ? atomicAdd(ctr0, (unsigned long long)t0) : 0ull;
+        bbase[1] = t1 ? atomicAdd(ctr1, (unsigned long long)t1) : 0ull;
+    }
+    __syncthreads();
+    *off0 = (int64_t)bbase[0] + wtot[0][w] + (x0 - c0);
+    *off1 = (int64_t)bbase[1] + wtot[1][w] + (x1 - c1);
+}
+
+constexpr uint32_t CM_NONE = 0xFFFFFFFFu, CM_CARRY = 0xFFFFFFFEu;
+
+// one block per tile of CM_THREADS * CM_EPT sorted events; lane t takes events base + r * CM_THREADS + t
+__global__ __launch_bounds__(CM_THREADS) void chain_match_k(ChainArgs a) {
+    __shared__ int64_t stack_mem[STACK * CM_THREADS];
     int64_t* stk = stack_mem + threadIdx.x;
-    const int stride = 256;
+    const int stride = CM_THREADS;
     const Plan* P = a.plan;
-    int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    bool active = p < a.n;
-    bool has = false, carry = false;
-    int64_t qhit = -1;
-    ChainAcc acc{&a, p, -1, -1};
-    uint32_t key = 0;
-    if (active) {
-        key = a.key ? a.key[p] : 0u;
+    const int64_t base = (int64_t)blockIdx.x * (CM_THREADS * CM_EPT);
+    const FastPred f0 = P->fast[0];
+    uint32_t res[CM_EPT];
+    uint32_t nmatch = 0, ncarry = 0;
+#pragma unroll
+    for (int r = 0; r < CM_EPT; ++r) {
+        const int64_t p = base + r * CM_THREADS + threadIdx.x;
+        res[r] = CM_NONE;
+        if (p >= a.n) continue;
+        ChainAcc acc{&a, p, -1, -1};
+        const uint32_t key = a.key ? a.key[p] : 0u;
         if (p > 0 && a.ts[p] < a.ts[p - 1] && (!a.key || a.key[p - 1] == key)) atomicOr(&a.flags[1], 1);
-        const FastPred f0 = P->fast[0];
         bool c0 = false;
         if (qstream_of(a, p) == a.s0)
             c0 = f0.kind == FP_TRUE ? true
                  : f0.kind == FP_NONE ? pass(a.code, P->st[0].filter, a.consts, acc, stk, stride) : fast_pass(f0, acc);
-        if (c0) {
-            if (P->n_states == 1) {
-                has = true;
-                qhit = p;
-            } else {
-                int64_t end = a.key ? (int64_t)a.seg_end[key] : a.n;
-                int64_t r = chain_scan(a, acc, p + 1, end, a.ts[p], stk, stride);
-                if (r >= 0) { has = true; qhit = r; }
-                else if (r == -2) carry = true;
-            }
-        }
-    }
-    int64_t slot = wave_reserve(has, a.out_count);
-    if (has) {
-        if (slot >= a.out_cap) atomicOr(&a.flags[0], 1);
-        else emit_match(a, acc, slot, qhit, key, a.seq_base + (a.orig ? (int64_t)a.orig[p] : p), stk, stride);
-    }
-    int64_t cs = wave_reserve(carry, a.carry_count);
-    if (carry) {
-        if (cs >= a.carry_cap) {
-            atomicOr(&a.flags[0], 1);
+        if (!c0) continue;
+        if (P->n_states == 1) {
+            res[r] = (uint32_t)p;
         } else {
-            a.carry_key[cs] = key;
-            a.carry_ts[cs] = a.ts[p];
-            a.carry_seq[cs] = a.seq_base + (a.orig ? (int64_t)a.orig[p] : p);
-            uint32_t nm = 0;
-            for (int c = 0; c < P->n_cols; ++c) {
-                a.carry_vals[(int64_t)c * a.carry_cap + cs] = load_col(a.cols[c], P->col_kind[c], p);
-                if (a.nulls[c] && a.nulls[c][p]) nm |= 1u << c;
+            const int64_t end = a.key ? (int64_t)a.seg_end[key] : a.n;
+            const int64_t q = chain_scan(a, acc, p + 1, end, a.ts[p], stk, stride);
+            res[r] = q >= 0 ? (uint32_t)q : q == -2 ? CM_CARRY : CM_NONE;
+        }
+        nmatch += res[r] < CM_CARRY;
+        ncarry += res[r] == CM_CARRY;
+    }
+    int64_t slot, cs;
+    block_reserve2(nmatch, ncarry, a.out_count, a.carry_count, &slot, &cs);
+#pragma unroll
+    for (int r = 0; r < CM_EPT; ++r) {
+        if (res[r] == CM_NONE) continue;
+        const int64_t p = base + r * CM_THREADS + threadIdx.x;
+        const uint32_t key = a.key ? a.key[p] : 0u;
+        const int64_t seq = a.seq_base + (a.orig ? (int64_t)a.orig[p] : p);
+        if (res[r] != CM_CARRY) {
+            if (slot >= a.out_cap) {
+                atomicOr(&a.flags[0], 1);
+            } else {
+                ChainAcc acc{&a, p, -1, -1};
+                emit_match(a, acc, slot, (int64_t)res[r], key, seq, stk, stride);
             }
-            a.carry_nulls[cs] = nm;
+            ++slot;
+        } else {
+            if (cs >= a.carry_cap) {
+                atomicOr(&a.flags[0], 1);
+            } else {
+                a.carry_key[cs] = key;
+                a.carry_ts[cs] = a.ts[p];
+                a.carry_seq[cs] = seq;
+                uint32_t nm = 0;
+                for (int c = 0; c < P->n_cols; ++c) {
+                    a.carry_vals[(int64_t)c * a.carry_cap + cs] = load_col(a.cols[c], P->col_kind[c], p);
+                    if (a.nulls[c] && a.nulls[c][p]) nm |= 1u << c;
+                }
+                a.carry_nulls[cs] = nm;
+            }
+            ++cs;
         }
     }
 }
@@ -537,7 +594,8 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
 
 void chain_match(const ChainArgs& a, hipStream_t stream) {
     if (a.n <= 0) return;
-    hipLaunchKernelGGL(chain_match_k, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, stream, a);
+    const int64_t tile = CM_THREADS * CM_EPT;
+    hipLaunchKernelGGL(chain_match_k, dim3((unsigned)((a.n + tile - 1) / tile)), dim3(CM_THREADS), 0, stream, a);
 }
 
 void chain_carry(const ChainArgs& a, hipStream_t stream) {

@@ -145,7 +145,7 @@ def test_generic_nfa_synthetic_on_gpu(name, batches, oracle_built):
         ref = synth.run(o, tr)
     finally:
         o.close()
-    p = ProductAdapter(app)
+    p = ProductAdapter(app, force_generic=True)  # chain-eligible queries too: both kernels on the same query
     try:
         assert p.rt.query_paths() == [1]
         got = synth.run(p, tr, batches)
