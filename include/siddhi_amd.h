@@ -112,6 +112,8 @@ typedef struct sdg_stats {
     /* device ms per kernel (HIP events on the engine's stream), summed over the flush's queries */
     double ms_kg_hist, ms_kg_prefix, ms_kg_scatter, ms_chain_carry, ms_chain_match;
     double ms_nfa;             /* generic keyed-NFA kernel */
+    double ms_chain_emit;      /* chain path: match-record emission (ms_chain_match is then the deque pass) */
+    int32_t deque;             /* chain path took the deque kernel (1 stack, 2 complete-all), 0 forward scans */
 } sdg_stats;
 int sdg_last_stats(sdg_engine* e, sdg_stats* out);
 

@@ -75,7 +75,9 @@ class Stats(ctypes.Structure):
                 ("ms_kg_hist", ctypes.c_double), ("ms_kg_prefix", ctypes.c_double),
                 ("ms_kg_scatter", ctypes.c_double), ("ms_chain_carry", ctypes.c_double),
                 ("ms_chain_match", ctypes.c_double),
-                ("ms_nfa", ctypes.c_double)]
+                ("ms_nfa", ctypes.c_double),
+                ("ms_chain_emit", ctypes.c_double),
+                ("deque", ctypes.c_int32)]
 
 
 _lib = None

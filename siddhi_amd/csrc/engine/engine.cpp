@@ -108,7 +108,7 @@ struct PushChunk {
 
 struct QueryRt {
     HostQuery hq;
-    DevBuf d_plan, d_code, d_consts;
+    DevBuf d_plan, d_code, d_consts, d_args, o_mq, o_ovf, o_ovfc;
     bool string_keys = true;                        // all partition keys are string attributes (ids used as keys)
     std::unordered_map<std::string, uint32_t> keydict;
     int64_t seq = 0;
@@ -130,6 +130,8 @@ struct QueryRt {
     DevBuf o_ts, o_key, o_vals, o_nulls, o_emit, o_first, counters, flags;
     int64_t out_n = 0, out_cap = 0;
     bool polled = true;
+    bool nulls_valid = true;                        // false: the last flush wrote no null bits (none possible)
+    bool carry_nullable = false;                    // the carried partials came from a batch with null columns
     // host copies for sdg_poll
     std::vector<int64_t> h_ts;
     std::vector<uint8_t> h_expired;
@@ -212,6 +214,102 @@ bool host_key(sdg_engine* e, QueryRt& q, int qpos, const PushChunk& c, int64_t r
     if (it == q.keydict.end()) it = q.keydict.emplace(s, (uint32_t)q.keydict.size()).first;
     *key = it->second;
     return true;
+}
+
+// chain_match_k's LDS tile: the columns the state-1 filter reads from its own event (the scanned rows), and
+// whether any filter / select needs the bytecode interpreter (its stack lives in LDS)
+void chain_staging(const HostQuery& h, ChainArgs& a, bool carry_nullable) {
+    const Plan& P = h.plan;
+    ChainSpec& sp = a.sp;
+    sp.n_states = P.n_states;
+    sp.has_within = P.has_within;
+    sp.within_ms = P.within_ms;
+    sp.f0 = P.fast[0];
+    sp.prog0 = P.st[0].filter;
+    if (P.n_states > 1) {
+        sp.f1 = P.fast[1];
+        sp.prog1 = P.st[1].filter;
+    }
+    sp.n_out = P.n_out;
+    sp.n_cols = P.n_cols;
+    for (int c = 0; c < P.n_cols; ++c) sp.col_kind[c] = P.col_kind[c];
+    for (int j = 0; j < P.n_out; ++j) {
+        const Prog pr = P.out_prog[j];
+        sp.out_prog[j] = pr;
+        sp.out_direct[j] = pr.len == 1 && h.code[pr.start].op == OP_LOAD;
+        if (sp.out_direct[j]) sp.out_ins[j] = h.code[pr.start];
+    }
+    for (int c = 0; c < MAX_COLS; ++c) a.stage_of[c] = -1;
+    a.n_stage = 0;
+    auto stage = [&](int col) {
+        if (col < 0 || col >= P.n_cols || a.stage_of[col] >= 0 || a.n_stage >= CM_SCOLS) return;
+        a.stage_of[col] = (int8_t)a.n_stage;
+        a.stage_col[a.n_stage++] = col;
+    };
+    bool stack = P.fast[0].kind == FP_NONE;
+    // e2 filter as a typed scan (chain.hip scan_typed) when it has one of the common shapes
+    sp.scan_mode = SCAN_GENERIC;
+    if (P.n_states > 1) {
+        const FastPred& f = P.fast[1];
+        auto plain = [](int8_t i) { return i == 0 || i == -1; };
+        if (f.kind == FP_TRUE) {
+            sp.scan_mode = SCAN_TRUE;
+            sp.scan_t = VK_I64;
+        } else if (f.kind == FP_CONST && f.sa == 1 && plain(f.ia)) {
+            sp.scan_mode = SCAN_CONST;
+            sp.scan_col = f.ca; sp.scan_col_kind = f.ka; sp.scan_t = f.t; sp.scan_op = f.op; sp.scan_e2_left = 1;
+            sp.scan_konst = f.konst;
+        } else if (f.kind == FP_SLOT && plain(f.ia) && plain(f.ib) && f.sa == 1 && f.sb == 0) {
+            sp.scan_mode = SCAN_E1;
+            sp.scan_col = f.ca; sp.scan_col_kind = f.ka; sp.scan_t = f.t; sp.scan_op = f.op; sp.scan_e2_left = 1;
+            sp.e1_col = f.cb; sp.e1_col_kind = f.kb;
+        } else if (f.kind == FP_SLOT && plain(f.ia) && plain(f.ib) && f.sa == 0 && f.sb == 1) {
+            sp.scan_mode = SCAN_E1;
+            sp.scan_col = f.cb; sp.scan_col_kind = f.kb; sp.scan_t = f.t; sp.scan_op = f.op; sp.scan_e2_left = 0;
+            sp.e1_col = f.ca; sp.e1_col_kind = f.ka;
+        }
+        if (f.kind == FP_CONST || f.kind == FP_SLOT) {
+            if (f.sa == 1) stage(f.ca);
+            if (f.kind == FP_SLOT && f.sb == 1) stage(f.cb);
+        } else if (f.kind == FP_NONE) {
+            stack = true;
+            const Prog pr = P.st[1].filter;
+            for (int i = pr.start; i < pr.start + pr.len; ++i)
+                if (h.code[i].op == OP_LOAD && h.code[i].a == 1) stage(h.code[i].b);
+        }
+    }
+    for (int j = 0; j < P.n_out; ++j) {
+        const Prog pr = P.out_prog[j];
+        if (!(pr.len == 1 && h.code[pr.start].op == OP_LOAD)) stack = true;
+    }
+    a.lds_stack = stack;
+    a.generic = stack || (P.n_states > 1 && sp.scan_mode == SCAN_GENERIC);
+    a.scan_lds = (sp.scan_mode == SCAN_CONST || sp.scan_mode == SCAN_E1) && a.stage_of[sp.scan_col] >= 0 &&
+                 a.nulls[sp.scan_col] == nullptr;
+    // outputs are plain attributes of null-free columns: no output can be null
+    bool nullable = false;
+    for (int j = 0; j < P.n_out; ++j) {
+        if (!sp.out_direct[j]) { nullable = true; break; }
+        const Instr& in = sp.out_ins[j];
+        if (!(in.c == 0 || in.c == -1) || in.a >= P.n_states || a.nulls[in.b]) nullable = true;
+    }
+    if (a.cin_n > 0 && carry_nullable) nullable = true;  // carried partials keep their batch's null bits
+    a.write_nulls = nullable;
+    // deque path (chain.hip chain_deque_k): one stream, c1 = `e2.x OP e1.x` (OP ordering) or independent of e1,
+    // c0 a FastPred, plain-attribute selects
+    a.deque_mode = DQ_OFF;
+    const bool one_stream = P.n_states == 2 && a.qstream == nullptr && P.st[0].stream == P.st[1].stream;
+    const bool ordering = sp.scan_op == CMP_GT || sp.scan_op == CMP_GE || sp.scan_op == CMP_LT || sp.scan_op == CMP_LE;
+    if (one_stream && !a.generic && P.fast[0].kind != FP_NONE) {
+        if (sp.scan_mode == SCAN_E1 && ordering && sp.e1_col == sp.scan_col && sp.e1_col_kind == sp.scan_col_kind)
+            a.deque_mode = DQ_STACK;
+        else if (sp.scan_mode == SCAN_CONST || sp.scan_mode == SCAN_TRUE)
+            a.deque_mode = DQ_ALL;
+    }
+    if (a.deque_mode == DQ_ALL && sp.scan_mode == SCAN_TRUE) sp.scan_col = 0, sp.scan_col_kind = P.col_kind[0];
+    const FastPred& f0 = P.fast[0];
+    a.f0_on_x = f0.kind == FP_CONST && f0.sa == 0 && (f0.ia == 0 || f0.ia == -1) && f0.ca == sp.scan_col &&
+                f0.ka == sp.scan_col_kind;
 }
 
 void flush_query(sdg_engine* e, QueryRt& q) {
@@ -479,7 +577,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     a.carry_count = counters + 1;
     a.flags = flags;
     a.out_ts = (int64_t*)q.o_ts.ensure(cap * 8);
-    a.out_key = (uint32_t*)q.o_key.ensure(cap * 4);
+    a.out_key = nullptr;  // not read back
     a.out_vals = (int64_t*)q.o_vals.ensure((size_t)std::max(P.n_out, 1) * cap * 8);
     a.out_nulls = (uint32_t*)q.o_nulls.ensure(cap * 4);
     a.out_emit_seq = (int64_t*)q.o_emit.ensure(cap * 8);
@@ -498,9 +596,31 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     a.cin_vals = cin.vals.as<int64_t>();
     a.cin_nulls = cin.nulls.as<uint32_t>();
     a.cin_cap = cin.cap;
-    chain_carry(a, st);
+    chain_staging(h, a, q.carry_nullable);
+    q.nulls_valid = a.write_nulls;
+    q.carry_nullable = false;
+    for (int k = 0; k < nc; ++k) q.carry_nullable |= a.nulls[k] != nullptr;
+    if (a.deque_mode != DQ_OFF && nrows > 0) {
+        a.mq = (uint32_t*)q.o_mq.ensure((size_t)nrows * 4);
+        a.ovf_rows = (uint32_t*)q.o_ovf.ensure((size_t)nrows * 4);
+        a.ovf_count = (unsigned long long*)q.o_ovfc.ensure(8);
+        HIPCHECK(hipMemsetAsync(a.ovf_count, 0, 8, st));
+    }
+    ChainArgs* d_a = (ChainArgs*)q.d_args.ensure(2 * sizeof(ChainArgs));
+    HIPCHECK(hipMemcpyAsync(d_a, &a, sizeof a, hipMemcpyHostToDevice, st));  // `a` outlives the sync below
+    ChainArgs ae = a;  // emit-only pass over mq
+    ae.mq_in = a.mq;
+    HIPCHECK(hipMemcpyAsync(d_a + 1, &ae, sizeof ae, hipMemcpyHostToDevice, st));
+    chain_carry(a, d_a, st);
     HIPCHECK(hipEventRecord(e->ev[8], st));
-    chain_match(a, st);
+    if (a.deque_mode != DQ_OFF && nrows > 0) {
+        chain_deque(a, d_a, st);
+        HIPCHECK(hipEventRecord(e->ev[9], st));
+        chain_match(ae, d_a + 1, st);
+    } else {
+        HIPCHECK(hipEventRecord(e->ev[9], st));
+        chain_match(a, d_a, st);
+    }
     e->stats.match_launches += (cin.n > 0) + (nrows > 0);
     HIPCHECK(hipEventRecord(e->ev[2], st));
     unsigned long long hc[2];
@@ -525,8 +645,11 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     }
     HIPCHECK(hipEventElapsedTime(&t, e->ev[1], e->ev[8]));
     e->stats.ms_chain_carry += t;
-    HIPCHECK(hipEventElapsedTime(&t, e->ev[8], e->ev[2]));
+    HIPCHECK(hipEventElapsedTime(&t, e->ev[8], e->ev[9]));
     e->stats.ms_chain_match += t;
+    HIPCHECK(hipEventElapsedTime(&t, e->ev[9], e->ev[2]));
+    e->stats.ms_chain_emit += t;
+    e->stats.deque = a.deque_mode;
     e->stats.events += nrows;
     if (hf[0]) {
         e->stats.overflow += 1;
@@ -554,7 +677,7 @@ int do_flush(sdg_engine* e) {
     e->stats.keygroup_launches = e->stats.match_launches = 0;
     e->stats.overflow = 0;
     e->stats.ms_kg_hist = e->stats.ms_kg_prefix = e->stats.ms_kg_scatter = 0;
-    e->stats.ms_chain_carry = e->stats.ms_chain_match = 0;
+    e->stats.ms_chain_carry = e->stats.ms_chain_match = e->stats.ms_chain_emit = 0;
     e->stats.ms_nfa = 0;
     for (auto& q : e->qs) flush_query(e, *q);
     e->stats.ms_total = e->stats.ms_keygroup + e->stats.ms_match;
@@ -774,7 +897,7 @@ int sdg_poll(sdg_engine* e, int qi, sdg_out* out) {
             HIPCHECK(hipMemcpyAsync(ts.data(), q.o_ts.p, n * 8, hipMemcpyDeviceToHost, st));
             HIPCHECK(hipMemcpyAsync(emit.data(), q.o_emit.p, n * 8, hipMemcpyDeviceToHost, st));
             HIPCHECK(hipMemcpyAsync(first.data(), q.o_first.p, n * 8, hipMemcpyDeviceToHost, st));
-            HIPCHECK(hipMemcpyAsync(nulls.data(), q.o_nulls.p, n * 4, hipMemcpyDeviceToHost, st));
+            if (q.nulls_valid) HIPCHECK(hipMemcpyAsync(nulls.data(), q.o_nulls.p, n * 4, hipMemcpyDeviceToHost, st));
             for (int j = 0; j < na; ++j)
                 HIPCHECK(hipMemcpyAsync(vals.data() + (size_t)j * q.out_cap, (int64_t*)q.o_vals.p + (size_t)j * q.out_cap,
                                         n * 8, hipMemcpyDeviceToHost, st));

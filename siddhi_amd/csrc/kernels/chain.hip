@@ -1,0 +1,590 @@
+// gfx950 chain matcher: PATTERN `every e1=S0[c0] -> e2=S1[c1] [within T]` (and `every e1=S0[c0]`), whose
+// partials never interact. Over the key-sorted view, every event is a candidate e1; its e2 is
+// the first later event of its key that passes c1 while the partial is alive (a forward scan).
+//
+//   reference: StreamPreStateProcessor.processAndReturn / isExpired / updateState
+//              (core/query/input/stream/state/StreamPreStateProcessor.java:364-403, :118-129, :308-323),
+//              PatternMultiProcessStreamReceiver (state/receiver/PatternMultiProcessStreamReceiver.java:27-51).
+//
+// chain_match_k: one block per tile of CM_TILE sorted events. The tile plus a halo of CM_HALO rows is staged in
+// LDS (ts, the query-stream byte and the columns the e2 filter reads), so scans run out of LDS; a scan that
+// leaves the halo continues in HBM. c1 of the common shapes (`e2.x OP const`, `e2.x OP e1.y`, none) is a typed
+// loop with the e1 operand hoisted; anything else runs the bytecode. One global atomic per block reserves the
+// block's match / carry ranges.
+// chain_carry_k: partials carried in from the previous batch scan the new batch's key segment.
+#include <hip/hip_runtime.h>
+
+#include "../engine/eval.h"
+#include "kernels.h"
+#include "wave.h"
+
+namespace sdg {
+
+extern __shared__ int64_t cm_lds[];
+
+namespace {
+
+// rows [lo, hi) of the sorted view mirrored in LDS (lo == hi: none). Offsets are in int64 words of cm_lds,
+// oqs in bytes.
+struct View {
+    int64_t lo = 0, hi = 0;
+    int32_t ots = 0, oc0 = 0, oc1 = 0, oqs = 0;
+};
+
+__device__ __forceinline__ bool in_view(const View& v, int64_t r) { return r >= v.lo && r < v.hi; }
+
+__device__ __forceinline__ int64_t ts_row(const ChainArgs& a, const View& v, int64_t r) {
+    return in_view(v, r) ? cm_lds[v.ots + (r - v.lo)] : a.ts[r];
+}
+__device__ __forceinline__ int qs_row(const ChainArgs& a, const View& v, int64_t r) {
+    if (!a.qstream) return 0;
+    return in_view(v, r) ? (int)((const uint8_t*)cm_lds)[v.oqs + (r - v.lo)] : (int)a.qstream[r];
+}
+__device__ __forceinline__ int64_t col_row(const ChainArgs& a, const View& v, int col, uint8_t kind, int64_t r) {
+    const int s = a.stage_of[col];
+    if (s >= 0 && in_view(v, r)) return cm_lds[(s == 0 ? v.oc0 : v.oc1) + (r - v.lo)];
+    return load_col(a.cols[col], kind, r);
+}
+__device__ __forceinline__ bool null_row(const ChainArgs& a, int col, int64_t r) {
+    return a.nulls[col] ? a.nulls[col][r] != 0 : false;
+}
+
+// attribute access for the bytecode / FastPred evaluators (eval.h): slot 0 = e1 (a row, or a carried partial),
+// slot 1 = e2 (the scanned row)
+struct ChainAcc {
+    const ChainArgs* A;
+    View V;
+    int64_t r0, c0, r1;
+    __device__ void load(int slot, int col, int chain, uint8_t kind, int64_t* v, bool* null) {
+        *v = 0;
+        *null = true;
+        if (!(chain == 0 || chain == -1)) return;  // a plain state's chain holds exactly one event
+        int64_t row;
+        if (slot == 0) {
+            if (c0 >= 0) {
+                *v = A->cin_vals[(int64_t)col * A->cin_cap + c0];
+                *null = (A->cin_nulls[c0] >> col) & 1u;
+                return;
+            }
+            row = r0;
+        } else if (slot == 1) {
+            row = r1;
+        } else {
+            return;
+        }
+        if (row < 0) return;
+        *v = col_row(*A, V, col, kind, row);
+        *null = null_row(*A, col, row);
+    }
+    __device__ bool slot_empty(int slot, int chain) {
+        if (!(chain == 0 || chain == -1)) return true;
+        if (slot == 0) return !(c0 >= 0 || r0 >= 0);
+        if (slot == 1) return r1 < 0;
+        return true;
+    }
+};
+
+// comparison kind -> C type (eval.h cmp(): bool compares as (v != 0), strings as dictionary ids)
+template <int K> struct KT;
+template <> struct KT<VK_I32> { using T = int32_t; static __device__ T get(int64_t v) { return (int32_t)v; } };
+template <> struct KT<VK_I64> { using T = int64_t; static __device__ T get(int64_t v) { return v; } };
+template <> struct KT<VK_F32> { using T = float; static __device__ T get(int64_t v) { return bits_f32(v); } };
+template <> struct KT<VK_F64> { using T = double; static __device__ T get(int64_t v) { return bits_f64(v); } };
+template <> struct KT<VK_BOOL> { using T = int; static __device__ T get(int64_t v) { return v != 0; } };
+template <> struct KT<VK_STR> { using T = uint32_t; static __device__ T get(int64_t v) { return (uint32_t)v; } };
+
+constexpr uint8_t OP_ALWAYS = 254, OP_NEVER = 255;
+
+// a comparison operator as wave-uniform masks: x OP y == (lt && x<y) || (eq && x==y) || (gt && x>y) || (ne && x!=y)
+// (NaN: <, ==, > all false, so only != holds -- Java's double/float semantics)
+struct CmpMask {
+    bool lt, eq, gt, ne;
+};
+__device__ __forceinline__ CmpMask cmp_mask(uint8_t op) {
+    switch (op) {
+        case CMP_EQ: return {false, true, false, false};
+        case CMP_NE: return {false, false, false, true};
+        case CMP_GT: return {false, false, true, false};
+        case CMP_GE: return {false, true, true, false};
+        case CMP_LT: return {true, false, false, false};
+        case CMP_LE: return {true, true, false, false};
+        case OP_ALWAYS: return {true, true, true, true};
+        default: return {false, false, false, false};
+    }
+}
+template <class T>
+__device__ __forceinline__ bool cmp_m(const CmpMask& m, T x, T y) {
+    return (m.lt && x < y) || (m.eq && x == y) || (m.gt && x > y) || (m.ne && !(x == y));
+}
+
+// typed scan: c1 == `e2.col OP k` (e2_left) or `k OP e2.col`, k uniform (a constant or the e1 operand)
+// returns: >= 0 the matching row; -1 expired (dead); -2 reached the end of the segment (carry)
+template <int K>
+__device__ int64_t scan_typed(const ChainArgs& a, const View& v, int64_t from, int64_t end, int64_t ts0, int64_t k,
+                              uint8_t op) {
+    using C = KT<K>;
+    const typename C::T y = C::get(k);
+    const ChainSpec& sp = a.sp;
+    const int col = sp.scan_col;
+    const uint8_t kind = sp.scan_col_kind;
+    const bool left = sp.scan_e2_left;
+    const int32_t has_within = sp.has_within;
+    const int64_t within = sp.within_ms;
+    const CmpMask m = cmp_mask(op);
+    const bool always = op == OP_ALWAYS;
+    int64_t q = from;
+    // LDS part: the scan column is staged and has no nulls
+    if (a.scan_lds) {
+        const int oc = a.stage_of[col] == 0 ? v.oc0 : v.oc1;
+        const int64_t e = min(end, v.hi);
+        const uint8_t* qs = (const uint8_t*)cm_lds + v.oqs;
+        const bool multi = a.qstream != nullptr;
+        for (; q < e; ++q) {
+            const int i = (int)(q - v.lo);
+            if (has_within) {
+                int64_t d = ts0 - cm_lds[v.ots + i];
+                if (d < 0) d = -d;
+                if (d > within) return -1;
+            }
+            if (multi && qs[i] != a.s1) continue;
+            if (always) return q;
+            const typename C::T x = C::get(cvt(cm_lds[oc + i], kind, (uint8_t)K));
+            if (left ? cmp_m(m, x, y) : cmp_m(m, y, x)) return q;
+        }
+    }
+    for (; q < end; ++q) {
+        // StreamPreStateProcessor.isExpired: |start.ts - now| > within, checked before the event is processed
+        if (has_within) {
+            int64_t d = ts0 - ts_row(a, v, q);
+            if (d < 0) d = -d;
+            if (d > within) return -1;
+        }
+        if (qs_row(a, v, q) != a.s1) continue;
+        if (always) return q;
+        if (null_row(a, col, q)) continue;  // compare with null -> false
+        const typename C::T x = C::get(cvt(col_row(a, v, col, kind, q), kind, (uint8_t)K));
+        if (left ? cmp_m(m, x, y) : cmp_m(m, y, x)) return q;
+    }
+    return -2;
+}
+
+// scan the key's events after `from` (exclusive) for the e2 of a partial whose e1 is at ts0.
+// GEN = false: the query needs no bytecode (typed scan, FastPred / direct-load selects), so the interpreter is
+// not compiled into the kernel (registers, code size).
+template <bool GEN>
+__device__ __forceinline__ int64_t chain_scan(const ChainArgs& a, ChainAcc& acc, int64_t from, int64_t end,
+                                              int64_t ts0, int64_t* stk, int stride) {
+    const ChainSpec& sp = a.sp;
+    if (!GEN || sp.scan_mode != SCAN_GENERIC) {
+        int64_t k = sp.scan_konst;
+        uint8_t op = sp.scan_op;
+        if (sp.scan_mode == SCAN_TRUE) {
+            op = OP_ALWAYS;
+        } else if (sp.scan_mode == SCAN_E1) {  // e1 operand, hoisted out of the scan
+            bool nl;
+            acc.load(0, sp.e1_col, 0, sp.e1_col_kind, &k, &nl);
+            if (nl) op = OP_NEVER;
+            else k = cvt(k, sp.e1_col_kind, sp.scan_t);
+        }
+        switch (sp.scan_t) {
+            case VK_I32: return scan_typed<VK_I32>(a, acc.V, from, end, ts0, k, op);
+            case VK_I64: return scan_typed<VK_I64>(a, acc.V, from, end, ts0, k, op);
+            case VK_F32: return scan_typed<VK_F32>(a, acc.V, from, end, ts0, k, op);
+            case VK_F64: return scan_typed<VK_F64>(a, acc.V, from, end, ts0, k, op);
+            case VK_BOOL: return scan_typed<VK_BOOL>(a, acc.V, from, end, ts0, k, op);
+            default: return scan_typed<VK_STR>(a, acc.V, from, end, ts0, k, op);
+        }
+    }
+    if (!GEN) return -2;  // unreachable: the host picks GEN for SCAN_GENERIC
+    for (int64_t q = from; q < end; ++q) {
+        if (sp.has_within) {
+            int64_t d = ts0 - ts_row(a, acc.V, q);
+            if (d < 0) d = -d;
+            if (d > sp.within_ms) return -1;
+        }
+        if (qs_row(a, acc.V, q) != a.s1) continue;
+        acc.r1 = q;
+        const bool ok = sp.f1.kind == FP_NONE ? pass(a.code, sp.prog1, a.consts, acc, stk, stride)
+                                              : fast_pass(sp.f1, acc);
+        acc.r1 = -1;
+        if (ok) return q;
+    }
+    return -2;
+}
+
+template <bool GEN>
+__device__ __forceinline__ void emit_match(const ChainArgs& a, ChainAcc& acc, int64_t slot, int64_t q, uint32_t key,
+                                           int64_t first_seq, int64_t* stk, int stride) {
+    const ChainSpec& sp = a.sp;
+    a.out_ts[slot] = ts_row(a, acc.V, q);
+    if (a.out_key) a.out_key[slot] = key;
+    a.out_emit_seq[slot] = a.seq_base + (a.orig ? (int64_t)a.orig[q] : q);
+    a.out_first_seq[slot] = first_seq;
+    uint32_t nm = 0;
+    acc.r1 = sp.n_states > 1 ? q : -1;
+    for (int j = 0; j < sp.n_out; ++j) {
+        int64_t v;
+        bool nl;
+        if (!GEN || sp.out_direct[j]) {  // a plain attribute (`e1.id`)
+            const Instr& in = sp.out_ins[j];
+            acc.load(in.a, in.b, in.c, in.k, &v, &nl);
+        } else {
+            run(a.code, sp.out_prog[j], a.consts, acc, stk, stride, &v, &nl);
+        }
+        a.out_vals[(int64_t)j * a.out_cap + slot] = v;
+        if (nl) nm |= 1u << j;
+    }
+    if (a.write_nulls) a.out_nulls[slot] = nm;
+}
+
+__device__ __forceinline__ void emit_carry(const ChainArgs& a, const View& v, int64_t cs, int64_t p, uint32_t key,
+                                           int64_t seq) {
+    a.carry_key[cs] = key;
+    a.carry_ts[cs] = ts_row(a, v, p);
+    a.carry_seq[cs] = seq;
+    uint32_t nm = 0;
+    for (int c = 0; c < a.sp.n_cols; ++c) {
+        a.carry_vals[(int64_t)c * a.carry_cap + cs] = load_col(a.cols[c], a.sp.col_kind[c], p);
+        if (null_row(a, c, p)) nm |= 1u << c;
+    }
+    a.carry_nulls[cs] = nm;
+}
+
+constexpr uint32_t CM_NONE = 0xFFFFFFFFu, CM_CARRY = 0xFFFFFFFEu;
+static_assert(MQ_NONE == CM_NONE && MQ_CARRY == CM_CARRY, "emit-only mode reads mq as chain_match_k results");
+
+template <bool GEN>
+__global__ __launch_bounds__(CM_THREADS) void chain_match_k(const ChainArgs* __restrict__ pa) {
+    const ChainArgs& a = *pa;
+    const ChainSpec& sp = a.sp;
+    const int tid = threadIdx.x;
+    const int64_t base = (int64_t)blockIdx.x * CM_TILE;
+    const int stride = CM_THREADS;
+    View v;
+    v.lo = base;
+    v.hi = a.mq_in ? base : min(a.n, base + CM_ROWS);  // emit-only: nothing to stage
+    v.ots = a.lds_stack ? STACK * CM_THREADS : 0;
+    v.oc0 = v.ots + CM_ROWS;
+    v.oc1 = v.oc0 + CM_ROWS;
+    v.oqs = (v.ots + (1 + a.n_stage) * CM_ROWS) * 8;
+    const int ores = (v.oqs + (a.qstream ? CM_ROWS : 0) + 3) / 4;  // u32 index of the per-event results
+    int64_t* stk = cm_lds + tid;                                   // used only when a.lds_stack
+    uint32_t* res = (uint32_t*)cm_lds + ores;
+    __shared__ uint32_t wcnt[2][CM_EPT][CM_THREADS / 64];          // matches / carries per (round, wave)
+    __shared__ unsigned long long bbase[2];
+    const int lane = lane_id(), w = tid >> 6;
+    const uint64_t lt = lanemask_lt();
+    // ---- stage the tile + halo (coalesced) -------------------------------------------------------------
+    const int nr = (int)(v.hi - v.lo);
+    for (int i = tid; i < nr; i += CM_THREADS) cm_lds[v.ots + i] = a.ts[base + i];
+    for (int c = 0; c < a.n_stage; ++c) {
+        const int col = a.stage_col[c];
+        const uint8_t kind = sp.col_kind[col];
+        const int off = c == 0 ? v.oc0 : v.oc1;
+        for (int i = tid; i < nr; i += CM_THREADS) cm_lds[off + i] = load_col(a.cols[col], kind, base + i);
+    }
+    if (a.qstream)
+        for (int i = tid; i < nr; i += CM_THREADS) ((uint8_t*)cm_lds)[v.oqs + i] = a.qstream[base + i];
+    __syncthreads();
+    // ---- match: lane tid takes events base + r * CM_THREADS + tid ---------------------------------------
+#pragma unroll 1
+    for (int r = 0; r < CM_EPT; ++r) {
+        const int64_t p = base + r * CM_THREADS + tid;
+        uint32_t out = CM_NONE;
+        if (p < a.n && a.mq_in) {
+            out = a.mq_in[p];  // MQ_NONE == CM_NONE, MQ_CARRY == CM_CARRY
+        } else if (p < a.n) {
+            ChainAcc acc{&a, v, p, -1, -1};
+            const uint32_t key = a.key ? a.key[p] : 0u;
+            const int64_t tp = ts_row(a, v, p);
+            if (p > 0 && tp < ts_row(a, v, p - 1) && (!a.key || a.key[p - 1] == key)) atomicOr(&a.flags[1], 1);
+            bool c0 = false;
+            if (qs_row(a, v, p) == a.s0)
+                c0 = sp.f0.kind == FP_TRUE ? true
+                     : (GEN && sp.f0.kind == FP_NONE) ? pass(a.code, sp.prog0, a.consts, acc, stk, stride)
+                                                      : fast_pass(sp.f0, acc);
+            if (c0) {
+                if (sp.n_states == 1) {
+                    out = (uint32_t)p;
+                } else {
+                    const int64_t end = a.key ? (int64_t)a.seg_end[key] : a.n;
+                    const int64_t q = chain_scan<GEN>(a, acc, p + 1, end, tp, stk, stride);
+                    out = q >= 0 ? (uint32_t)q : q == -2 ? CM_CARRY : CM_NONE;
+                }
+            }
+        }
+        res[r * CM_THREADS + tid] = out;
+        const uint64_t bm = __ballot(out < CM_CARRY), bc = __ballot(out == CM_CARRY);
+        if (lane == 0) {
+            wcnt[0][r][w] = (uint32_t)__popcll(bm);
+            wcnt[1][r][w] = (uint32_t)__popcll(bc);
+        }
+    }
+    __syncthreads();
+    // round-major exclusive scan over (round, wave): the matches of one round are consecutive slots in lane
+    // order, so every store below writes one contiguous run (coalesced)
+    if (tid < 2) {
+        uint32_t run = 0;
+        for (int r = 0; r < CM_EPT; ++r)
+            for (int x = 0; x < CM_THREADS / 64; ++x) {
+                const uint32_t c = wcnt[tid][r][x];
+                wcnt[tid][r][x] = run;
+                run += c;
+            }
+        bbase[tid] = run ? atomicAdd(tid == 0 ? a.out_count : a.carry_count, (unsigned long long)run) : 0ull;
+    }
+    __syncthreads();
+    // ---- emit -------------------------------------------------------------------------------------------
+#pragma unroll 1
+    for (int r = 0; r < CM_EPT; ++r) {
+        const uint32_t out = res[r * CM_THREADS + tid];
+        const uint64_t bm = __ballot(out < CM_CARRY), bc = __ballot(out == CM_CARRY);
+        if (out == CM_NONE) continue;
+        const int64_t p = base + r * CM_THREADS + tid;
+        const uint32_t key = a.key ? a.key[p] : 0u;
+        const int64_t seq = a.seq_base + (a.orig ? (int64_t)a.orig[p] : p);
+        if (out != CM_CARRY) {
+            const int64_t slot = (int64_t)bbase[0] + wcnt[0][r][w] + __popcll(bm & lt);
+            if (slot >= a.out_cap) {
+                atomicOr(&a.flags[0], 1);
+            } else {
+                ChainAcc acc{&a, v, p, -1, -1};
+                emit_match<GEN>(a, acc, slot, (int64_t)out, key, seq, stk, stride);
+            }
+        } else {
+            const int64_t cs = (int64_t)bbase[1] + wcnt[1][r][w] + __popcll(bc & lt);
+            if (cs >= a.carry_cap) atomicOr(&a.flags[0], 1);
+            else emit_carry(a, v, cs, p, key, seq);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Deque path. For `every e1=S[c0] -> e2=S[e2.x OP e1.x]` with OP in {<, <=, >, >=} (one stream, one column),
+// the partials pending at any time in one key, in arrival order, have monotonic x: an event with value x
+// completes exactly a suffix of them (those with `x OP y`), and if it starts a partial itself its y = x is
+// then the extreme value. Expiry (`within`) removes a prefix. So one pass over a key's events with a deque
+// is the reference's result, with O(1) amortised work per event instead of a forward scan per partial.
+// DQ_ALL: c1 does not involve e1 (`e2.x OP const`, or none): an event passing c1 completes every partial.
+// Each lane owns DQ_CHUNK consecutive rows: it pushes partials from its rows only, then keeps popping over
+// the following rows of the key (no pushes) until its deque drains, or carries what is left at the key's end.
+// Deque entries live in an LDS ring (DQ_DEPTH per lane, [entry][lane] = conflict-free); a lane that would
+// exceed it evicts its oldest entry to ovf_rows (resolved by chain_ovf_k with the forward scan).
+// Every row gets exactly one mq write: its e2 row, MQ_NONE (no partial / expired / cannot match), MQ_CARRY or
+// MQ_OVF (then overwritten by chain_ovf_k).
+template <int K>
+__global__ __launch_bounds__(DQ_THREADS) void chain_deque_k(const ChainArgs* __restrict__ pa) {
+    using C = KT<K>;
+    using T = typename C::T;
+    const ChainArgs& a = *pa;
+    const ChainSpec& sp = a.sp;
+    __shared__ int64_t dq_y[DQ_DEPTH][DQ_THREADS];
+    __shared__ int64_t dq_ts[DQ_DEPTH][DQ_THREADS];
+    __shared__ uint32_t dq_row[DQ_DEPTH][DQ_THREADS];
+    const int tid = threadIdx.x;
+    const int64_t c0 = ((int64_t)blockIdx.x * DQ_THREADS + tid) * DQ_CHUNK;
+    if (c0 >= a.n) return;
+    const int64_t c1 = min(a.n, c0 + DQ_CHUNK);
+    const int col = sp.scan_col;
+    const uint8_t kind = sp.scan_col_kind;
+    const uint8_t* xnull = a.nulls[col];
+    const bool stack = a.deque_mode == DQ_STACK;
+    const CmpMask m = cmp_mask(stack ? sp.scan_op : (sp.scan_mode == SCAN_TRUE ? OP_ALWAYS : sp.scan_op));
+    const bool left = sp.scan_e2_left;
+    const T kc = C::get(sp.scan_konst);
+    const int32_t has_within = sp.has_within;
+    const int64_t within = sp.within_ms;
+    const FastPred& f0 = sp.f0;
+    int head = 0, cnt = 0;
+    uint32_t cur_key = a.key ? a.key[c0] : 0u;
+    int64_t prev_ts = (c0 > 0 && (!a.key || a.key[c0 - 1] == cur_key)) ? a.ts[c0 - 1] : INT64_MIN;
+
+    // one row q: expire the oldest entries, complete a suffix (or all), then (push) start a partial
+    auto step = [&](int64_t q, int64_t tq, int64_t xraw, bool xn, bool push) {
+        if (has_within) {
+            while (cnt > 0) {
+                int64_t d = dq_ts[head][tid] - tq;
+                if (d < 0) d = -d;
+                if (d <= within) break;
+                a.mq[dq_row[head][tid]] = MQ_NONE;  // expired before completing
+                head = (head + 1) & (DQ_DEPTH - 1);
+                --cnt;
+            }
+        }
+        const T x = C::get(cvt(xraw, kind, (uint8_t)K));
+        if (stack) {
+            if (!xn) {
+                while (cnt > 0) {
+                    const int top = (head + cnt - 1) & (DQ_DEPTH - 1);
+                    const T y = C::get(dq_y[top][tid]);
+                    if (!(left ? cmp_m(m, x, y) : cmp_m(m, y, x))) break;
+                    a.mq[dq_row[top][tid]] = (uint32_t)q;
+                    --cnt;
+                }
+            }
+        } else if (cnt > 0 && (sp.scan_mode == SCAN_TRUE || (!xn && (left ? cmp_m(m, x, kc) : cmp_m(m, kc, x))))) {
+            for (; cnt > 0; --cnt, head = (head + 1) & (DQ_DEPTH - 1)) a.mq[dq_row[head][tid]] = (uint32_t)q;
+        }
+        if (!push) return;
+        // e1: the every-seed starts a partial when c0 passes (visible from the next row on)
+        bool c0ok;
+        if (a.f0_on_x) {
+            c0ok = !xn && cmp(f0.op, f0.t, cvt(xraw, kind, f0.t), f0.konst);
+        } else {
+            ChainAcc acc{&a, View{}, q, -1, -1};
+            c0ok = f0.kind == FP_TRUE ? true : fast_pass(f0, acc);
+        }
+        // an e1 whose operand is null / NaN can never complete (compare -> false): no partial
+        if (!c0ok || (stack && (xn || !(x == x)))) {
+            a.mq[q] = MQ_NONE;
+            return;
+        }
+        if (cnt == DQ_DEPTH) {  // evict the oldest to the forward-scan fallback
+            const uint32_t r = dq_row[head][tid];
+            a.mq[r] = MQ_OVF;
+            a.ovf_rows[atomicAdd(a.ovf_count, 1ull)] = r;
+            head = (head + 1) & (DQ_DEPTH - 1);
+            --cnt;
+        }
+        const int slot = (head + cnt) & (DQ_DEPTH - 1);
+        dq_y[slot][tid] = (int64_t)xraw;  // raw payload, converted at compare time
+        dq_ts[slot][tid] = tq;
+        dq_row[slot][tid] = (uint32_t)q;
+        ++cnt;
+    };
+    auto carry_all = [&]() {
+        for (; cnt > 0; --cnt, head = (head + 1) & (DQ_DEPTH - 1)) a.mq[dq_row[head][tid]] = MQ_CARRY;
+    };
+
+    // own rows, DQ_GROUP at a time (contiguous per lane)
+    for (int64_t g = c0; g < c1; g += DQ_GROUP) {
+        int64_t ts[DQ_GROUP], xr[DQ_GROUP];
+        uint32_t ky[DQ_GROUP];
+        bool xn[DQ_GROUP];
+#pragma unroll
+        for (int j = 0; j < DQ_GROUP; ++j) {
+            const int64_t q = min(g + j, c1 - 1);
+            ts[j] = a.ts[q];
+            xr[j] = load_col(a.cols[col], kind, q);
+            ky[j] = a.key ? a.key[q] : 0u;
+            xn[j] = xnull ? xnull[q] != 0 : false;
+        }
+#pragma unroll
+        for (int j = 0; j < DQ_GROUP; ++j) {
+            const int64_t q = g + j;
+            if (q >= c1) break;
+            if (ky[j] != cur_key) {  // key segment ends inside the chunk: its pending partials carry
+                carry_all();
+                cur_key = ky[j];
+                prev_ts = INT64_MIN;
+            }
+            if (ts[j] < prev_ts) atomicOr(&a.flags[1], 1);
+            prev_ts = ts[j];
+            step(q, ts[j], xr[j], xn[j], true);
+        }
+    }
+    // continuation: pop over the key's following rows until the deque drains
+    const int64_t end = a.key ? (int64_t)a.seg_end[cur_key] : a.n;
+    for (int64_t q = c1; q < end && cnt > 0; ++q) {
+        const int64_t tq = a.ts[q];
+        step(q, tq, load_col(a.cols[col], kind, q), xnull ? xnull[q] != 0 : false, false);
+    }
+    carry_all();  // reached the end of the key's segment in this batch
+}
+
+// rows evicted from a lane's deque: the forward scan of the generic path
+__global__ __launch_bounds__(256) void chain_ovf_k(const ChainArgs* __restrict__ pa) {
+    const ChainArgs& a = *pa;
+    __shared__ int64_t stack_mem[STACK * 256];
+    int64_t* stk = stack_mem + threadIdx.x;
+    const int64_t total = (int64_t)*a.ovf_count;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int64_t p = a.ovf_rows[i];
+        ChainAcc acc{&a, View{}, p, -1, -1};
+        const uint32_t key = a.key ? a.key[p] : 0u;
+        const int64_t end = a.key ? (int64_t)a.seg_end[key] : a.n;
+        const int64_t q = chain_scan<true>(a, acc, p + 1, end, a.ts[p], stk, 256);
+        a.mq[p] = q >= 0 ? (uint32_t)q : q == -2 ? MQ_CARRY : MQ_NONE;
+    }
+}
+
+__global__ __launch_bounds__(256) void chain_carry_k(const ChainArgs* __restrict__ pa) {
+    const ChainArgs& a = *pa;
+    __shared__ int64_t stack_mem[STACK * 256];
+    int64_t* stk = stack_mem + threadIdx.x;
+    const int stride = 256;
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    bool has = false, carry = false;
+    int64_t qhit = -1;
+    const View v;  // empty: everything from HBM
+    ChainAcc acc{&a, v, -1, c, -1};
+    uint32_t key = 0;
+    if (c < a.cin_n) {
+        key = a.cin_key[c];
+        int64_t b = 0, e = a.n;
+        if (a.key) {
+            b = key < (uint32_t)a.K ? (int64_t)a.seg_start[key] : 0;
+            e = key < (uint32_t)a.K ? (int64_t)a.seg_end[key] : 0;
+        }
+        const int64_t r = chain_scan<true>(a, acc, b, e, a.cin_ts[c], stk, stride);
+        if (r >= 0) { has = true; qhit = r; }
+        else if (r == -2) carry = true;
+    }
+    const int64_t slot = wave_reserve(has, a.out_count);
+    if (has) {
+        if (slot >= a.out_cap) atomicOr(&a.flags[0], 1);
+        else emit_match<true>(a, acc, slot, qhit, key, a.cin_seq[c], stk, stride);
+    }
+    const int64_t cs = wave_reserve(carry, a.carry_count);
+    if (carry) {
+        if (cs >= a.carry_cap) {
+            atomicOr(&a.flags[0], 1);
+        } else {
+            a.carry_key[cs] = key;
+            a.carry_ts[cs] = a.cin_ts[c];
+            a.carry_seq[cs] = a.cin_seq[c];
+            for (int k = 0; k < a.sp.n_cols; ++k)
+                a.carry_vals[(int64_t)k * a.carry_cap + cs] = a.cin_vals[(int64_t)k * a.cin_cap + c];
+            a.carry_nulls[cs] = a.cin_nulls[c];
+        }
+    }
+}
+
+}  // namespace
+
+size_t chain_lds_bytes(const ChainArgs& a) {
+    size_t b = (a.lds_stack ? (size_t)STACK * CM_THREADS * 8 : 0) + (size_t)(1 + a.n_stage) * CM_ROWS * 8;
+    b += a.qstream ? CM_ROWS : 0;
+    b = (b + 3) & ~size_t(3);
+    return b + (size_t)CM_EPT * CM_THREADS * 4;
+}
+
+void chain_match(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
+    if (a.n <= 0) return;
+    const dim3 grid((unsigned)((a.n + CM_TILE - 1) / CM_TILE));
+    if (a.generic)
+        hipLaunchKernelGGL(chain_match_k<true>, grid, dim3(CM_THREADS), chain_lds_bytes(a), stream, d_a);
+    else
+        hipLaunchKernelGGL(chain_match_k<false>, grid, dim3(CM_THREADS), chain_lds_bytes(a), stream, d_a);
+}
+
+void chain_deque(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
+    if (a.n <= 0) return;
+    const dim3 grid((unsigned)((a.n + (int64_t)DQ_THREADS * DQ_CHUNK - 1) / ((int64_t)DQ_THREADS * DQ_CHUNK)));
+    switch (a.sp.scan_t) {
+        case VK_I32: hipLaunchKernelGGL(chain_deque_k<VK_I32>, grid, dim3(DQ_THREADS), 0, stream, d_a); break;
+        case VK_I64: hipLaunchKernelGGL(chain_deque_k<VK_I64>, grid, dim3(DQ_THREADS), 0, stream, d_a); break;
+        case VK_F32: hipLaunchKernelGGL(chain_deque_k<VK_F32>, grid, dim3(DQ_THREADS), 0, stream, d_a); break;
+        case VK_F64: hipLaunchKernelGGL(chain_deque_k<VK_F64>, grid, dim3(DQ_THREADS), 0, stream, d_a); break;
+        case VK_BOOL: hipLaunchKernelGGL(chain_deque_k<VK_BOOL>, grid, dim3(DQ_THREADS), 0, stream, d_a); break;
+        default: hipLaunchKernelGGL(chain_deque_k<VK_STR>, grid, dim3(DQ_THREADS), 0, stream, d_a); break;
+    }
+    hipLaunchKernelGGL(chain_ovf_k, dim3(512), dim3(256), 0, stream, d_a);
+}
+
+void chain_carry(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
+    if (a.cin_n <= 0) return;
+    hipLaunchKernelGGL(chain_carry_k, dim3((unsigned)((a.cin_n + 255) / 256)), dim3(256), 0, stream, d_a);
+}
+
+}  // namespace sdg

@@ -50,7 +50,34 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks = nul
 // One block per tile of CM_THREADS * CM_EPT sorted events; the block reserves its output range with one atomic.
 constexpr int CM_THREADS = 256;
 constexpr int CM_EPT = 8;
+constexpr int CM_TILE = CM_THREADS * CM_EPT;
+constexpr int CM_HALO = 256;                         // rows staged past the tile (scans continue in HBM beyond)
+constexpr int CM_ROWS = CM_TILE + CM_HALO;
+constexpr int CM_SCOLS = 2;                          // columns of the state-1 filter staged in LDS
+// the part of the plan the chain kernels read, copied into their argument block: ChainArgs is read through a
+// __restrict__ const kernel pointer, so these loads are scalar (SMEM) and the values provably wave-uniform
+struct ChainSpec {
+    int32_t n_states, has_within;
+    int64_t within_ms;
+    FastPred f0, f1;
+    Prog prog0, prog1;                // state filters (bytecode, when f0/f1 are FP_NONE)
+    int32_t n_out, n_cols;
+    Prog out_prog[MAX_OUT];
+    Instr out_ins[MAX_OUT];           // the select expression when it is one OP_LOAD (out_direct)
+    uint8_t out_direct[MAX_OUT];
+    uint8_t col_kind[MAX_COLS];
+    // the e2 filter as a typed scan: `e2.scan_col OP k` (scan_e2_left) or `k OP e2.scan_col`, compared as kind
+    // scan_t; k = scan_konst (SCAN_CONST) or e1.e1_col converted to scan_t (SCAN_E1); SCAN_TRUE: no filter;
+    // SCAN_GENERIC: f1 / the bytecode per row
+    int32_t scan_mode;
+    int32_t scan_col, e1_col;
+    uint8_t scan_col_kind, e1_col_kind, scan_t, scan_op, scan_e2_left;
+    int64_t scan_konst;
+};
+enum ScanMode : int32_t { SCAN_GENERIC = 0, SCAN_TRUE = 1, SCAN_CONST = 2, SCAN_E1 = 3 };
+
 struct ChainArgs {
+    ChainSpec sp;
     const Plan* plan;                 // device copy
     const Instr* code;
     const int64_t* consts;
@@ -70,9 +97,9 @@ struct ChainArgs {
     int64_t out_cap;
     unsigned long long* out_count;
     int64_t* out_ts;
-    uint32_t* out_key;
+    uint32_t* out_key;                // nullptr: not written
     int64_t* out_vals;                // [n_out][out_cap]
-    uint32_t* out_nulls;              // [out_cap] bit per output attribute
+    uint32_t* out_nulls;              // [out_cap] bit per output attribute (written when write_nulls)
     int64_t* out_emit_seq;            // sequence number of the event that completed the match
     int64_t* out_first_seq;           // sequence number of e1
     // partials still pending at the end of the batch
@@ -92,9 +119,35 @@ struct ChainArgs {
     const uint32_t* cin_nulls;
     int64_t cin_cap;
     int* flags;                       // [0] overflow, [1] non-monotonic timestamps within a key
+    // LDS staging (chain_match_k): columns mirrored in LDS and their slot per column (-1: HBM only)
+    int32_t n_stage;
+    int32_t stage_col[CM_SCOLS];
+    int8_t stage_of[MAX_COLS];
+    int32_t lds_stack;                // 1: some filter / select runs the bytecode (needs the LDS stack)
+    int32_t generic;                  // 1: bytecode or SCAN_GENERIC needed -> chain_match_k<true>
+    int32_t scan_lds;                 // 1: the typed scan's column is staged and has no nulls (LDS-only loop)
+    // deque path (chain_deque_k): per-row match results mq[n] (e2 row | MQ_NONE | MQ_CARRY), rows whose lane
+    // deque overflowed go to ovf_rows for a forward scan (chain_ovf_k); chain_match_k then only emits
+    int32_t deque_mode;               // DQ_OFF / DQ_STACK (x OP top.y pops a suffix) / DQ_ALL (a match completes all)
+    int32_t f0_on_x;                  // c0 is `scan_col OP const` (evaluated on the loaded value)
+    uint32_t* mq;                     // [n]
+    unsigned long long* ovf_count;
+    uint32_t* ovf_rows;               // [n]
+    const uint32_t* mq_in;            // chain_match_k: results to emit (nullptr: scan itself)
+    int32_t write_nulls;              // 0: no output can be null (out_nulls is not written)
 };
-void chain_match(const ChainArgs& a, hipStream_t stream);
-void chain_carry(const ChainArgs& a, hipStream_t stream);
+enum DequeMode : int32_t { DQ_OFF = 0, DQ_STACK = 1, DQ_ALL = 2 };
+constexpr uint32_t MQ_NONE = 0xFFFFFFFFu, MQ_CARRY = 0xFFFFFFFEu, MQ_OVF = 0xFFFFFFFDu;
+constexpr int DQ_THREADS = 256;
+constexpr int DQ_CHUNK = 64;                         // consecutive sorted rows per lane
+constexpr int DQ_GROUP = 8;                          // rows loaded per step
+constexpr int DQ_DEPTH = 8;                          // deque entries per lane (LDS ring); more -> ovf_rows
+size_t chain_lds_bytes(const ChainArgs& a);
+// deque path: rows -> mq (+ overflow rows resolved by forward scans)
+void chain_deque(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
+// kernel arguments are read from a device copy (d_a) of `a`: the struct is too large to index as a kernarg
+void chain_match(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
+void chain_carry(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
 
 // ---- generic keyed NFA (nfa.h): one lane per partition key walks that key's events in order --------------
 struct NfaArgs {

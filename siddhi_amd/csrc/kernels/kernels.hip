@@ -1,4 +1,5 @@
-// gfx950 kernels of the pattern/sequence path: key grouping and the chain matcher.
+// gfx950 kernels of the pattern/sequence path: key grouping and the generic keyed NFA (the chain matcher is
+// in chain.hip).
 //
 // Wave64 throughout: ballots are 64-bit, lane masks use __lanemask_lt(), compaction is ballot + mbcnt with one
 // atomic per wave. Everything is integer/byte work bound by HBM, so no MFMA.
@@ -8,28 +9,11 @@
 
 #include "../engine/eval.h"
 #include "kernels.h"
+#include "wave.h"
 
 namespace sdg {
 
 namespace {
-
-__device__ __forceinline__ int lane_id() { return __lane_id(); }
-
-__device__ __forceinline__ uint64_t lanemask_lt() {
-    int l = lane_id();
-    return l == 0 ? 0ull : (~0ull >> (64 - l));
-}
-
-// wave-level compaction: returns this lane's slot (valid only where `take`), one atomic per wave
-__device__ __forceinline__ int64_t wave_reserve(bool take, unsigned long long* counter) {
-    uint64_t m = __ballot(take);
-    if (m == 0) return -1;
-    int leader = __ffsll((unsigned long long)m) - 1;
-    unsigned long long base = 0;
-    if (lane_id() == leader) base = atomicAdd(counter, (unsigned long long)__popcll(m));
-    base = __shfl(base, leader);
-    return (int64_t)base + __popcll(m & lanemask_lt());
-}
 
 // ---------------------------------------------------------------------------------------------------------
 // key grouping: LSD radix passes
@@ -233,246 +217,6 @@ __global__ __launch_bounds__(256) void rx_segments(const uint32_t* __restrict__ 
     if (p == n - 1 || keys[p + 1] != k) seg_end[k] = (uint32_t)(p + 1);
 }
 
-// ---------------------------------------------------------------------------------------------------------
-// chain matcher
-
-struct ChainAcc {
-    const ChainArgs* A;
-    int64_t r0, c0, r1;
-    __device__ void load(int slot, int col, int chain, uint8_t kind, int64_t* v, bool* null) {
-        *v = 0;
-        *null = true;
-        if (!(chain == 0 || chain == -1)) return;  // a plain state's chain holds exactly one event
-        int64_t row;
-        if (slot == 0) {
-            if (c0 >= 0) {
-                *v = A->cin_vals[(int64_t)col * A->cin_cap + c0];
-                *null = (A->cin_nulls[c0] >> col) & 1u;
-                return;
-            }
-            row = r0;
-        } else if (slot == 1) {
-            row = r1;
-        } else {
-            return;
-        }
-        if (row < 0) return;
-        *v = load_col(A->cols[col], kind, row);
-        *null = A->nulls[col] ? A->nulls[col][row] != 0 : false;
-    }
-    __device__ bool slot_empty(int slot, int chain) {
-        if (!(chain == 0 || chain == -1)) return true;
-        if (slot == 0) return !(c0 >= 0 || r0 >= 0);
-        if (slot == 1) return r1 < 0;
-        return true;
-    }
-};
-
-__device__ __forceinline__ int qstream_of(const ChainArgs& a, int64_t row) {
-    return a.qstream ? (int)a.qstream[row] : 0;
-}
-
-// scan the key's events after `from` (exclusive) for the e2 of a partial whose e1 is at ts0.
-// returns: >= 0 the matching row; -1 expired (dead); -2 reached the end of the segment (carry)
-__device__ __forceinline__ int64_t chain_scan(const ChainArgs& a, ChainAcc& acc, int64_t from, int64_t end, int64_t ts0,
-                                              int64_t* stk, int stride) {
-    const Plan* P = a.plan;
-    const int32_t has_within = P->has_within;
-    const int64_t within = P->within_ms;
-    const Prog c1 = P->st[1].filter;
-    const FastPred f1 = P->fast[1];
-    for (int64_t q = from; q < end; ++q) {
-        int64_t tq = a.ts[q];
-        // StreamPreStateProcessor.isExpired: |start.ts - now| > within, checked before the event is processed
-        if (has_within) {
-            int64_t d = ts0 - tq;
-            if (d < 0) d = -d;
-            if (d > within) return -1;
-        }
-        if (qstream_of(a, q) == a.s1) {
-            acc.r1 = q;
-            bool ok = f1.kind == FP_TRUE ? true
-                      : f1.kind == FP_NONE ? pass(a.code, c1, a.consts, acc, stk, stride)
-                                           : fast_pass(f1, acc);
-            if (ok) return q;
-            acc.r1 = -1;
-        }
-    }
-    return -2;
-}
-
-// select expressions: a plain attribute (`e1.id`) is loaded directly, anything else runs the bytecode
-__device__ __forceinline__ void eval_out(const ChainArgs& a, const Prog pr, ChainAcc& acc, int64_t* stk, int stride,
-                                         int64_t* v, bool* nl) {
-    if (pr.len == 1 && a.code[pr.start].op == OP_LOAD) {
-        const Instr in = a.code[pr.start];
-        acc.load(in.a, in.b, in.c, in.k, v, nl);
-    } else {
-        run(a.code, pr, a.consts, acc, stk, stride, v, nl);
-    }
-}
-
-__device__ __forceinline__ void emit_match(const ChainArgs& a, ChainAcc& acc, int64_t slot, int64_t q, uint32_t key,
-                                           int64_t first_seq, int64_t* stk, int stride) {
-    const Plan* P = a.plan;
-    a.out_ts[slot] = a.ts[q];
-    a.out_key[slot] = key;
-    a.out_emit_seq[slot] = a.seq_base + (a.orig ? (int64_t)a.orig[q] : q);
-    a.out_first_seq[slot] = first_seq;
-    uint32_t nm = 0;
-    acc.r1 = P->n_states > 1 ? q : -1;
-    for (int j = 0; j < P->n_out; ++j) {
-        int64_t v;
-        bool nl;
-        eval_out(a, P->out_prog[j], acc, stk, stride, &v, &nl);
-        a.out_vals[(int64_t)j * a.out_cap + slot] = v;
-        if (nl) nm |= 1u << j;
-    }
-    a.out_nulls[slot] = nm;
-}
-
-// block-wide exclusive scan of two per-thread counts; one atomic per block and counter reserves the block's
-// output range (per-wave reservations on one global counter serialise in L2 at ~10^8/s)
-__device__ __forceinline__ void block_reserve2(uint32_t c0, uint32_t c1, unsigned long long* ctr0,
-                                               unsigned long long* ctr1, int64_t* off0, int64_t* off1) {
-    __shared__ uint32_t wtot[2][CM_THREADS / 64];
-    __shared__ unsigned long long bbase[2];
-    const int lane = lane_id(), w = threadIdx.x >> 6;
-    uint32_t x0 = c0, x1 = c1;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y0 = __shfl_up(x0, d), y1 = __shfl_up(x1, d);
-        if (lane >= d) { x0 += y0; x1 += y1; }
-    }
-    if (lane == 63) { wtot[0][w] = x0; wtot[1][w] = x1; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t t0 = 0, t1 = 0;
-        for (int v = 0; v < CM_THREADS / 64; ++v) {
-            uint32_t u0 = wtot[0][v], u1 = wtot[1][v];
-            wtot[0][v] = t0; wtot[1][v] = t1;
-            t0 += u0; t1 += u1;
-        }
-        bbase[0] = t0 ? atomicAdd(ctr0, (unsigned long long)t0) : 0ull;
-        bbase[1] = t1 ? atomicAdd(ctr1, (unsigned long long)t1) : 0ull;
-    }
-    __syncthreads();
-    *off0 = (int64_t)bbase[0] + wtot[0][w] + (x0 - c0);
-    *off1 = (int64_t)bbase[1] + wtot[1][w] + (x1 - c1);
-}
-
-constexpr uint32_t CM_NONE = 0xFFFFFFFFu, CM_CARRY = 0xFFFFFFFEu;
-
-// one block per tile of CM_THREADS * CM_EPT sorted events; lane t takes events base + r * CM_THREADS + t
-__global__ __launch_bounds__(CM_THREADS) void chain_match_k(ChainArgs a) {
-    __shared__ int64_t stack_mem[STACK * CM_THREADS];
-    int64_t* stk = stack_mem + threadIdx.x;
-    const int stride = CM_THREADS;
-    const Plan* P = a.plan;
-    const int64_t base = (int64_t)blockIdx.x * (CM_THREADS * CM_EPT);
-    const FastPred f0 = P->fast[0];
-    uint32_t res[CM_EPT];
-    uint32_t nmatch = 0, ncarry = 0;
-#pragma unroll
-    for (int r = 0; r < CM_EPT; ++r) {
-        const int64_t p = base + r * CM_THREADS + threadIdx.x;
-        res[r] = CM_NONE;
-        if (p >= a.n) continue;
-        ChainAcc acc{&a, p, -1, -1};
-        const uint32_t key = a.key ? a.key[p] : 0u;
-        if (p > 0 && a.ts[p] < a.ts[p - 1] && (!a.key || a.key[p - 1] == key)) atomicOr(&a.flags[1], 1);
-        bool c0 = false;
-        if (qstream_of(a, p) == a.s0)
-            c0 = f0.kind == FP_TRUE ? true
-                 : f0.kind == FP_NONE ? pass(a.code, P->st[0].filter, a.consts, acc, stk, stride) : fast_pass(f0, acc);
-        if (!c0) continue;
-        if (P->n_states == 1) {
-            res[r] = (uint32_t)p;
-        } else {
-            const int64_t end = a.key ? (int64_t)a.seg_end[key] : a.n;
-            const int64_t q = chain_scan(a, acc, p + 1, end, a.ts[p], stk, stride);
-            res[r] = q >= 0 ? (uint32_t)q : q == -2 ? CM_CARRY : CM_NONE;
-        }
-        nmatch += res[r] < CM_CARRY;
-        ncarry += res[r] == CM_CARRY;
-    }
-    int64_t slot, cs;
-    block_reserve2(nmatch, ncarry, a.out_count, a.carry_count, &slot, &cs);
-#pragma unroll
-    for (int r = 0; r < CM_EPT; ++r) {
-        if (res[r] == CM_NONE) continue;
-        const int64_t p = base + r * CM_THREADS + threadIdx.x;
-        const uint32_t key = a.key ? a.key[p] : 0u;
-        const int64_t seq = a.seq_base + (a.orig ? (int64_t)a.orig[p] : p);
-        if (res[r] != CM_CARRY) {
-            if (slot >= a.out_cap) {
-                atomicOr(&a.flags[0], 1);
-            } else {
-                ChainAcc acc{&a, p, -1, -1};
-                emit_match(a, acc, slot, (int64_t)res[r], key, seq, stk, stride);
-            }
-            ++slot;
-        } else {
-            if (cs >= a.carry_cap) {
-                atomicOr(&a.flags[0], 1);
-            } else {
-                a.carry_key[cs] = key;
-                a.carry_ts[cs] = a.ts[p];
-                a.carry_seq[cs] = seq;
-                uint32_t nm = 0;
-                for (int c = 0; c < P->n_cols; ++c) {
-                    a.carry_vals[(int64_t)c * a.carry_cap + cs] = load_col(a.cols[c], P->col_kind[c], p);
-                    if (a.nulls[c] && a.nulls[c][p]) nm |= 1u << c;
-                }
-                a.carry_nulls[cs] = nm;
-            }
-            ++cs;
-        }
-    }
-}
-
-__global__ __launch_bounds__(256) void chain_carry_k(ChainArgs a) {
-    __shared__ int64_t stack_mem[STACK * 256];
-    int64_t* stk = stack_mem + threadIdx.x;
-    const int stride = 256;
-    const Plan* P = a.plan;
-    int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    bool active = c < a.cin_n;
-    bool has = false, carry = false;
-    int64_t qhit = -1;
-    ChainAcc acc{&a, -1, c, -1};
-    uint32_t key = 0;
-    if (active) {
-        key = a.cin_key[c];
-        int64_t b = 0, e = a.n;
-        if (a.key) {
-            b = key < (uint32_t)a.K ? (int64_t)a.seg_start[key] : 0;
-            e = key < (uint32_t)a.K ? (int64_t)a.seg_end[key] : 0;
-        }
-        int64_t r = chain_scan(a, acc, b, e, a.cin_ts[c], stk, stride);
-        if (r >= 0) { has = true; qhit = r; }
-        else if (r == -2) carry = true;
-    }
-    int64_t slot = wave_reserve(has, a.out_count);
-    if (has) {
-        if (slot >= a.out_cap) atomicOr(&a.flags[0], 1);
-        else emit_match(a, acc, slot, qhit, key, a.cin_seq[c], stk, stride);
-    }
-    int64_t cs = wave_reserve(carry, a.carry_count);
-    if (carry) {
-        if (cs >= a.carry_cap) {
-            atomicOr(&a.flags[0], 1);
-        } else {
-            a.carry_key[cs] = key;
-            a.carry_ts[cs] = a.cin_ts[c];
-            a.carry_seq[cs] = a.cin_seq[c];
-            for (int k = 0; k < P->n_cols; ++k)
-                a.carry_vals[(int64_t)k * a.carry_cap + cs] = a.cin_vals[(int64_t)k * a.cin_cap + c];
-            a.carry_nulls[cs] = a.cin_nulls[c];
-        }
-    }
-}
-
 // one lane per key: the key's arena is private to the lane, so the state machine runs without atomics; only
 // the output slot reservation is shared
 __global__ __launch_bounds__(256) void nfa_k(NfaArgs a) {
@@ -590,17 +334,6 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
     hipLaunchKernelGGL(rx_segments, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, stream, a.keys_sorted, a.n,
                        a.seg_start, a.seg_end);
     if (marks) (void)hipEventRecord(marks[3], stream);
-}
-
-void chain_match(const ChainArgs& a, hipStream_t stream) {
-    if (a.n <= 0) return;
-    const int64_t tile = CM_THREADS * CM_EPT;
-    hipLaunchKernelGGL(chain_match_k, dim3((unsigned)((a.n + tile - 1) / tile)), dim3(CM_THREADS), 0, stream, a);
-}
-
-void chain_carry(const ChainArgs& a, hipStream_t stream) {
-    if (a.cin_n <= 0) return;
-    hipLaunchKernelGGL(chain_carry_k, dim3((unsigned)((a.cin_n + 255) / 256)), dim3(256), 0, stream, a);
 }
 
 void nfa_run(const NfaArgs& a, hipStream_t stream) {

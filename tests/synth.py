@@ -73,3 +73,50 @@ def run(adapter, tr, batches=1):
             adapter.flush()
     return [(o["name"], o["ts"], tuple(o["values"])) for o in adapter.outputs()
             if o["kind"] == "query" and not o["expired"]]
+
+
+# ---- chain-path shapes (every e1=S[c0] -> e2=S[c1], one stream): deque (stack / complete-all) and scan ----
+def chain_app(c0, c1, within="within 30 milliseconds", sel="e1.id as a, e2.id as b"):
+    return part("@info(name='q') from every e1=S[%s] -> e2=S%s %s select %s insert into O;"
+                % (c0, "[%s]" % c1 if c1 else "", within, sel))
+
+
+CHAIN_APPS = {  # name -> (app, expected sdg_stats.deque: 1 stack, 2 complete-all, 0 forward scan)
+    "gt": (chain_app("price>20", "price>e1.price"), 1),
+    "ge": (chain_app("price>20", "price>=e1.price"), 1),
+    "lt": (chain_app("price<80", "price<e1.price"), 1),
+    "le_flipped": (chain_app("price<80", "e1.price>=price"), 1),
+    "int_gt_nowithin": (chain_app("volume>10", "volume>e1.volume", within=""), 1),
+    "const": (chain_app("price>20", "price>90"), 2),
+    "no_filter": (chain_app("volume<50", ""), 2),
+    "ne_const": (chain_app("price>20", "price!=e1.price"), 0),
+    "cross_col": (chain_app("price>20", "volume>e1.price"), 0),
+    "e1_const_e2": (chain_app("price>20", "e1.volume>50"), 0),
+    "arith_sel": (chain_app("price>20", "price>e1.price", sel="e1.id as a, e2.price - e1.price as d"), 0),
+}
+
+
+def descending_trace(n, keys=3, seed=0, run=200):
+    """long descending price runs per key (deque overflow: every pending partial stays pending)"""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        k = int(rng.integers(0, keys))
+        price = float(100.0 - (i % run) * 0.25) if rng.random() < 0.97 else float(np.round(rng.uniform(0, 100), 1))
+        out.append(("S", 1000 + i // 4, [i, "k%d" % k, price, int(rng.integers(0, 100))]))
+    return out
+
+
+def nan_trace(n, keys=4, seed=0, nan_rate=0.05, null_rate=0.05):
+    rng = np.random.default_rng(seed)
+    out = []
+    ts = 1000 + np.cumsum(rng.integers(0, 3, size=n))
+    for i in range(n):
+        price = float(np.round(rng.uniform(0, 100), 1))
+        u = rng.random()
+        if u < nan_rate:
+            price = float("nan")
+        elif u < nan_rate + null_rate:
+            price = None
+        out.append(("S", int(ts[i]), [i, "k%d" % rng.integers(0, keys), price, int(rng.integers(0, 100))]))
+    return out

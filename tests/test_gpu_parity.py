@@ -170,3 +170,33 @@ def test_generic_nfa_many_keys_on_gpu(oracle_built):
         p.close()
     assert len(ref) > 100
     assert got == ref
+
+
+# ---- chain path: deque kernel (stack / complete-all) and forward scans on one stream ----------------------
+@pytest.mark.parametrize("name", sorted(synth.CHAIN_APPS))
+@pytest.mark.parametrize("shape", ["k5_b1", "k200_b4", "desc_b3", "nan_b2"])
+def test_chain_shapes_on_gpu(name, shape, oracle_built):
+    app, deque = synth.CHAIN_APPS[name]
+    seed = zlib.crc32((name + shape).encode()) % 1000
+    if shape == "k5_b1":
+        tr, batches = synth.trace(4000, keys=5, seed=seed, two_streams=False), 1
+    elif shape == "k200_b4":
+        tr, batches = synth.trace(20000, keys=200, seed=seed, two_streams=False), 4
+    elif shape == "desc_b3":
+        tr, batches = synth.descending_trace(6000, keys=3, seed=seed), 3
+    else:
+        tr, batches = synth.nan_trace(5000, seed=seed), 2
+    o = Oracle(app)
+    try:
+        ref = synth.run(o, tr)
+    finally:
+        o.close()
+    p = ProductAdapter(app)
+    try:
+        assert p.rt.query_paths() == [0]
+        got = synth.run(p, tr, batches)
+        assert p.rt.stats().deque == deque
+    finally:
+        p.close()
+    assert len(ref) > 0
+    assert got == ref
