@@ -105,103 +105,112 @@ struct RxPass {
     int bits;
 };
 
-// stable tile scatter
+// stable tile scatter. Tile element e = w * 1024 + r * 64 + lane belongs to wave w (16 rounds r), so a wave
+// ranks its own elements in order with wave-private digit counters (ballot match over the digit bits; the
+// LDS ops of one wave are in order, so no block barrier while counting). Then per digit: prefix over waves
+// and the tile's digit starts; each column is staged in LDS in digit order and written out as coalesced runs
+// (keys and original rows together as one 8-byte word).
 __global__ __launch_bounds__(RX_THREADS) void rx_scatter(RxPass a) {
-    constexpr int R = RX_TILE / RX_THREADS;  // rounds (16): element r*256 + t of the tile
-    __shared__ uint32_t cnt[1 << RX_MAXBITS];
-    __shared__ uint32_t wavecnt[RX_THREADS / 64][1 << RX_MAXBITS];
+    constexpr int R = RX_TILE / RX_THREADS;  // 16 elements per lane
+    constexpr int NW = RX_THREADS / 64;
+    __shared__ uint16_t wc[NW][1 << RX_MAXBITS];  // per-wave digit counts (<= 1024), then per-wave digit bases
     __shared__ uint32_t tstart[1 << RX_MAXBITS];
     __shared__ uint32_t gbase[1 << RX_MAXBITS];
     __shared__ uint32_t dest[RX_TILE];
     __shared__ uint64_t stage[RX_TILE];
-    const int t = threadIdx.x, w = t >> 6;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const int64_t base = (int64_t)blockIdx.x * RX_TILE;
     const int64_t tile_n = min((int64_t)RX_TILE, a.n - base);
+    const int64_t wbase = base + w * (R * 64);
     for (int d = t; d < a.nb; d += RX_THREADS) {
-        cnt[d] = 0;
         gbase[d] = a.offsets[(int64_t)blockIdx.x * a.nb + d];
-        for (int v = 0; v < RX_THREADS / 64; ++v) wavecnt[v][d] = 0;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) wc[v][d] = 0;
     }
     __syncthreads();
     const uint64_t lt = lanemask_lt();
     uint32_t rank[R];
-    uint16_t dig[R];
+    uint8_t dig[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        int64_t i = base + r * RX_THREADS + t;
-        bool valid = i < a.n;
-        uint32_t d = valid ? digit_of(a.keys_in[i], a.shift, a.mask) : 0u;
+        const int64_t i = wbase + r * 64 + lane;
+        const bool valid = i < a.n;
+        const uint32_t d = valid ? digit_of(a.keys_in[i], a.shift, a.mask) : 0u;
         uint64_t peers = __ballot(valid);
         for (int bit = 0; bit < a.bits; ++bit) {
-            bool on = (d >> bit) & 1u;
-            uint64_t b = __ballot(on);
+            const bool on = (d >> bit) & 1u;
+            const uint64_t b = __ballot(on);
             peers &= on ? b : ~b;
         }
-        int leader = peers ? __ffsll((unsigned long long)peers) - 1 : 0;
-        if (valid && lane_id() == leader) wavecnt[w][d] = (uint32_t)__popcll(peers);
-        __syncthreads();
-        uint32_t pre = 0;
-        if (valid) {
-            pre = cnt[d];
-            for (int v = 0; v < w; ++v) pre += wavecnt[v][d];
-        }
-        rank[r] = pre + (uint32_t)__popcll(peers & lt);
-        dig[r] = (uint16_t)d;
-        __syncthreads();
-        for (int dd = t; dd < a.nb; dd += RX_THREADS) {
-            uint32_t s = 0;
-            for (int v = 0; v < RX_THREADS / 64; ++v) {
-                s += wavecnt[v][dd];
-                wavecnt[v][dd] = 0;
-            }
-            cnt[dd] += s;
-        }
-        __syncthreads();
+        const uint32_t before = valid ? wc[w][d] : 0u;
+        rank[r] = before + (uint32_t)__popcll(peers & lt);
+        dig[r] = (uint8_t)d;
+        const int leader = peers ? __ffsll((unsigned long long)peers) - 1 : -1;
+        if (valid && lane == leader) wc[w][d] = (uint16_t)(before + (uint32_t)__popcll(peers));
     }
-    // tile-local start of each digit run (exclusive scan of cnt over nb <= 256 digits)
-    if (t < 256) tstart[t] = t < a.nb ? cnt[t] : 0;
     __syncthreads();
+    // per digit: exclusive prefix over waves (in place) and the digit's tile total
+    uint32_t tot = 0;
+    if (t < 256) {
+        if (t < a.nb) {
+#pragma unroll
+            for (int v = 0; v < NW; ++v) {
+                const uint32_t c = wc[v][t];
+                wc[v][t] = (uint16_t)tot;
+                tot += c;
+            }
+        }
+        tstart[t] = tot;
+    }
+    __syncthreads();
+    // exclusive scan of the digit totals (nb <= 256) -> tile-local start of each digit run
     for (int off = 1; off < 256; off <<= 1) {
-        uint32_t x = (t < 256 && t >= off) ? tstart[t - off] : 0;
+        const uint32_t x = (t < 256 && t >= off) ? tstart[t - off] : 0u;
         __syncthreads();
         if (t < 256) tstart[t] += x;
         __syncthreads();
     }
-    if (t < 256) tstart[t] -= (t < a.nb ? cnt[t] : 0);
+    if (t < 256) tstart[t] -= tot;
     __syncthreads();
     uint32_t sp[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        int64_t i = base + r * RX_THREADS + t;
-        sp[r] = tstart[dig[r]] + rank[r];
-        if (i < a.n) dest[sp[r]] = gbase[dig[r]] + rank[r];
+        const int64_t i = wbase + r * 64 + lane;
+        const uint32_t wr = wc[w][dig[r]] + rank[r];  // rank among the tile's elements of this digit
+        sp[r] = tstart[dig[r]] + wr;
+        if (i < a.n) dest[sp[r]] = gbase[dig[r]] + wr;
     }
-    __syncthreads();
-    // keys, original rows, then every payload column: stage in digit order, write runs out coalesced
-    for (int c = -2; c < a.ncols; ++c) {
-        int wd = c < 0 ? 4 : a.width[c];
+    // keys | original rows as one word, then every payload column
+    for (int c = -1; c < a.ncols; ++c) {
+        const int wd = c < 0 ? 8 : a.width[c];
+        const void* src = c < 0 ? nullptr : a.src[c];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            int64_t i = base + r * RX_THREADS + t;
+            const int64_t i = wbase + r * 64 + lane;
             if (i < a.n) {
                 uint64_t v;
-                if (c == -2) v = a.keys_in[i];
-                else if (c == -1) v = a.orig_in ? a.orig_in[i] : (uint32_t)i;
-                else if (wd == 8) v = ((const uint64_t*)a.src[c])[i];
-                else if (wd == 4) v = ((const uint32_t*)a.src[c])[i];
-                else v = ((const uint8_t*)a.src[c])[i];
+                if (c < 0) v = (uint64_t)a.keys_in[i] | ((uint64_t)(a.orig_in ? a.orig_in[i] : (uint32_t)i) << 32);
+                else if (wd == 8) v = ((const uint64_t*)src)[i];
+                else if (wd == 4) v = ((const uint32_t*)src)[i];
+                else v = ((const uint8_t*)src)[i];
                 stage[sp[r]] = v;
             }
         }
         __syncthreads();
+        void* dst = c < 0 ? nullptr : a.dst[c];
         for (int j = t; j < tile_n; j += RX_THREADS) {
-            uint32_t o = dest[j];
-            uint64_t v = stage[j];
-            if (c == -2) a.keys_out[o] = (uint32_t)v;
-            else if (c == -1) a.orig_out[o] = (uint32_t)v;
-            else if (wd == 8) ((uint64_t*)a.dst[c])[o] = v;
-            else if (wd == 4) ((uint32_t*)a.dst[c])[o] = (uint32_t)v;
-            else ((uint8_t*)a.dst[c])[o] = (uint8_t)v;
+            const uint32_t o = dest[j];
+            const uint64_t v = stage[j];
+            if (c < 0) {
+                a.keys_out[o] = (uint32_t)v;
+                a.orig_out[o] = (uint32_t)(v >> 32);
+            } else if (wd == 8) {
+                ((uint64_t*)dst)[o] = v;
+            } else if (wd == 4) {
+                ((uint32_t*)dst)[o] = (uint32_t)v;
+            } else {
+                ((uint8_t*)dst)[o] = (uint8_t)v;
+            }
         }
         __syncthreads();
     }
