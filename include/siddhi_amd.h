@@ -59,6 +59,7 @@ typedef struct sdg_opts {
 } sdg_opts;
 #define SDG_COMPILE_ONLY 1
 #define SDG_FORCE_GENERIC 2    /* run every query on the generic keyed-NFA kernel (testing: both kernels on one query) */
+#define SDG_NO_FUSED 4         /* chain path: always key-sort with the full radix (testing: both chain kernels on one query) */
 
 typedef struct sdg_out {
     int64_t n;                 /* output events */
@@ -114,6 +115,8 @@ typedef struct sdg_stats {
     double ms_nfa;             /* generic keyed-NFA kernel */
     double ms_chain_emit;      /* chain path: match-record emission (ms_chain_match is then the deque pass) */
     int32_t deque;             /* chain path took the deque kernel (1 stack, 2 complete-all), 0 forward scans */
+    int32_t fused;             /* chain path: 1 fused bucket matcher, 2 tried it and fell back to the radix path */
+    int64_t fused_ovf;         /* fused path: partials resolved by the key-filtered bucket scan in HBM */
 } sdg_stats;
 int sdg_last_stats(sdg_engine* e, sdg_stats* out);
 

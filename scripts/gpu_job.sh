@@ -15,7 +15,7 @@ run() {  # name timeout cmd...
     local rc=$?
     echo "== $name rc=$rc" | tee -a "$OUT/steps.log"
     tail -5 "$OUT/$name.log"
-    if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+    if [ $rc -ne 0 ]; then
         echo "fatal rc=$rc in $name: stopping" | tee -a "$OUT/steps.log"; exit $rc
     fi
     return 0

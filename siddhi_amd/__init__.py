@@ -77,7 +77,9 @@ class Stats(ctypes.Structure):
                 ("ms_chain_match", ctypes.c_double),
                 ("ms_nfa", ctypes.c_double),
                 ("ms_chain_emit", ctypes.c_double),
-                ("deque", ctypes.c_int32)]
+                ("deque", ctypes.c_int32),
+                ("fused", ctypes.c_int32),
+                ("fused_ovf", ctypes.c_int64)]
 
 
 _lib = None
@@ -191,11 +193,12 @@ class InputHandler:
 
 
 class SiddhiAppRuntime:
-    def __init__(self, app_text, device=0, batch_capacity=0, compile_only=False, force_generic=False):
+    def __init__(self, app_text, device=0, batch_capacity=0, compile_only=False, force_generic=False, fused=True):
         L = load_library()
         self._L = L
         h = ctypes.c_void_p()
-        opts = _Opts(device, batch_capacity, 0, (1 if compile_only else 0) | (2 if force_generic else 0))
+        opts = _Opts(device, batch_capacity, 0,
+                     (1 if compile_only else 0) | (2 if force_generic else 0) | (0 if fused else 4))
         _check(L.sdg_compile(app_text.encode(), ctypes.byref(opts), ctypes.byref(h)))
         self._h = h
         self.playback = "@app:playback" in app_text.replace(" ", "").lower()

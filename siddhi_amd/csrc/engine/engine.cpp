@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <numeric>
@@ -116,6 +117,7 @@ struct QueryRt {
     DevBuf st_ts, st_qs, st_key, st_cols[MAX_COLS], st_nulls[MAX_COLS];
     // sorted view
     DevBuf so_ts, so_qs, so_key, so_orig, so_cols[MAX_COLS], so_nulls[MAX_COLS], seg, kg_counts, kg_gsum;
+    DevBuf bk_plan;                                 // fused path: bstart[257] + bseg[257]
     // carries (double buffered)
     struct Carry {
         DevBuf key, ts, seq, vals, nulls;
@@ -163,6 +165,7 @@ struct sdg_engine {
     std::vector<std::vector<const char*>> out_names;
     bool compile_only = false;
     bool force_generic = false;
+    bool no_fused = false;
 };
 
 namespace {
@@ -407,9 +410,31 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     }
     // sorted positions and original rows are 32-bit on the device
     if (nrows >= (int64_t)0xFFFFFFF0) throw CompileError(SDG_ERR_CAPACITY, "a flush holds more than 2^32 - 16 events");
-    // ---- 2. key grouping ---------------------------------------------------------------------------------
     uint32_t K = 1;
     if (partitioned) K = q.string_keys ? (uint32_t)std::max<size_t>(e->strings.strs.size(), 1) : (uint32_t)std::max<size_t>(q.keydict.size(), 1);
+    // fused bucket path (chain.hip chain_fused_k): one radix pass into 2^bbits buckets + per-block regrouping in LDS
+    // instead of the full key sort. Shapes it covers: see kernels.h; anything else (or a batch that breaks its
+    // time-order precondition) runs the radix path below.
+    int kbits = 0;
+    while ((1ll << kbits) < (int64_t)K) ++kbits;
+    bool try_fused = false;
+    if (P.chain && partitioned && !multi_stream && nrows > 0 && !e->no_fused && P.n_states == 2 && P.has_within &&
+        nc >= 1 && kbits <= 16 && P.fast[0].kind != FP_NONE) {
+        ChainArgs pa;
+        std::memset(&pa, 0, sizeof pa);
+        for (int k = 0; k < nc; ++k) pa.nulls[k] = d_nulls[k];
+        pa.cin_n = q.carry[q.cur].n;
+        chain_staging(h, pa, q.carry_nullable);
+        const ChainSpec& ps = pa.sp;
+        const bool typed = ps.scan_mode == SCAN_TRUE ||
+                           ((ps.scan_mode == SCAN_CONST || ps.scan_mode == SCAN_E1) && ps.scan_col < nc && !d_nulls[ps.scan_col]);
+        try_fused = !pa.generic && typed && ps.scan_col >= 0 && ps.scan_col < nc;
+    }
+    e->stats.fused = 0;
+    const bool carry_nullable0 = q.carry_nullable;
+    // returns false when the fused path found its precondition broken (nothing of the batch is committed then)
+    auto run = [&](bool fused) -> bool {
+    // ---- 2. key grouping ---------------------------------------------------------------------------------
     const int64_t* v_ts = d_ts;
     const uint8_t* v_qs = d_qs;
     const uint32_t* v_key = nullptr;
@@ -420,6 +445,10 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     for (int k = 0; k < nc; ++k) { v_cols[k] = d_cols[k]; v_nulls[k] = d_nulls[k]; }
     HIPCHECK(hipEventRecord(e->ev[0], st));
     const uint32_t* v_segend = nullptr;
+    int* flags = (int*)q.flags.ensure(16);
+    int bbits = 0;
+    uint32_t* b_start = nullptr;
+    uint32_t* b_seg = nullptr;
     if (partitioned && nrows > 0) {
         KeyGroupArgs a;
         std::memset(&a, 0, sizeof a);
@@ -447,7 +476,24 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         a.orig_sorted = (uint32_t*)q.so_orig.ensure(nrows * 4);
         a.seg_start = (uint32_t*)q.seg.ensure((size_t)K * 4);
         a.seg_end = (uint32_t*)q.kg_gsum.ensure((size_t)K * 4);
-        keygroup(a, st, &e->ev[4]);
+        if (fused) {
+            bbits = std::max(1, std::min(8, kbits));
+            b_start = (uint32_t*)q.bk_plan.ensure(2 * 257 * 4);
+            b_seg = b_start + 257;
+            HIPCHECK(hipMemsetAsync(flags, 0, 16, st));
+            bucketize(a, bbits, 0 /* ts is payload column 0 */, flags + 3, b_start, b_seg, FU_OWN, st, &e->ev[4]);
+            if (getenv("SDG_DEBUG")) {  // validate the bucket plan on the host before the matcher reads it
+                std::vector<uint32_t> hp(2 * 257);
+                HIPCHECK(hipMemcpyAsync(hp.data(), b_start, 2 * 257 * 4, hipMemcpyDeviceToHost, st));
+                HIPCHECK(hipStreamSynchronize(st));
+                const int nbk = 1 << bbits;
+                bool okp = hp[nbk] == (uint32_t)nrows && hp[257 + nbk] <= (uint32_t)chain_fused_grid(nrows, nbk);
+                for (int d = 0; d < nbk; ++d) okp = okp && hp[d] <= hp[d + 1] && hp[257 + d] <= hp[257 + d + 1];
+                if (!okp) throw DeviceError("fused bucket plan inconsistent (n=" + std::to_string(nrows) + ")");
+            }
+        } else {
+            keygroup(a, st, &e->ev[4]);
+        }
         v_key = a.keys_sorted;
         v_seg = a.seg_start;
         v_segend = a.seg_end;
@@ -493,7 +539,6 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         int64_t cap = 2 * nrows + 4096;
         q.out_cap = cap;
         unsigned long long* counters = (unsigned long long*)q.counters.ensure(16);
-        int* flags = (int*)q.flags.ensure(16);
         HIPCHECK(hipMemsetAsync(counters, 0, 16, st));
         HIPCHECK(hipMemsetAsync(flags, 0, 16, st));
         a.out_cap = cap;
@@ -544,7 +589,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         e->stats.matches += q.out_n;
         e->stats.path = 1;
         q.seq += nrows;
-        return;
+        return true;
     }
     // ---- 3. chain matcher -------------------------------------------------------------------------------
     QueryRt::Carry& cin = q.carry[q.cur];
@@ -570,9 +615,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     a.s1 = P.n_states > 1 ? h.stream_pos(P.st[1].stream) : a.s0;
     a.out_cap = cap;
     unsigned long long* counters = (unsigned long long*)q.counters.ensure(16);
-    int* flags = (int*)q.flags.ensure(16);
     HIPCHECK(hipMemsetAsync(counters, 0, 16, st));
-    HIPCHECK(hipMemsetAsync(flags, 0, 16, st));
+    if (!fused) HIPCHECK(hipMemsetAsync(flags, 0, 16, st));  // fused: cleared before bucketize (mono flag)
     a.out_count = counters;
     a.carry_count = counters + 1;
     a.flags = flags;
@@ -600,7 +644,16 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     q.nulls_valid = a.write_nulls;
     q.carry_nullable = false;
     for (int k = 0; k < nc; ++k) q.carry_nullable |= a.nulls[k] != nullptr;
-    if (a.deque_mode != DQ_OFF && nrows > 0) {
+    if (fused) {
+        a.deque_mode = DQ_OFF;
+        a.bstart = b_start;
+        a.bseg = b_seg;
+        a.nb = 1 << bbits;
+        a.bbits = bbits;
+        a.lbits = std::max(0, kbits - bbits);
+        a.seg_start = a.seg_end = nullptr;
+    }
+    if ((a.deque_mode != DQ_OFF || fused) && nrows > 0) {
         a.mq = (uint32_t*)q.o_mq.ensure((size_t)nrows * 4);
         a.ovf_rows = (uint32_t*)q.o_ovf.ensure((size_t)nrows * 4);
         a.ovf_count = (unsigned long long*)q.o_ovfc.ensure(8);
@@ -611,9 +664,57 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     ChainArgs ae = a;  // emit-only pass over mq
     ae.mq_in = a.mq;
     HIPCHECK(hipMemcpyAsync(d_a + 1, &ae, sizeof ae, hipMemcpyHostToDevice, st));
+    static const bool dbg = getenv("SDG_DEBUG") != nullptr;
+    auto dbg_sync = [&](const char* what) {  // SDG_DEBUG: name the kernel an asynchronous fault came from
+        if (!dbg) return;
+        hipError_t err = hipStreamSynchronize(st);
+        if (err != hipSuccess) throw DeviceError(std::string(what) + ": " + hipGetErrorString(err));
+    };
+    dbg_sync("bucketize / staging");
     chain_carry(a, d_a, st);
+    dbg_sync("chain_carry_k");
     HIPCHECK(hipEventRecord(e->ev[8], st));
-    if (a.deque_mode != DQ_OFF && nrows > 0) {
+    if (fused) {
+        const int64_t grid = chain_fused_grid(nrows, a.nb);
+        static int64_t* trace = nullptr;
+        static int64_t trace_n = 0;
+        if (dbg) {  // host-mapped progress trace, readable after a device fault
+            if (trace_n < grid * 4) {
+                if (trace) (void)hipHostFree(trace);
+                HIPCHECK(hipHostMalloc((void**)&trace, (size_t)(grid * 4 + 64) * 8, hipHostMallocMapped));
+                trace_n = grid * 4;
+            }
+            for (int64_t i = 0; i < grid * 4 + 64; ++i) trace[i] = -1;
+            void* dp = nullptr;
+            HIPCHECK(hipHostGetDevicePointer(&dp, trace, 0));
+            a.dbg = (volatile int64_t*)dp;
+            HIPCHECK(hipMemcpyAsync(d_a, &a, sizeof a, hipMemcpyHostToDevice, st));
+        }
+        chain_fused(a, d_a, grid, st);
+        if (dbg) {
+            hipError_t err = hipStreamSynchronize(st);
+            if (err != hipSuccess) {
+                std::string m = "chain_fused_k: " + std::string(hipGetErrorString(err)) + "; grid " + std::to_string(grid) +
+                                " nb " + std::to_string(a.nb) + " bbits " + std::to_string(a.bbits) + " lbits " +
+                                std::to_string(a.lbits) + " n " + std::to_string(nrows) + "; unfinished waves:";
+                for (int i = 0; i < 16; ++i) m += (i % 8 ? "," : " | ") + std::to_string(trace[grid * 4 + i]);
+                char pb[64];
+                for (int k = 0; k < nc; ++k) { snprintf(pb, sizeof pb, " col%d=%p", k, a.cols[k]); m += pb; }
+                snprintf(pb, sizeof pb, " out_vals=%p", (void*)a.out_vals); m += pb;
+                int shown = 0;
+                for (int64_t i = 0; i < grid * 4 && shown < 40; ++i)
+                    if (trace[i] != 100 && trace[i] != 99) {
+                        m += " [" + std::to_string(i / 4) + "." + std::to_string(i % 4) + "]=" + std::to_string(trace[i]);
+                        ++shown;
+                    }
+                fprintf(stderr, "%s\n", m.c_str());
+                throw DeviceError(m);
+            }
+        }
+        HIPCHECK(hipEventRecord(e->ev[9], st));
+        chain_fovf(a, d_a, st);
+        dbg_sync("chain_fovf_k");
+    } else if (a.deque_mode != DQ_OFF && nrows > 0) {
         chain_deque(a, d_a, st);
         HIPCHECK(hipEventRecord(e->ev[9], st));
         chain_match(ae, d_a + 1, st);
@@ -623,11 +724,20 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     }
     e->stats.match_launches += (cin.n > 0) + (nrows > 0);
     HIPCHECK(hipEventRecord(e->ev[2], st));
-    unsigned long long hc[2];
+    unsigned long long hc[2], hovf = 0;
     int hf[4];
     HIPCHECK(hipMemcpyAsync(hc, counters, 16, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipMemcpyAsync(hf, flags, 16, hipMemcpyDeviceToHost, st));
+    if (fused) HIPCHECK(hipMemcpyAsync(&hovf, a.ovf_count, 8, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
+    if (fused && hf[2]) throw DeviceError("fused matcher bounds check failed: bits " + std::to_string(hf[2]));
+    if (fused && hf[3]) {  // batch timestamps not in arrival order (or a block's span over 2^32 ms): radix path
+        e->stats.fused = 2;
+        q.carry_nullable = carry_nullable0;
+        return false;
+    }
+    e->stats.fused = fused ? 1 : e->stats.fused;
+    e->stats.fused_ovf += (int64_t)hovf;
     float ms_kg = 0, ms_m = 0;
     HIPCHECK(hipEventElapsedTime(&ms_kg, e->ev[0], e->ev[1]));
     HIPCHECK(hipEventElapsedTime(&ms_m, e->ev[1], e->ev[2]));
@@ -667,6 +777,9 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     e->stats.matches += q.out_n;
     e->stats.path = 0;
     q.seq += nrows;
+    return true;
+    };
+    if (!run(try_fused)) run(false);
 }
 
 int do_flush(sdg_engine* e) {
@@ -679,6 +792,7 @@ int do_flush(sdg_engine* e) {
     e->stats.ms_kg_hist = e->stats.ms_kg_prefix = e->stats.ms_kg_scatter = 0;
     e->stats.ms_chain_carry = e->stats.ms_chain_match = e->stats.ms_chain_emit = 0;
     e->stats.ms_nfa = 0;
+    e->stats.fused_ovf = 0;
     for (auto& q : e->qs) flush_query(e, *q);
     e->stats.ms_total = e->stats.ms_keygroup + e->stats.ms_match;
     e->pending.clear();
@@ -720,6 +834,7 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             if (opts->batch_capacity > 0) e->capacity = opts->batch_capacity;
             e->compile_only = (opts->flags & SDG_COMPILE_ONLY) != 0;
             e->force_generic = (opts->flags & SDG_FORCE_GENERIC) != 0;
+            e->no_fused = (opts->flags & SDG_NO_FUSED) != 0;
         }
         if (opts && opts->max_partials > 0) {
             if (opts->max_partials > 4096) throw CompileError(SDG_ERR_ARG, "max_partials must be <= 4096");

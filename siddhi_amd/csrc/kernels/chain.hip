@@ -121,7 +121,7 @@ __device__ __forceinline__ bool cmp_m(const CmpMask& m, T x, T y) {
 // returns: >= 0 the matching row; -1 expired (dead); -2 reached the end of the segment (carry)
 template <int K>
 __device__ int64_t scan_typed(const ChainArgs& a, const View& v, int64_t from, int64_t end, int64_t ts0, int64_t k,
-                              uint8_t op) {
+                              uint8_t op, uint32_t kf) {
     using C = KT<K>;
     const typename C::T y = C::get(k);
     const ChainSpec& sp = a.sp;
@@ -152,7 +152,9 @@ __device__ int64_t scan_typed(const ChainArgs& a, const View& v, int64_t from, i
             if (left ? cmp_m(m, x, y) : cmp_m(m, y, x)) return q;
         }
     }
+    const bool filt = a.bstart != nullptr;  // bucket view: other keys' rows are interleaved
     for (; q < end; ++q) {
+        if (filt && a.key[q] != kf) continue;
         // StreamPreStateProcessor.isExpired: |start.ts - now| > within, checked before the event is processed
         if (has_within) {
             int64_t d = ts0 - ts_row(a, v, q);
@@ -173,7 +175,7 @@ __device__ int64_t scan_typed(const ChainArgs& a, const View& v, int64_t from, i
 // not compiled into the kernel (registers, code size).
 template <bool GEN>
 __device__ __forceinline__ int64_t chain_scan(const ChainArgs& a, ChainAcc& acc, int64_t from, int64_t end,
-                                              int64_t ts0, int64_t* stk, int stride) {
+                                              int64_t ts0, int64_t* stk, int stride, uint32_t kf = 0) {
     const ChainSpec& sp = a.sp;
     if (!GEN || sp.scan_mode != SCAN_GENERIC) {
         int64_t k = sp.scan_konst;
@@ -187,16 +189,17 @@ __device__ __forceinline__ int64_t chain_scan(const ChainArgs& a, ChainAcc& acc,
             else k = cvt(k, sp.e1_col_kind, sp.scan_t);
         }
         switch (sp.scan_t) {
-            case VK_I32: return scan_typed<VK_I32>(a, acc.V, from, end, ts0, k, op);
-            case VK_I64: return scan_typed<VK_I64>(a, acc.V, from, end, ts0, k, op);
-            case VK_F32: return scan_typed<VK_F32>(a, acc.V, from, end, ts0, k, op);
-            case VK_F64: return scan_typed<VK_F64>(a, acc.V, from, end, ts0, k, op);
-            case VK_BOOL: return scan_typed<VK_BOOL>(a, acc.V, from, end, ts0, k, op);
-            default: return scan_typed<VK_STR>(a, acc.V, from, end, ts0, k, op);
+            case VK_I32: return scan_typed<VK_I32>(a, acc.V, from, end, ts0, k, op, kf);
+            case VK_I64: return scan_typed<VK_I64>(a, acc.V, from, end, ts0, k, op, kf);
+            case VK_F32: return scan_typed<VK_F32>(a, acc.V, from, end, ts0, k, op, kf);
+            case VK_F64: return scan_typed<VK_F64>(a, acc.V, from, end, ts0, k, op, kf);
+            case VK_BOOL: return scan_typed<VK_BOOL>(a, acc.V, from, end, ts0, k, op, kf);
+            default: return scan_typed<VK_STR>(a, acc.V, from, end, ts0, k, op, kf);
         }
     }
     if (!GEN) return -2;  // unreachable: the host picks GEN for SCAN_GENERIC
     for (int64_t q = from; q < end; ++q) {
+        if (a.bstart && a.key[q] != kf) continue;
         if (sp.has_within) {
             int64_t d = ts0 - ts_row(a, acc.V, q);
             if (d < 0) d = -d;
@@ -210,6 +213,23 @@ __device__ __forceinline__ int64_t chain_scan(const ChainArgs& a, ChainAcc& acc,
         if (ok) return q;
     }
     return -2;
+}
+
+// An Instr read as whole dwords. Reading its byte fields through a reference into the kernel-argument block
+// let the compiler form a scalar-load base at the unaligned byte address of `k`; SMEM drops the low address bits,
+// so `b` came back as the op/k/a/pad word (observed on gfx950, ROCm 7.2).
+__device__ __forceinline__ Instr load_instr(const Instr* p) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+    const uint32_t w0 = w[0];
+    Instr in;
+    in.op = (uint8_t)(w0 & 0xFF);
+    in.k = (uint8_t)((w0 >> 8) & 0xFF);
+    in.a = (uint8_t)((w0 >> 16) & 0xFF);
+    in.pad = 0;
+    in.b = (int32_t)w[1];
+    in.c = (int32_t)w[2];
+    in.imm = (int32_t)w[3];
+    return in;
 }
 
 template <bool GEN>
@@ -226,7 +246,7 @@ __device__ __forceinline__ void emit_match(const ChainArgs& a, ChainAcc& acc, in
         int64_t v;
         bool nl;
         if (!GEN || sp.out_direct[j]) {  // a plain attribute (`e1.id`)
-            const Instr& in = sp.out_ins[j];
+            const Instr in = load_instr(&sp.out_ins[j]);
             acc.load(in.a, in.b, in.c, in.k, &v, &nl);
         } else {
             run(a.code, sp.out_prog[j], a.consts, acc, stk, stride, &v, &nl);
@@ -522,11 +542,15 @@ __global__ __launch_bounds__(256) void chain_carry_k(const ChainArgs* __restrict
     if (c < a.cin_n) {
         key = a.cin_key[c];
         int64_t b = 0, e = a.n;
-        if (a.key) {
+        if (a.bstart) {  // bucket view: the key's bucket, key-filtered
+            const uint32_t bk = key & ((1u << a.bbits) - 1u);
+            b = a.bstart[bk];
+            e = a.bstart[bk + 1];
+        } else if (a.key) {
             b = key < (uint32_t)a.K ? (int64_t)a.seg_start[key] : 0;
             e = key < (uint32_t)a.K ? (int64_t)a.seg_end[key] : 0;
         }
-        const int64_t r = chain_scan<true>(a, acc, b, e, a.cin_ts[c], stk, stride);
+        const int64_t r = chain_scan<true>(a, acc, b, e, a.cin_ts[c], stk, stride, key);
         if (r >= 0) { has = true; qhit = r; }
         else if (r == -2) carry = true;
     }
@@ -546,6 +570,341 @@ __global__ __launch_bounds__(256) void chain_carry_k(const ChainArgs* __restrict
             for (int k = 0; k < a.sp.n_cols; ++k)
                 a.carry_vals[(int64_t)k * a.carry_cap + cs] = a.cin_vals[(int64_t)k * a.cin_cap + c];
             a.carry_nulls[cs] = a.cin_nulls[c];
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------------------------------------------------
+// Fused bucket matcher (kernels.h). Block = (bucket b, segment s): rows [lo, lo + own) of the bucket are its
+// candidates, rows [lo, lo + nr) (own + halo) are staged. Staging regroups the rows by local key (key >> bbits)
+// with a stable counting sort in LDS (wave-private ballot-match ranking, as rx_scatter), so the rows of one key
+// form one run in s_ts / s_x in arrival order -- the key-sorted view of chain_match_k, built per block in LDS
+// instead of by a second radix pass over HBM.
+// soft bounds checks (debugging aid): a failed check sets bit `id` of flags[2] and the access is skipped
+#define FU_OK(cond, id) ((cond) ? true : (atomicOr(&a.flags[2], 1 << (id)), false))
+// SDG_DEBUG progress trace: the last stage each wave reached, readable by the host after a fault
+#define FU_TRACE(stage)                                                                                     \
+    do {                                                                                                    \
+        if (a.dbg && lane == 0) a.dbg[(int64_t)blockIdx.x * 4 + w] = (stage);                              \
+    } while (0)
+
+static_assert(FU_THREADS == 256, "chain_fused_k: one thread per local key in the run tables");
+static_assert(FU_ROWS < 65536, "chain_fused_k: u16 rows / run offsets");
+
+template <int K>
+__global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __restrict__ pa) {
+    using C = KT<K>;
+    using T = typename C::T;
+    constexpr int NW = FU_THREADS / 64;
+    constexpr int WROWS = FU_ROWS / NW;  // staged rows ranked by one wave (contiguous)
+    const ChainArgs& a = *pa;
+    const ChainSpec& sp = a.sp;
+    __shared__ uint32_t s_ts[FU_ROWS];   // ts - ts of the block's first staged row (bucket rows are time-ordered)
+    __shared__ int64_t s_x[FU_ROWS];
+    __shared__ uint16_t s_row[FU_ROWS];
+    __shared__ uint8_t s_lk[FU_ROWS];
+    __shared__ uint16_t wc[NW][256];
+    __shared__ uint16_t lstart[256], lend[256];
+    __shared__ uint32_t wcnt[3][FU_PT][NW];
+    __shared__ unsigned long long bbase[3];
+    __shared__ int sb[2];
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    // XCD-aware block order: the hardware deals consecutive block ids round-robin to the 8 XCDs; virtual id v
+    // gives each XCD a contiguous run of segments, so neighbouring segments (which share halo rows) hit one L2
+    const uint32_t G8 = gridDim.x / 8;
+    const uint32_t v = (blockIdx.x & 7u) * G8 + (blockIdx.x >> 3);
+    if (t == 0) sb[0] = -1;
+    __syncthreads();
+    if (t < a.nb && a.bseg[t] <= v && v < a.bseg[t + 1]) {
+        sb[0] = t;
+        sb[1] = (int)(v - a.bseg[t]);
+    }
+    __syncthreads();
+    const int b = sb[0];
+    FU_TRACE(1);
+    if (b < 0) { FU_TRACE(99); return; }  // block-uniform: past the plan
+    const int64_t be = a.bstart[b + 1];
+    const int64_t lo = (int64_t)a.bstart[b] + (int64_t)sb[1] * FU_OWN;
+    const int own = (int)min((int64_t)FU_OWN, be - lo);
+    const int nr = (int)min((int64_t)FU_ROWS, be - lo);
+    const bool to_end = lo + nr == be;  // the staged rows reach the bucket's (= batch's) end for every key
+    const int col = sp.scan_col;
+    const uint8_t kind = sp.scan_col_kind;
+    const int nl = 1 << a.lbits;
+    // ---- stage: coalesced loads (all rounds in flight), stable rank by local key -----------------------------
+    for (int d = t; d < 256; d += FU_THREADS)
+#pragma unroll
+        for (int x = 0; x < NW; ++x) wc[x][d] = 0;
+    if (!FU_OK(lo >= 0 && nr >= 1 && lo + nr <= a.n && b < a.nb, 1)) return;
+    const int64_t tbase = a.ts[lo];
+    const int64_t tlast = a.ts[lo + nr - 1];
+    uint32_t rkey[FU_PT];
+    int64_t rts[FU_PT], rx[FU_PT];
+    const void* xcol = a.cols[col];
+#pragma unroll
+    for (int r = 0; r < FU_PT; ++r) {
+        const int row = w * WROWS + r * 64 + lane;
+        const int64_t g = lo + min(row, nr - 1);  // clamped: rows past nr are loaded but not staged
+        rkey[r] = a.key[g];
+        rts[r] = a.ts[g];
+        rx[r] = kind == VK_F64 || kind == VK_I64 ? ((const int64_t*)xcol)[g] : load_col(xcol, kind, g);
+    }
+    FU_TRACE(2);
+    if (tlast - tbase > (int64_t)0xFFFFFFFF) {  // staged span does not fit the u32 offsets
+        if (t == 0) atomicOr(&a.flags[3], 1);     // -> the host reruns the batch on the radix path
+        return;                                   // block-uniform
+    }
+    __syncthreads();
+    FU_TRACE(3);
+    const uint64_t lt = lanemask_lt();
+    uint32_t rank[FU_PT];
+    uint8_t dig[FU_PT];
+#pragma unroll
+    for (int r = 0; r < FU_PT; ++r) {
+        const int row = w * WROWS + r * 64 + lane;
+        const bool valid = row < nr;
+        const uint32_t d = valid ? rkey[r] >> a.bbits : 0u;
+        uint64_t peers = __ballot(valid);
+        for (int bit = 0; bit < a.lbits; ++bit) {
+            const bool on = (d >> bit) & 1u;
+            const uint64_t m = __ballot(on);
+            peers &= on ? m : ~m;
+        }
+        const uint32_t before = valid ? wc[w][d] : 0u;
+        rank[r] = before + (uint32_t)__popcll(peers & lt);
+        dig[r] = (uint8_t)d;
+        const int leader = peers ? __ffsll((unsigned long long)peers) - 1 : -1;
+        if (valid && lane == leader) wc[w][d] = (uint16_t)(before + (uint32_t)__popcll(peers));
+    }
+    __syncthreads();
+    uint32_t tot = 0;
+    if (t < nl) {
+#pragma unroll
+        for (int x = 0; x < NW; ++x) {
+            const uint32_t c = wc[x][t];
+            wc[x][t] = (uint16_t)tot;
+            tot += c;
+        }
+    }
+    lend[t] = (uint16_t)tot;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {  // inclusive scan of the run lengths (<= FU_ROWS: fits u16)
+        const uint32_t x = t >= off ? lend[t - off] : 0u;
+        __syncthreads();
+        lend[t] = (uint16_t)(lend[t] + x);
+        __syncthreads();
+    }
+    lstart[t] = (uint16_t)(lend[t] - tot);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < FU_PT; ++r) {
+        const int row = w * WROWS + r * 64 + lane;
+        if (row < nr) {
+            const uint32_t pos = lstart[dig[r]] + wc[w][dig[r]] + rank[r];
+            if (!FU_OK(pos < (uint32_t)nr, 2)) continue;
+            s_ts[pos] = (uint32_t)(rts[r] - tbase);
+            s_x[pos] = rx[r];
+            s_row[pos] = (uint16_t)row;
+            s_lk[pos] = dig[r];
+        }
+    }
+    __syncthreads();
+    FU_TRACE(4);
+    // ---- match: position pos = k * FU_THREADS + t (a run of consecutive positions per round) ---------------
+    const bool stream_e1 = sp.scan_mode == SCAN_E1;
+    const bool e1_is_x = stream_e1 && sp.e1_col == col && sp.e1_col_kind == kind;
+    const CmpMask m = cmp_mask(sp.scan_mode == SCAN_TRUE ? OP_ALWAYS : sp.scan_op);
+    const bool left = sp.scan_e2_left;
+    const int32_t has_within = sp.has_within;
+    const int64_t within = sp.within_ms;
+    const FastPred& f0 = sp.f0;
+    uint32_t res[FU_PT];
+#pragma unroll 1
+    for (int k = 0; k < FU_PT; ++k) {
+        const int pos = k * FU_THREADS + t;
+        uint32_t out = MQ_NONE;
+        if (pos < nr && s_row[pos] < own) {
+            const int64_t p = lo + s_row[pos];
+            const int64_t xr = s_x[pos];
+            bool c0;
+            if (a.f0_on_x) {
+                c0 = cmp(f0.op, f0.t, cvt(xr, kind, f0.t), f0.konst);
+            } else {
+                ChainAcc acc{&a, View{}, p, -1, -1};
+                c0 = f0.kind == FP_TRUE ? true : fast_pass(f0, acc);
+            }
+            if (c0) {
+                // the e1 operand of the e2 filter, hoisted (null -> the compare is false for every row)
+                T y = C::get(sp.scan_konst);
+                CmpMask mm = m;
+                if (stream_e1) {
+                    int64_t yv = xr;
+                    if (!e1_is_x) {
+                        if (a.nulls[sp.e1_col] && a.nulls[sp.e1_col][p]) mm = CmpMask{false, false, false, false};
+                        yv = load_col(a.cols[sp.e1_col], sp.e1_col_kind, p);
+                        yv = cvt(yv, sp.e1_col_kind, (uint8_t)K);
+                    } else {
+                        yv = cvt(yv, kind, (uint8_t)K);
+                    }
+                    y = C::get(yv);
+                }
+                const int64_t ts0 = (int64_t)s_ts[pos];
+                int end = (int)lend[s_lk[pos]];
+                if (!FU_OK(end <= nr && end > pos, 4)) end = pos + 1;
+                out = to_end ? MQ_CARRY : MQ_OVF;  // ran off the staged rows
+                for (int q = pos + 1; q < end; ++q) {
+                    if (has_within) {
+                        int64_t d = ts0 - (int64_t)s_ts[q];
+                        if (d < 0) d = -d;
+                        if (d > within) { out = MQ_NONE; break; }  // isExpired: dead
+                    }
+                    const T x = C::get(cvt(s_x[q], kind, (uint8_t)K));
+                    if (left ? cmp_m(mm, x, y) : cmp_m(mm, y, x)) { out = (uint32_t)q; break; }
+                }
+            }
+        }
+        res[k] = out;
+        const uint64_t bm = __ballot(out < MQ_OVF), bc = __ballot(out == MQ_CARRY), bo = __ballot(out == MQ_OVF);
+        if (lane == 0) {
+            wcnt[0][k][w] = (uint32_t)__popcll(bm);
+            wcnt[1][k][w] = (uint32_t)__popcll(bc);
+            wcnt[2][k][w] = (uint32_t)__popcll(bo);
+        }
+    }
+    FU_TRACE(5);
+    __syncthreads();
+    if (t < 3) {
+        uint32_t run = 0;
+        for (int k = 0; k < FU_PT; ++k)
+            for (int x = 0; x < NW; ++x) {
+                const uint32_t c = wcnt[t][k][x];
+                wcnt[t][k][x] = run;
+                run += c;
+            }
+        unsigned long long* ctr = t == 0 ? a.out_count : t == 1 ? a.carry_count : a.ovf_count;
+        bbase[t] = run ? atomicAdd(ctr, (unsigned long long)run) : 0ull;
+    }
+    __syncthreads();
+    // ---- emit matches: slots and rows of every round first, then each column's loads for all rounds together
+    // (independent loads in flight instead of one dependent chain per match) -------------------------------
+    constexpr uint32_t NOSLOT = 0xFFFFFFFFu;
+    uint32_t slot[FU_PT], prow[FU_PT], qrow[FU_PT];
+    bool any_co = false;  // this lane has carries / overflow rows
+#pragma unroll
+    for (int k = 0; k < FU_PT; ++k) {
+        const uint32_t out = res[k];
+        const uint64_t bm = __ballot(out < MQ_OVF);
+        const int pos = k * FU_THREADS + t;
+        slot[k] = NOSLOT;
+        prow[k] = qrow[k] = 0;
+        any_co |= out == MQ_CARRY || out == MQ_OVF;
+        if (out < MQ_OVF) {
+            const uint64_t sl = bbase[0] + wcnt[0][k][w] + (uint32_t)__popcll(bm & lt);
+            if (sl >= (uint64_t)a.out_cap) {
+                atomicOr(&a.flags[0], 1);
+            } else {
+                slot[k] = (uint32_t)sl;
+                prow[k] = s_row[pos];
+                qrow[k] = FU_OK(out < (uint32_t)nr, 5) ? s_row[out] : s_row[pos];
+                FU_OK(prow[k] < (uint32_t)nr && qrow[k] < (uint32_t)nr, 6);
+                a.out_ts[sl] = tbase + (int64_t)s_ts[out];
+            }
+        }
+    }
+    {
+        uint32_t op[FU_PT], oq[FU_PT];
+#pragma unroll
+        for (int k = 0; k < FU_PT; ++k)
+            if (slot[k] != NOSLOT) {
+                op[k] = a.orig[lo + prow[k]];
+                oq[k] = a.orig[lo + qrow[k]];
+            }
+#pragma unroll
+        for (int k = 0; k < FU_PT; ++k)
+            if (slot[k] != NOSLOT) {
+                a.out_emit_seq[slot[k]] = a.seq_base + (int64_t)oq[k];
+                a.out_first_seq[slot[k]] = a.seq_base + (int64_t)op[k];
+            }
+    }
+    FU_TRACE(6);
+    uint32_t nm[FU_PT];
+#pragma unroll
+    for (int k = 0; k < FU_PT; ++k) nm[k] = 0;
+    for (int j = 0; j < sp.n_out; ++j) {
+        const Instr in = load_instr(&sp.out_ins[j]);  // a plain attribute (the fused path has no select bytecode)
+        const bool ok = (in.c == 0 || in.c == -1) && in.a < 2;
+        const void* cp = a.cols[in.b];
+        const uint8_t* np = a.nulls[in.b];
+        int64_t v[FU_PT];
+#pragma unroll
+        for (int k = 0; k < FU_PT; ++k)
+            if (slot[k] != NOSLOT) {
+                const int64_t g = lo + (in.a == 0 ? prow[k] : qrow[k]);
+                v[k] = ok ? load_col(cp, in.k, g) : 0;
+                if (!ok || (np && np[g])) nm[k] |= 1u << j;
+            }
+#pragma unroll
+        for (int k = 0; k < FU_PT; ++k)
+            if (slot[k] != NOSLOT) a.out_vals[(int64_t)j * a.out_cap + slot[k]] = v[k];
+    }
+    if (a.write_nulls) {
+#pragma unroll
+        for (int k = 0; k < FU_PT; ++k)
+            if (slot[k] != NOSLOT) a.out_nulls[slot[k]] = nm[k];
+    }
+    // ---- carries / overflow rows (few: the batch end, long windows) ---------------------------------------------
+    FU_TRACE(7);
+    if (__ballot(any_co) == 0) { FU_TRACE(100); return; }  // wave-uniform
+#pragma unroll 1
+    for (int k = 0; k < FU_PT; ++k) {
+        const uint32_t out = res[k];
+        const uint64_t bc = __ballot(out == MQ_CARRY), bo = __ballot(out == MQ_OVF);
+        if (out != MQ_CARRY && out != MQ_OVF) continue;
+        const int pos = k * FU_THREADS + t;
+        const int64_t p = lo + s_row[pos];
+        if (out == MQ_CARRY) {
+            const int64_t cs = (int64_t)bbase[1] + wcnt[1][k][w] + __popcll(bc & lt);
+            if (cs >= a.carry_cap) atomicOr(&a.flags[0], 1);
+            else if (FU_OK(p < a.n, 7)) emit_carry(a, View{}, cs, p, a.key[p], a.seq_base + (int64_t)a.orig[p]);
+        } else {
+            const int64_t os = (int64_t)bbase[2] + wcnt[2][k][w] + __popcll(bo & lt);
+            if (FU_OK(os < a.n, 8)) a.ovf_rows[os] = (uint32_t)p;  // os < the batch's rows (capacity n)
+        }
+    }
+    FU_TRACE(100);
+}
+
+// fused path: partials whose scan left the staged rows -- the forward scan over the rest of the key's bucket
+// in HBM (key-filtered), then emitted directly (match / carry)
+__global__ __launch_bounds__(256) void chain_fovf_k(const ChainArgs* __restrict__ pa) {
+    const ChainArgs& a = *pa;
+    const int64_t total = (int64_t)*a.ovf_count;
+    for (int64_t i0 = (int64_t)blockIdx.x * 256; i0 < total; i0 += (int64_t)gridDim.x * 256) {
+        const int64_t i = i0 + threadIdx.x;
+        bool has = false, carry = false;
+        int64_t p = -1, qhit = -1;
+        uint32_t key = 0;
+        ChainAcc acc{&a, View{}, -1, -1, -1};
+        if (i < total) {
+            p = a.ovf_rows[i];
+            acc.r0 = p;
+            key = a.key[p];
+            const int64_t end = a.bstart[(key & ((1u << a.bbits) - 1u)) + 1];
+            const int64_t q = chain_scan<false>(a, acc, p + 1, end, a.ts[p], nullptr, 0, key);
+            if (q >= 0) { has = true; qhit = q; }
+            else if (q == -2) carry = true;
+        }
+        const int64_t slot = wave_reserve(has, a.out_count);
+        const int64_t seq = p >= 0 ? a.seq_base + (int64_t)a.orig[p] : 0;
+        if (has) {
+            if (slot >= a.out_cap) atomicOr(&a.flags[0], 1);
+            else emit_match<false>(a, acc, slot, qhit, key, seq, nullptr, 0);
+        }
+        const int64_t cs = wave_reserve(carry, a.carry_count);
+        if (carry) {
+            if (cs >= a.carry_cap) atomicOr(&a.flags[0], 1);
+            else emit_carry(a, View{}, cs, p, key, seq);
         }
     }
 }
@@ -585,6 +944,28 @@ void chain_deque(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
 void chain_carry(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
     if (a.cin_n <= 0) return;
     hipLaunchKernelGGL(chain_carry_k, dim3((unsigned)((a.cin_n + 255) / 256)), dim3(256), 0, stream, d_a);
+}
+
+int64_t chain_fused_grid(int64_t n, int nb) {
+    const int64_t g = (n + FU_OWN - 1) / FU_OWN + nb;
+    return (g + 7) / 8 * 8;
+}
+
+void chain_fused(const ChainArgs& a, const ChainArgs* d_a, int64_t grid, hipStream_t stream) {
+    if (a.n <= 0) return;
+    switch (a.sp.scan_t) {
+        case VK_I32: hipLaunchKernelGGL(chain_fused_k<VK_I32>, dim3((unsigned)grid), dim3(FU_THREADS), 0, stream, d_a); break;
+        case VK_I64: hipLaunchKernelGGL(chain_fused_k<VK_I64>, dim3((unsigned)grid), dim3(FU_THREADS), 0, stream, d_a); break;
+        case VK_F32: hipLaunchKernelGGL(chain_fused_k<VK_F32>, dim3((unsigned)grid), dim3(FU_THREADS), 0, stream, d_a); break;
+        case VK_F64: hipLaunchKernelGGL(chain_fused_k<VK_F64>, dim3((unsigned)grid), dim3(FU_THREADS), 0, stream, d_a); break;
+        case VK_BOOL: hipLaunchKernelGGL(chain_fused_k<VK_BOOL>, dim3((unsigned)grid), dim3(FU_THREADS), 0, stream, d_a); break;
+        default: hipLaunchKernelGGL(chain_fused_k<VK_STR>, dim3((unsigned)grid), dim3(FU_THREADS), 0, stream, d_a); break;
+    }
+}
+
+void chain_fovf(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
+    if (a.n <= 0) return;
+    hipLaunchKernelGGL(chain_fovf_k, dim3(512), dim3(256), 0, stream, d_a);
 }
 
 }  // namespace sdg

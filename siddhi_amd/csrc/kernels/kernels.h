@@ -46,6 +46,15 @@ void keygroup_bind(KeyGroupArgs& a, void* base);
 // the last scatter, after the segment kernel
 void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks = nullptr);
 
+// ---- bucket grouping (fused chain path): ONE radix pass on the key's low `bits` bits --------------------
+// Rows of a bucket end up contiguous and in arrival order (stable); key k is in bucket k & (2^bits - 1). The
+// pass also checks that the batch's timestamps are non-decreasing in arrival order (mono_flag != 0 otherwise,
+// the precondition of the fused matcher's per-bucket time order). Outputs bstart[nb + 1] (bucket row ranges)
+// and bseg[nb + 1] (exclusive prefix over buckets of ceil(len / seg_rows): the matcher's block plan).
+// marks (optional, 4 events) as keygroup().
+void bucketize(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, uint32_t* bstart, uint32_t* bseg,
+               int seg_rows, hipStream_t stream, hipEvent_t* marks = nullptr);
+
 // ---- chain matcher: `every e1=S0[c0] -> e2=S1[c1] within T` (independent partials) ---------------------
 // One block per tile of CM_THREADS * CM_EPT sorted events; the block reserves its output range with one atomic.
 constexpr int CM_THREADS = 256;
@@ -135,6 +144,12 @@ struct ChainArgs {
     uint32_t* ovf_rows;               // [n]
     const uint32_t* mq_in;            // chain_match_k: results to emit (nullptr: scan itself)
     int32_t write_nulls;              // 0: no output can be null (out_nulls is not written)
+    // fused bucket path (chain_fused_k): the view is bucket-ordered (bucketize), not key-sorted. bstart != nullptr
+    // switches chain_carry_k / chain_fovf_k to scanning a key's bucket with a key filter.
+    const uint32_t* bstart;           // [nb + 1] bucket row ranges
+    const uint32_t* bseg;             // [nb + 1] block plan (exclusive prefix of segments per bucket)
+    int32_t nb, bbits, lbits;         // buckets = 2^bbits; local key = key >> bbits < 2^lbits <= 256
+    volatile int64_t* dbg;            // SDG_DEBUG: host-mapped progress trace [block * 4 + wave] (nullptr: off)
 };
 enum DequeMode : int32_t { DQ_OFF = 0, DQ_STACK = 1, DQ_ALL = 2 };
 constexpr uint32_t MQ_NONE = 0xFFFFFFFFu, MQ_CARRY = 0xFFFFFFFEu, MQ_OVF = 0xFFFFFFFDu;
@@ -148,6 +163,24 @@ void chain_deque(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
 // kernel arguments are read from a device copy (d_a) of `a`: the struct is too large to index as a kernarg
 void chain_match(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
 void chain_carry(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
+
+// ---- fused bucket matcher -------------------------------------------------------------------------------
+// One block per segment of FU_OWN rows of one bucket: the segment plus FU_HALO following rows of the bucket
+// are staged in LDS and regrouped by local key there (stable counting sort), so each candidate's forward scan
+// walks its key's run in LDS. A scan that leaves the staged rows before the bucket ends goes to chain_fovf_k
+// (the same scan over the bucket in HBM, key-filtered); one that reaches the bucket end is carried.
+// Preconditions (host): partitioned, one stream, two states, `within`, typed e2 scan without nulls, FastPred
+// e1 filter, plain-attribute selects, K <= 2^16, batch timestamps non-decreasing (checked by bucketize).
+constexpr int FU_THREADS = 256;
+constexpr int FU_PT = 16;                            // staged rows per lane
+constexpr int FU_ROWS = FU_THREADS * FU_PT;          // 4096 rows in LDS
+constexpr int FU_HALO = 1024;
+constexpr int FU_OWN = FU_ROWS - FU_HALO;            // candidate rows per block
+// grid size for n rows in nb buckets (a multiple of 8: the XCD remap needs it)
+int64_t chain_fused_grid(int64_t n, int nb);
+void chain_fused(const ChainArgs& a, const ChainArgs* d_a, int64_t grid, hipStream_t stream);
+// the rows chain_fused_k handed over (ovf_rows / ovf_count): key-filtered bucket scans in HBM, emitted directly
+void chain_fovf(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
 
 // ---- generic keyed NFA (nfa.h): one lane per partition key walks that key's events in order --------------
 struct NfaArgs {

@@ -103,6 +103,8 @@ struct RxPass {
     uint32_t mask;
     int nb;
     int bits;
+    int mono_col;             // >= 0: payload column holding ts; flag a decrease in arrival order (bucketize)
+    int* mono_flag;
 };
 
 // stable tile scatter. Tile element e = w * 1024 + r * 64 + lane belongs to wave w (16 rounds r), so a wave
@@ -194,6 +196,12 @@ __global__ __launch_bounds__(RX_THREADS) void rx_scatter(RxPass a) {
                 else if (wd == 4) v = ((const uint32_t*)src)[i];
                 else v = ((const uint8_t*)src)[i];
                 stage[sp[r]] = v;
+            }
+            if (a.mono_col >= 0 && c == a.mono_col) {  // arrival-order timestamps: compare with row i - 1
+                const uint64_t raw = i < a.n ? ((const uint64_t*)src)[i] : 0ull;
+                uint64_t prev = __shfl_up(raw, 1);
+                if (lane == 0 && i > 0 && i < a.n) prev = ((const uint64_t*)src)[i - 1];
+                if (i > 0 && i < a.n && (int64_t)raw < (int64_t)prev) *a.mono_flag = 1;
             }
         }
         __syncthreads();
@@ -335,6 +343,7 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
         rp.mask = mask;
         rp.nb = nb;
         rp.bits = b;
+        rp.mono_col = -1;
         hipLaunchKernelGGL(rx_scatter, dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, rp);
     }
     if (marks) (void)hipEventRecord(marks[2], stream);
@@ -342,6 +351,76 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
     (void)hipMemsetAsync(a.seg_end, 0, (size_t)a.K * 4, stream);
     hipLaunchKernelGGL(rx_segments, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, stream, a.keys_sorted, a.n,
                        a.seg_start, a.seg_end);
+    if (marks) (void)hipEventRecord(marks[3], stream);
+}
+
+namespace {
+// bucket row ranges and the fused matcher's block plan (one block, nb <= 256)
+__global__ __launch_bounds__(256) void bk_plan(const uint32_t* __restrict__ tot, int64_t n, int nb, int seg_rows,
+                                               uint32_t* __restrict__ bstart, uint32_t* __restrict__ bseg) {
+    __shared__ uint32_t part[256];
+    const int d = threadIdx.x;
+    uint32_t s0 = 0, len = 0;
+    if (d < nb) {
+        s0 = tot[d];
+        const uint32_t s1 = d + 1 < nb ? tot[d + 1] : (uint32_t)n;
+        len = s1 - s0;
+        bstart[d] = s0;
+    }
+    const uint32_t segs = (len + (uint32_t)seg_rows - 1) / (uint32_t)seg_rows;
+    part[d] = segs;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+        const uint32_t x = d >= off ? part[d - off] : 0u;
+        __syncthreads();
+        part[d] += x;
+        __syncthreads();
+    }
+    if (d < nb) bseg[d] = part[d] - segs;
+    if (d == 255) {
+        bstart[nb] = (uint32_t)n;
+        bseg[nb] = part[255];
+    }
+}
+}  // namespace
+
+void bucketize(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, uint32_t* bstart, uint32_t* bseg,
+               int seg_rows, hipStream_t stream, hipEvent_t* marks) {
+    const int nb = 1 << bits;
+    const uint32_t mask = (uint32_t)nb - 1;
+    const int64_t nt = rx_ntiles(a.n);
+    const int ng = (int)((nt + KG_GROUP - 1) / KG_GROUP);
+    if (marks) (void)hipEventRecord(marks[0], stream);
+    hipLaunchKernelGGL(rx_hist, dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, a.keys, a.n, 0, mask, nb, a.counts);
+    const int64_t gk = (int64_t)ng * nb;
+    hipLaunchKernelGGL(rx_p1, dim3((unsigned)((gk + 255) / 256)), dim3(256), 0, stream, a.counts, (int)nt, nb, a.gsum);
+    hipLaunchKernelGGL(rx_p2, dim3(1), dim3(256), 0, stream, a.gsum, ng, nb, a.tot);
+    hipLaunchKernelGGL(rx_p3, dim3((unsigned)((gk + 255) / 256)), dim3(256), 0, stream, a.counts, a.gsum, a.tot,
+                       (int)nt, nb);
+    if (marks) (void)hipEventRecord(marks[1], stream);
+    RxPass rp;
+    std::memset(&rp, 0, sizeof rp);
+    rp.keys_in = a.keys;
+    rp.keys_out = a.keys_sorted;
+    rp.orig_in = nullptr;
+    rp.orig_out = a.orig_sorted;
+    rp.ncols = a.ncols;
+    for (int c = 0; c < a.ncols; ++c) {
+        rp.src[c] = a.src[c];
+        rp.dst[c] = a.dst[c];
+        rp.width[c] = a.width[c];
+    }
+    rp.offsets = a.counts;
+    rp.n = a.n;
+    rp.shift = 0;
+    rp.mask = mask;
+    rp.nb = nb;
+    rp.bits = bits;
+    rp.mono_col = ts_col;
+    rp.mono_flag = mono_flag;
+    hipLaunchKernelGGL(rx_scatter, dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, rp);
+    if (marks) (void)hipEventRecord(marks[2], stream);
+    hipLaunchKernelGGL(bk_plan, dim3(1), dim3(256), 0, stream, a.tot, a.n, nb, seg_rows, bstart, bseg);
     if (marks) (void)hipEventRecord(marks[3], stream);
 }
 

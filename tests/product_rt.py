@@ -8,8 +8,8 @@ TAG = {sa.INT: "i", sa.LONG: "l", sa.FLOAT: "f", sa.DOUBLE: "d", sa.BOOL: "b", s
 
 
 class ProductAdapter:
-    def __init__(self, app, force_generic=False):
-        self.rt = sa.SiddhiAppRuntime(app, force_generic=force_generic)
+    def __init__(self, app, force_generic=False, fused=True):
+        self.rt = sa.SiddhiAppRuntime(app, force_generic=force_generic, fused=fused)
         self.handlers = {}
         self.records = []
 

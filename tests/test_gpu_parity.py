@@ -55,8 +55,8 @@ def oracle_c_rows(app, cols, symbols=None):
         o.close()
 
 
-def product_c_rows(app, cols, symbols=None, batches=1):
-    rt = sa.SiddhiAppRuntime(app)
+def product_c_rows(app, cols, symbols=None, batches=1, fused=True, expect_fused=None):
+    rt = sa.SiddhiAppRuntime(app, fused=fused)
     try:
         h = rt.getInputHandler("StockStream")
         n = len(cols["ts"])
@@ -68,6 +68,8 @@ def product_c_rows(app, cols, symbols=None, batches=1):
             symcol = sym_ids[cols["key"][s:e]] if sym_ids is not None else np.full(e - s, rt.intern("IBM"), np.uint32)
             h.send_columns(cols["ts"][s:e], [cols["id"][s:e], symcol, cols["price"][s:e], cols["volume"][s:e]])
             rt.flush(deliver=False)
+            if expect_fused is not None:
+                assert rt.stats().fused == expect_fused
             types, ts, vals, nulls = rt.raw_outputs(0)
             rows += [(ts[i], (vals[0][i], vals[1][i])) for i in range(len(ts))]
         return rows
@@ -84,14 +86,63 @@ def test_c1_matches_oracle(adversarial, oracle_built):
     assert got == ref
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("batches", [1, 7])
-def test_c2_matches_oracle(batches, oracle_built):
+def test_c2_matches_oracle(batches, fused, oracle_built):
     keys = 300
     cols = w.c2_columns(60_000, keys=keys, per_ms=2)
     syms = w.symbols(keys)
     ref = oracle_c_rows(w.C2_APP, cols, syms)
-    got = product_c_rows(w.C2_APP, cols, syms, batches=batches)
+    got = product_c_rows(w.C2_APP, cols, syms, batches=batches, fused=fused, expect_fused=1 if fused else 0)
     assert len(ref) > 1000
+    assert got == ref
+
+
+@pytest.mark.parametrize("keys", [1, 37, 700, 20_000])
+def test_c2_fused_key_counts(keys, oracle_built):
+    """fused bucket path across bucket / local-key widths: 1 key (one bucket), < 256 keys (one key per bucket),
+    > 256 keys (local keys regrouped in LDS), 20k keys (8 + 7 bits); 3 batches (carries)"""
+    cols = w.c2_columns(40_000, keys=keys, per_ms=3)
+    syms = w.symbols(keys)
+    ref = oracle_c_rows(w.C2_APP, cols, syms)
+    got = product_c_rows(w.C2_APP, cols, syms, batches=3, expect_fused=1)
+    assert len(ref) > 100
+    assert got == ref
+
+
+def test_c2_fused_overflow_scans(oracle_built):
+    """a long window with few keys: partials outlive the staged halo and finish in the key-filtered HBM scan"""
+    app = w.C2_APP.replace("within 1 sec", "within 100 sec")
+    cols = w.c2_columns(30_000, keys=2, per_ms=1)
+    cols["price"] = np.ascontiguousarray(np.round(np.linspace(30.0, 20.5, len(cols["ts"])) +
+                                                  (np.arange(len(cols["ts"])) % 4001 == 4000) * 5.0, 2))
+    syms = w.symbols(2)
+    ref = oracle_c_rows(app, cols, syms)
+    rt = sa.SiddhiAppRuntime(app)
+    try:
+        h = rt.getInputHandler("StockStream")
+        ids = np.array([rt.intern(s) for s in syms], dtype=np.uint32)
+        h.send_columns(cols["ts"], [cols["id"], ids[cols["key"]], cols["price"], cols["volume"]])
+        rt.flush(deliver=False)
+        st = rt.stats()
+        types, ts, vals, nulls = rt.raw_outputs(0)
+        got = [(ts[i], (vals[0][i], vals[1][i])) for i in range(len(ts))]
+    finally:
+        rt.shutdown()
+    assert st.fused == 1 and st.fused_ovf > 0
+    assert len(ref) > 100
+    assert got == ref
+
+
+def test_c2_fused_falls_back_on_unordered_batch(oracle_built):
+    """per-key ordered but globally unordered timestamps: the fused precondition fails, the radix path runs"""
+    keys = 50
+    cols = w.c2_columns(20_000, keys=keys, per_ms=2)
+    cols["ts"] = np.ascontiguousarray(cols["ts"] + (cols["key"] % 2) * 3)  # odd keys 3 ms later
+    syms = w.symbols(keys)
+    ref = oracle_c_rows(w.C2_APP, cols, syms)
+    got = product_c_rows(w.C2_APP, cols, syms, batches=2, expect_fused=2)
+    assert len(ref) > 100
     assert got == ref
 
 
@@ -173,9 +224,13 @@ def test_generic_nfa_many_keys_on_gpu(oracle_built):
 
 
 # ---- chain path: deque kernel (stack / complete-all) and forward scans on one stream ----------------------
+FUSED_SHAPES = {"gt", "ge", "lt", "le_flipped", "const", "no_filter", "ne_const", "cross_col"}
+
+
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("name", sorted(synth.CHAIN_APPS))
 @pytest.mark.parametrize("shape", ["k5_b1", "k200_b4", "desc_b3", "nan_b2"])
-def test_chain_shapes_on_gpu(name, shape, oracle_built):
+def test_chain_shapes_on_gpu(name, shape, fused, oracle_built):
     app, deque = synth.CHAIN_APPS[name]
     seed = zlib.crc32((name + shape).encode()) % 1000
     if shape == "k5_b1":
@@ -191,11 +246,15 @@ def test_chain_shapes_on_gpu(name, shape, oracle_built):
         ref = synth.run(o, tr)
     finally:
         o.close()
-    p = ProductAdapter(app)
+    p = ProductAdapter(app, fused=fused)
     try:
         assert p.rt.query_paths() == [0]
         got = synth.run(p, tr, batches)
-        assert p.rt.stats().deque == deque
+        st = p.rt.stats()
+        if not fused:
+            assert st.fused == 0 and st.deque == deque
+        elif name in FUSED_SHAPES and shape != "nan_b2":  # nan_b2: nulls in the scanned column -> radix path
+            assert st.fused == 1
     finally:
         p.close()
     assert len(ref) > 0
