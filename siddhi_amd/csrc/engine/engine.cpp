@@ -645,6 +645,9 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     q.carry_nullable = false;
     for (int k = 0; k < nc; ++k) q.carry_nullable |= a.nulls[k] != nullptr;
     if (fused) {
+        static const char* skip = getenv("SDG_FU_SKIP");
+        a.fu_skip = skip ? atoi(skip) : 0;
+        a.fu_mode = getenv("SDG_FU_NODEQUE") ? DQ_OFF : a.deque_mode;
         a.deque_mode = DQ_OFF;
         a.bstart = b_start;
         a.bseg = b_seg;

@@ -590,9 +590,18 @@ __global__ __launch_bounds__(256) void chain_carry_k(const ChainArgs* __restrict
     } while (0)
 
 static_assert(FU_THREADS == 256, "chain_fused_k: one thread per local key in the run tables");
+static_assert(FU_PT <= 32, "chain_fused_k: a lane's deque is a 32-bit mask over its positions");
+constexpr uint16_t R_NONE = 0xFFFF, R_CARRY = 0xFFFE, R_OVF = 0xFFFD;
+// LDS swizzle of the per-position arrays: the deque pass gives lane t the positions [16t, 16t + 16), so
+// unswizzled, one step of a wave hits every lane's element at a 16-position stride (one or two banks). XOR-ing
+// the low 4 bits with the next 4 spreads those over the banks; runs of consecutive positions stay permuted
+// within their aligned group of 16 (conflict-free for the per-round `k * 256 + t` accesses too).
+static_assert(FU_PT == 16, "sw() swizzles at the deque chunk size");
+__device__ __forceinline__ int sw(int p) { return p ^ ((p >> 4) & 15); }
 static_assert(FU_ROWS < 65536, "chain_fused_k: u16 rows / run offsets");
 
-template <int K>
+// SAME: the scanned column's kind is the comparison kind (no conversion in the scan loop)
+template <int K, bool SAME>
 __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __restrict__ pa) {
     using C = KT<K>;
     using T = typename C::T;
@@ -604,6 +613,7 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
     __shared__ int64_t s_x[FU_ROWS];
     __shared__ uint16_t s_row[FU_ROWS];
     __shared__ uint8_t s_lk[FU_ROWS];
+    __shared__ uint16_t s_res[FU_ROWS];  // per position: e2 position | R_NONE | R_CARRY | R_OVF
     __shared__ uint16_t wc[NW][256];
     __shared__ uint16_t lstart[256], lend[256];
     __shared__ uint32_t wcnt[3][FU_PT][NW];
@@ -655,6 +665,10 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
         if (t == 0) atomicOr(&a.flags[3], 1);     // -> the host reruns the batch on the radix path
         return;                                   // block-uniform
     }
+    if (a.fu_skip & 4) {
+        if (rts[0] == -12345 && rx[FU_PT - 1] == 7 && rkey[3] == 9) a.flags[2] = 1;  // keep the loads alive
+        return;
+    }
     __syncthreads();
     FU_TRACE(3);
     const uint64_t lt = lanemask_lt();
@@ -703,67 +717,118 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
         if (row < nr) {
             const uint32_t pos = lstart[dig[r]] + wc[w][dig[r]] + rank[r];
             if (!FU_OK(pos < (uint32_t)nr, 2)) continue;
-            s_ts[pos] = (uint32_t)(rts[r] - tbase);
-            s_x[pos] = rx[r];
-            s_row[pos] = (uint16_t)row;
-            s_lk[pos] = dig[r];
+            s_ts[sw(pos)] = (uint32_t)(rts[r] - tbase);
+            s_x[sw(pos)] = rx[r];
+            s_row[sw(pos)] = (uint16_t)row;
+            s_lk[sw(pos)] = dig[r];
+            s_res[sw(pos)] = R_NONE;
         }
     }
     __syncthreads();
     FU_TRACE(4);
+    if (a.fu_skip & 8) return;
     // ---- match: position pos = k * FU_THREADS + t (a run of consecutive positions per round) ---------------
     const bool stream_e1 = sp.scan_mode == SCAN_E1;
     const bool e1_is_x = stream_e1 && sp.e1_col == col && sp.e1_col_kind == kind;
     const CmpMask m = cmp_mask(sp.scan_mode == SCAN_TRUE ? OP_ALWAYS : sp.scan_op);
     const bool left = sp.scan_e2_left;
-    const int32_t has_within = sp.has_within;
-    const int64_t within = sp.within_ms;
+    // bucket rows are time-ordered (bucketize checked it), so a later row's offset is never below the start's
+    const uint64_t within_u = sp.has_within ? (uint64_t)sp.within_ms : ~0ull;
     const FastPred& f0 = sp.f0;
-    uint32_t res[FU_PT];
+    const bool f0_on_x = a.f0_on_x;
+    const bool f0_typed = f0_on_x && SAME && f0.t == K;  // c0 = `x OP const` in the scan's own type
+    const CmpMask m0 = cmp_mask(f0.op);
+    const T k0 = C::get(f0.konst);
+    const T kc = C::get(sp.scan_konst);
+    const uint16_t ran_off = to_end ? R_CARRY : R_OVF;  // a partial still pending when its key's staged rows end
+    auto c0_at = [&](int pos, int64_t xr, T xv) -> bool {  // the e1 filter of the row at `pos`
+        if (f0_typed) return cmp_m(m0, xv, k0);
+        if (f0_on_x) return cmp(f0.op, f0.t, cvt(xr, kind, f0.t), f0.konst);
+        ChainAcc acc{&a, View{}, lo + s_row[sw(pos)], -1, -1};
+        return f0.kind == FP_TRUE ? true : fast_pass(f0, acc);
+    };
+    if (a.fu_mode != DQ_OFF) {
+        // ---- monotone-deque pass (chain_deque_k), one lane per FU_PT consecutive positions: the lane
+        // pushes partials from its own positions only and keeps popping over the following positions of the key
+        // until its deque drains. The deque is a bit mask over the lane's positions (bit i = position p0 + i
+        // pending); arrival order = position order, so the front is the lowest bit and the top the highest.
+        const bool stack = a.fu_mode == DQ_STACK;
+        const int p0 = t * FU_PT;
+        uint32_t pend = 0;
+        int cur_end = p0 < nr ? (int)lend[s_lk[sw(p0)]] : 0;
+        int q = p0;
+        for (; q < nr; ++q) {
+            if (q >= p0 + FU_PT && pend == 0) break;
+            if (q == cur_end) {  // the key's staged rows end here: its pending partials ran off
+                for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = ran_off;
+                if (q >= p0 + FU_PT) break;
+                cur_end = (int)lend[s_lk[sw(q)]];
+            }
+            const uint32_t tq = s_ts[sw(q)];
+            const int64_t xr = s_x[sw(q)];
+            const T x = SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K));
+            // StreamPreStateProcessor.expireEvents: the expired prefix (oldest first)
+            while (pend) {
+                const int f = __builtin_ctz(pend);
+                if ((uint64_t)(tq - s_ts[sw(p0 + f)]) <= within_u) break;
+                pend &= pend - 1;  // s_res stays R_NONE: died before completing
+            }
+            if (stack) {  // x completes the suffix of partials whose e1 value it beats
+                while (pend) {
+                    const int tp = 31 - __builtin_clz(pend);
+                    const T y = SAME ? C::get(s_x[sw(p0 + tp)]) : C::get(cvt(s_x[sw(p0 + tp)], kind, (uint8_t)K));
+                    if (!(left ? cmp_m(m, x, y) : cmp_m(m, y, x))) break;
+                    s_res[sw(p0 + tp)] = (uint16_t)q;
+                    pend &= ~(1u << tp);
+                }
+            } else if (pend && (left ? cmp_m(m, x, kc) : cmp_m(m, kc, x))) {  // complete-all
+                for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = (uint16_t)q;
+            }
+            // e1: this lane's own (non-halo) rows start partials, visible from the next row on
+            if (q < p0 + FU_PT && s_row[sw(q)] < own && c0_at(q, xr, x) && (!stack || x == x)) pend |= 1u << (q - p0);
+        }
+        for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = ran_off;  // staged rows ended
+    } else {
+        // ---- forward scans: one lane per candidate, its key's run in LDS
 #pragma unroll 1
+        for (int k = 0; k < FU_PT; ++k) {
+            const int pos = k * FU_THREADS + t;
+            if (!(pos < nr && s_row[sw(pos)] < own)) continue;
+            const int64_t p = lo + s_row[sw(pos)];
+            const int64_t xr = s_x[sw(pos)];
+            const T xv = SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K));
+            if (!c0_at(pos, xr, xv)) continue;
+            // the e1 operand of the e2 filter, hoisted (null -> the compare is false for every row)
+            T y = kc;
+            CmpMask mm = m;
+            if (stream_e1) {
+                if (e1_is_x) {
+                    y = xv;
+                } else {
+                    if (a.nulls[sp.e1_col] && a.nulls[sp.e1_col][p]) mm = CmpMask{false, false, false, false};
+                    y = C::get(cvt(load_col(a.cols[sp.e1_col], sp.e1_col_kind, p), sp.e1_col_kind, (uint8_t)K));
+                }
+            }
+            const uint32_t t0 = s_ts[sw(pos)];
+            int end = (int)lend[s_lk[sw(pos)]];
+            if (!FU_OK(end <= nr && end > pos, 4)) end = pos + 1;
+            if (a.fu_skip & 1) end = pos + 1;
+            uint16_t out = ran_off;
+            for (int q = pos + 1; q < end; ++q) {
+                if ((uint64_t)(s_ts[sw(q)] - t0) > within_u) { out = R_NONE; break; }  // isExpired: dead
+                const T x = SAME ? C::get(s_x[sw(q)]) : C::get(cvt(s_x[sw(q)], kind, (uint8_t)K));
+                if (left ? cmp_m(mm, x, y) : cmp_m(mm, y, x)) { out = (uint16_t)q; break; }
+            }
+            s_res[sw(pos)] = out;
+        }
+    }
+    __syncthreads();
+    uint32_t res[FU_PT];
+#pragma unroll
     for (int k = 0; k < FU_PT; ++k) {
         const int pos = k * FU_THREADS + t;
-        uint32_t out = MQ_NONE;
-        if (pos < nr && s_row[pos] < own) {
-            const int64_t p = lo + s_row[pos];
-            const int64_t xr = s_x[pos];
-            bool c0;
-            if (a.f0_on_x) {
-                c0 = cmp(f0.op, f0.t, cvt(xr, kind, f0.t), f0.konst);
-            } else {
-                ChainAcc acc{&a, View{}, p, -1, -1};
-                c0 = f0.kind == FP_TRUE ? true : fast_pass(f0, acc);
-            }
-            if (c0) {
-                // the e1 operand of the e2 filter, hoisted (null -> the compare is false for every row)
-                T y = C::get(sp.scan_konst);
-                CmpMask mm = m;
-                if (stream_e1) {
-                    int64_t yv = xr;
-                    if (!e1_is_x) {
-                        if (a.nulls[sp.e1_col] && a.nulls[sp.e1_col][p]) mm = CmpMask{false, false, false, false};
-                        yv = load_col(a.cols[sp.e1_col], sp.e1_col_kind, p);
-                        yv = cvt(yv, sp.e1_col_kind, (uint8_t)K);
-                    } else {
-                        yv = cvt(yv, kind, (uint8_t)K);
-                    }
-                    y = C::get(yv);
-                }
-                const int64_t ts0 = (int64_t)s_ts[pos];
-                int end = (int)lend[s_lk[pos]];
-                if (!FU_OK(end <= nr && end > pos, 4)) end = pos + 1;
-                out = to_end ? MQ_CARRY : MQ_OVF;  // ran off the staged rows
-                for (int q = pos + 1; q < end; ++q) {
-                    if (has_within) {
-                        int64_t d = ts0 - (int64_t)s_ts[q];
-                        if (d < 0) d = -d;
-                        if (d > within) { out = MQ_NONE; break; }  // isExpired: dead
-                    }
-                    const T x = C::get(cvt(s_x[q], kind, (uint8_t)K));
-                    if (left ? cmp_m(mm, x, y) : cmp_m(mm, y, x)) { out = (uint32_t)q; break; }
-                }
-            }
-        }
+        const uint16_t r16 = pos < nr ? s_res[sw(pos)] : R_NONE;
+        const uint32_t out = r16 == R_NONE ? MQ_NONE : r16 == R_CARRY ? MQ_CARRY : r16 == R_OVF ? MQ_OVF : (uint32_t)r16;
         res[k] = out;
         const uint64_t bm = __ballot(out < MQ_OVF), bc = __ballot(out == MQ_CARRY), bo = __ballot(out == MQ_OVF);
         if (lane == 0) {
@@ -788,6 +853,7 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
     __syncthreads();
     // ---- emit matches: slots and rows of every round first, then each column's loads for all rounds together
     // (independent loads in flight instead of one dependent chain per match) -------------------------------
+    if (a.fu_skip & 2) return;
     constexpr uint32_t NOSLOT = 0xFFFFFFFFu;
     uint32_t slot[FU_PT], prow[FU_PT], qrow[FU_PT];
     bool any_co = false;  // this lane has carries / overflow rows
@@ -805,10 +871,10 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
                 atomicOr(&a.flags[0], 1);
             } else {
                 slot[k] = (uint32_t)sl;
-                prow[k] = s_row[pos];
-                qrow[k] = FU_OK(out < (uint32_t)nr, 5) ? s_row[out] : s_row[pos];
+                prow[k] = s_row[sw(pos)];
+                qrow[k] = FU_OK(out < (uint32_t)nr, 5) ? s_row[sw(out)] : s_row[sw(pos)];
                 FU_OK(prow[k] < (uint32_t)nr && qrow[k] < (uint32_t)nr, 6);
-                a.out_ts[sl] = tbase + (int64_t)s_ts[out];
+                a.out_ts[sl] = tbase + (int64_t)s_ts[sw(out)];
             }
         }
     }
@@ -837,13 +903,21 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
         const void* cp = a.cols[in.b];
         const uint8_t* np = a.nulls[in.b];
         int64_t v[FU_PT];
+        if (ok && (in.k == VK_I64 || in.k == VK_F64)) {  // 8-byte column: plain loads, all rounds in flight
+            const int64_t* c8 = (const int64_t*)cp;
 #pragma unroll
-        for (int k = 0; k < FU_PT; ++k)
-            if (slot[k] != NOSLOT) {
-                const int64_t g = lo + (in.a == 0 ? prow[k] : qrow[k]);
-                v[k] = ok ? load_col(cp, in.k, g) : 0;
-                if (!ok || (np && np[g])) nm[k] |= 1u << j;
-            }
+            for (int k = 0; k < FU_PT; ++k)
+                if (slot[k] != NOSLOT) v[k] = c8[lo + (in.a == 0 ? prow[k] : qrow[k])];
+        } else {
+#pragma unroll
+            for (int k = 0; k < FU_PT; ++k)
+                if (slot[k] != NOSLOT) v[k] = ok ? load_col(cp, in.k, lo + (in.a == 0 ? prow[k] : qrow[k])) : 0;
+        }
+        if (!ok || np) {
+#pragma unroll
+            for (int k = 0; k < FU_PT; ++k)
+                if (slot[k] != NOSLOT && (!ok || np[lo + (in.a == 0 ? prow[k] : qrow[k])])) nm[k] |= 1u << j;
+        }
 #pragma unroll
         for (int k = 0; k < FU_PT; ++k)
             if (slot[k] != NOSLOT) a.out_vals[(int64_t)j * a.out_cap + slot[k]] = v[k];
@@ -862,7 +936,7 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
         const uint64_t bc = __ballot(out == MQ_CARRY), bo = __ballot(out == MQ_OVF);
         if (out != MQ_CARRY && out != MQ_OVF) continue;
         const int pos = k * FU_THREADS + t;
-        const int64_t p = lo + s_row[pos];
+        const int64_t p = lo + s_row[sw(pos)];
         if (out == MQ_CARRY) {
             const int64_t cs = (int64_t)bbase[1] + wcnt[1][k][w] + __popcll(bc & lt);
             if (cs >= a.carry_cap) atomicOr(&a.flags[0], 1);
@@ -953,14 +1027,22 @@ int64_t chain_fused_grid(int64_t n, int nb) {
 
 void chain_fused(const ChainArgs& a, const ChainArgs* d_a, int64_t grid, hipStream_t stream) {
     if (a.n <= 0) return;
+    const dim3 g((unsigned)grid), b(FU_THREADS);
+    const bool same = a.sp.scan_col_kind == a.sp.scan_t;
+#define FU_LAUNCH(KK)                                                                                    \
+    do {                                                                                                 \
+        if (same) hipLaunchKernelGGL((chain_fused_k<KK, true>), g, b, 0, stream, d_a);                   \
+        else hipLaunchKernelGGL((chain_fused_k<KK, false>), g, b, 0, stream, d_a);                       \
+    } while (0)
     switch (a.sp.scan_t) {
-        case VK_I32: hipLaunchKernelGGL(chain_fused_k<VK_I32>, dim3((unsigned)grid), dim3(FU_THREADS), 0, stream, d_a); break;
-        case VK_I64: hipLaunchKernelGGL(chain_fused_k<VK_I64>, dim3((unsigned)grid), dim3(FU_THREADS), 0, stream, d_a); break;
-        case VK_F32: hipLaunchKernelGGL(chain_fused_k<VK_F32>, dim3((unsigned)grid), dim3(FU_THREADS), 0, stream, d_a); break;
-        case VK_F64: hipLaunchKernelGGL(chain_fused_k<VK_F64>, dim3((unsigned)grid), dim3(FU_THREADS), 0, stream, d_a); break;
-        case VK_BOOL: hipLaunchKernelGGL(chain_fused_k<VK_BOOL>, dim3((unsigned)grid), dim3(FU_THREADS), 0, stream, d_a); break;
-        default: hipLaunchKernelGGL(chain_fused_k<VK_STR>, dim3((unsigned)grid), dim3(FU_THREADS), 0, stream, d_a); break;
+        case VK_I32: FU_LAUNCH(VK_I32); break;
+        case VK_I64: FU_LAUNCH(VK_I64); break;
+        case VK_F32: FU_LAUNCH(VK_F32); break;
+        case VK_F64: FU_LAUNCH(VK_F64); break;
+        case VK_BOOL: FU_LAUNCH(VK_BOOL); break;
+        default: FU_LAUNCH(VK_STR); break;
     }
+#undef FU_LAUNCH
 }
 
 void chain_fovf(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {

@@ -150,6 +150,9 @@ struct ChainArgs {
     const uint32_t* bseg;             // [nb + 1] block plan (exclusive prefix of segments per bucket)
     int32_t nb, bbits, lbits;         // buckets = 2^bbits; local key = key >> bbits < 2^lbits <= 256
     volatile int64_t* dbg;            // SDG_DEBUG: host-mapped progress trace [block * 4 + wave] (nullptr: off)
+    int32_t fu_mode;                  // chain_fused_k: DQ_STACK / DQ_ALL -> chunked deque pass, DQ_OFF -> forward scans
+    int32_t fu_skip;                  // SDG_FU_SKIP (phase timing only, results invalid): 1 scan, 2 emit, 4 stop
+                                      // after the loads, 8 stop after the LDS regrouping
 };
 enum DequeMode : int32_t { DQ_OFF = 0, DQ_STACK = 1, DQ_ALL = 2 };
 constexpr uint32_t MQ_NONE = 0xFFFFFFFFu, MQ_CARRY = 0xFFFFFFFEu, MQ_OVF = 0xFFFFFFFDu;

@@ -98,10 +98,14 @@ def test_c2_matches_oracle(batches, fused, oracle_built):
     assert got == ref
 
 
+@pytest.mark.parametrize("deque", [True, False])
 @pytest.mark.parametrize("keys", [1, 37, 700, 20_000])
-def test_c2_fused_key_counts(keys, oracle_built):
+def test_c2_fused_key_counts(keys, deque, oracle_built, monkeypatch):
     """fused bucket path across bucket / local-key widths: 1 key (one bucket), < 256 keys (one key per bucket),
-    > 256 keys (local keys regrouped in LDS), 20k keys (8 + 7 bits); 3 batches (carries)"""
+    > 256 keys (local keys regrouped in LDS), 20k keys (8 + 7 bits); 3 batches (carries); the chunked deque
+    pass and (SDG_FU_NODEQUE) the per-candidate forward scans"""
+    if not deque:
+        monkeypatch.setenv("SDG_FU_NODEQUE", "1")
     cols = w.c2_columns(40_000, keys=keys, per_ms=3)
     syms = w.symbols(keys)
     ref = oracle_c_rows(w.C2_APP, cols, syms)
