@@ -14,7 +14,10 @@ of the keys it owns; no data-path
 collective — only the batch-boundary all-gather of per-rank match counts (RCCL over xGMI). scaling = weak.
 
 Roofline: algorithmic bytes per step B = N_in*28 + N_match*28 (ts 8 + key 4 + price 8 + id 8 in,
-ts 8 + key 4 + two ids out); achieved = B / duration of the dominant kernel (HIP events on the engine stream).
+ts 8 + key 4 + two ids out). The dominant kernel is launched once per step and covers the whole batch, so its
+algorithmic bytes per launch are B; achieved = B / its average launch duration (HIP events recorded on the engine
+stream around that launch). traffic = HBM bytes per launch of that kernel from the committed rocprofv3 --pmc passes
+(profiles/pmc_traffic.json: FETCH_SIZE doubled per the gfx950 note of the MI355X guide, plus WRITE_SIZE).
 CPU baseline: the oracle (C++ restatement of the reference engine, one core) on a bounded sample of the same
 workload.
 """
@@ -170,6 +173,15 @@ def main():
     dom = max(per_kernel, key=per_kernel.get)
     step_bytes = n * B_IN + (matches / K) * B_OUT
     achieved = step_bytes / (per_kernel[dom] / 1000.0) / 1e9
+    kernel_names = {"ms_chain_match": "chain_fused_k" if st.fused == 1 else "chain_deque_k",
+                    "ms_kg_scatter": "rx_scatter", "ms_kg_hist": "rx_hist", "ms_chain_carry": "chain_carry_k"}
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(tpath):
+        tj = json.load(open(tpath))
+        ent = tj.get("kernels", {}).get(kernel_names.get(dom, ""))
+        if ent and tj.get("events_per_launch") == n:
+            traffic = ent["fetch_bytes"] + ent["write_bytes"]
     out = {
         "metric": "input events/sec matched (node) at 1/2/4/8 MI355X; % HBM roofline",
         "value": value,
@@ -186,9 +198,12 @@ def main():
         "config": {"workload": "C2: partition with (symbol of StockStream) every e1=StockStream[price>20] -> "
                                "e2=StockStream[price>e1.price] within 1 sec",
                    "events_per_gpu_per_step": n, "keys_per_gpu": keys, "parallelism": "key-hash shards x%d" % world,
-                   "matches_per_step": total_matches / K},
-        "roofline": {"bound": "hbm", "kernel": dom.replace("ms_", ""), "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                   "matches_per_step": total_matches / K, "path": "fused bucket matcher" if st.fused == 1 else
+                   "radix key sort + chain kernels"},
+        "roofline": {"bound": "hbm", "kernel": kernel_names.get(dom, dom), "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_unit": "bytes per launch (rocprofv3 --pmc, profiles/pmc_traffic.json)",
+                     "algorithmic_bytes_per_launch": step_bytes, "launches_per_step": 1,
                      "step_frac": step_bytes / (ms_per_step / 1000.0) / 1e9 / HBM_PEAK_GBS,
                      "kernel_ms": per_kernel},
     }

@@ -22,3 +22,19 @@ for k, cs in acc.items():
     print(k)
     for c, v in sorted(cs.items()):
         print("   %-24s %14.4g  (n=%d)" % (c, sum(v) / len(v), len(v)))
+
+# --traffic: write profiles/pmc_traffic.json (HBM bytes per launch per kernel) for bench.py's roofline.traffic.
+# FETCH_SIZE / WRITE_SIZE are in KB; FETCH_SIZE is doubled per the gfx950 note of MI355X_MICROARCH.md (it tallies
+# 128-B memory-side read requests at 64 B).
+if len(sys.argv) > 3 and sys.argv[3] == "--traffic":
+    import json
+    events = int(sys.argv[4])
+    out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, gpurun_out/%s" % tag, "events_per_launch": events,
+           "kernels": {}}
+    for k, cs in acc.items():
+        if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
+            f = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"]) * 1024 * 2
+            w = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"]) * 1024
+            out["kernels"][k.split("<")[0]] = {"fetch_bytes": f, "write_bytes": w}
+    json.dump(out, open("profiles/pmc_traffic.json", "w"), indent=1)
+    print("wrote profiles/pmc_traffic.json")

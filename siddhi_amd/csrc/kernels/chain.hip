@@ -747,45 +747,66 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
         ChainAcc acc{&a, View{}, lo + s_row[sw(pos)], -1, -1};
         return f0.kind == FP_TRUE ? true : fast_pass(f0, acc);
     };
-    if (a.fu_mode != DQ_OFF) {
+    if (a.fu_skip & 16) {
+        // phase timing: no matching
+    } else if (a.fu_mode != DQ_OFF) {
         // ---- monotone-deque pass (chain_deque_k), one lane per FU_PT consecutive positions: the lane
         // pushes partials from its own positions only and keeps popping over the following positions of the key
         // until its deque drains. The deque is a bit mask over the lane's positions (bit i = position p0 + i
         // pending); arrival order = position order, so the front is the lowest bit and the top the highest.
+        // The chunk's rows are prefetched into registers (static indices: the loop over them is unrolled); the
+        // front's ts and the top's value are cached and re-read from LDS only when the front / top changes.
         const bool stack = a.fu_mode == DQ_STACK;
         const int p0 = t * FU_PT;
-        uint32_t pend = 0;
-        int cur_end = p0 < nr ? (int)lend[s_lk[sw(p0)]] : 0;
-        int q = p0;
-        for (; q < nr; ++q) {
-            if (q >= p0 + FU_PT && pend == 0) break;
-            if (q == cur_end) {  // the key's staged rows end here: its pending partials ran off
-                for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = ran_off;
-                if (q >= p0 + FU_PT) break;
-                cur_end = (int)lend[s_lk[sw(q)]];
-            }
-            const uint32_t tq = s_ts[sw(q)];
-            const int64_t xr = s_x[sw(q)];
-            const T x = SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K));
-            // StreamPreStateProcessor.expireEvents: the expired prefix (oldest first)
-            while (pend) {
-                const int f = __builtin_ctz(pend);
-                if ((uint64_t)(tq - s_ts[sw(p0 + f)]) <= within_u) break;
-                pend &= pend - 1;  // s_res stays R_NONE: died before completing
+        uint32_t pend = 0, tf = 0;
+        T ytop = T(0);
+        // one row (ts tq, value x) against the pending partials: expire the prefix, then complete (a suffix / all).
+        // The front's ts (tf) and the top's value (ytop) are cached; pops only ever remove from the top, so tf
+        // changes only by expiry or by emptying.
+        auto step = [&](int q, uint32_t tq, T x) {
+            // StreamPreStateProcessor.expireEvents: the expired prefix (oldest first); s_res stays R_NONE
+            while (pend && (uint64_t)(tq - tf) > within_u) {
+                pend &= pend - 1;
+                if (pend) tf = s_ts[sw(p0 + __builtin_ctz(pend))];
             }
             if (stack) {  // x completes the suffix of partials whose e1 value it beats
-                while (pend) {
+                while (pend && (left ? cmp_m(m, x, ytop) : cmp_m(m, ytop, x))) {
                     const int tp = 31 - __builtin_clz(pend);
-                    const T y = SAME ? C::get(s_x[sw(p0 + tp)]) : C::get(cvt(s_x[sw(p0 + tp)], kind, (uint8_t)K));
-                    if (!(left ? cmp_m(m, x, y) : cmp_m(m, y, x))) break;
                     s_res[sw(p0 + tp)] = (uint16_t)q;
                     pend &= ~(1u << tp);
+                    if (pend) {
+                        const int64_t yr = s_x[sw(p0 + 31 - __builtin_clz(pend))];
+                        ytop = SAME ? C::get(yr) : C::get(cvt(yr, kind, (uint8_t)K));
+                    }
                 }
             } else if (pend && (left ? cmp_m(m, x, kc) : cmp_m(m, kc, x))) {  // complete-all
                 for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = (uint16_t)q;
             }
+        };
+        const int pe = min(p0 + FU_PT, nr);
+        int cur_end = p0 < nr ? (int)lend[s_lk[sw(p0)]] : 0;
+#pragma unroll 1
+        for (int q = p0; q < pe; ++q) {
+            const uint32_t tq = s_ts[sw(q)];
+            const int64_t xr = s_x[sw(q)];
+            const T x = SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K));
+            step(q, tq, x);
             // e1: this lane's own (non-halo) rows start partials, visible from the next row on
-            if (q < p0 + FU_PT && s_row[sw(q)] < own && c0_at(q, xr, x) && (!stack || x == x)) pend |= 1u << (q - p0);
+            if (s_row[sw(q)] < own && c0_at(q, xr, x) && (!stack || x == x)) {
+                if (!pend) tf = tq;
+                pend |= 1u << (q - p0);
+                ytop = x;
+            }
+            if (q + 1 == cur_end) {  // the key's staged rows end here: its pending partials ran off
+                for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = ran_off;
+                if (q + 1 < pe) cur_end = (int)lend[s_lk[sw(q + 1)]];
+            }
+        }
+        // continuation over the key's following positions (no pushes) until the deque drains
+#pragma unroll 1
+        for (int q = pe; q < cur_end && pend; ++q) {
+            const int64_t xr = s_x[sw(q)];
+            step(q, s_ts[sw(q)], SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K)));
         }
         for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = ran_off;  // staged rows ended
     } else {
@@ -848,7 +869,8 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
                 run += c;
             }
         unsigned long long* ctr = t == 0 ? a.out_count : t == 1 ? a.carry_count : a.ovf_count;
-        bbase[t] = run ? atomicAdd(ctr, (unsigned long long)run) : 0ull;
+        if (a.fu_skip & 32) bbase[t] = t == 0 ? (unsigned long long)v * FU_OWN : 0ull;  // phase timing only
+        else bbase[t] = run ? atomicAdd(ctr, (unsigned long long)run) : 0ull;
     }
     __syncthreads();
     // ---- emit matches: slots and rows of every round first, then each column's loads for all rounds together
@@ -902,25 +924,26 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
         const bool ok = (in.c == 0 || in.c == -1) && in.a < 2;
         const void* cp = a.cols[in.b];
         const uint8_t* np = a.nulls[in.b];
-        int64_t v[FU_PT];
+        int64_t* const ov = a.out_vals + (int64_t)j * a.out_cap;
         if (ok && (in.k == VK_I64 || in.k == VK_F64)) {  // 8-byte column: plain loads, all rounds in flight
             const int64_t* c8 = (const int64_t*)cp;
+            int64_t v[FU_PT];
 #pragma unroll
             for (int k = 0; k < FU_PT; ++k)
                 if (slot[k] != NOSLOT) v[k] = c8[lo + (in.a == 0 ? prow[k] : qrow[k])];
+#pragma unroll
+            for (int k = 0; k < FU_PT; ++k)
+                if (slot[k] != NOSLOT) ov[slot[k]] = v[k];
         } else {
 #pragma unroll
             for (int k = 0; k < FU_PT; ++k)
-                if (slot[k] != NOSLOT) v[k] = ok ? load_col(cp, in.k, lo + (in.a == 0 ? prow[k] : qrow[k])) : 0;
+                if (slot[k] != NOSLOT) ov[slot[k]] = ok ? load_col(cp, in.k, lo + (in.a == 0 ? prow[k] : qrow[k])) : 0;
         }
         if (!ok || np) {
 #pragma unroll
             for (int k = 0; k < FU_PT; ++k)
                 if (slot[k] != NOSLOT && (!ok || np[lo + (in.a == 0 ? prow[k] : qrow[k])])) nm[k] |= 1u << j;
         }
-#pragma unroll
-        for (int k = 0; k < FU_PT; ++k)
-            if (slot[k] != NOSLOT) a.out_vals[(int64_t)j * a.out_cap + slot[k]] = v[k];
     }
     if (a.write_nulls) {
 #pragma unroll
