@@ -133,11 +133,17 @@ __global__ __launch_bounds__(RX_THREADS) void rx_scatter(RxPass a) {
     const uint64_t lt = lanemask_lt();
     uint32_t rank[R];
     uint8_t dig[R];
+    uint32_t kreg[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int64_t i = wbase + r * 64 + lane;
+        kreg[r] = i < a.n ? a.keys_in[i] : 0u;
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int64_t i = wbase + r * 64 + lane;
         const bool valid = i < a.n;
-        const uint32_t d = valid ? digit_of(a.keys_in[i], a.shift, a.mask) : 0u;
+        const uint32_t d = valid ? digit_of(kreg[r], a.shift, a.mask) : 0u;
         uint64_t peers = __ballot(valid);
         for (int bit = 0; bit < a.bits; ++bit) {
             const bool on = (d >> bit) & 1u;
@@ -182,45 +188,71 @@ __global__ __launch_bounds__(RX_THREADS) void rx_scatter(RxPass a) {
         sp[r] = tstart[dig[r]] + wr;
         if (i < a.n) dest[sp[r]] = gbase[dig[r]] + wr;
     }
-    // keys | original rows as one word, then every payload column
-    for (int c = -1; c < a.ncols; ++c) {
-        const int wd = c < 0 ? 8 : a.width[c];
-        const void* src = c < 0 ? nullptr : a.src[c];
+    // keys | original rows as one word, then every payload column. Software-pipelined: column c + 1 is loaded
+    // into registers before column c's stores are issued, so waiting for those loads (vmcnt counts loads and
+    // stores in issue order on gfx9) never waits for the stores.
+    auto load_word = [&](int c, uint64_t* v) {
+        const int wd = a.width[c];
+        const void* src = a.src[c];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int64_t i = wbase + r * 64 + lane;
+            uint64_t x = 0;
             if (i < a.n) {
-                uint64_t v;
-                if (c < 0) v = (uint64_t)a.keys_in[i] | ((uint64_t)(a.orig_in ? a.orig_in[i] : (uint32_t)i) << 32);
-                else if (wd == 8) v = ((const uint64_t*)src)[i];
-                else if (wd == 4) v = ((const uint32_t*)src)[i];
-                else v = ((const uint8_t*)src)[i];
-                stage[sp[r]] = v;
+                if (wd == 8) x = ((const uint64_t*)src)[i];
+                else if (wd == 4) x = ((const uint32_t*)src)[i];
+                else x = ((const uint8_t*)src)[i];
             }
-            if (a.mono_col >= 0 && c == a.mono_col) {  // arrival-order timestamps: compare with row i - 1
-                const uint64_t raw = i < a.n ? ((const uint64_t*)src)[i] : 0ull;
-                uint64_t prev = __shfl_up(raw, 1);
-                if (lane == 0 && i > 0 && i < a.n) prev = ((const uint64_t*)src)[i - 1];
-                if (i > 0 && i < a.n && (int64_t)raw < (int64_t)prev) *a.mono_flag = 1;
+            v[r] = x;
+        }
+    };
+    uint64_t cur[R], nxt[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int64_t i = wbase + r * 64 + lane;
+        cur[r] = (uint64_t)kreg[r] | ((uint64_t)(a.orig_in ? (i < a.n ? a.orig_in[i] : 0u) : (uint32_t)i) << 32);
+    }
+    for (int c = -1; c < a.ncols; ++c) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int64_t i = wbase + r * 64 + lane;
+            if (i < a.n) stage[sp[r]] = cur[r];
+        }
+        if (a.mono_col >= 0 && c == a.mono_col) {  // arrival-order timestamps: compare with row i - 1
+            const uint64_t* src = (const uint64_t*)a.src[c];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int64_t i = wbase + r * 64 + lane;
+                uint64_t prev = __shfl_up(cur[r], 1);
+                if (lane == 0 && i > 0 && i < a.n) prev = src[i - 1];
+                if (i > 0 && i < a.n && (int64_t)cur[r] < (int64_t)prev) *a.mono_flag = 1;
             }
         }
         __syncthreads();
+        if (c + 1 < a.ncols) load_word(c + 1, nxt);
+        const int wd = c < 0 ? 8 : a.width[c];
         void* dst = c < 0 ? nullptr : a.dst[c];
-        for (int j = t; j < tile_n; j += RX_THREADS) {
-            const uint32_t o = dest[j];
-            const uint64_t v = stage[j];
-            if (c < 0) {
-                a.keys_out[o] = (uint32_t)v;
-                a.orig_out[o] = (uint32_t)(v >> 32);
-            } else if (wd == 8) {
-                ((uint64_t*)dst)[o] = v;
-            } else if (wd == 4) {
-                ((uint32_t*)dst)[o] = (uint32_t)v;
-            } else {
-                ((uint8_t*)dst)[o] = (uint8_t)v;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int j = r * RX_THREADS + t;
+            if (j < tile_n) {
+                const uint32_t o = dest[j];
+                const uint64_t v = stage[j];
+                if (c < 0) {
+                    a.keys_out[o] = (uint32_t)v;
+                    a.orig_out[o] = (uint32_t)(v >> 32);
+                } else if (wd == 8) {
+                    ((uint64_t*)dst)[o] = v;
+                } else if (wd == 4) {
+                    ((uint32_t*)dst)[o] = (uint32_t)v;
+                } else {
+                    ((uint8_t*)dst)[o] = (uint8_t)v;
+                }
             }
         }
         __syncthreads();
+#pragma unroll
+        for (int r = 0; r < R; ++r) cur[r] = nxt[r];
     }
 }
 
