@@ -873,8 +873,9 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
         else bbase[t] = run ? atomicAdd(ctr, (unsigned long long)run) : 0ull;
     }
     __syncthreads();
-    // ---- emit matches: slots and rows of every round first, then each column's loads for all rounds together
-    // (independent loads in flight instead of one dependent chain per match) -------------------------------
+    // ---- emit matches: slots and rows of every round first (LDS only), then every load of every round, then
+    // the stores. Loads are issued before any store: gfx9's vmcnt retires loads and stores in issue order, so a
+    // load issued after a store would wait for that store too. --------------------------------------------------
     if (a.fu_skip & 2) return;
     constexpr uint32_t NOSLOT = 0xFFFFFFFFu;
     uint32_t slot[FU_PT], prow[FU_PT], qrow[FU_PT];
@@ -895,50 +896,57 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
                 slot[k] = (uint32_t)sl;
                 prow[k] = s_row[sw(pos)];
                 qrow[k] = FU_OK(out < (uint32_t)nr, 5) ? s_row[sw(out)] : s_row[sw(pos)];
-                FU_OK(prow[k] < (uint32_t)nr && qrow[k] < (uint32_t)nr, 6);
-                a.out_ts[sl] = tbase + (int64_t)s_ts[sw(out)];
             }
         }
     }
+    FU_TRACE(6);
+    // the common select: <= 2 plain 8-byte attributes of e1 / e2 without nulls (block-uniform)
+    const int n_out = sp.n_out;
+    Instr in0 = {}, in1 = {};
+    if (n_out >= 1) in0 = load_instr(&sp.out_ins[0]);
+    if (n_out >= 2) in1 = load_instr(&sp.out_ins[1]);
+    auto plain8 = [&](const Instr& in) {
+        return (in.c == 0 || in.c == -1) && in.a < 2 && (in.k == VK_I64 || in.k == VK_F64) && !a.nulls[in.b];
+    };
+    const bool fast = n_out <= 2 && (n_out < 1 || plain8(in0)) && (n_out < 2 || plain8(in1));
+    const int jfrom = fast ? n_out : 0;  // output columns left to the general loop below
     {
+        const int64_t* c0p = n_out >= 1 ? (const int64_t*)a.cols[in0.b] : nullptr;
+        const int64_t* c1p = n_out >= 2 ? (const int64_t*)a.cols[in1.b] : nullptr;
         uint32_t op[FU_PT], oq[FU_PT];
+        int64_t v0[FU_PT], v1[FU_PT];
 #pragma unroll
         for (int k = 0; k < FU_PT; ++k)
             if (slot[k] != NOSLOT) {
                 op[k] = a.orig[lo + prow[k]];
                 oq[k] = a.orig[lo + qrow[k]];
+                if (fast && n_out >= 1) v0[k] = c0p[lo + (in0.a == 0 ? prow[k] : qrow[k])];
+                if (fast && n_out >= 2) v1[k] = c1p[lo + (in1.a == 0 ? prow[k] : qrow[k])];
             }
+        int64_t* const ov0 = a.out_vals;
+        int64_t* const ov1 = a.out_vals + a.out_cap;
 #pragma unroll
         for (int k = 0; k < FU_PT; ++k)
             if (slot[k] != NOSLOT) {
+                a.out_ts[slot[k]] = tbase + (int64_t)s_ts[sw(res[k])];
                 a.out_emit_seq[slot[k]] = a.seq_base + (int64_t)oq[k];
                 a.out_first_seq[slot[k]] = a.seq_base + (int64_t)op[k];
+                if (fast && n_out >= 1) ov0[slot[k]] = v0[k];
+                if (fast && n_out >= 2) ov1[slot[k]] = v1[k];
             }
     }
-    FU_TRACE(6);
     uint32_t nm[FU_PT];
 #pragma unroll
     for (int k = 0; k < FU_PT; ++k) nm[k] = 0;
-    for (int j = 0; j < sp.n_out; ++j) {
+    for (int j = jfrom; j < n_out; ++j) {
         const Instr in = load_instr(&sp.out_ins[j]);  // a plain attribute (the fused path has no select bytecode)
         const bool ok = (in.c == 0 || in.c == -1) && in.a < 2;
         const void* cp = a.cols[in.b];
         const uint8_t* np = a.nulls[in.b];
         int64_t* const ov = a.out_vals + (int64_t)j * a.out_cap;
-        if (ok && (in.k == VK_I64 || in.k == VK_F64)) {  // 8-byte column: plain loads, all rounds in flight
-            const int64_t* c8 = (const int64_t*)cp;
-            int64_t v[FU_PT];
 #pragma unroll
-            for (int k = 0; k < FU_PT; ++k)
-                if (slot[k] != NOSLOT) v[k] = c8[lo + (in.a == 0 ? prow[k] : qrow[k])];
-#pragma unroll
-            for (int k = 0; k < FU_PT; ++k)
-                if (slot[k] != NOSLOT) ov[slot[k]] = v[k];
-        } else {
-#pragma unroll
-            for (int k = 0; k < FU_PT; ++k)
-                if (slot[k] != NOSLOT) ov[slot[k]] = ok ? load_col(cp, in.k, lo + (in.a == 0 ? prow[k] : qrow[k])) : 0;
-        }
+        for (int k = 0; k < FU_PT; ++k)
+            if (slot[k] != NOSLOT) ov[slot[k]] = ok ? load_col(cp, in.k, lo + (in.a == 0 ? prow[k] : qrow[k])) : 0;
         if (!ok || np) {
 #pragma unroll
             for (int k = 0; k < FU_PT; ++k)
