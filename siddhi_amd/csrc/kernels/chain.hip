@@ -589,15 +589,15 @@ __global__ __launch_bounds__(256) void chain_carry_k(const ChainArgs* __restrict
         if (a.dbg && lane == 0) a.dbg[(int64_t)blockIdx.x * 4 + w] = (stage);                              \
     } while (0)
 
-static_assert(FU_THREADS == 256, "chain_fused_k: one thread per local key in the run tables");
+static_assert(FU_THREADS >= 256, "chain_fused_k: one thread per local key in the run tables");
 static_assert(FU_PT <= 32, "chain_fused_k: a lane's deque is a 32-bit mask over its positions");
 constexpr uint16_t R_NONE = 0xFFFF, R_CARRY = 0xFFFE, R_OVF = 0xFFFD;
-// LDS swizzle of the per-position arrays: the deque pass gives lane t the positions [16t, 16t + 16), so
-// unswizzled, one step of a wave hits every lane's element at a 16-position stride (one or two banks). XOR-ing
-// the low 4 bits with the next 4 spreads those over the banks; runs of consecutive positions stay permuted
-// within their aligned group of 16 (conflict-free for the per-round `k * 256 + t` accesses too).
-static_assert(FU_PT == 16, "sw() swizzles at the deque chunk size");
-__device__ __forceinline__ int sw(int p) { return p ^ ((p >> 4) & 15); }
+// LDS swizzle of the per-position arrays: the deque pass gives lane t the positions [FU_PT t, FU_PT (t + 1)), so
+// unswizzled, one step of a wave hits every lane's element at an FU_PT-position stride (few banks). XOR-ing the
+// low log2(FU_PT) bits with the next ones spreads those over the banks; runs of consecutive positions stay
+// permuted within their aligned group of FU_PT (still conflict-free for the per-round `k * FU_THREADS + t` accesses).
+static_assert((FU_PT & (FU_PT - 1)) == 0, "sw() swizzles at the deque chunk size");
+__device__ __forceinline__ int sw(int p) { return p ^ ((p / FU_PT) & (FU_PT - 1)); }
 static_assert(FU_ROWS < 65536, "chain_fused_k: u16 rows / run offsets");
 
 // SAME: the scanned column's kind is the comparison kind (no conversion in the scan loop)
@@ -666,7 +666,7 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
         return;                                   // block-uniform
     }
     if (a.fu_skip & 4) {
-        if (rts[0] == -12345 && rx[FU_PT - 1] == 7 && rkey[3] == 9) a.flags[2] = 1;  // keep the loads alive
+        if (rts[0] == -12345 && rx[FU_PT - 1] == 7 && rkey[FU_PT / 2] == 9) a.flags[2] = 1;  // keep the loads alive
         return;
     }
     __syncthreads();
@@ -701,15 +701,15 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
             tot += c;
         }
     }
-    lend[t] = (uint16_t)tot;
+    if (t < 256) lend[t] = (uint16_t)tot;
     __syncthreads();
     for (int off = 1; off < 256; off <<= 1) {  // inclusive scan of the run lengths (<= FU_ROWS: fits u16)
-        const uint32_t x = t >= off ? lend[t - off] : 0u;
+        const uint32_t x = (t < 256 && t >= off) ? lend[t - off] : 0u;
         __syncthreads();
-        lend[t] = (uint16_t)(lend[t] + x);
+        if (t < 256) lend[t] = (uint16_t)(lend[t] + x);
         __syncthreads();
     }
-    lstart[t] = (uint16_t)(lend[t] - tot);
+    if (t < 256) lstart[t] = (uint16_t)(lend[t] - tot);
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < FU_PT; ++r) {

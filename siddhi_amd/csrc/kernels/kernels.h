@@ -174,8 +174,8 @@ void chain_carry(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
 // (the same scan over the bucket in HBM, key-filtered); one that reaches the bucket end is carried.
 // Preconditions (host): partitioned, one stream, two states, `within`, typed e2 scan without nulls, FastPred
 // e1 filter, plain-attribute selects, K <= 2^16, batch timestamps non-decreasing (checked by bucketize).
-constexpr int FU_THREADS = 256;
-constexpr int FU_PT = 16;                            // staged rows per lane
+constexpr int FU_THREADS = 512;
+constexpr int FU_PT = 8;                             // staged rows per lane (= the deque chunk)
 constexpr int FU_ROWS = FU_THREADS * FU_PT;          // 4096 rows in LDS
 constexpr int FU_HALO = 1024;
 constexpr int FU_OWN = FU_ROWS - FU_HALO;            // candidate rows per block
