@@ -198,7 +198,7 @@ def main():
         "config": {"workload": "C2: partition with (symbol of StockStream) every e1=StockStream[price>20] -> "
                                "e2=StockStream[price>e1.price] within 1 sec",
                    "events_per_gpu_per_step": n, "keys_per_gpu": keys, "parallelism": "key-hash shards x%d" % world,
-                   "matches_per_step": total_matches / K, "path": "fused bucket matcher" if st.fused == 1 else
+                   "matches_per_step": total_matches / K, "overflow_scans_last_step": st.fused_ovf, "path": "fused bucket matcher" if st.fused == 1 else
                    "radix key sort + chain kernels"},
         "roofline": {"bound": "hbm", "kernel": kernel_names.get(dom, dom), "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -175,9 +175,9 @@ void chain_carry(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
 // Preconditions (host): partitioned, one stream, two states, `within`, typed e2 scan without nulls, FastPred
 // e1 filter, plain-attribute selects, K <= 2^16, batch timestamps non-decreasing (checked by bucketize).
 constexpr int FU_THREADS = 512;
-constexpr int FU_PT = 8;                             // staged rows per lane (= the deque chunk)
+constexpr int FU_PT = 4;                             // staged rows per lane (= the deque chunk)
 constexpr int FU_ROWS = FU_THREADS * FU_PT;          // 4096 rows in LDS
-constexpr int FU_HALO = 1024;
+constexpr int FU_HALO = 512;
 constexpr int FU_OWN = FU_ROWS - FU_HALO;            // candidate rows per block
 // grid size for n rows in nb buckets (a multiple of 8: the XCD remap needs it)
 int64_t chain_fused_grid(int64_t n, int nb);
