@@ -154,7 +154,10 @@ __device__ int64_t scan_typed(const ChainArgs& a, const View& v, int64_t from, i
     }
     const bool filt = a.bstart != nullptr;  // bucket view: other keys' rows are interleaved
     for (; q < end; ++q) {
-        if (filt && a.key[q] != kf) continue;
+        if (filt) {  // bucket view rows are time-ordered: past the window at any row, no later row can match
+            if (has_within && ts_row(a, v, q) - ts0 > within) return -1;
+            if (a.key[q] != kf) continue;
+        }
         // StreamPreStateProcessor.isExpired: |start.ts - now| > within, checked before the event is processed
         if (has_within) {
             int64_t d = ts0 - ts_row(a, v, q);
@@ -199,7 +202,10 @@ __device__ __forceinline__ int64_t chain_scan(const ChainArgs& a, ChainAcc& acc,
     }
     if (!GEN) return -2;  // unreachable: the host picks GEN for SCAN_GENERIC
     for (int64_t q = from; q < end; ++q) {
-        if (a.bstart && a.key[q] != kf) continue;
+        if (a.bstart) {  // bucket view: time-ordered rows (see scan_typed)
+            if (sp.has_within && ts_row(a, acc.V, q) - ts0 > sp.within_ms) return -1;
+            if (a.key[q] != kf) continue;
+        }
         if (sp.has_within) {
             int64_t d = ts0 - ts_row(a, acc.V, q);
             if (d < 0) d = -d;
@@ -575,6 +581,105 @@ __global__ __launch_bounds__(256) void chain_carry_k(const ChainArgs* __restrict
 }
 
 
+// Carried partials (typed scans): one WAVE per carried partial scans its key's rows 64 at a time, coalesced; the
+// first lane that completes the partial or proves it dead decides (rows are in arrival order, so this is the
+// lane-serial scan_typed result). One lane per partial scanning ~a window of the bucket serially was the latency
+// tail of the step (chain_carry_k: 0.2 ms for ~10^4 partials).
+template <int K>
+__device__ int64_t wave_scan_typed(const ChainArgs& a, int64_t from, int64_t end, int64_t ts0, int64_t k, uint8_t op,
+                                   uint32_t kf) {
+    using C = KT<K>;
+    const typename C::T y = C::get(k);
+    const ChainSpec& sp = a.sp;
+    const int col = sp.scan_col;
+    const uint8_t kind = sp.scan_col_kind;
+    const bool left = sp.scan_e2_left, always = op == OP_ALWAYS, filt = a.bstart != nullptr;
+    const int32_t has_within = sp.has_within;
+    const int64_t within = sp.within_ms;
+    const CmpMask m = cmp_mask(op);
+    const int lane = lane_id();
+    for (int64_t q0 = from; q0 < end; q0 += 64) {
+        const int64_t q = q0 + lane;
+        bool stop = false, hit = false;
+        if (q < end) {
+            const int64_t d = a.ts[q] - ts0;
+            if (filt && has_within && d > within) {
+                stop = true;  // time-ordered bucket: no later row of the key is alive
+            } else if (!filt || a.key[q] == kf) {
+                if (has_within && (d < 0 ? -d : d) > within) stop = true;  // isExpired at this event of the key
+                else if (qs_row(a, View{}, q) == a.s1) {
+                    if (always) hit = true;
+                    else if (!null_row(a, col, q)) {
+                        const typename C::T x = C::get(cvt(load_col(a.cols[col], kind, q), kind, (uint8_t)K));
+                        hit = left ? cmp_m(m, x, y) : cmp_m(m, y, x);
+                    }
+                }
+            }
+        }
+        const uint64_t bh = __ballot(hit), any = bh | __ballot(stop);
+        if (any) {
+            const int l = __ffsll((unsigned long long)any) - 1;
+            return ((bh >> l) & 1u) ? q0 + l : -1;
+        }
+    }
+    return -2;
+}
+
+__global__ __launch_bounds__(256) void chain_carry_wave_k(const ChainArgs* __restrict__ pa) {
+    const ChainArgs& a = *pa;
+    const ChainSpec& sp = a.sp;
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= a.cin_n) return;  // wave-uniform
+    const uint32_t key = a.cin_key[c];
+    int64_t b = 0, e = a.n;
+    if (a.bstart) {
+        const uint32_t bk = key & ((1u << a.bbits) - 1u);
+        b = a.bstart[bk];
+        e = a.bstart[bk + 1];
+    } else if (a.key) {
+        b = key < (uint32_t)a.K ? (int64_t)a.seg_start[key] : 0;
+        e = key < (uint32_t)a.K ? (int64_t)a.seg_end[key] : 0;
+    }
+    ChainAcc acc{&a, View{}, -1, c, -1};
+    int64_t k = sp.scan_konst;
+    uint8_t op = sp.scan_op;
+    if (sp.scan_mode == SCAN_TRUE) {
+        op = OP_ALWAYS;
+    } else if (sp.scan_mode == SCAN_E1) {
+        bool nl;
+        acc.load(0, sp.e1_col, 0, sp.e1_col_kind, &k, &nl);
+        if (nl) op = OP_NEVER;
+        else k = cvt(k, sp.e1_col_kind, sp.scan_t);
+    }
+    const int64_t ts0 = a.cin_ts[c];
+    int64_t r;
+    switch (sp.scan_t) {
+        case VK_I32: r = wave_scan_typed<VK_I32>(a, b, e, ts0, k, op, key); break;
+        case VK_I64: r = wave_scan_typed<VK_I64>(a, b, e, ts0, k, op, key); break;
+        case VK_F32: r = wave_scan_typed<VK_F32>(a, b, e, ts0, k, op, key); break;
+        case VK_F64: r = wave_scan_typed<VK_F64>(a, b, e, ts0, k, op, key); break;
+        case VK_BOOL: r = wave_scan_typed<VK_BOOL>(a, b, e, ts0, k, op, key); break;
+        default: r = wave_scan_typed<VK_STR>(a, b, e, ts0, k, op, key); break;
+    }
+    if (lane_id() != 0 || r == -1) return;
+    if (r >= 0) {
+        const int64_t slot = (int64_t)atomicAdd(a.out_count, 1ull);
+        if (slot >= a.out_cap) atomicOr(&a.flags[0], 1);
+        else emit_match<false>(a, acc, slot, r, key, a.cin_seq[c], nullptr, 0);
+        return;
+    }
+    const int64_t cs = (int64_t)atomicAdd(a.carry_count, 1ull);
+    if (cs >= a.carry_cap) {
+        atomicOr(&a.flags[0], 1);
+        return;
+    }
+    a.carry_key[cs] = key;
+    a.carry_ts[cs] = ts0;
+    a.carry_seq[cs] = a.cin_seq[c];
+    for (int j = 0; j < sp.n_cols; ++j) a.carry_vals[(int64_t)j * a.carry_cap + cs] = a.cin_vals[(int64_t)j * a.cin_cap + c];
+    a.carry_nulls[cs] = a.cin_nulls[c];
+}
+
 // ---------------------------------------------------------------------------------------------------------
 // Fused bucket matcher (kernels.h). Block = (bucket b, segment s): rows [lo, lo + own) of the bucket are its
 // candidates, rows [lo, lo + nr) (own + halo) are staged. Staging regroups the rows by local key (key >> bbits)
@@ -741,6 +846,12 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
     const T k0 = C::get(f0.konst);
     const T kc = C::get(sp.scan_konst);
     const uint16_t ran_off = to_end ? R_CARRY : R_OVF;  // a partial still pending when its key's staged rows end
+    // ... unless the staged span already reaches past its window: every later row of the bucket (so every later
+    // event of its key) has ts >= tlast, where the partial is expired (isExpired) -- dead, no HBM scan needed
+    const uint32_t tl_off = (uint32_t)(tlast - tbase);
+    auto ran_res = [&](int pos) -> uint16_t {
+        return (!to_end && (uint64_t)(tl_off - s_ts[sw(pos)]) > within_u) ? R_NONE : ran_off;
+    };
     auto c0_at = [&](int pos, int64_t xr, T xv) -> bool {  // the e1 filter of the row at `pos`
         if (f0_typed) return cmp_m(m0, xv, k0);
         if (f0_on_x) return cmp(f0.op, f0.t, cvt(xr, kind, f0.t), f0.konst);
@@ -798,7 +909,7 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
                 ytop = x;
             }
             if (q + 1 == cur_end) {  // the key's staged rows end here: its pending partials ran off
-                for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = ran_off;
+                for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = ran_res(p0 + __builtin_ctz(pend));
                 if (q + 1 < pe) cur_end = (int)lend[s_lk[sw(q + 1)]];
             }
         }
@@ -808,7 +919,7 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
             const int64_t xr = s_x[sw(q)];
             step(q, s_ts[sw(q)], SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K)));
         }
-        for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = ran_off;  // staged rows ended
+        for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = ran_res(p0 + __builtin_ctz(pend));
     } else {
         // ---- forward scans: one lane per candidate, its key's run in LDS
 #pragma unroll 1
@@ -834,7 +945,7 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
             int end = (int)lend[s_lk[sw(pos)]];
             if (!FU_OK(end <= nr && end > pos, 4)) end = pos + 1;
             if (a.fu_skip & 1) end = pos + 1;
-            uint16_t out = ran_off;
+            uint16_t out = ran_res(pos);
             for (int q = pos + 1; q < end; ++q) {
                 if ((uint64_t)(s_ts[sw(q)] - t0) > within_u) { out = R_NONE; break; }  // isExpired: dead
                 const T x = SAME ? C::get(s_x[sw(q)]) : C::get(cvt(s_x[sw(q)], kind, (uint8_t)K));
@@ -1048,7 +1159,10 @@ void chain_deque(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
 
 void chain_carry(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
     if (a.cin_n <= 0) return;
-    hipLaunchKernelGGL(chain_carry_k, dim3((unsigned)((a.cin_n + 255) / 256)), dim3(256), 0, stream, d_a);
+    if (!a.generic && a.sp.scan_mode != SCAN_GENERIC && !getenv("SDG_CARRY_LANE"))
+        hipLaunchKernelGGL(chain_carry_wave_k, dim3((unsigned)((a.cin_n + 3) / 4)), dim3(256), 0, stream, d_a);
+    else
+        hipLaunchKernelGGL(chain_carry_k, dim3((unsigned)((a.cin_n + 255) / 256)), dim3(256), 0, stream, d_a);
 }
 
 int64_t chain_fused_grid(int64_t n, int nb) {

@@ -112,13 +112,13 @@ struct RxPass {
 // LDS ops of one wave are in order, so no block barrier while counting). Then per digit: prefix over waves
 // and the tile's digit starts; each column is staged in LDS in digit order and written out as coalesced runs
 // (keys and original rows together as one 8-byte word).
-__global__ __launch_bounds__(RX_THREADS) void rx_scatter(RxPass a) {
+__global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {  // 4 waves/SIMD: 2 blocks per CU
     constexpr int R = RX_TILE / RX_THREADS;  // 16 elements per lane
     constexpr int NW = RX_THREADS / 64;
     __shared__ uint16_t wc[NW][1 << RX_MAXBITS];  // per-wave digit counts (<= 1024), then per-wave digit bases
     __shared__ uint32_t tstart[1 << RX_MAXBITS];
     __shared__ uint32_t gbase[1 << RX_MAXBITS];
-    __shared__ uint32_t dest[RX_TILE];
+    __shared__ uint8_t sdig[RX_TILE];  // digit of each staged element: its destination is gbase + rank in the run
     __shared__ uint64_t stage[RX_TILE];
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const int64_t base = (int64_t)blockIdx.x * RX_TILE;
@@ -180,14 +180,17 @@ __global__ __launch_bounds__(RX_THREADS) void rx_scatter(RxPass a) {
     }
     if (t < 256) tstart[t] -= tot;
     __syncthreads();
-    uint32_t sp[R];
+    static_assert(RX_TILE <= 65536, "staged positions packed as u16 pairs");
+    uint32_t sp2[R / 2];  // staged position of element r: u16 half (r & 1) of sp2[r / 2] (registers)
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int64_t i = wbase + r * 64 + lane;
         const uint32_t wr = wc[w][dig[r]] + rank[r];  // rank among the tile's elements of this digit
-        sp[r] = tstart[dig[r]] + wr;
-        if (i < a.n) dest[sp[r]] = gbase[dig[r]] + wr;
+        const uint32_t p = tstart[dig[r]] + wr;
+        sp2[r / 2] = (r & 1) ? (sp2[r / 2] | (p << 16)) : p;
+        if (i < a.n) sdig[p] = dig[r];
     }
+    auto sp_of = [&](int r) -> uint32_t { return (sp2[r / 2] >> ((r & 1) * 16)) & 0xFFFFu; };
     // keys | original rows as one word, then every payload column. Software-pipelined: column c + 1 is loaded
     // into registers before column c's stores are issued, so waiting for those loads (vmcnt counts loads and
     // stores in issue order on gfx9) never waits for the stores.
@@ -216,7 +219,7 @@ __global__ __launch_bounds__(RX_THREADS) void rx_scatter(RxPass a) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int64_t i = wbase + r * 64 + lane;
-            if (i < a.n) stage[sp[r]] = cur[r];
+            if (i < a.n) stage[sp_of(r)] = cur[r];
         }
         if (a.mono_col >= 0 && c == a.mono_col) {  // arrival-order timestamps: compare with row i - 1
             const uint64_t* src = (const uint64_t*)a.src[c];
@@ -236,7 +239,8 @@ __global__ __launch_bounds__(RX_THREADS) void rx_scatter(RxPass a) {
         for (int r = 0; r < R; ++r) {
             const int j = r * RX_THREADS + t;
             if (j < tile_n) {
-                const uint32_t o = dest[j];
+                const uint32_t dj = sdig[j];
+                const uint32_t o = gbase[dj] + (uint32_t)j - tstart[dj];
                 const uint64_t v = stage[j];
                 if (c < 0) {
                     a.keys_out[o] = (uint32_t)v;
