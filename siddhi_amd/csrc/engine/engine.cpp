@@ -56,6 +56,26 @@ struct DevBuf {
     T* as() const { return (T*)p; }
 };
 
+// pinned host staging for the per-flush kernel arguments and read-backs: hipMemcpyAsync from pageable memory
+// goes through a bounce buffer on the host thread (tens of us per copy on the flush's critical path)
+struct HostPin {
+    void* p = nullptr;
+    size_t cap = 0;
+    HostPin() = default;
+    HostPin(const HostPin&) = delete;
+    HostPin& operator=(const HostPin&) = delete;
+    ~HostPin() { if (p) (void)hipHostFree(p); }
+    void* ensure(size_t bytes) {
+        if (bytes > cap) {
+            if (p) HIPCHECK(hipHostFree(p));
+            p = nullptr;
+            HIPCHECK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+            cap = bytes;
+        }
+        return p;
+    }
+};
+
 int width_of(uint8_t kind) {
     switch (kind) {
         case VK_I64: case VK_F64: return 8;
@@ -110,6 +130,7 @@ struct PushChunk {
 struct QueryRt {
     HostQuery hq;
     DevBuf d_plan, d_code, d_consts, d_args, o_mq, o_ovf, o_ovfc;
+    HostPin h_args, h_ret;  // chain path: ChainArgs pair; counters (16 B) | flags (16 B) | overflow count (8 B)
     bool string_keys = true;                        // all partition keys are string attributes (ids used as keys)
     std::unordered_map<std::string, uint32_t> keydict;
     int64_t seq = 0;
@@ -663,10 +684,11 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         HIPCHECK(hipMemsetAsync(a.ovf_count, 0, 8, st));
     }
     ChainArgs* d_a = (ChainArgs*)q.d_args.ensure(2 * sizeof(ChainArgs));
-    HIPCHECK(hipMemcpyAsync(d_a, &a, sizeof a, hipMemcpyHostToDevice, st));  // `a` outlives the sync below
-    ChainArgs ae = a;  // emit-only pass over mq
-    ae.mq_in = a.mq;
-    HIPCHECK(hipMemcpyAsync(d_a + 1, &ae, sizeof ae, hipMemcpyHostToDevice, st));
+    ChainArgs* h_a = (ChainArgs*)q.h_args.ensure(2 * sizeof(ChainArgs));  // pinned; read before the sync below
+    h_a[0] = a;
+    h_a[1] = a;  // emit-only pass over mq
+    h_a[1].mq_in = a.mq;
+    HIPCHECK(hipMemcpyAsync(d_a, h_a, 2 * sizeof(ChainArgs), hipMemcpyHostToDevice, st));
     static const bool dbg = getenv("SDG_DEBUG") != nullptr;
     auto dbg_sync = [&](const char* what) {  // SDG_DEBUG: name the kernel an asynchronous fault came from
         if (!dbg) return;
@@ -720,15 +742,18 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     } else if (a.deque_mode != DQ_OFF && nrows > 0) {
         chain_deque(a, d_a, st);
         HIPCHECK(hipEventRecord(e->ev[9], st));
-        chain_match(ae, d_a + 1, st);
+        chain_match(h_a[1], d_a + 1, st);
     } else {
         HIPCHECK(hipEventRecord(e->ev[9], st));
         chain_match(a, d_a, st);
     }
     e->stats.match_launches += (cin.n > 0) + (nrows > 0);
     HIPCHECK(hipEventRecord(e->ev[2], st));
-    unsigned long long hc[2], hovf = 0;
-    int hf[4];
+    uint8_t* ret = (uint8_t*)q.h_ret.ensure(40);
+    unsigned long long* hc = (unsigned long long*)ret;
+    int* hf = (int*)(ret + 16);
+    unsigned long long& hovf = *(unsigned long long*)(ret + 32);
+    hovf = 0;
     HIPCHECK(hipMemcpyAsync(hc, counters, 16, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipMemcpyAsync(hf, flags, 16, hipMemcpyDeviceToHost, st));
     if (fused) HIPCHECK(hipMemcpyAsync(&hovf, a.ovf_count, 8, hipMemcpyDeviceToHost, st));

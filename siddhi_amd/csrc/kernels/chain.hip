@@ -598,86 +598,115 @@ __device__ int64_t wave_scan_typed(const ChainArgs& a, int64_t from, int64_t end
     const int64_t within = sp.within_ms;
     const CmpMask m = cmp_mask(op);
     const int lane = lane_id();
-    for (int64_t q0 = from; q0 < end; q0 += 64) {
-        const int64_t q = q0 + lane;
-        bool stop = false, hit = false;
-        if (q < end) {
-            const int64_t d = a.ts[q] - ts0;
-            if (filt && has_within && d > within) {
-                stop = true;  // time-ordered bucket: no later row of the key is alive
-            } else if (!filt || a.key[q] == kf) {
-                if (has_within && (d < 0 ? -d : d) > within) stop = true;  // isExpired at this event of the key
-                else if (qs_row(a, View{}, q) == a.s1) {
-                    if (always) hit = true;
-                    else if (!null_row(a, col, q)) {
-                        const typename C::T x = C::get(cvt(load_col(a.cols[col], kind, q), kind, (uint8_t)K));
-                        hit = left ? cmp_m(m, x, y) : cmp_m(m, y, x);
+    constexpr int U = 4;  // rows per lane per round: U independent loads in flight (the scan is latency-bound)
+    for (int64_t q0 = from; q0 < end; q0 += 64 * U) {
+        uint64_t bh[U], bs[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t q = q0 + u * 64 + lane;
+            bool stop = false, hit = false;
+            if (q < end) {
+                const int64_t d = a.ts[q] - ts0;
+                if (filt && has_within && d > within) {
+                    stop = true;  // time-ordered bucket: no later row of the key is alive
+                } else if (!filt || a.key[q] == kf) {
+                    if (has_within && (d < 0 ? -d : d) > within) stop = true;  // isExpired at this event of the key
+                    else if (qs_row(a, View{}, q) == a.s1) {
+                        if (always) hit = true;
+                        else if (!null_row(a, col, q)) {
+                            const typename C::T x = C::get(cvt(load_col(a.cols[col], kind, q), kind, (uint8_t)K));
+                            hit = left ? cmp_m(m, x, y) : cmp_m(m, y, x);
+                        }
                     }
                 }
             }
+            bh[u] = __ballot(hit);
+            bs[u] = __ballot(stop);
         }
-        const uint64_t bh = __ballot(hit), any = bh | __ballot(stop);
-        if (any) {
-            const int l = __ffsll((unsigned long long)any) - 1;
-            return ((bh >> l) & 1u) ? q0 + l : -1;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t any = bh[u] | bs[u];
+            if (any) {
+                const int l = __ffsll((unsigned long long)any) - 1;
+                return ((bh[u] >> l) & 1u) ? q0 + u * 64 + l : -1;
+            }
         }
     }
     return -2;
 }
 
+constexpr int CW_PER_WAVE = 16;  // carried partials resolved one after another by one wave
+
+// Block = 4 waves x CW_PER_WAVE partials; lane i of a wave keeps the result of its i-th partial, and the block
+// reserves its match / carry output with one atomic per counter (one atomic per partial serialised in L2:
+// ~10^8/s, 0.2 ms for 2 x 10^4 carries).
 __global__ __launch_bounds__(256) void chain_carry_wave_k(const ChainArgs* __restrict__ pa) {
     const ChainArgs& a = *pa;
     const ChainSpec& sp = a.sp;
-    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (c >= a.cin_n) return;  // wave-uniform
-    const uint32_t key = a.cin_key[c];
-    int64_t b = 0, e = a.n;
-    if (a.bstart) {
-        const uint32_t bk = key & ((1u << a.bbits) - 1u);
-        b = a.bstart[bk];
-        e = a.bstart[bk + 1];
-    } else if (a.key) {
-        b = key < (uint32_t)a.K ? (int64_t)a.seg_start[key] : 0;
-        e = key < (uint32_t)a.K ? (int64_t)a.seg_end[key] : 0;
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const int64_t c_base = ((int64_t)blockIdx.x * 4 + w) * CW_PER_WAVE;
+    int64_t mine = -1;  // lane i: the scan result of partial c_base + i
+    for (int i = 0; i < CW_PER_WAVE; ++i) {
+        const int64_t c = c_base + i;
+        if (c >= a.cin_n) break;  // wave-uniform
+        const uint32_t key = a.cin_key[c];
+        int64_t b = 0, e = a.n;
+        if (a.bstart) {
+            const uint32_t bk = key & ((1u << a.bbits) - 1u);
+            b = a.bstart[bk];
+            e = a.bstart[bk + 1];
+        } else if (a.key) {
+            b = key < (uint32_t)a.K ? (int64_t)a.seg_start[key] : 0;
+            e = key < (uint32_t)a.K ? (int64_t)a.seg_end[key] : 0;
+        }
+        ChainAcc acc{&a, View{}, -1, c, -1};
+        int64_t k = sp.scan_konst;
+        uint8_t op = sp.scan_op;
+        if (sp.scan_mode == SCAN_TRUE) {
+            op = OP_ALWAYS;
+        } else if (sp.scan_mode == SCAN_E1) {
+            bool nl;
+            acc.load(0, sp.e1_col, 0, sp.e1_col_kind, &k, &nl);
+            if (nl) op = OP_NEVER;
+            else k = cvt(k, sp.e1_col_kind, sp.scan_t);
+        }
+        const int64_t ts0 = a.cin_ts[c];
+        int64_t r;
+        switch (sp.scan_t) {
+            case VK_I32: r = wave_scan_typed<VK_I32>(a, b, e, ts0, k, op, key); break;
+            case VK_I64: r = wave_scan_typed<VK_I64>(a, b, e, ts0, k, op, key); break;
+            case VK_F32: r = wave_scan_typed<VK_F32>(a, b, e, ts0, k, op, key); break;
+            case VK_F64: r = wave_scan_typed<VK_F64>(a, b, e, ts0, k, op, key); break;
+            case VK_BOOL: r = wave_scan_typed<VK_BOOL>(a, b, e, ts0, k, op, key); break;
+            default: r = wave_scan_typed<VK_STR>(a, b, e, ts0, k, op, key); break;
+        }
+        if (lane == i) mine = r;
     }
-    ChainAcc acc{&a, View{}, -1, c, -1};
-    int64_t k = sp.scan_konst;
-    uint8_t op = sp.scan_op;
-    if (sp.scan_mode == SCAN_TRUE) {
-        op = OP_ALWAYS;
-    } else if (sp.scan_mode == SCAN_E1) {
-        bool nl;
-        acc.load(0, sp.e1_col, 0, sp.e1_col_kind, &k, &nl);
-        if (nl) op = OP_NEVER;
-        else k = cvt(k, sp.e1_col_kind, sp.scan_t);
+    const int64_t c = c_base + lane;
+    const bool valid = lane < CW_PER_WAVE && c < a.cin_n;
+    const bool has = valid && mine >= 0, carry = valid && mine == -2;
+    int64_t slot, cs;
+    block_reserve2<256>(has, carry, a.out_count, a.carry_count, &slot, &cs);
+    if (has) {
+        if (slot >= a.out_cap) {
+            atomicOr(&a.flags[0], 1);
+        } else {
+            ChainAcc acc{&a, View{}, -1, c, -1};
+            emit_match<false>(a, acc, slot, mine, a.cin_key[c], a.cin_seq[c], nullptr, 0);
+        }
     }
-    const int64_t ts0 = a.cin_ts[c];
-    int64_t r;
-    switch (sp.scan_t) {
-        case VK_I32: r = wave_scan_typed<VK_I32>(a, b, e, ts0, k, op, key); break;
-        case VK_I64: r = wave_scan_typed<VK_I64>(a, b, e, ts0, k, op, key); break;
-        case VK_F32: r = wave_scan_typed<VK_F32>(a, b, e, ts0, k, op, key); break;
-        case VK_F64: r = wave_scan_typed<VK_F64>(a, b, e, ts0, k, op, key); break;
-        case VK_BOOL: r = wave_scan_typed<VK_BOOL>(a, b, e, ts0, k, op, key); break;
-        default: r = wave_scan_typed<VK_STR>(a, b, e, ts0, k, op, key); break;
+    if (carry) {
+        if (cs >= a.carry_cap) {
+            atomicOr(&a.flags[0], 1);
+        } else {
+            a.carry_key[cs] = a.cin_key[c];
+            a.carry_ts[cs] = a.cin_ts[c];
+            a.carry_seq[cs] = a.cin_seq[c];
+            for (int j = 0; j < sp.n_cols; ++j)
+                a.carry_vals[(int64_t)j * a.carry_cap + cs] = a.cin_vals[(int64_t)j * a.cin_cap + c];
+            a.carry_nulls[cs] = a.cin_nulls[c];
+        }
     }
-    if (lane_id() != 0 || r == -1) return;
-    if (r >= 0) {
-        const int64_t slot = (int64_t)atomicAdd(a.out_count, 1ull);
-        if (slot >= a.out_cap) atomicOr(&a.flags[0], 1);
-        else emit_match<false>(a, acc, slot, r, key, a.cin_seq[c], nullptr, 0);
-        return;
-    }
-    const int64_t cs = (int64_t)atomicAdd(a.carry_count, 1ull);
-    if (cs >= a.carry_cap) {
-        atomicOr(&a.flags[0], 1);
-        return;
-    }
-    a.carry_key[cs] = key;
-    a.carry_ts[cs] = ts0;
-    a.carry_seq[cs] = a.cin_seq[c];
-    for (int j = 0; j < sp.n_cols; ++j) a.carry_vals[(int64_t)j * a.carry_cap + cs] = a.cin_vals[(int64_t)j * a.cin_cap + c];
-    a.carry_nulls[cs] = a.cin_nulls[c];
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -1160,7 +1189,8 @@ void chain_deque(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
 void chain_carry(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
     if (a.cin_n <= 0) return;
     if (!a.generic && a.sp.scan_mode != SCAN_GENERIC && !getenv("SDG_CARRY_LANE"))
-        hipLaunchKernelGGL(chain_carry_wave_k, dim3((unsigned)((a.cin_n + 3) / 4)), dim3(256), 0, stream, d_a);
+        hipLaunchKernelGGL(chain_carry_wave_k, dim3((unsigned)((a.cin_n + 4 * CW_PER_WAVE - 1) / (4 * CW_PER_WAVE))),
+                           dim3(256), 0, stream, d_a);
     else
         hipLaunchKernelGGL(chain_carry_k, dim3((unsigned)((a.cin_n + 255) / 256)), dim3(256), 0, stream, d_a);
 }
