@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Secondary throughput lines for the other BASELINE.json configs (bench.py measures C2 only).
+
+C1: unpartitioned chain query on 1M ticks, one flush per step, consecutive batches of one stream.
+C3: the count-quantifier SEQUENCE on `--c3-keys` keys x 100 events (generic keyed NFA, nfa_k); the literal query
+    never matches under the reference semantics, so the `<1:5>` form is timed too.
+Inputs are device-resident; one JSON line per config. Timing brackets K flushes with torch.cuda.synchronize().
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def run(rt, stream, n, ts, cols, steps, warmup):
+    span = int(ts[-1].item() - ts[0].item()) + 1
+    tss = [ts + s * span for s in range(steps + warmup)]
+    torch.cuda.synchronize()
+
+    def step(s):
+        rt.push_device(stream, n, tss[s].data_ptr(), [c.data_ptr() for c in cols])
+        rt.flush(deliver=False)
+        return rt.stats()
+
+    for s in range(warmup):
+        step(s)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    m = 0
+    for s in range(warmup, warmup + steps):
+        m += step(s).matches
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return n * steps / dt, dt * 1000 / steps, m / steps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--c1-events", type=int, default=1_000_000)
+    ap.add_argument("--c3-keys", type=int, default=1_000_000)
+    ap.add_argument("--only", default="c1,c3,c3m")
+    ap.add_argument("--c3-steps", type=int, default=2)
+    args = ap.parse_args()
+    torch.cuda.init()
+    import siddhi_amd as sa
+    from siddhi_amd import workloads as w
+    dev = torch.device("cuda", 0)
+    only = args.only.split(",")
+    if "c1" in only:
+        n = args.c1_events
+        c = w.c1_columns(n)
+        rt = sa.SiddhiAppRuntime(w.C1_APP, device=0)
+        sym = np.full(n, rt.intern("IBM"), dtype=np.int32)
+        cols = [torch.from_numpy(c["id"]).to(dev), torch.from_numpy(sym).to(dev),
+                torch.from_numpy(c["price"]).to(dev), torch.from_numpy(c["volume"]).to(dev)]
+        ev, ms, m = run(rt, "StockStream", n, torch.from_numpy(c["ts"]).to(dev), cols, args.steps, args.warmup)
+        print(json.dumps({"config": "C1 unpartitioned, %d events/step" % n, "events_per_s": ev, "ms_per_step": ms,
+                          "matches_per_step": m}), flush=True)
+    for tag in ("c3", "c3m"):
+        if tag not in only:
+            continue
+        keys = args.c3_keys
+        c = w.c3_columns(keys)
+        n = len(c["ts"])
+        app = w.C3_APP if tag == "c3" else w.C3_APP.replace("<2:5>", "<1:5>")
+        rt = sa.SiddhiAppRuntime(app, device=0, batch_capacity=n + 1)  # one flush per step (no auto-flush)
+        ih = rt.getInputHandler("S")
+        cols = [c["id"], c["key"], c["price"], c["volume"]]
+        span = int(c["ts"][-1] - c["ts"][0]) + 1
+        # long partition keys: host push (the key's toString dictionary is built on the host), so this rate
+        # includes the host key mapping and the H2D copy
+        for s in range(args.warmup):
+            ih.send_columns(c["ts"] + s * span, cols)
+            rt.flush(deliver=False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        m = 0
+        dev_ms = 0.0
+        for s in range(args.warmup, args.warmup + args.c3_steps):
+            ih.send_columns(c["ts"] + s * span, cols)
+            rt.flush(deliver=False)
+            st = rt.stats()
+            m += st.matches
+            dev_ms += st.ms_keygroup + st.ms_match
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        print(json.dumps({"config": "C3 %s, %d keys x 100 events/step (host push)" % ("<2:5>" if tag == "c3" else "<1:5>", keys),
+                          "events_per_s_end_to_end": n * args.c3_steps / dt, "ms_per_step": dt * 1000 / args.c3_steps,
+                          "device_ms_per_step": dev_ms / args.c3_steps, "events_per_s_device": n * args.c3_steps / (dev_ms / 1000),
+                          "matches_per_step": m / args.c3_steps, "events_per_flush": st.events}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -615,7 +615,9 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     // ---- 3. chain matcher -------------------------------------------------------------------------------
     QueryRt::Carry& cin = q.carry[q.cur];
     QueryRt::Carry& cout = q.carry[q.cur ^ 1];
-    int64_t cap = nrows + cin.n + 1;
+    // output / carry capacity with slack: a buffer that grows inside a timed flush costs a hipFree (device sync)
+    // plus a multi-GB hipMalloc, so round up once instead of growing with every larger carry-in count
+    int64_t cap = nrows + nrows / 8 + cin.n + 4096;
     q.out_cap = cap;
     ChainArgs a;
     std::memset(&a, 0, sizeof a);

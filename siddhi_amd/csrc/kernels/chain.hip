@@ -943,10 +943,21 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
             }
         }
         // continuation over the key's following positions (no pushes) until the deque drains
+        // software-pipelined: row q + 1 is read from LDS while row q is processed (the step's branches depend on
+        // the row, so without this every step waits out an LDS round trip)
+        if (pe < cur_end && pend) {
+            uint32_t tn = s_ts[sw(pe)];
+            int64_t xn = s_x[sw(pe)];
 #pragma unroll 1
-        for (int q = pe; q < cur_end && pend; ++q) {
-            const int64_t xr = s_x[sw(q)];
-            step(q, s_ts[sw(q)], SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K)));
+            for (int q = pe; q < cur_end && pend; ++q) {
+                const uint32_t tq = tn;
+                const int64_t xr = xn;
+                if (q + 1 < cur_end) {
+                    tn = s_ts[sw(q + 1)];
+                    xn = s_x[sw(q + 1)];
+                }
+                step(q, tq, SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K)));
+            }
         }
         for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = ran_res(p0 + __builtin_ctz(pend));
     } else {
