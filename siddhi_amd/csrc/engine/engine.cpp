@@ -127,8 +127,50 @@ struct PushChunk {
     std::vector<const uint8_t*> d_nulls;
 };
 
+// integral partition values -> dictionary id (open addressing). Java's toString is injective on int/long and
+// equal values of either type print the same, so the value itself can stand for its string in front of keydict.
+struct IntKeyCache {
+    std::vector<int64_t> k;
+    std::vector<uint32_t> v;  // id + 1 (0 = empty slot)
+    size_t n = 0;
+    static uint64_t mix(uint64_t z) {
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    }
+    bool find(int64_t x, uint32_t* id) const {
+        if (k.empty()) return false;
+        const size_t m = k.size() - 1;
+        for (size_t i = mix((uint64_t)x) & m;; i = (i + 1) & m) {
+            if (!v[i]) return false;
+            if (k[i] == x) { *id = v[i] - 1; return true; }
+        }
+    }
+    void insert(int64_t x, uint32_t id) {
+        if (2 * (n + 1) > k.size()) {
+            std::vector<int64_t> ok;
+            std::vector<uint32_t> ov;
+            ok.swap(k);
+            ov.swap(v);
+            const size_t cap = std::max<size_t>(1024, ok.size() * 2);
+            k.assign(cap, 0);
+            v.assign(cap, 0);
+            n = 0;
+            for (size_t i = 0; i < ok.size(); ++i)
+                if (ov[i]) insert(ok[i], ov[i] - 1);
+        }
+        const size_t m = k.size() - 1;
+        size_t i = mix((uint64_t)x) & m;
+        while (v[i]) i = (i + 1) & m;
+        k[i] = x;
+        v[i] = id + 1;
+        ++n;
+    }
+};
+
 struct QueryRt {
     HostQuery hq;
+    IntKeyCache intkeys;
     DevBuf d_plan, d_code, d_consts, d_args, o_mq, o_ovf, o_ovfc;
     HostPin h_args, h_ret;  // chain path: ChainArgs pair; counters (16 B) | flags (16 B) | overflow count (8 B)
     bool string_keys = true;                        // all partition keys are string attributes (ids used as keys)
@@ -225,6 +267,12 @@ bool host_key(sdg_engine* e, QueryRt& q, int qpos, const PushChunk& c, int64_t r
         *key = ((const uint32_t*)col)[row];
         return true;
     }
+    int64_t iv = 0;
+    const bool integral = kind == VK_I32 || kind == VK_I64;
+    if (integral) {
+        iv = kind == VK_I32 ? (int64_t)((const int32_t*)col)[row] : ((const int64_t*)col)[row];
+        if (q.intkeys.find(iv, key)) return true;
+    }
     std::string s;
     switch (kind) {
         case VK_I32: s = std::to_string(((const int32_t*)col)[row]); break;
@@ -237,6 +285,7 @@ bool host_key(sdg_engine* e, QueryRt& q, int qpos, const PushChunk& c, int64_t r
     auto it = q.keydict.find(s);
     if (it == q.keydict.end()) it = q.keydict.emplace(s, (uint32_t)q.keydict.size()).first;
     *key = it->second;
+    if (integral) q.intkeys.insert(iv, *key);
     return true;
 }
 
@@ -383,26 +432,52 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         for (int k = 0; k < nc; ++k) cols[k].reserve((size_t)n * width_of(P.col_kind[k]));
         for (const PushChunk* c : parts) {
             if (c->device) throw CompileError(SDG_ERR_UNSUPPORTED, "mixed / multi-stream device-resident batches");
-            int qpos = h.stream_pos(c->stream);
-            for (int64_t r = 0; r < c->n; ++r) {
-                uint32_t key = 0;
-                if (partitioned && !host_key(e, q, qpos, *c, r, &key)) continue;  // null key: dropped
-                ts.push_back(c->ts[r]);
-                qs.push_back((uint8_t)qpos);
-                if (partitioned) keys.push_back(key);
-                for (int k = 0; k < nc; ++k) {
-                    int w = width_of(P.col_kind[k]);
-                    int ai = h.col_attr[qpos][k];
-                    size_t off = cols[k].size();
-                    cols[k].resize(off + w, 0);
-                    bool isnull = false;
-                    if (ai >= 0) {
-                        std::memcpy(&cols[k][off], c->cols[ai].data() + r * w, w);
-                        isnull = !c->nulls[ai].empty() && c->nulls[ai][r];
+            const int qpos = h.stream_pos(c->stream);
+            // rows kept (null partition key: dropped), then each column appended as a whole (bulk copy when no
+            // row was dropped)
+            std::vector<int64_t> kept;
+            bool all = true;
+            const size_t base = ts.size();
+            if (partitioned) {
+                keys.reserve(keys.size() + (size_t)c->n);
+                for (int64_t r = 0; r < c->n; ++r) {
+                    uint32_t key = 0;
+                    if (!host_key(e, q, qpos, *c, r, &key)) {
+                        if (all) {
+                            all = false;
+                            kept.reserve((size_t)c->n);
+                            for (int64_t r2 = 0; r2 < r; ++r2) kept.push_back(r2);
+                        }
+                        continue;
                     }
-                    nulls[k].push_back(isnull);
-                    if (isnull) any_null[k] = true;
+                    keys.push_back(key);
+                    if (!all) kept.push_back(r);
                 }
+            }
+            const size_t m = all ? (size_t)c->n : kept.size();
+            if (all) ts.insert(ts.end(), c->ts.begin(), c->ts.begin() + c->n);
+            else for (int64_t r : kept) ts.push_back(c->ts[r]);
+            qs.resize(base + m, (uint8_t)qpos);
+            for (int k = 0; k < nc; ++k) {
+                const int w = width_of(P.col_kind[k]);
+                const int ai = h.col_attr[qpos][k];
+                const size_t off = cols[k].size();
+                cols[k].resize(off + m * w, 0);
+                nulls[k].resize(base + m, 0);
+                if (ai < 0) continue;  // a column of another stream of the query: zeros, not null
+                const uint8_t* src = c->cols[ai].data();
+                const bool has_nulls = !c->nulls[ai].empty();
+                if (all) {
+                    std::memcpy(&cols[k][off], src, m * w);
+                    if (has_nulls) std::memcpy(&nulls[k][base], c->nulls[ai].data(), m);
+                } else {
+                    for (size_t j = 0; j < m; ++j) {
+                        std::memcpy(&cols[k][off + j * w], src + kept[j] * w, w);
+                        if (has_nulls) nulls[k][base + j] = c->nulls[ai][kept[j]];
+                    }
+                }
+                if (has_nulls)
+                    for (size_t j = 0; j < m && !any_null[k]; ++j) any_null[k] = nulls[k][base + j] != 0;
             }
         }
         nrows = (int64_t)ts.size();
