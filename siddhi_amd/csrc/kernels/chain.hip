@@ -724,14 +724,15 @@ __global__ __launch_bounds__(256) void chain_carry_wave_k(const ChainArgs* __res
     } while (0)
 
 static_assert(FU_THREADS >= 256, "chain_fused_k: one thread per local key in the run tables");
-static_assert(FU_PT <= 32, "chain_fused_k: a lane's deque is a 32-bit mask over its positions");
+static_assert(FU_DQ <= 32, "chain_fused_k: a lane's deque is a 32-bit mask over its positions");
+static_assert(FU_DQ >= FU_PT && FU_ROWS % FU_DQ == 0, "chain_fused_k: deque chunks tile the staged rows");
 constexpr uint16_t R_NONE = 0xFFFF, R_CARRY = 0xFFFE, R_OVF = 0xFFFD;
-// LDS swizzle of the per-position arrays: the deque pass gives lane t the positions [FU_PT t, FU_PT (t + 1)), so
-// unswizzled, one step of a wave hits every lane's element at an FU_PT-position stride (few banks). XOR-ing the
-// low log2(FU_PT) bits with the next ones spreads those over the banks; runs of consecutive positions stay
-// permuted within their aligned group of FU_PT (still conflict-free for the per-round `k * FU_THREADS + t` accesses).
-static_assert((FU_PT & (FU_PT - 1)) == 0, "sw() swizzles at the deque chunk size");
-__device__ __forceinline__ int sw(int p) { return p ^ ((p / FU_PT) & (FU_PT - 1)); }
+// LDS swizzle of the per-position arrays: the deque pass gives lane t the positions [FU_DQ t, FU_DQ (t + 1)), so
+// unswizzled, one step of a wave hits every lane's element at an FU_DQ-position stride (few banks). XOR-ing the
+// low log2(FU_DQ) bits with the next ones spreads those over the banks; runs of consecutive positions stay
+// permuted within their aligned group of FU_DQ (still conflict-free for the per-round `k * FU_THREADS + t` accesses).
+static_assert((FU_DQ & (FU_DQ - 1)) == 0, "sw() swizzles at the deque chunk size");
+__device__ __forceinline__ int sw(int p) { return p ^ ((p / FU_DQ) & (FU_DQ - 1)); }
 static_assert(FU_ROWS < 65536, "chain_fused_k: u16 rows / run offsets");
 
 // SAME: the scanned column's kind is the comparison kind (no conversion in the scan loop)
@@ -890,14 +891,14 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
     if (a.fu_skip & 16) {
         // phase timing: no matching
     } else if (a.fu_mode != DQ_OFF) {
-        // ---- monotone-deque pass (chain_deque_k), one lane per FU_PT consecutive positions: the lane
+        // ---- monotone-deque pass (chain_deque_k), one lane per FU_DQ consecutive positions: the lane
         // pushes partials from its own positions only and keeps popping over the following positions of the key
         // until its deque drains. The deque is a bit mask over the lane's positions (bit i = position p0 + i
         // pending); arrival order = position order, so the front is the lowest bit and the top the highest.
         // The chunk's rows are prefetched into registers (static indices: the loop over them is unrolled); the
         // front's ts and the top's value are cached and re-read from LDS only when the front / top changes.
         const bool stack = a.fu_mode == DQ_STACK;
-        const int p0 = t * FU_PT;
+        const int p0 = t * FU_DQ;  // lanes with p0 >= nr (whole waves past FU_ROWS / FU_DQ) have no chunk
         uint32_t pend = 0, tf = 0;
         T ytop = T(0);
         // one row (ts tq, value x) against the pending partials: expire the prefix, then complete (a suffix / all).
@@ -923,7 +924,7 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
                 for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = (uint16_t)q;
             }
         };
-        const int pe = min(p0 + FU_PT, nr);
+        const int pe = min(p0 + FU_DQ, nr);
         int cur_end = p0 < nr ? (int)lend[s_lk[sw(p0)]] : 0;
 #pragma unroll 1
         for (int q = p0; q < pe; ++q) {

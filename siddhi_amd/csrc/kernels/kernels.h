@@ -176,7 +176,14 @@ void chain_carry(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
 // e1 filter, plain-attribute selects, K <= 2^16, batch timestamps non-decreasing (checked by bucketize).
 constexpr int FU_THREADS = 512;
 constexpr int FU_PT = 4;                             // staged rows per lane (= the deque chunk)
-constexpr int FU_ROWS = FU_THREADS * FU_PT;          // 4096 rows in LDS
+constexpr int FU_ROWS = FU_THREADS * FU_PT;          // 2048 rows in LDS
+#ifndef SDG_FU_DQ
+#define SDG_FU_DQ 4
+#endif
+// deque chunk: positions per lane in the monotone-deque pass (FU_ROWS / FU_DQ lanes work, the other waves idle).
+// Longer chunks pay a lane's continuation over the key's following rows (~ the window) once per more rows, but
+// lengthen the block's critical path: measured 8 -> 2.85 ms vs 4 -> 2.65 ms (r1ab), so the pass is latency-bound
+constexpr int FU_DQ = SDG_FU_DQ;
 constexpr int FU_HALO = 512;
 constexpr int FU_OWN = FU_ROWS - FU_HALO;            // candidate rows per block
 // grid size for n rows in nb buckets (a multiple of 8: the XCD remap needs it)
