@@ -45,7 +45,8 @@ __global__ __launch_bounds__(256) void rx_p1(const uint32_t* __restrict__ counts
     int g = (int)(idx / nb), d = (int)(idx % nb);
     int b0 = g * KG_GROUP, b1 = min(ntiles, b0 + KG_GROUP);
     uint32_t s = 0;
-    for (int b = b0; b < b1; ++b) s += counts[(int64_t)b * nb + d];
+#pragma unroll 8
+    for (int b = b0; b < b1; ++b) s += counts[(int64_t)b * nb + d];  // independent loads: keep 8 in flight
     gsum[idx] = s;
 }
 
@@ -55,7 +56,19 @@ __global__ __launch_bounds__(256) void rx_p2(uint32_t* __restrict__ gsum, int ng
     int d = threadIdx.x;
     uint32_t run = 0;
     if (d < nb) {
-        for (int g = 0; g < ng; ++g) {
+        // 8 groups per round: the loads of a round are issued together (the scan itself is a register chain)
+        int g = 0;
+        for (; g + 8 <= ng; g += 8) {
+            uint32_t c[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) c[j] = gsum[(int64_t)(g + j) * nb + d];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                gsum[(int64_t)(g + j) * nb + d] = run;
+                run += c[j];
+            }
+        }
+        for (; g < ng; ++g) {
             uint32_t c = gsum[(int64_t)g * nb + d];
             gsum[(int64_t)g * nb + d] = run;
             run += c;
@@ -81,7 +94,18 @@ __global__ __launch_bounds__(256) void rx_p3(uint32_t* __restrict__ counts, cons
     int g = (int)(idx / nb), d = (int)(idx % nb);
     uint32_t run = tot[d] + gsum[idx];
     int b0 = g * KG_GROUP, b1 = min(ntiles, b0 + KG_GROUP);
-    for (int b = b0; b < b1; ++b) {
+    int b = b0;
+    for (; b + 8 <= b1; b += 8) {  // as rx_p2: a round's loads issued together
+        uint32_t c[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) c[j] = counts[(int64_t)(b + j) * nb + d];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            counts[(int64_t)(b + j) * nb + d] = run;
+            run += c[j];
+        }
+    }
+    for (; b < b1; ++b) {
         uint32_t c = counts[(int64_t)b * nb + d];
         counts[(int64_t)b * nb + d] = run;
         run += c;
