@@ -263,3 +263,48 @@ def test_chain_shapes_on_gpu(name, shape, fused, oracle_built):
         p.close()
     assert len(ref) > 0
     assert got == ref
+
+
+# ---- numeric partition keys through the host push (IntKeyCache + column-wise assembly, null keys dropped) -----
+NUM_KEY_APP = ("@app:playback define stream P (id long, k long, price double, v int); "
+               "partition with (%s of P) begin @info(name = 'query1') "
+               "from every e1=P[price>20] -> e2=P[price>e1.price] within 40 milliseconds "
+               "select e1.id as a, e2.id as b insert into M; end;")
+
+
+@pytest.mark.parametrize("attr", ["k", "v"])
+@pytest.mark.parametrize("null_rate", [0.0, 0.05])
+def test_numeric_partition_keys_host_push(attr, null_rate, oracle_built):
+    rng = np.random.default_rng(5)
+    n = 6000
+    ts = w.T0 + np.arange(n, dtype=np.int64) // 3
+    ids = np.arange(n, dtype=np.int64)
+    kcol = rng.integers(-40, 40, n).astype(np.int64) * 1_000_000_007  # long keys beyond int range
+    vcol = rng.integers(-30, 30, n).astype(np.int32)
+    price = np.rint((10.0 + 20.0 * rng.random(n)) * 100.0) / 100.0
+    knull = (rng.random(n) < null_rate).astype(np.uint8)
+    app = NUM_KEY_APP % attr
+    o = Oracle(app)
+    try:
+        for i in range(n):
+            kv = None if (attr == "k" and knull[i]) else int(kcol[i])
+            vv = None if (attr == "v" and knull[i]) else int(vcol[i])
+            o.send("P", int(ts[i]), [int(ids[i]), kv, float(price[i]), vv])
+        ref = [(r["ts"], tuple(v[1] for v in r["values"])) for r in o.outputs() if r["kind"] == "query"]
+    finally:
+        o.close()
+    rt = sa.SiddhiAppRuntime(app)
+    try:
+        h = rt.getInputHandler("P")
+        nulls = [None, knull if attr == "k" else None, None, knull if attr == "v" else None]
+        got = []
+        for s, e in ((0, 2500), (2500, n)):  # two flushes: the int-key cache and partials persist across them
+            h.send_columns(ts[s:e], [ids[s:e], kcol[s:e], price[s:e], vcol[s:e]],
+                           [None if m is None else m[s:e] for m in nulls])
+            rt.flush(deliver=False)
+            types, ots, vals, onulls = rt.raw_outputs(0)
+            got += [(ots[i], (vals[0][i], vals[1][i])) for i in range(len(ots))]
+    finally:
+        rt.shutdown()
+    assert len(ref) > 200
+    assert got == ref
