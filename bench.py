@@ -80,6 +80,51 @@ def cpu_baseline(cols, syms, sample):
     return n / dt, matches, dt
 
 
+def cpu_baseline_sharded(cols, syms, sample, threads):
+    """The same oracle, key-sharded over `threads` host threads (one Oracle instance per shard; keys are
+    independent). ctypes drops the GIL inside orc_send_batch, so the shards run in parallel."""
+    import threading
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from oracle_rt import Oracle, lib
+    from siddhi_amd import workloads as w
+    L = lib()
+    n = sample
+    key = cols["key"][:n]
+    jobs = []
+    for sh in range(threads):
+        idx = np.nonzero(key % threads == sh)[0]
+        o = Oracle(w.C2_APP)
+        L.orc_count_only(o.h, 1)
+        ids = np.array([L.orc_intern(o.h, s.encode()) for s in syms], dtype=np.int64)
+        m = len(idx)
+        slots = np.empty((m, 4), dtype=np.int64)
+        slots[:, 0] = cols["id"][idx]
+        slots[:, 1] = ids[key[idx]]
+        slots[:, 2] = cols["price"][idx].view(np.int64)
+        slots[:, 3] = cols["volume"][idx]
+        jobs.append({"o": o, "m": m, "slots": slots, "offs": np.arange(m, dtype=np.int64) * 4,
+                     "strm": np.full(m, o.stream("StockStream"), dtype=np.int32),
+                     "ts": np.ascontiguousarray(cols["ts"][idx]), "rc": -1})
+
+    def work(j):
+        j["rc"] = L.orc_send_batch(j["o"].h, j["m"], j["strm"].ctypes.data, j["ts"].ctypes.data,
+                                   j["offs"].ctypes.data, j["slots"].ctypes.data, None)
+
+    ths = [threading.Thread(target=work, args=(j,)) for j in jobs]
+    t = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t
+    matches = sum(L.orc_output_count(j["o"].h) for j in jobs)
+    for j in jobs:
+        j["o"].close()
+    if any(j["rc"] != 0 for j in jobs):
+        raise RuntimeError("oracle failed")
+    return n / dt, matches, dt
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -212,6 +257,13 @@ def main():
         out["cpu_baseline"] = {"value": rate, "unit": "events/s", "cores": 1, "kind": "port",
                                "sample": "first %d events of the C2 stream (%.1f s, %d matches), oracle restatement"
                                          % (min(args.cpu_sample, n), dt, cm)}
+        thr = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+        srate, scm, sdt = cpu_baseline_sharded(cols, syms, min(args.cpu_sample, n), thr)
+        if scm != cm:
+            raise RuntimeError("key-sharded CPU baseline disagrees with the single-thread run: %d vs %d" % (scm, cm))
+        out["cpu_baseline_sharded"] = {"value": srate, "unit": "events/s", "cores": thr, "kind": "port",
+                                       "sample": "same events, key-sharded over %d threads (%.2f s, %d matches)"
+                                                 % (thr, sdt, scm)}
     else:
         out["cpu_baseline"] = None
     rt.shutdown()
