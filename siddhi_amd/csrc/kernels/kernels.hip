@@ -27,10 +27,26 @@ __global__ __launch_bounds__(RX_THREADS) void rx_hist(const uint32_t* __restrict
     for (int d = threadIdx.x; d < nb; d += RX_THREADS) h[d] = 0;
     __syncthreads();
     int64_t base = (int64_t)blockIdx.x * RX_TILE;
+    if (base + RX_TILE <= n && (((uintptr_t)(keys + base)) & 15) == 0) {
+        // full, 16-B aligned tile: 4 keys per load, every load of the thread in flight before the atomics
+        constexpr int V = RX_TILE / RX_THREADS / 4;
+        const uint4* kv = reinterpret_cast<const uint4*>(keys + base);
+        uint4 x[V];
+#pragma unroll
+        for (int r = 0; r < V; ++r) x[r] = kv[r * RX_THREADS + threadIdx.x];
+#pragma unroll
+        for (int r = 0; r < V; ++r) {
+            atomicAdd(&h[digit_of(x[r].x, shift, mask)], 1u);
+            atomicAdd(&h[digit_of(x[r].y, shift, mask)], 1u);
+            atomicAdd(&h[digit_of(x[r].z, shift, mask)], 1u);
+            atomicAdd(&h[digit_of(x[r].w, shift, mask)], 1u);
+        }
+    } else {
 #pragma unroll 4
-    for (int r = 0; r < RX_TILE / RX_THREADS; ++r) {
-        int64_t i = base + r * RX_THREADS + threadIdx.x;
-        if (i < n) atomicAdd(&h[digit_of(keys[i], shift, mask)], 1u);
+        for (int r = 0; r < RX_TILE / RX_THREADS; ++r) {
+            int64_t i = base + r * RX_THREADS + threadIdx.x;
+            if (i < n) atomicAdd(&h[digit_of(keys[i], shift, mask)], 1u);
+        }
     }
     __syncthreads();
     for (int d = threadIdx.x; d < nb; d += RX_THREADS) counts[(int64_t)blockIdx.x * nb + d] = h[d];
