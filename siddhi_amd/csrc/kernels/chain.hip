@@ -926,16 +926,29 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
         };
         const int pe = min(p0 + FU_DQ, nr);
         int cur_end = p0 < nr ? (int)lend[s_lk[sw(p0)]] : 0;
-#pragma unroll 1
-        for (int q = p0; q < pe; ++q) {
-            const uint32_t tq = s_ts[sw(q)];
-            const int64_t xr = s_x[sw(q)];
+        // the chunk's own rows, read from LDS up front (all reads in flight together)
+        uint32_t cts[FU_DQ];
+        int64_t cx[FU_DQ];
+        uint16_t crow[FU_DQ];
+#pragma unroll
+        for (int i = 0; i < FU_DQ; ++i) {
+            const int q = min(p0 + i, FU_ROWS - 1);
+            cts[i] = s_ts[sw(q)];
+            cx[i] = s_x[sw(q)];
+            crow[i] = s_row[sw(q)];
+        }
+#pragma unroll
+        for (int i = 0; i < FU_DQ; ++i) {
+            const int q = p0 + i;
+            if (q >= pe) break;
+            const uint32_t tq = cts[i];
+            const int64_t xr = cx[i];
             const T x = SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K));
             step(q, tq, x);
             // e1: this lane's own (non-halo) rows start partials, visible from the next row on
-            if (s_row[sw(q)] < own && c0_at(q, xr, x) && (!stack || x == x)) {
+            if (crow[i] < own && c0_at(q, xr, x) && (!stack || x == x)) {
                 if (!pend) tf = tq;
-                pend |= 1u << (q - p0);
+                pend |= 1u << i;
                 ytop = x;
             }
             if (q + 1 == cur_end) {  // the key's staged rows end here: its pending partials ran off
