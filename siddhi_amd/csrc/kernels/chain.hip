@@ -637,6 +637,48 @@ __device__ int64_t wave_scan_typed(const ChainArgs& a, int64_t from, int64_t end
 
 constexpr int CW_PER_WAVE = 16;  // carried partials resolved one after another by one wave
 
+// the typed e2 scan of partial (row p / carried c): the e1 operand hoisted as chain_scan does
+__device__ __forceinline__ int64_t wave_scan_partial(const ChainArgs& a, ChainAcc& acc, int64_t b, int64_t e,
+                                                     int64_t ts0, uint32_t key) {
+    const ChainSpec& sp = a.sp;
+    int64_t k = sp.scan_konst;
+    uint8_t op = sp.scan_op;
+    if (sp.scan_mode == SCAN_TRUE) {
+        op = OP_ALWAYS;
+    } else if (sp.scan_mode == SCAN_E1) {
+        bool nl;
+        acc.load(0, sp.e1_col, 0, sp.e1_col_kind, &k, &nl);
+        if (nl) op = OP_NEVER;
+        else k = cvt(k, sp.e1_col_kind, sp.scan_t);
+    }
+    switch (sp.scan_t) {
+        case VK_I32: return wave_scan_typed<VK_I32>(a, b, e, ts0, k, op, key);
+        case VK_I64: return wave_scan_typed<VK_I64>(a, b, e, ts0, k, op, key);
+        case VK_F32: return wave_scan_typed<VK_F32>(a, b, e, ts0, k, op, key);
+        case VK_F64: return wave_scan_typed<VK_F64>(a, b, e, ts0, k, op, key);
+        case VK_BOOL: return wave_scan_typed<VK_BOOL>(a, b, e, ts0, k, op, key);
+        default: return wave_scan_typed<VK_STR>(a, b, e, ts0, k, op, key);
+    }
+}
+
+// rows evicted from a lane's deque (chain_deque_k), typed scans: one wave per row, CW_PER_WAVE rows per wave, the
+// key's following rows scanned 256 at a time (chain_ovf_k's lane-serial scan of up to a window of rows was half
+// of the C1 flush)
+__global__ __launch_bounds__(256) void chain_ovf_wave_k(const ChainArgs* __restrict__ pa) {
+    const ChainArgs& a = *pa;
+    const int64_t total = (int64_t)*a.ovf_count;
+    const int64_t stride = (int64_t)gridDim.x * 4 * CW_PER_WAVE;
+    for (int64_t i = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * CW_PER_WAVE; i < total;
+         i += (i % CW_PER_WAVE == CW_PER_WAVE - 1) ? stride - (CW_PER_WAVE - 1) : 1) {  // wave-uniform
+        const int64_t p = a.ovf_rows[i];
+        ChainAcc acc{&a, View{}, p, -1, -1};
+        const uint32_t key = a.key ? a.key[p] : 0u;
+        const int64_t end = a.key ? (int64_t)a.seg_end[key] : a.n;
+        const int64_t q = wave_scan_partial(a, acc, p + 1, end, a.ts[p], key);
+        if (lane_id() == 0) a.mq[p] = q >= 0 ? (uint32_t)q : q == -2 ? MQ_CARRY : MQ_NONE;
+    }
+}
+
 // Block = 4 waves x CW_PER_WAVE partials; lane i of a wave keeps the result of its i-th partial, and the block
 // reserves its match / carry output with one atomic per counter (one atomic per partial serialised in L2:
 // ~10^8/s, 0.2 ms for 2 x 10^4 carries).
@@ -1208,7 +1250,12 @@ void chain_deque(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
         case VK_BOOL: hipLaunchKernelGGL(chain_deque_k<VK_BOOL>, grid, dim3(DQ_THREADS), 0, stream, d_a); break;
         default: hipLaunchKernelGGL(chain_deque_k<VK_STR>, grid, dim3(DQ_THREADS), 0, stream, d_a); break;
     }
-    hipLaunchKernelGGL(chain_ovf_k, dim3(512), dim3(256), 0, stream, d_a);
+    if (!a.generic && a.sp.scan_mode != SCAN_GENERIC && !a.bstart && !getenv("SDG_OVF_LANE"))
+        hipLaunchKernelGGL(chain_ovf_wave_k,
+                           dim3((unsigned)std::min<int64_t>(4096, (a.n + 4 * CW_PER_WAVE - 1) / (4 * CW_PER_WAVE))),
+                           dim3(256), 0, stream, d_a);  // grid-stride over ovf_count (<= n)
+    else
+        hipLaunchKernelGGL(chain_ovf_k, dim3(512), dim3(256), 0, stream, d_a);
 }
 
 void chain_carry(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
