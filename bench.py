@@ -80,6 +80,47 @@ def cpu_baseline(cols, syms, sample):
     return n / dt, matches, dt
 
 
+def parity_check(cols, syms, sample, dev_cols, device):
+    """Outside the timed region: the first `sample` events of this rank's bench stream through a fresh runtime on
+    the GPU (device-resident, the bench's own path) and through the oracle; the match rows (ts, e1id, e2id) must be
+    identical and in the same delivery order, or the bench fails."""
+    import siddhi_amd as sa
+    from siddhi_amd import workloads as w
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from oracle_rt import Oracle, lib
+    n = sample
+    rt = sa.SiddhiAppRuntime(w.C2_APP, device=device)
+    sym_ids = np.array([rt.intern(s) for s in syms], dtype=np.uint32)
+    d_id, d_sym, d_price, d_vol, d_ts = dev_cols
+    assert int(sym_ids[cols["key"][0]]) == int(d_sym[0].item())  # same dictionary ids as the bench runtime
+    rt.push_device("StockStream", n, d_ts.data_ptr(), [d_id.data_ptr(), d_sym.data_ptr(), d_price.data_ptr(),
+                                                       d_vol.data_ptr()])
+    rt.flush(deliver=False)
+    gts, gvals, gnulls, _ = rt.poll_arrays(0)
+    rt.shutdown()
+    o = Oracle(w.C2_APP)
+    L = lib()
+    ids = np.array([L.orc_intern(o.h, s.encode()) for s in syms], dtype=np.int64)
+    slots = np.empty((n, 4), dtype=np.int64)
+    slots[:, 0] = cols["id"][:n]
+    slots[:, 1] = ids[cols["key"][:n]]
+    slots[:, 2] = cols["price"][:n].view(np.int64)
+    slots[:, 3] = cols["volume"][:n]
+    rc = L.orc_send_batch(o.h, n, np.full(n, o.stream("StockStream"), dtype=np.int32).ctypes.data,
+                          np.ascontiguousarray(cols["ts"][:n]).ctypes.data,
+                          (np.arange(n, dtype=np.int64) * 4).ctypes.data, slots.ctypes.data, None)
+    if rc != 0:
+        raise RuntimeError("oracle failed")
+    ots, ovals, onulls = o.query_arrays(2)
+    o.close()
+    ok = (len(gts) == len(ots) and np.array_equal(gts, ots) and np.array_equal(gvals.T, ovals)
+          and not gnulls.any() and not onulls.any())
+    if not ok:
+        raise RuntimeError("GPU match rows differ from the oracle on the first %d bench events (%d vs %d rows)"
+                           % (n, len(gts), len(ots)))
+    return {"events": n, "matches": int(len(ots)), "bit_exact": True}
+
+
 def cpu_baseline_sharded(cols, syms, sample, threads):
     """The same oracle, key-sharded over `threads` host threads (one Oracle instance per shard; keys are
     independent). ctypes drops the GIL inside orc_send_batch, so the shards run in parallel."""
@@ -134,6 +175,9 @@ def main():
     ap.add_argument("--keys", type=int, default=10_000, help="keys per GPU")
     ap.add_argument("--cpu-sample", type=int, default=3_000_000)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--parity-sample", type=int, default=3_000_000,
+                    help="events of the bench stream re-run through a fresh runtime and the oracle (bit-exact check)")
+    ap.add_argument("--no-parity", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -267,6 +311,14 @@ def main():
     else:
         out["cpu_baseline"] = None
     rt.shutdown()
+    if not args.no_parity:
+        ps = min(args.parity_sample if world == 1 else args.parity_sample // 3, n)
+        out["parity"] = parity_check(cols, syms, ps, (d_id[:ps], d_sym[:ps], d_price[:ps], d_vol[:ps], d_ts0[:ps]),
+                                     local)
+        if dist is not None:  # every rank checked its own shard
+            okt = torch.tensor([1], dtype=torch.int64, device=dev)
+            dist.all_reduce(okt)
+            out["parity"]["ranks_checked"] = int(okt.item())
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

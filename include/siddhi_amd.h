@@ -22,7 +22,10 @@
  * Conventions (mirroring the reference): compile errors are returned as status codes with a thread-local
  * message (SiddhiAppCreationException / SiddhiAppValidationException / OperationNotSupportedException); one
  * handle is single-threaded (the reference serialises a query under patternSyncObject); the engine owns the
- * copies it makes of pushed data; poll results are valid until the next sdg_flush / sdg_poll / sdg_destroy.
+ * copies it makes of pushed data; poll results are valid until the next sdg_poll / sdg_destroy. Results are never
+ * dropped: a flush (explicit, or the automatic one sdg_push runs when batch_capacity events are buffered) appends
+ * to the query's backlog, and sdg_poll hands out the whole backlog. A flush consumes its batch even when it fails
+ * (the error names the query); queries flushed before the failing one keep their results.
  *
  * Value encoding of columns: INT int32, LONG int64, FLOAT float, DOUBLE double, BOOL uint8, STRING uint32
  * (ids from sdg_intern: equal strings <=> equal ids). Nulls: optional per-column uint8 arrays (1 = null).
@@ -69,6 +72,10 @@ typedef struct sdg_out {
     const int32_t* types;      /* [n_attrs] sdg_type */
     const int64_t* const* values; /* [n_attrs][n] 64-bit payload (float/double as bit patterns) */
     const uint8_t* const* nulls;  /* [n_attrs][n] 1 = null */
+    const int64_t* event_seq;  /* [n] sequence number of the input event whose processing emitted the row (per
+                                  query, counting the events of the query's streams from 0): consecutive rows with
+                                  equal event_seq are the one Event[] the reference hands to the callback for that
+                                  event (StateMultiProcessStreamReceiver.processAndClear :47-68) */
 } sdg_out;
 
 int sdg_compile(const char* siddhi_app, const sdg_opts* opts, sdg_engine** out);
@@ -94,6 +101,8 @@ int sdg_push(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const void
 int sdg_push_device(sdg_engine* e, int stream, int64_t n, const int64_t* d_ts, const void* const* d_cols,
                     const uint8_t* const* d_nulls);
 int sdg_advance_time(sdg_engine* e, int64_t ts);
+/* events buffered since the last flush (a push that reaches batch_capacity flushes: the count drops) */
+int64_t sdg_pending(sdg_engine* e);
 int sdg_flush(sdg_engine* e);
 int sdg_sync(sdg_engine* e);
 int sdg_poll(sdg_engine* e, int query, sdg_out* out);

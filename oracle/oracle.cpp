@@ -2421,3 +2421,22 @@ extern "C" int orc_output_list_item(orc_engine* e, int64_t i, int j, int k, int6
 extern "C" void orc_clear_outputs(orc_engine* e) { e->rt.outputs.clear(); }
 extern "C" void orc_count_only(orc_engine* e, int on) { e->rt.countOnly = on != 0; }
 extern "C" int64_t orc_output_count(orc_engine* e) { return e->rt.outCount; }
+
+// bulk export of the query-callback outputs (kind 0, non-list values) in delivery order: ts[n], vals[n][nv]
+// (row-major), nulls[n][nv]; returns the number of rows written (at most cap)
+extern "C" int64_t orc_export_query_outputs(orc_engine* e, int64_t cap, int nv, int64_t* ts, int64_t* vals,
+                                            uint8_t* nulls) {
+    int64_t k = 0;
+    for (const OutputRec& r : e->rt.outputs) {
+        if (r.kind != 0 || r.expired) continue;
+        if (k >= cap) break;
+        ts[k] = r.ts;
+        for (int j = 0; j < nv; ++j) {
+            const bool ok = j < (int)r.vals.size();
+            vals[k * nv + j] = ok ? r.vals[j].raw : 0;
+            nulls[k * nv + j] = ok ? r.vals[j].null : 1;
+        }
+        ++k;
+    }
+    return k;
+}

@@ -64,7 +64,8 @@ class _Out(ctypes.Structure):
                 ("expired", ctypes.POINTER(ctypes.c_uint8)), ("n_attrs", ctypes.c_int32),
                 ("types", ctypes.POINTER(ctypes.c_int32)),
                 ("values", ctypes.POINTER(ctypes.POINTER(ctypes.c_int64))),
-                ("nulls", ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)))]
+                ("nulls", ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8))),
+                ("event_seq", ctypes.POINTER(ctypes.c_int64))]
 
 
 class Stats(ctypes.Structure):
@@ -120,6 +121,8 @@ def load_library():
     L.sdg_push.argtypes = [P, I32, I64, P, P, P]
     L.sdg_push_device.argtypes = [P, I32, I64, P, P, P]
     L.sdg_advance_time.argtypes = [P, I64]
+    L.sdg_pending.restype = I64
+    L.sdg_pending.argtypes = [P]
     L.sdg_flush.argtypes = [P]
     L.sdg_sync.argtypes = [P]
     L.sdg_poll.argtypes = [P, I32, ctypes.POINTER(_Out)]
@@ -289,7 +292,13 @@ class SiddhiAppRuntime:
             keep += [arr, nl]
             cols[a] = ctypes.cast(arr, ctypes.c_void_p)
             nulls[a] = ctypes.cast(nl, ctypes.c_void_p) if any(r[1][a] is None for r in rows) else None
+        self._push(idx, n, ts, cols, nulls)
+
+    def _push(self, idx, n, ts, cols, nulls):
+        before = self._L.sdg_pending(self._h)
         _check(self._L.sdg_push(self._h, idx, n, ts, cols, nulls))
+        if self._L.sdg_pending(self._h) < before + n:  # the push filled the batch and flushed it
+            self._deliver()
 
     def _push_columns(self, idx, types, ts, columns, nulls=None):
         import numpy as np
@@ -307,7 +316,7 @@ class SiddhiAppRuntime:
                 m = np.ascontiguousarray(nulls[a], dtype=np.uint8)
                 keep.append(m)
                 nl[a] = m.ctypes.data
-        _check(self._L.sdg_push(self._h, idx, n, ts.ctypes.data, cols, nl))
+        self._push(idx, n, ts.ctypes.data, cols, nl)
 
     def push_device(self, stream_id, n, ts_ptr, col_ptrs):
         """Device-resident columns (e.g. torch CUDA tensors' data_ptr()); kept alive by the caller."""
@@ -356,14 +365,35 @@ class SiddhiAppRuntime:
         return evs
 
     def _deliver(self):
+        # one callback invocation per match, in delivery order: the receivers hand every returned StateEvent to
+        # QuerySelector.process as its own chunk (SingleProcessStreamReceiver.processAndClear :66-71,
+        # StateMultiProcessStreamReceiver.processAndClear :58-66), so QueryCallback.receiveStreamEvent and
+        # StreamCallback.receive(ComplexEvent) each see a one-event Event[] stamped with that event's timestamp
         for q, (name, target, types, names) in enumerate(self._queries):
             evs = self.poll(q)
-            if not evs:
-                continue
-            for cb in self._callbacks.get(name, []):
-                cb.receive(evs[-1].timestamp, evs, None)
-            for cb in self._callbacks.get(target, []):
-                cb.receive(evs)
+            for ev in evs:
+                for cb in self._callbacks.get(name, []):
+                    cb.receive(ev.timestamp, [ev], None)
+                for cb in self._callbacks.get(target, []):
+                    cb.receive([ev])
+
+    def poll_arrays(self, q):
+        """numpy view of one poll: (ts[n], values[n_attrs][n] int64 payloads, nulls[n_attrs][n], event_seq[n]);
+        copies, so they stay valid after the next poll"""
+        import numpy as np
+        out = _Out()
+        _check(self._L.sdg_poll(self._h, q, ctypes.byref(out)))
+        n, na = out.n, out.n_attrs
+        if n == 0:
+            z = np.zeros(0, np.int64)
+            return z, np.zeros((na, 0), np.int64), np.zeros((na, 0), np.uint8), z
+        ts = np.ctypeslib.as_array(out.ts, (n,)).copy()
+        seq = np.ctypeslib.as_array(out.event_seq, (n,)).copy()
+        vals = np.stack([np.ctypeslib.as_array(out.values[j], (n,)).copy() for j in range(na)]) if na else \
+            np.zeros((0, n), np.int64)
+        nulls = np.stack([np.ctypeslib.as_array(out.nulls[j], (n,)).copy() for j in range(na)]) if na else \
+            np.zeros((0, n), np.uint8)
+        return ts, vals, nulls, seq
 
     def raw_outputs(self, q):
         """(types, ts[n], values[attr][n] payload ints, nulls[attr][n]) straight from sdg_poll"""

@@ -197,8 +197,14 @@ struct QueryRt {
     bool polled = true;
     bool nulls_valid = true;                        // false: the last flush wrote no null bits (none possible)
     bool carry_nullable = false;                    // the carried partials came from a batch with null columns
+    // delivered rows not yet polled, in delivery order (drain(): an auto-flush inside sdg_push, or several
+    // sdg_flush calls before one sdg_poll, keep appending here -- never overwritten)
+    std::vector<int64_t> acc_ts, acc_seq;
+    std::vector<std::vector<int64_t>> acc_vals;
+    std::vector<std::vector<uint8_t>> acc_nulls;
+    HostPin h_rb;                                   // pinned read-back staging
     // host copies for sdg_poll
-    std::vector<int64_t> h_ts;
+    std::vector<int64_t> h_ts, h_seq;
     std::vector<uint8_t> h_expired;
     std::vector<std::vector<int64_t>> h_vals;
     std::vector<std::vector<uint8_t>> h_nulls;
@@ -541,7 +547,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     for (int k = 0; k < nc; ++k) { v_cols[k] = d_cols[k]; v_nulls[k] = d_nulls[k]; }
     HIPCHECK(hipEventRecord(e->ev[0], st));
     const uint32_t* v_segend = nullptr;
-    int* flags = (int*)q.flags.ensure(16);
+    int* flags = (int*)q.flags.ensure(32);  // [0] output overflow [1] decreasing ts [2] bounds [3] mono [4] key range
     int bbits = 0;
     uint32_t* b_start = nullptr;
     uint32_t* b_seg = nullptr;
@@ -551,6 +557,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         a.n = nrows;
         a.K = (int32_t)K;
         a.keys = d_key;
+        a.key_flag = zero_copy ? flags + 4 : nullptr;  // caller-supplied device ids: range-check against K
         int c = 0;
         a.src[c] = d_ts; a.dst[c] = q.so_ts.ensure(nrows * 8); a.width[c] = 8; v_ts = (const int64_t*)a.dst[c]; ++c;
         if (d_qs) { a.src[c] = d_qs; a.dst[c] = q.so_qs.ensure(nrows); a.width[c] = 1; v_qs = (const uint8_t*)a.dst[c]; ++c; }
@@ -576,7 +583,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             bbits = std::max(1, std::min(8, kbits));
             b_start = (uint32_t*)q.bk_plan.ensure(2 * 257 * 4);
             b_seg = b_start + 257;
-            HIPCHECK(hipMemsetAsync(flags, 0, 16, st));
+            HIPCHECK(hipMemsetAsync(flags, 0, 32, st));
             bucketize(a, bbits, 0 /* ts is payload column 0 */, flags + 3, b_start, b_seg, FU_OWN, st, &e->ev[4]);
             if (getenv("SDG_DEBUG")) {  // validate the bucket plan on the host before the matcher reads it
                 std::vector<uint32_t> hp(2 * 257);
@@ -588,6 +595,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 if (!okp) throw DeviceError("fused bucket plan inconsistent (n=" + std::to_string(nrows) + ")");
             }
         } else {
+            HIPCHECK(hipMemsetAsync(flags, 0, 32, st));
             keygroup(a, st, &e->ev[4]);
         }
         v_key = a.keys_sorted;
@@ -636,7 +644,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         q.out_cap = cap;
         unsigned long long* counters = (unsigned long long*)q.counters.ensure(16);
         HIPCHECK(hipMemsetAsync(counters, 0, 16, st));
-        HIPCHECK(hipMemsetAsync(flags, 0, 16, st));
+        if (!(partitioned && nrows > 0)) HIPCHECK(hipMemsetAsync(flags, 0, 32, st));
         a.out_cap = cap;
         a.out_count = counters;
         a.flags = flags;
@@ -646,14 +654,18 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         a.out_nulls = (uint32_t*)q.o_nulls.ensure(cap * 4);
         a.out_emit_seq = (int64_t*)q.o_emit.ensure(cap * 8);
         a.out_sub = (int64_t*)q.o_first.ensure(cap * 8);
+        NfaArgs* h_na = (NfaArgs*)q.h_args.ensure(std::max(sizeof(NfaArgs), 2 * sizeof(ChainArgs)));
+        *h_na = a;
+        NfaArgs* d_na = (NfaArgs*)q.d_args.ensure(std::max(sizeof(NfaArgs), 2 * sizeof(ChainArgs)));
+        HIPCHECK(hipMemcpyAsync(d_na, h_na, sizeof(NfaArgs), hipMemcpyHostToDevice, st));
         HIPCHECK(hipEventRecord(e->ev[8], st));
-        nfa_run(a, st);
+        nfa_run(a, d_na, st);
         e->stats.match_launches += nrows > 0;
         HIPCHECK(hipEventRecord(e->ev[2], st));
         unsigned long long hc[2];
-        int hf[4];
+        int hf[8];
         HIPCHECK(hipMemcpyAsync(hc, counters, 16, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipMemcpyAsync(hf, flags, 16, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(hf, flags, 32, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
         float ms_kg = 0, ms_m = 0, t;
         HIPCHECK(hipEventElapsedTime(&ms_kg, e->ev[0], e->ev[1]));
@@ -671,6 +683,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         HIPCHECK(hipEventElapsedTime(&t, e->ev[8], e->ev[2]));
         e->stats.ms_nfa += t;
         e->stats.events += nrows;
+        if (hf[4]) throw CompileError(SDG_ERR_ARG, "device-resident partition key ids out of range (not from sdg_intern)");
         if (hf[0]) {
             e->stats.overflow += 1;
             throw CompileError(SDG_ERR_CAPACITY, "match buffer overflow in query '" + h.name + "'");
@@ -714,7 +727,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     a.out_cap = cap;
     unsigned long long* counters = (unsigned long long*)q.counters.ensure(16);
     HIPCHECK(hipMemsetAsync(counters, 0, 16, st));
-    if (!fused) HIPCHECK(hipMemsetAsync(flags, 0, 16, st));  // fused: cleared before bucketize (mono flag)
+    if (!(partitioned && nrows > 0)) HIPCHECK(hipMemsetAsync(flags, 0, 32, st));  // else cleared before grouping
     a.out_count = counters;
     a.carry_count = counters + 1;
     a.flags = flags;
@@ -760,8 +773,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         a.ovf_count = (unsigned long long*)q.o_ovfc.ensure(8);
         HIPCHECK(hipMemsetAsync(a.ovf_count, 0, 8, st));
     }
-    ChainArgs* d_a = (ChainArgs*)q.d_args.ensure(2 * sizeof(ChainArgs));
-    ChainArgs* h_a = (ChainArgs*)q.h_args.ensure(2 * sizeof(ChainArgs));  // pinned; read before the sync below
+    ChainArgs* d_a = (ChainArgs*)q.d_args.ensure(std::max(sizeof(NfaArgs), 2 * sizeof(ChainArgs)));
+    ChainArgs* h_a = (ChainArgs*)q.h_args.ensure(std::max(sizeof(NfaArgs), 2 * sizeof(ChainArgs)));  // pinned
     h_a[0] = a;
     h_a[1] = a;  // emit-only pass over mq
     h_a[1].mq_in = a.mq;
@@ -826,15 +839,16 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     }
     e->stats.match_launches += (cin.n > 0) + (nrows > 0);
     HIPCHECK(hipEventRecord(e->ev[2], st));
-    uint8_t* ret = (uint8_t*)q.h_ret.ensure(40);
+    uint8_t* ret = (uint8_t*)q.h_ret.ensure(56);
     unsigned long long* hc = (unsigned long long*)ret;
     int* hf = (int*)(ret + 16);
-    unsigned long long& hovf = *(unsigned long long*)(ret + 32);
+    unsigned long long& hovf = *(unsigned long long*)(ret + 48);
     hovf = 0;
     HIPCHECK(hipMemcpyAsync(hc, counters, 16, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipMemcpyAsync(hf, flags, 16, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(hf, flags, 32, hipMemcpyDeviceToHost, st));
     if (fused) HIPCHECK(hipMemcpyAsync(&hovf, a.ovf_count, 8, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
+    if (hf[4]) throw CompileError(SDG_ERR_ARG, "device-resident partition key ids out of range (not from sdg_intern)");
     if (fused && hf[2]) throw DeviceError("fused matcher bounds check failed: bits " + std::to_string(hf[2]));
     if (fused && hf[3]) {  // batch timestamps not in arrival order (or a block's span over 2^32 ms): radix path
         e->stats.fused = 2;
@@ -887,6 +901,56 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     if (!run(try_fused)) run(false);
 }
 
+// read the last flush's match records back (pinned staging) and append them to the query's delivery backlog in
+// the reference's delivery order: by emitting event, then by the partial's position in the pending list
+// (StateMultiProcessStreamReceiver.processAndClear :47-68, QuerySelector.processNoGroupBy :161-205)
+void drain(sdg_engine* e, QueryRt& q) {
+    if (q.polled) return;
+    q.polled = true;
+    const int64_t n = q.out_n;
+    if (n <= 0) return;
+    const int na = q.hq.plan.n_out;
+    uint8_t* hb = (uint8_t*)q.h_rb.ensure((size_t)n * (28 + 8 * (size_t)na));
+    int64_t* ts = (int64_t*)hb;
+    int64_t* emit = ts + n;
+    int64_t* first = emit + n;
+    int64_t* vals = first + n;
+    uint32_t* nulls = (uint32_t*)(vals + (size_t)na * n);
+    hipStream_t st = e->stream;
+    HIPCHECK(hipMemcpyAsync(ts, q.o_ts.p, n * 8, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(emit, q.o_emit.p, n * 8, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(first, q.o_first.p, n * 8, hipMemcpyDeviceToHost, st));
+    if (q.nulls_valid) HIPCHECK(hipMemcpyAsync(nulls, q.o_nulls.p, n * 4, hipMemcpyDeviceToHost, st));
+    for (int j = 0; j < na; ++j)
+        HIPCHECK(hipMemcpyAsync(vals + (size_t)j * n, (int64_t*)q.o_vals.p + (size_t)j * q.out_cap, n * 8,
+                                hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    if (!q.nulls_valid) std::memset(nulls, 0, (size_t)n * 4);
+    std::vector<int64_t> ord(n);
+    std::iota(ord.begin(), ord.end(), 0);
+    std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
+        return emit[x] != emit[y] ? emit[x] < emit[y] : first[x] < first[y];
+    });
+    const size_t b = q.acc_ts.size();
+    q.acc_ts.resize(b + n);
+    q.acc_seq.resize(b + n);
+    q.acc_vals.resize(na);
+    q.acc_nulls.resize(na);
+    for (int j = 0; j < na; ++j) {
+        q.acc_vals[j].resize(b + n);
+        q.acc_nulls[j].resize(b + n);
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t s = ord[i];
+        q.acc_ts[b + i] = ts[s];
+        q.acc_seq[b + i] = emit[s];
+        for (int j = 0; j < na; ++j) {
+            q.acc_vals[j][b + i] = vals[(size_t)j * n + s];
+            q.acc_nulls[j][b + i] = (nulls[s] >> j) & 1u;
+        }
+    }
+}
+
 int do_flush(sdg_engine* e) {
     if (e->compile_only) throw DeviceError("engine was compiled with SDG_COMPILE_ONLY");
     HIPCHECK(hipSetDevice(e->device));
@@ -898,10 +962,20 @@ int do_flush(sdg_engine* e) {
     e->stats.ms_chain_carry = e->stats.ms_chain_match = e->stats.ms_chain_emit = 0;
     e->stats.ms_nfa = 0;
     e->stats.fused_ovf = 0;
-    for (auto& q : e->qs) flush_query(e, *q);
+    // a flush consumes its batch whether or not it succeeds: a failing query must not make the next flush
+    // replay the events onto the queries that already committed them
+    struct Consume {
+        sdg_engine* e;
+        ~Consume() {
+            e->pending.clear();
+            e->pending_n = 0;
+        }
+    } consume{e};
+    for (auto& q : e->qs) {
+        drain(e, *q);  // earlier unpolled results go to the backlog first
+        flush_query(e, *q);
+    }
     e->stats.ms_total = e->stats.ms_keygroup + e->stats.ms_match;
-    e->pending.clear();
-    e->pending_n = 0;
     return SDG_OK;
 }
 
@@ -1081,6 +1155,8 @@ int sdg_push_device(sdg_engine* e, int stream, int64_t n, const int64_t* d_ts, c
     });
 }
 
+int64_t sdg_pending(sdg_engine* e) { return e ? e->pending_n : 0; }
+
 int sdg_advance_time(sdg_engine* e, int64_t) {
     if (!e) return fail(SDG_ERR_ARG, "null engine");
     return SDG_OK;  // no scheduler-driven states on the device path in this build
@@ -1103,44 +1179,25 @@ int sdg_poll(sdg_engine* e, int qi, sdg_out* out) {
     if (!e || qi < 0 || qi >= (int)e->qs.size() || !out) return fail(SDG_ERR_ARG, "bad poll arguments");
     return guarded([&]() {
         QueryRt& q = *e->qs[qi];
-        const Plan& P = q.hq.plan;
-        int64_t n = q.polled ? 0 : q.out_n;
-        int na = P.n_out;
-        q.h_ts.resize(n);
+        const int na = q.hq.plan.n_out;
+        if (!e->compile_only) drain(e, q);
+        const int64_t n = (int64_t)q.acc_ts.size();
+        q.h_ts.swap(q.acc_ts);
+        q.h_seq.swap(q.acc_seq);
+        q.h_vals.swap(q.acc_vals);
+        q.h_nulls.swap(q.acc_nulls);
+        q.acc_ts.clear();
+        q.acc_seq.clear();
+        q.acc_vals.clear();
+        q.acc_nulls.clear();
+        q.h_vals.resize(na);
+        q.h_nulls.resize(na);
         q.h_expired.assign(n, 0);
-        q.h_vals.assign(na, std::vector<int64_t>(n));
-        q.h_nulls.assign(na, std::vector<uint8_t>(n));
-        if (n > 0) {
-            std::vector<int64_t> ts(n), emit(n), first(n), vals((size_t)na * q.out_cap);
-            std::vector<uint32_t> nulls(n);
-            hipStream_t st = e->stream;
-            HIPCHECK(hipMemcpyAsync(ts.data(), q.o_ts.p, n * 8, hipMemcpyDeviceToHost, st));
-            HIPCHECK(hipMemcpyAsync(emit.data(), q.o_emit.p, n * 8, hipMemcpyDeviceToHost, st));
-            HIPCHECK(hipMemcpyAsync(first.data(), q.o_first.p, n * 8, hipMemcpyDeviceToHost, st));
-            if (q.nulls_valid) HIPCHECK(hipMemcpyAsync(nulls.data(), q.o_nulls.p, n * 4, hipMemcpyDeviceToHost, st));
-            for (int j = 0; j < na; ++j)
-                HIPCHECK(hipMemcpyAsync(vals.data() + (size_t)j * q.out_cap, (int64_t*)q.o_vals.p + (size_t)j * q.out_cap,
-                                        n * 8, hipMemcpyDeviceToHost, st));
-            HIPCHECK(hipStreamSynchronize(st));
-            // reference delivery order: by completing event, then by the partial's start (pending-list order)
-            std::vector<int64_t> ord(n);
-            std::iota(ord.begin(), ord.end(), 0);
-            std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
-                return emit[x] != emit[y] ? emit[x] < emit[y] : first[x] < first[y];
-            });
-            for (int64_t i = 0; i < n; ++i) {
-                int64_t s = ord[i];
-                q.h_ts[i] = ts[s];
-                for (int j = 0; j < na; ++j) {
-                    q.h_vals[j][i] = vals[(size_t)j * q.out_cap + s];
-                    q.h_nulls[j][i] = (nulls[s] >> j) & 1u;
-                }
-            }
-        }
-        q.polled = true;
         q.h_vptr.resize(na);
         q.h_nptr.resize(na);
         for (int j = 0; j < na; ++j) {
+            q.h_vals[j].resize(n);
+            q.h_nulls[j].resize(n);
             q.h_vptr[j] = q.h_vals[j].data();
             q.h_nptr[j] = q.h_nulls[j].data();
         }
@@ -1151,6 +1208,7 @@ int sdg_poll(sdg_engine* e, int qi, sdg_out* out) {
         out->types = e->out_types[qi].data();
         out->values = q.h_vptr.data();
         out->nulls = q.h_nptr.data();
+        out->event_seq = q.h_seq.data();
         return (int)SDG_OK;
     });
 }

@@ -19,7 +19,7 @@
 #include "eval.h"
 #include "plan.h"
 
-#define SDG_HD __host__ __device__
+#define SDG_HD __host__ __device__ __forceinline__
 
 namespace sdg {
 namespace nfa {
@@ -29,7 +29,7 @@ constexpr int16_t NIL = -1;
 
 struct Layout {
     int32_t ns, nn, nr, lcap, n_states, n_cols;
-    int64_t off_ps, off_pend, off_newe, off_se, off_nd, off_rc, bytes;
+    int64_t off_ps, off_pend, off_newe, off_ret, off_se, off_nd, off_rc, bytes;
     int32_t se_bytes, rc_bytes;
 };
 
@@ -85,6 +85,8 @@ inline Layout make_layout(int n_states, int n_cols, int ns) {
     o += (int64_t)2 * L.lcap * n_states;
     L.off_newe = o;
     o += (int64_t)2 * L.lcap * n_states;
+    L.off_ret = o;  // StateEvents one processAndReturn call returns (emitted after its loop)
+    o += (int64_t)2 * L.lcap;
     o = (o + 7) & ~7;
     L.off_se = o;
     o += (int64_t)L.se_bytes * L.ns;
@@ -374,25 +376,39 @@ struct Ctx {
     }
 
     SDG_HD void add_state(int p, int16_t s) {
-        const StateRow& r = P->st[p];
-        PState& st = ps(p);
-        if (r.kind == PK_LOGICAL) {  // LogicalPreStateProcessor.addState :43-62
-            int q = r.partner;
-            if (r.is_start || r.seq) {
+        // iterative: a count state with min 0 forwards at once (CountPreStateProcessor.addState :97-125 ->
+        // CountPostStateProcessor.processMinCountReached), which may reach another such state. The every clone of
+        // each level is pushed before the forward chain continues: the chain only touches lists of later states,
+        // the clone the (earlier) every-group start, so the order of the two does not change any list.
+        for (int level = 0; level <= MAX_STATES; ++level) {
+            const StateRow& r = P->st[p];
+            PState& st = ps(p);
+            if (r.kind == PK_LOGICAL) {  // LogicalPreStateProcessor.addState :43-62
+                int q = r.partner;
+                if (r.is_start || r.seq) {
+                    if (st.nw == 0) push(newe(p), st.nw, s);
+                    if (ps(q).nw == 0) push(newe(q), ps(q).nw, s);
+                } else {
+                    push(newe(p), st.nw, s);
+                    push(newe(q), ps(q).nw, s);
+                }
+                return;
+            }
+            if (r.seq) {
                 if (st.nw == 0) push(newe(p), st.nw, s);
-                if (ps(q).nw == 0) push(newe(q), ps(q).nw, s);
             } else {
                 push(newe(p), st.nw, s);
-                push(newe(q), ps(q).nw, s);
             }
-            return;
+            if (!(r.kind == PK_COUNT && r.min_count == 0 && slots(s)[p] == NIL)) return;
+            if (r.selector_after) {
+                ps(p).changed = 1;
+                ps(p).returned = 1;
+            }
+            if (r.next_every >= 0) add_every_state(r.next_every, s);
+            if (r.next < 0) return;
+            p = r.next;
         }
-        if (r.seq) {
-            if (st.nw == 0) push(newe(p), st.nw, s);
-        } else {
-            push(newe(p), st.nw, s);
-        }
-        if (r.kind == PK_COUNT && r.min_count == 0 && slots(s)[p] == NIL) count_min_reached(p, s);
+        set_ovf();
     }
 
     SDG_HD void add_every_state(int p, int16_t s) {
@@ -477,12 +493,11 @@ struct Ctx {
         }
     }
 
-    SDG_HD void start_state_reset(int p, int depth) {  // CountPreStateProcessor.startStateReset :168-181
+    SDG_HD void start_state_reset(int p) {  // CountPreStateProcessor.startStateReset :168-181
         ps(p).start_reset = 1;
-        if (P->st[p].callback >= 0) {
-            if (depth > MAX_STATES) { set_ovf(); return; }
-            start_state_reset(p, depth + 1);
-        }
+        // the reference then calls countPostStateProcessor.thisStatePreProcessor.startStateReset() -- itself --
+        // whenever its own post has a callback: unbounded recursion (StackOverflowError); reported as an error
+        if (P->st[p].callback >= 0) set_ovf();
     }
 
     // ---- post-state processors ---------------------------------------------------------------------------
@@ -493,7 +508,7 @@ struct Ctx {
         if (r.selector_after) ps(p).returned = 1;
         if (r.next >= 0) add_state(r.next, s);
         if (r.next_every >= 0) add_every_state(r.next_every, s);
-        if (r.callback >= 0) start_state_reset(r.callback, 0);
+        if (r.callback >= 0) start_state_reset(r.callback);
     }
     SDG_HD void count_min_reached(int p, int16_t s) {  // CountPostStateProcessor.processMinCountReached
         const StateRow& r = P->st[p];
@@ -552,7 +567,7 @@ struct Ctx {
         PState& st = ps(p);
         int16_t* pd = pend(p);
         const int last = r.last;
-        int16_t ret[64];
+        int16_t* ret = (int16_t*)(base + L.off_ret);
         int nret = 0;
         for (int j = 0; j < st.pn;) {
             if (ovf()) return;
@@ -582,7 +597,7 @@ struct Ctx {
             process_se(p, s);
             if (ps(last).returned) {
                 ps(last).returned = 0;
-                if (nret < 64) ret[nret++] = s;
+                if (nret < L.lcap) ret[nret++] = s;
                 else { set_ovf(); return; }
             }
             bool erased = false;
@@ -604,7 +619,7 @@ struct Ctx {
                 if (r.seq) {  // SEQUENCE: no state change -> dropped (removeOnNoStateChange)
                     erase(pd, st.pn, j);
                     erased = true;
-                    if (r.kind != PK_LOGICAL && P->st[p].callback >= 0) start_state_reset(P->st[p].callback, 0);
+                    if (r.kind != PK_LOGICAL && P->st[p].callback >= 0) start_state_reset(P->st[p].callback);
                 }
             }
             if (!erased) ++j;
@@ -637,7 +652,7 @@ struct Ctx {
     }
 };
 
-SDG_HD inline void SEAcc::load(int slot, int col, int chain, uint8_t kind, int64_t* v, bool* null) {
+SDG_HD void SEAcc::load(int slot, int col, int chain, uint8_t kind, int64_t* v, bool* null) {
     (void)kind;
     *v = 0;
     *null = true;
@@ -648,7 +663,7 @@ SDG_HD inline void SEAcc::load(int slot, int col, int chain, uint8_t kind, int64
     *v = c->vals(r)[col];
     *null = (c->rc(r).nullmask >> col) & 1u;
 }
-SDG_HD inline bool SEAcc::slot_empty(int slot, int chain) {
+SDG_HD bool SEAcc::slot_empty(int slot, int chain) {
     if (slot < 0 || slot >= c->L.n_states) return true;
     return c->chain_at(se, slot, chain) == NIL;
 }
@@ -664,7 +679,7 @@ struct KeyEvents {
 };
 
 // initPartition on the key's first event ever, then every row through the receiver
-SDG_HD inline void run_key(Ctx& c, const KeyEvents& ev) {
+SDG_HD void run_key(Ctx& c, const KeyEvents& ev) {
     const Plan* P = c.P;
     const Layout& L = c.L;
     if (!(c.head().flags & 2)) {

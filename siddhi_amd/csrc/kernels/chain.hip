@@ -333,7 +333,7 @@ __global__ __launch_bounds__(CM_THREADS) void chain_match_k(const ChainArgs* __r
                 if (sp.n_states == 1) {
                     out = (uint32_t)p;
                 } else {
-                    const int64_t end = a.key ? (int64_t)a.seg_end[key] : a.n;
+                    const int64_t end = a.key ? (int64_t)a.seg_end[min(key, (uint32_t)a.K - 1u)] : a.n;
                     const int64_t q = chain_scan<GEN>(a, acc, p + 1, end, tp, stk, stride);
                     out = q >= 0 ? (uint32_t)q : q == -2 ? CM_CARRY : CM_NONE;
                 }
@@ -510,7 +510,7 @@ __global__ __launch_bounds__(DQ_THREADS) void chain_deque_k(const ChainArgs* __r
         }
     }
     // continuation: pop over the key's following rows until the deque drains
-    const int64_t end = a.key ? (int64_t)a.seg_end[cur_key] : a.n;
+    const int64_t end = a.key ? (int64_t)a.seg_end[min(cur_key, (uint32_t)a.K - 1u)] : a.n;
     for (int64_t q = c1; q < end && cnt > 0; ++q) {
         const int64_t tq = a.ts[q];
         step(q, tq, load_col(a.cols[col], kind, q), xnull ? xnull[q] != 0 : false, false);
@@ -528,7 +528,7 @@ __global__ __launch_bounds__(256) void chain_ovf_k(const ChainArgs* __restrict__
         const int64_t p = a.ovf_rows[i];
         ChainAcc acc{&a, View{}, p, -1, -1};
         const uint32_t key = a.key ? a.key[p] : 0u;
-        const int64_t end = a.key ? (int64_t)a.seg_end[key] : a.n;
+        const int64_t end = a.key ? (int64_t)a.seg_end[min(key, (uint32_t)a.K - 1u)] : a.n;
         const int64_t q = chain_scan<true>(a, acc, p + 1, end, a.ts[p], stk, 256);
         a.mq[p] = q >= 0 ? (uint32_t)q : q == -2 ? MQ_CARRY : MQ_NONE;
     }
@@ -673,7 +673,7 @@ __global__ __launch_bounds__(256) void chain_ovf_wave_k(const ChainArgs* __restr
         const int64_t p = a.ovf_rows[i];
         ChainAcc acc{&a, View{}, p, -1, -1};
         const uint32_t key = a.key ? a.key[p] : 0u;
-        const int64_t end = a.key ? (int64_t)a.seg_end[key] : a.n;
+        const int64_t end = a.key ? (int64_t)a.seg_end[min(key, (uint32_t)a.K - 1u)] : a.n;
         const int64_t q = wave_scan_partial(a, acc, p + 1, end, a.ts[p], key);
         if (lane_id() == 0) a.mq[p] = q >= 0 ? (uint32_t)q : q == -2 ? MQ_CARRY : MQ_NONE;
     }
@@ -855,7 +855,7 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
     for (int r = 0; r < FU_PT; ++r) {
         const int row = w * WROWS + r * 64 + lane;
         const bool valid = row < nr;
-        const uint32_t d = valid ? rkey[r] >> a.bbits : 0u;
+        const uint32_t d = valid ? (rkey[r] >> a.bbits) & (uint32_t)(nl - 1) : 0u;  // mask: no-op for keys < K
         uint64_t peers = __ballot(valid);
         for (int bit = 0; bit < a.lbits; ++bit) {
             const bool on = (d >> bit) & 1u;

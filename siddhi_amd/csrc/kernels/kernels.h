@@ -38,6 +38,7 @@ struct KeyGroupArgs {
     const void* src[MAX_COLS + 2];
     void* dst[MAX_COLS + 2];
     uint8_t width[MAX_COLS + 2];      // bytes per element (1, 4 or 8)
+    int* key_flag;                    // non-null: set to 1 when some key >= K (the first histogram pass checks)
 };
 // bytes of workspace for n events; fills the workspace pointers of `a` from `base`
 size_t keygroup_workspace(int64_t n, int32_t K, int32_t ncols, const uint8_t* widths);
@@ -219,6 +220,7 @@ struct NfaArgs {
     int64_t* out_sub;                 // emission ordinal within that event
     int* flags;                       // [0] output overflow, [2] arena overflow (some key ran out of partial slots)
 };
-void nfa_run(const NfaArgs& a, hipStream_t stream);
+// a: host copy (launch geometry); d_a: device copy the kernel reads
+void nfa_run(const NfaArgs& a, const NfaArgs* d_a, hipStream_t stream);
 
 }  // namespace sdg

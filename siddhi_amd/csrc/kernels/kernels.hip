@@ -21,8 +21,11 @@ namespace {
 __device__ __forceinline__ uint32_t digit_of(uint32_t k, int shift, uint32_t mask) { return (k >> shift) & mask; }
 
 // per-tile digit histogram: counts[tile * nb + d]
+// kcheck (first pass only): keys >= K (device-resident batches whose ids did not come from this engine) set
+// *kflag; every later kernel masks its key-derived indices, so such a batch fails the flush without a fault
 __global__ __launch_bounds__(RX_THREADS) void rx_hist(const uint32_t* __restrict__ keys, int64_t n, int shift,
-                                                      uint32_t mask, int nb, uint32_t* __restrict__ counts) {
+                                                      uint32_t mask, int nb, uint32_t* __restrict__ counts,
+                                                      uint32_t kcheck, int* __restrict__ kflag) {
     __shared__ uint32_t h[1 << RX_MAXBITS];
     for (int d = threadIdx.x; d < nb; d += RX_THREADS) h[d] = 0;
     __syncthreads();
@@ -36,6 +39,7 @@ __global__ __launch_bounds__(RX_THREADS) void rx_hist(const uint32_t* __restrict
         for (int r = 0; r < V; ++r) x[r] = kv[r * RX_THREADS + threadIdx.x];
 #pragma unroll
         for (int r = 0; r < V; ++r) {
+            if (kcheck && (x[r].x >= kcheck || x[r].y >= kcheck || x[r].z >= kcheck || x[r].w >= kcheck)) *kflag = 1;
             atomicAdd(&h[digit_of(x[r].x, shift, mask)], 1u);
             atomicAdd(&h[digit_of(x[r].y, shift, mask)], 1u);
             atomicAdd(&h[digit_of(x[r].z, shift, mask)], 1u);
@@ -45,7 +49,11 @@ __global__ __launch_bounds__(RX_THREADS) void rx_hist(const uint32_t* __restrict
 #pragma unroll 4
         for (int r = 0; r < RX_TILE / RX_THREADS; ++r) {
             int64_t i = base + r * RX_THREADS + threadIdx.x;
-            if (i < n) atomicAdd(&h[digit_of(keys[i], shift, mask)], 1u);
+            if (i < n) {
+                const uint32_t k = keys[i];
+                if (kcheck && k >= kcheck) *kflag = 1;
+                atomicAdd(&h[digit_of(k, shift, mask)], 1u);
+            }
         }
     }
     __syncthreads();
@@ -301,18 +309,22 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {  // 4 wa
 }
 
 // key segments of the sorted keys
-__global__ __launch_bounds__(256) void rx_segments(const uint32_t* __restrict__ keys, int64_t n,
+__global__ __launch_bounds__(256) void rx_segments(const uint32_t* __restrict__ keys, int64_t n, uint32_t K,
                                                    uint32_t* __restrict__ seg_start, uint32_t* __restrict__ seg_end) {
     int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     uint32_t k = keys[p];
+    if (k >= K) return;  // flagged by rx_hist
     if (p == 0 || keys[p - 1] != k) seg_start[k] = (uint32_t)p;
     if (p == n - 1 || keys[p + 1] != k) seg_end[k] = (uint32_t)(p + 1);
 }
 
 // one lane per key: the key's arena is private to the lane, so the state machine runs without atomics; only
 // the output slot reservation is shared
-__global__ __launch_bounds__(256) void nfa_k(NfaArgs a) {
+__global__ __launch_bounds__(256) void nfa_k(const NfaArgs* __restrict__ pa) {
+    // arguments from a device copy: indexing a by-value kernel argument (cols[col]) makes the compiler copy the
+    // whole struct to scratch per lane
+    const NfaArgs& a = *pa;
     __shared__ int64_t stack_mem[STACK * 256];
     const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (k >= a.K) return;
@@ -394,7 +406,8 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
         uint32_t mask = (uint32_t)nb - 1;
         const uint32_t* kin = p == 0 ? a.keys : a.tmp_keys[(p - 1) & 1];
         bool last = p == npass - 1;
-        hipLaunchKernelGGL(rx_hist, dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, kin, a.n, shift, mask, nb, a.counts);
+        hipLaunchKernelGGL(rx_hist, dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, kin, a.n, shift, mask, nb, a.counts,
+                           p == 0 && a.key_flag ? (uint32_t)a.K : 0u, a.key_flag);
         int64_t gk = (int64_t)ng * nb;
         hipLaunchKernelGGL(rx_p1, dim3((unsigned)((gk + 255) / 256)), dim3(256), 0, stream, a.counts, (int)nt, nb, a.gsum);
         hipLaunchKernelGGL(rx_p2, dim3(1), dim3(256), 0, stream, a.gsum, ng, nb, a.tot);
@@ -426,7 +439,7 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
     (void)hipMemsetAsync(a.seg_start, 0, (size_t)a.K * 4, stream);
     (void)hipMemsetAsync(a.seg_end, 0, (size_t)a.K * 4, stream);
     hipLaunchKernelGGL(rx_segments, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, stream, a.keys_sorted, a.n,
-                       a.seg_start, a.seg_end);
+                       (uint32_t)a.K, a.seg_start, a.seg_end);
     if (marks) (void)hipEventRecord(marks[3], stream);
 }
 
@@ -467,7 +480,8 @@ void bucketize(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, uint
     const int64_t nt = rx_ntiles(a.n);
     const int ng = (int)((nt + KG_GROUP - 1) / KG_GROUP);
     if (marks) (void)hipEventRecord(marks[0], stream);
-    hipLaunchKernelGGL(rx_hist, dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, a.keys, a.n, 0, mask, nb, a.counts);
+    hipLaunchKernelGGL(rx_hist, dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, a.keys, a.n, 0, mask, nb, a.counts,
+                       a.key_flag ? (uint32_t)a.K : 0u, a.key_flag);
     const int64_t gk = (int64_t)ng * nb;
     hipLaunchKernelGGL(rx_p1, dim3((unsigned)((gk + 255) / 256)), dim3(256), 0, stream, a.counts, (int)nt, nb, a.gsum);
     hipLaunchKernelGGL(rx_p2, dim3(1), dim3(256), 0, stream, a.gsum, ng, nb, a.tot);
@@ -500,9 +514,9 @@ void bucketize(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, uint
     if (marks) (void)hipEventRecord(marks[3], stream);
 }
 
-void nfa_run(const NfaArgs& a, hipStream_t stream) {
+void nfa_run(const NfaArgs& a, const NfaArgs* d_a, hipStream_t stream) {
     if (a.K <= 0 || a.n <= 0) return;
-    hipLaunchKernelGGL(nfa_k, dim3((unsigned)((a.K + 255) / 256)), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(nfa_k, dim3((unsigned)((a.K + 255) / 256)), dim3(256), 0, stream, d_a);
 }
 
 }  // namespace sdg

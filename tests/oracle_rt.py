@@ -49,6 +49,8 @@ def lib():
         L.orc_count_only.argtypes = [P, I32]
         L.orc_output_count.restype = I64
         L.orc_output_count.argtypes = [P]
+        L.orc_export_query_outputs.restype = I64
+        L.orc_export_query_outputs.argtypes = [P, I64, I32, P, P, P]
         L.orc_last_error.restype = ctypes.c_char_p
         _lib = L
     return _lib
@@ -154,6 +156,16 @@ class Oracle:
         if t == STRING:
             return ("s", self.L.orc_string(self.h, slot).decode())
         return ("?", slot)
+
+    def query_arrays(self, nv):
+        """query-callback rows as numpy arrays (ts[n], vals[n][nv] slots, nulls[n][nv]) in delivery order"""
+        import numpy as np
+        cap = self.L.orc_num_outputs(self.h)
+        ts = np.zeros(cap, np.int64)
+        vals = np.zeros((cap, nv), np.int64)
+        nulls = np.zeros((cap, nv), np.uint8)
+        k = self.L.orc_export_query_outputs(self.h, cap, nv, ts.ctypes.data, vals.ctypes.data, nulls.ctypes.data)
+        return ts[:k], vals[:k], nulls[:k]
 
     def outputs(self):
         L = self.L

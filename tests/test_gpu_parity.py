@@ -308,3 +308,146 @@ def test_numeric_partition_keys_host_push(attr, null_rate, oracle_built):
         rt.shutdown()
     assert len(ref) > 200
     assert got == ref
+
+
+# ---- parity at the benchmark's own regime (VERDICT r1 "what's weak" 1) ------------------------------------
+def oracle_batch_rows(app, stream, ts, slot_cols, nv):
+    """the oracle fed through orc_send_batch (one send(ts, data) per event): query rows as arrays"""
+    from oracle_rt import lib
+    o = Oracle(app)
+    try:
+        L = lib()
+        n = len(ts)
+        slots = np.ascontiguousarray(np.stack([np.asarray(c).astype(np.int64) for c in slot_cols], axis=1))
+        na = slots.shape[1]
+        rc = L.orc_send_batch(o.h, n, np.full(n, o.stream(stream), np.int32).ctypes.data,
+                              np.ascontiguousarray(ts, np.int64).ctypes.data,
+                              (np.arange(n, dtype=np.int64) * na).ctypes.data, slots.ctypes.data, None)
+        assert rc == 0
+        return o.query_arrays(nv)
+    finally:
+        o.close()
+
+
+def test_c2_bench_regime_vs_oracle(oracle_built):
+    """2M events over 10k keys at the bench's rate (100 events/ms: ~10 events per key-window), device-resident,
+    fused path; the whole match list must equal the oracle's, in delivery order"""
+    import torch
+    n, keys = 2_000_000, 10_000
+    cols = w.c2_columns(n, keys=keys, per_ms=100)
+    syms = w.symbols(keys)
+    from oracle_rt import lib
+    o_ids = None
+    rt = sa.SiddhiAppRuntime(w.C2_APP)
+    try:
+        sym_ids = np.array([rt.intern(s) for s in syms], dtype=np.uint32)
+        dev = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in
+               [("ts", cols["ts"]), ("id", cols["id"]), ("sym", sym_ids[cols["key"]].astype(np.int32)),
+                ("price", cols["price"]), ("vol", cols["volume"])]}
+        rt.push_device("StockStream", n, dev["ts"].data_ptr(),
+                       [dev["id"].data_ptr(), dev["sym"].data_ptr(), dev["price"].data_ptr(), dev["vol"].data_ptr()])
+        rt.flush(deliver=False)
+        assert rt.stats().fused == 1
+        gts, gvals, gnulls, gseq = rt.poll_arrays(0)
+    finally:
+        rt.shutdown()
+    o = Oracle(w.C2_APP)
+    try:
+        L = lib()
+        o_ids = np.array([L.orc_intern(o.h, s.encode()) for s in syms], dtype=np.int64)
+    finally:
+        o.close()
+    ots, ovals, _ = oracle_batch_rows(w.C2_APP, "StockStream", cols["ts"],
+                                      [cols["id"], o_ids[cols["key"]], cols["price"].view(np.int64), cols["volume"]], 2)
+    assert len(ots) > 500_000
+    assert np.array_equal(gts, ots) and np.array_equal(gvals.T, ovals) and not gnulls.any()
+    assert np.all(np.diff(gseq) >= 0)  # delivery order: by emitting event
+
+
+@pytest.mark.parametrize("query", ["<1:5>", "<2:5>"])
+def test_c3_long_keys_vs_oracle(query, oracle_built):
+    """C3 generator (long partition keys, 10^4 keys x 100 events) through the host push, generic keyed NFA; the
+    <1:5> form matches, the literal <2:5> form never does"""
+    keys = 10_000
+    c = w.c3_columns(keys)
+    app = w.C3_APP.replace("<2:5>", query)
+    rt = sa.SiddhiAppRuntime(app)
+    try:
+        assert rt.query_paths() == [1]
+        rt.getInputHandler("S").send_columns(c["ts"], [c["id"], c["key"], c["price"], c["volume"]])
+        rt.flush(deliver=False)
+        gts, gvals, gnulls, _ = rt.poll_arrays(0)
+    finally:
+        rt.shutdown()
+    ots, ovals, onulls = oracle_batch_rows(app, "S", c["ts"], [c["id"], c["key"], c["price"].view(np.int64),
+                                                               c["volume"]], 4)
+    if query == "<1:5>":
+        assert len(ots) > 10_000
+    else:
+        assert len(ots) == 0
+    assert np.array_equal(gts, ots) and np.array_equal(gvals.T, ovals) and np.array_equal(gnulls.T, onulls)
+
+
+def test_auto_flush_is_lossless(oracle_built):
+    """a small batch_capacity: sdg_push flushes by itself several times; every match still reaches the callback
+    exactly once, in order (auto-flush used to overwrite unpolled results)"""
+    keys = 300
+    cols = w.c2_columns(60_000, keys=keys, per_ms=2)
+    syms = w.symbols(keys)
+    ref = oracle_c_rows(w.C2_APP, cols, syms)
+
+    class CB(sa.QueryCallback):
+        def __init__(self):
+            self.rows = []
+
+        def receive(self, timestamp, inEvents, removeEvents):  # noqa: N803
+            assert len(inEvents) == 1 and inEvents[0].timestamp == timestamp
+            self.rows.append((timestamp, tuple(inEvents[0].data)))
+
+    rt = sa.SiddhiAppRuntime(w.C2_APP, batch_capacity=7_000)
+    cb = CB()
+    rt.addCallback("query1", cb)
+    try:
+        h = rt.getInputHandler("StockStream")
+        sym_ids = np.array([rt.intern(s) for s in syms], dtype=np.uint32)
+        n = len(cols["ts"])
+        for s in range(0, n, 2_500):  # pushes straddle the capacity: auto-flushes mid-stream
+            e = min(n, s + 2_500)
+            h.send_columns(cols["ts"][s:e], [cols["id"][s:e], sym_ids[cols["key"][s:e]], cols["price"][s:e],
+                                             cols["volume"][s:e]])
+        rt.flush()
+    finally:
+        rt.shutdown()
+    assert len(ref) > 1000
+    assert [(t, v) for t, v in cb.rows] == ref
+
+
+def test_failed_flush_consumes_its_batch(oracle_built):
+    """device-resident key ids that did not come from sdg_intern: the flush fails with ValueError (no fault), and
+    the next flush does not replay the bad batch"""
+    import torch
+    keys = 50
+    cols = w.c2_columns(20_000, keys=keys, per_ms=2)
+    syms = w.symbols(keys)
+    ref = oracle_c_rows(w.C2_APP, cols, syms)
+    rt = sa.SiddhiAppRuntime(w.C2_APP)
+    try:
+        sym_ids = np.array([rt.intern(s) for s in syms], dtype=np.uint32)
+        n = len(cols["ts"])
+        bad = sym_ids[cols["key"]].astype(np.int64)
+        bad[n // 2] = 1 << 30
+        dev = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in
+               [("ts", cols["ts"]), ("id", cols["id"]), ("bad", bad.astype(np.int32)),
+                ("sym", sym_ids[cols["key"]].astype(np.int32)), ("price", cols["price"]), ("vol", cols["volume"])]}
+        rt.push_device("StockStream", n, dev["ts"].data_ptr(),
+                       [dev["id"].data_ptr(), dev["bad"].data_ptr(), dev["price"].data_ptr(), dev["vol"].data_ptr()])
+        with pytest.raises(ValueError):
+            rt.flush(deliver=False)
+        rt.push_device("StockStream", n, dev["ts"].data_ptr(),
+                       [dev["id"].data_ptr(), dev["sym"].data_ptr(), dev["price"].data_ptr(), dev["vol"].data_ptr()])
+        rt.flush(deliver=False)
+        types, ts, vals, nulls = rt.raw_outputs(0)
+        got = [(ts[i], (vals[0][i], vals[1][i])) for i in range(len(ts))]
+    finally:
+        rt.shutdown()
+    assert got == ref
