@@ -106,9 +106,10 @@ def parity_check(cols, syms, sample, dev_cols, device):
     slots[:, 1] = ids[cols["key"][:n]]
     slots[:, 2] = cols["price"][:n].view(np.int64)
     slots[:, 3] = cols["volume"][:n]
-    rc = L.orc_send_batch(o.h, n, np.full(n, o.stream("StockStream"), dtype=np.int32).ctypes.data,
-                          np.ascontiguousarray(cols["ts"][:n]).ctypes.data,
-                          (np.arange(n, dtype=np.int64) * 4).ctypes.data, slots.ctypes.data, None)
+    strm = np.full(n, o.stream("StockStream"), dtype=np.int32)  # named: temporaries die before the call
+    tsa = np.ascontiguousarray(cols["ts"][:n])
+    offs = np.arange(n, dtype=np.int64) * 4
+    rc = L.orc_send_batch(o.h, n, strm.ctypes.data, tsa.ctypes.data, offs.ctypes.data, slots.ctypes.data, None)
     if rc != 0:
         raise RuntimeError("oracle failed")
     ots, ovals, onulls = o.query_arrays(2)

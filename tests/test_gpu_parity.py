@@ -311,18 +311,25 @@ def test_numeric_partition_keys_host_push(attr, null_rate, oracle_built):
 
 
 # ---- parity at the benchmark's own regime (VERDICT r1 "what's weak" 1) ------------------------------------
-def oracle_batch_rows(app, stream, ts, slot_cols, nv):
-    """the oracle fed through orc_send_batch (one send(ts, data) per event): query rows as arrays"""
+def oracle_batch_rows(app, stream, ts, slot_cols, nv, str_col=None):
+    """the oracle fed through orc_send_batch (one send(ts, data) per event): query rows as arrays.
+    str_col = (attribute index, key index column, symbol list): that column becomes this oracle's string ids"""
     from oracle_rt import lib
     o = Oracle(app)
     try:
         L = lib()
         n = len(ts)
+        if str_col is not None:
+            ai, kidx, syms = str_col
+            ids = np.array([L.orc_intern(o.h, s.encode()) for s in syms], dtype=np.int64)
+            slot_cols = list(slot_cols)
+            slot_cols[ai] = ids[kidx]
         slots = np.ascontiguousarray(np.stack([np.asarray(c).astype(np.int64) for c in slot_cols], axis=1))
         na = slots.shape[1]
-        rc = L.orc_send_batch(o.h, n, np.full(n, o.stream(stream), np.int32).ctypes.data,
-                              np.ascontiguousarray(ts, np.int64).ctypes.data,
-                              (np.arange(n, dtype=np.int64) * na).ctypes.data, slots.ctypes.data, None)
+        strm = np.full(n, o.stream(stream), np.int32)  # named: a temporary's buffer dies before the call
+        tsa = np.ascontiguousarray(ts, np.int64)
+        offs = np.arange(n, dtype=np.int64) * na
+        rc = L.orc_send_batch(o.h, n, strm.ctypes.data, tsa.ctypes.data, offs.ctypes.data, slots.ctypes.data, None)
         assert rc == 0
         return o.query_arrays(nv)
     finally:
@@ -336,8 +343,6 @@ def test_c2_bench_regime_vs_oracle(oracle_built):
     n, keys = 2_000_000, 10_000
     cols = w.c2_columns(n, keys=keys, per_ms=100)
     syms = w.symbols(keys)
-    from oracle_rt import lib
-    o_ids = None
     rt = sa.SiddhiAppRuntime(w.C2_APP)
     try:
         sym_ids = np.array([rt.intern(s) for s in syms], dtype=np.uint32)
@@ -351,14 +356,9 @@ def test_c2_bench_regime_vs_oracle(oracle_built):
         gts, gvals, gnulls, gseq = rt.poll_arrays(0)
     finally:
         rt.shutdown()
-    o = Oracle(w.C2_APP)
-    try:
-        L = lib()
-        o_ids = np.array([L.orc_intern(o.h, s.encode()) for s in syms], dtype=np.int64)
-    finally:
-        o.close()
     ots, ovals, _ = oracle_batch_rows(w.C2_APP, "StockStream", cols["ts"],
-                                      [cols["id"], o_ids[cols["key"]], cols["price"].view(np.int64), cols["volume"]], 2)
+                                      [cols["id"], None, cols["price"].view(np.int64), cols["volume"]], 2,
+                                      str_col=(1, cols["key"], syms))
     assert len(ots) > 500_000
     assert np.array_equal(gts, ots) and np.array_equal(gvals.T, ovals) and not gnulls.any()
     assert np.all(np.diff(gseq) >= 0)  # delivery order: by emitting event
