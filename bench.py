@@ -38,6 +38,14 @@ B_OUT = 28
 HBM_PEAK_GBS = 8000.0
 
 
+T_START = time.time()
+
+
+def log(msg):
+    """progress on stderr (the JSON line is the only stdout output)"""
+    print("[bench %6.1fs] %s" % (time.time() - T_START, msg), file=sys.stderr, flush=True)
+
+
 def gen_shard(n, keys, rank, world, seed=7):
     """C2 columns of this rank's shard (numpy, chunked to bound host memory)."""
     from siddhi_amd import workloads as w
@@ -49,6 +57,30 @@ def gen_shard(n, keys, rank, world, seed=7):
         for k in out:
             out[k].append(c[k])
     return {k: np.concatenate(v) for k, v in out.items()}
+
+
+def end_to_end(cols, syms, n, steps, device):
+    """host SoA push -> flush -> poll of every match to host memory, per step (PCIe both ways, host assembly and
+    the delivery-order sort included): the rate a host application sees, beside the device-resident value"""
+    import siddhi_amd as sa
+    from siddhi_amd import workloads as w
+    rt = sa.SiddhiAppRuntime(w.C2_APP, device=device, batch_capacity=n + 1)
+    sym_ids = np.array([rt.intern(s) for s in syms], dtype=np.uint32)
+    h = rt.getInputHandler("StockStream")
+    symcol = sym_ids[cols["key"][:n]]
+    span = int(cols["ts"][n - 1] - cols["ts"][0]) + 1
+    rows = 0
+    t = time.perf_counter()
+    for s in range(steps):
+        h.send_columns(cols["ts"][:n] + s * span, [cols["id"][:n], symcol, cols["price"][:n], cols["volume"][:n]])
+        rt.flush(deliver=False)
+        ts, vals, nulls, seq = rt.poll_arrays(0)
+        rows += len(ts)
+    dt = time.perf_counter() - t
+    rt.shutdown()
+    return {"value": n * steps / dt, "unit": "events/s", "ms_per_step": dt * 1000 / steps, "events_per_step": n,
+            "matches_delivered_per_step": rows / steps,
+            "path": "host columns (sdg_push) -> device flush -> sdg_poll into host arrays, delivery order"}
 
 
 def cpu_baseline(cols, syms, sample):
@@ -179,6 +211,7 @@ def main():
     ap.add_argument("--parity-sample", type=int, default=3_000_000,
                     help="events of the bench stream re-run through a fresh runtime and the oracle (bit-exact check)")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--e2e-steps", type=int, default=1, help="end-to-end (host push -> poll) steps, 0 = skip")
     args = ap.parse_args()
 
     import torch
@@ -195,6 +228,7 @@ def main():
     from siddhi_amd import workloads as w
 
     n, keys = args.events, args.keys
+    log("generating %d events x %d keys (rank %d/%d)" % (n, keys, rank, world))
     cols = gen_shard(n, keys, rank, world)
     from siddhi_amd import shard
     syms = []  # this rank's keys: the first `keys` global key names that hash to this rank (shard.py)
@@ -221,6 +255,7 @@ def main():
         rt.push_device("StockStream", n, ts_steps[s].data_ptr(),
                        [d_id.data_ptr(), d_sym.data_ptr(), d_price.data_ptr(), d_vol.data_ptr()])
         rt.flush(deliver=False)
+        rt.discard()  # matches stay in HBM (device-resident measurement)
         st = rt.stats()
         if dist is not None:  # batch-boundary match-count all-gather (global output offsets)
             cnt = torch.tensor([st.matches], dtype=torch.int64, device=dev)
@@ -228,8 +263,10 @@ def main():
             dist.all_gather(allc, cnt)
         return st
 
+    log("warm-up (%d steps)" % args.warmup)
     for s in range(args.warmup):
         step(s)
+    log("timed steps (%d)" % args.steps)
     keys_k = ["ms_kg_hist", "ms_kg_prefix", "ms_kg_scatter", "ms_chain_carry", "ms_chain_match"]
     acc = {k: 0.0 for k in keys_k}
     matches = 0
@@ -298,11 +335,13 @@ def main():
                      "kernel_ms": per_kernel},
     }
     if rank == 0 and world == 1 and not args.no_cpu:
+        log("cpu baseline (oracle, 1 thread, %d events)" % min(args.cpu_sample, n))
         rate, cm, dt = cpu_baseline(cols, syms, min(args.cpu_sample, n))
         out["cpu_baseline"] = {"value": rate, "unit": "events/s", "cores": 1, "kind": "port",
                                "sample": "first %d events of the C2 stream (%.1f s, %d matches), oracle restatement"
                                          % (min(args.cpu_sample, n), dt, cm)}
         thr = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+        log("cpu baseline, key-sharded over %d threads" % thr)
         srate, scm, sdt = cpu_baseline_sharded(cols, syms, min(args.cpu_sample, n), thr)
         if scm != cm:
             raise RuntimeError("key-sharded CPU baseline disagrees with the single-thread run: %d vs %d" % (scm, cm))
@@ -312,7 +351,11 @@ def main():
     else:
         out["cpu_baseline"] = None
     rt.shutdown()
+    if args.e2e_steps > 0 and world == 1:
+        log("end-to-end (host push -> poll), %d step(s)" % args.e2e_steps)
+        out["end_to_end"] = end_to_end(cols, syms, n, args.e2e_steps, local)
     if not args.no_parity:
+        log("parity leg (GPU vs oracle on the bench stream's first events)")
         ps = min(args.parity_sample if world == 1 else args.parity_sample // 3, n)
         out["parity"] = parity_check(cols, syms, ps, (d_id[:ps], d_sym[:ps], d_price[:ps], d_vol[:ps], d_ts0[:ps]),
                                      local)
@@ -320,6 +363,7 @@ def main():
             okt = torch.tensor([1], dtype=torch.int64, device=dev)
             dist.all_reduce(okt)
             out["parity"]["ranks_checked"] = int(okt.item())
+    log("done")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -106,6 +106,9 @@ int64_t sdg_pending(sdg_engine* e);
 int sdg_flush(sdg_engine* e);
 int sdg_sync(sdg_engine* e);
 int sdg_poll(sdg_engine* e, int query, sdg_out* out);
+/* drop every query's unpolled results without reading them back (measurement of the device-resident path; an
+ * application that wants its matches polls instead) */
+int sdg_discard(sdg_engine* e);
 
 /* introspection for measurement: device time of the last flush per kernel family, algorithmic bytes,
  * match count, and which kernel path each query took (0 = chain, 1 = generic). */

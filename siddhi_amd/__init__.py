@@ -126,6 +126,7 @@ def load_library():
     L.sdg_flush.argtypes = [P]
     L.sdg_sync.argtypes = [P]
     L.sdg_poll.argtypes = [P, I32, ctypes.POINTER(_Out)]
+    L.sdg_discard.argtypes = [P]
     L.sdg_last_stats.argtypes = [P, ctypes.POINTER(Stats)]
     _lib = L
     return L
@@ -331,6 +332,10 @@ class SiddhiAppRuntime:
         _check(self._L.sdg_flush(self._h))
         if deliver:
             self._deliver()
+
+    def discard(self):
+        """drop the unpolled results of every query (device-resident measurement only)"""
+        _check(self._L.sdg_discard(self._h))
 
     def stats(self):
         s = Stats()

@@ -1213,6 +1213,18 @@ int sdg_poll(sdg_engine* e, int qi, sdg_out* out) {
     });
 }
 
+int sdg_discard(sdg_engine* e) {
+    if (!e) return fail(SDG_ERR_ARG, "null engine");
+    for (auto& q : e->qs) {
+        q->polled = true;
+        q->acc_ts.clear();
+        q->acc_seq.clear();
+        q->acc_vals.clear();
+        q->acc_nulls.clear();
+    }
+    return SDG_OK;
+}
+
 int sdg_last_stats(sdg_engine* e, sdg_stats* out) {
     if (!e || !out) return fail(SDG_ERR_ARG, "null argument");
     *out = e->stats;
