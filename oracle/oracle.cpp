@@ -11,6 +11,7 @@
 //   CountPre / CountPost         query/input/stream/state/CountPreStateProcessor.java, CountPostStateProcessor.java
 //   LogicalPre / LogicalPost     query/input/stream/state/LogicalPreStateProcessor.java, LogicalPostStateProcessor.java
 //   AbsentPre / AbsentPost       query/input/stream/state/AbsentStreamPreStateProcessor.java, AbsentStreamPostStateProcessor.java
+//   AbsentLogicalPre / Post      query/input/stream/state/AbsentLogicalPreStateProcessor.java, AbsentLogicalPostStateProcessor.java
 //   Inner runtimes               query/input/stream/state/runtime/*.java
 //   Receivers                    query/input/{Single,Multi,StateMulti}ProcessStreamReceiver.java + state/receiver/*.java
 //   Lowering                     util/parser/StateInputStreamParser.java:76-408
@@ -33,6 +34,7 @@
 #include <functional>
 #include <list>
 #include <map>
+#include <set>
 #include <memory>
 #include <string>
 #include <unordered_map>
@@ -411,10 +413,15 @@ struct PreState {
     std::list<StEv> pending, newAndEvery;
     bool stateChanged = false, initialized = false, started = false;
     bool successCondition = false, startStateReset = false;  // CountStreamPreState
-    int64_t lastScheduledTime = 0;                           // LogicalStreamPreState (absent)
+    int64_t lastScheduledTime = 0;                           // AbsentStreamPreState
+    int64_t lastArrivalTime = 0;                             // AbsentLogicalPreStateProcessor.LogicalStreamPreState
     bool active = true;
     int activeUseCount = 0;
-    bool canDestroy() const { return !cur.first && pending.empty() && newAndEvery.empty() && !initialized; }
+    // StreamPreState.canDestroy :444-448 (&& lastArrivalTime == 0: LogicalStreamPreState.canDestroy :403-405;
+    // the field stays 0 for every other kind)
+    bool canDestroy() const {
+        return !cur.first && pending.empty() && newAndEvery.empty() && !initialized && lastArrivalTime == 0;
+    }
 };
 using PS = std::shared_ptr<PreState>;
 
@@ -690,6 +697,7 @@ struct PreProc : Processor {
     PreStateHolder holder;
     int nstates = 0;  // MetaStateEvent stream event count
     int noutputs = 0;
+    int nattrs = 0;   // attributes of this state's stream (StreamEventFactory.newInstance output size)
 
     void process(Chunk&) override { throw OracleError("process method of StreamPreStateProcessor should not be called"); }
     virtual bool isAbsent() const { return false; }
@@ -834,6 +842,15 @@ struct PreProc : Processor {
     virtual bool removeOnNoStateChange() const { return stateType == sql::StateType::SEQUENCE; }
     virtual Chunk processAndReturn(const SEv& ev);  // :364-403
     virtual void partitionCreated() {}
+    // EntryValveProcessor -> process(ComplexEventChunk) of a TIMER event (absent processors only)
+    virtual void processTimer(int64_t) { throw OracleError("timer delivered to a non-absent processor"); }
+    virtual void updateLastArrivalTime(int64_t) { throw OracleError("updateLastArrivalTime on a non-absent processor"); }
+    SEv emptyStreamEvent() const {  // StreamEventFactory.newInstance(): timestamp -1, all attributes null
+        SEv n(new StreamEvent());
+        n->ts = -1;
+        n->data.resize(nattrs);
+        return n;
+    }
 };
 
 // CountPreStateProcessor.java
@@ -1005,6 +1022,11 @@ struct LogicalPre : PreProc {
         Hold st(holder);
         return st->newAndEvery.empty();
     }
+    void removeFromPending(const StEv& se) {  // getPendingStateEventList().remove(stateEvent): first occurrence
+        Hold st(holder);
+        for (auto it = st->pending.begin(); it != st->pending.end(); ++it)
+            if (*it == se) { st->pending.erase(it); return; }
+    }
     void addToNewAndEvery(const StEv& se) {
         Hold st(holder);
         st->newAndEvery.push_back(se);
@@ -1086,16 +1108,7 @@ struct LogicalPost : Post {
     sql::LogicalType type = sql::LogicalType::AND;
     LogicalPre* partnerPre = nullptr;
     LogicalPost* partnerPost = nullptr;
-    void processSE(StEv se, Chunk& c) override {  // LogicalPostStateProcessor.java:59-87
-        if (type == sql::LogicalType::AND) {
-            bool proceed = se->se[partnerPre->stateId] != nullptr;
-            if (proceed) Post::processSE(se, c);
-            else thisPre->stateChanged();
-        } else {
-            Post::processSE(se, c);
-            if (partnerPost->nextProcessor && thisPre->thisLast == partnerPost) partnerPost->isEventReturned = true;
-        }
-    }
+    void processSE(StEv se, Chunk& c) override;  // LogicalPostStateProcessor.java:59-87 (after AbsentLogicalPre)
     void setNextStatePreProcessor(PreProc* p) override {
         nextStatePre = p;
         partnerPost->nextStatePre = p;
@@ -1118,19 +1131,27 @@ struct SchedState {
 };
 using SSP = std::shared_ptr<SchedState>;
 
-struct AbsentPre;
 struct Scheduler {
     Engine* eng = nullptr;
-    AbsentPre* target = nullptr;  // EntryValveProcessor.setToLast(absentProcessor)
+    PreProc* target = nullptr;  // EntryValveProcessor.setToLast(absentProcessor)
     bool partitioned = false;
     SSP single;
     JHashMap<SSP> map;
+    // heads of the non-empty queues (not reference state: lets onTimeChange skip the full map walk, which finds
+    // nothing due, when the earliest head is later than the clock)
+    std::multiset<int64_t> heads;
     SSP getState();
     void returnState(const SSP& s);
     void notifyAt(int64_t t) {
         SSP s = getState();
+        if (s->queue.empty()) heads.insert(t);
         s->queue.push_back(t);
         returnState(s);
+    }
+    void popHead(const SSP& s) {
+        heads.erase(heads.find(s->queue.front()));
+        s->queue.pop_front();
+        if (!s->queue.empty()) heads.insert(s->queue.front());
     }
     void sendTimerEvents(const SSP& s);
     void onTimeChange(int64_t now);  // playback TimeChangeListener
@@ -1181,7 +1202,7 @@ struct AbsentPre : PreProc {
     int64_t waitingTime = -1;
     Scheduler* scheduler = nullptr;
     bool isAbsent() const override { return true; }
-    void updateLastArrivalTime(int64_t ts) {  // :68-78
+    void updateLastArrivalTime(int64_t ts) override {  // :68-78
         Hold st(holder);
         st->lastScheduledTime = ts + waitingTime;
         scheduler->notifyAt(st->lastScheduledTime);
@@ -1219,7 +1240,7 @@ struct AbsentPre : PreProc {
         }
     }
     void sendEvent(const StEv& se, const PS& st);
-    void processTimer(int64_t currentTimeOfChunk);  // process(ComplexEventChunk) :151-227
+    void processTimer(int64_t currentTimeOfChunk) override;  // process(ComplexEventChunk) :151-227
     bool removeOnNoStateChange() const override { return false; }
     Chunk processAndReturn(const SEv& ev) override {  // :257-274
         Hold st(holder);
@@ -1248,8 +1269,196 @@ void AbsentPost::processSE(StEv se, Chunk&) {  // AbsentStreamPostStateProcessor
     if (thisPre->isStartState) {
         if (nextEveryStatePre && nextEveryStatePre == thisPre) nextEveryStatePre->addEveryState(se);
     }
-    static_cast<AbsentPre*>(thisPre)->updateLastArrivalTime(s->ts);
+    thisPre->updateLastArrivalTime(s->ts);
 }
+
+// AbsentLogicalPreStateProcessor.java: one side of `not A [for T] and/or B` (the other side is a LogicalPre or
+// another AbsentLogicalPre), with its own scheduler
+struct AbsentLogicalPre : LogicalPre {
+    int64_t waitingTime = -1;
+    Scheduler* scheduler = nullptr;
+    bool isAbsent() const override { return true; }
+    void updateLastArrivalTime(int64_t ts) override {  // :65-75
+        Hold st(holder);
+        st->lastArrivalTime = ts;
+    }
+    void addStateImpl(const StEv& se, const PS& st) override {  // :77-97
+        if (!st->active) return;
+        LogicalPre::addStateImpl(se, st);
+        if (!isStartState && waitingTime != -1) {
+            scheduler->notifyAt(se->ts + waitingTime);
+            if (partner->isAbsent()) {
+                auto* pa = static_cast<AbsentLogicalPre*>(partner);
+                pa->scheduler->notifyAt(se->ts + pa->waitingTime);
+            }
+        }
+    }
+    void addEveryState(const StEv& se) override {  // :99-118
+        StEv cl = cloneStateEvent(se);
+        cl->type = CURRENT;
+        if (cl->se[stateId]) cl->ts = cl->se[stateId]->ts;  // the timestamp of the last arrived event
+        cl->se[stateId] = nullptr;
+        cl->se[partner->stateId] = nullptr;
+        Hold st(holder);
+        st->newAndEvery.push_back(cl);
+        partner->addToNewAndEvery(cl);
+    }
+    bool waitingTimePassed(int64_t currentTime, StateEvent* se) const {  // :220-228
+        if (!se->se[stateId]) return currentTime >= se->ts + waitingTime;
+        return currentTime >= se->se[stateId]->ts + waitingTime;
+    }
+    void setActive(bool a) {  // :252-259
+        Hold st(holder);
+        st->active = a;
+    }
+    void sendEvent(const StEv& se, const PS& st) {  // :230-250
+        if (thisPost->nextProcessor) {
+            Chunk one;
+            one.add(se);
+            thisPost->nextProcessor->process(one);
+        }
+        if (thisPost->nextStatePre) thisPost->nextStatePre->addState(se);
+        if (thisPost->nextEveryStatePre) {
+            thisPost->nextEveryStatePre->addEveryState(se);
+        } else if (isStartState) {
+            st->active = false;
+            if (logicalType == sql::LogicalType::OR && partner->isAbsent())
+                static_cast<AbsentLogicalPre*>(partner)->setActive(false);
+        }
+        if (thisPost->callbackPre) thisPost->callbackPre->startStateReset();
+    }
+    void processTimer(int64_t currentTime) override {  // process(ComplexEventChunk) :121-209
+        Hold st(holder);
+        if (!st->active) return;
+        bool notProcessed = true;
+        if (currentTime >= st->lastArrivalTime + waitingTime) {
+            if (isStartState && stateType == sql::StateType::SEQUENCE && st->newAndEvery.empty() && st->pending.empty()) {
+                StEv se = newStateEvent();
+                addState(se);
+            } else if (stateType == sql::StateType::SEQUENCE && !st->newAndEvery.empty()) {
+                resetState();
+            }
+            updateState();
+            StEv expired;
+            std::vector<StEv> ret;
+            for (auto it = st->pending.begin(); it != st->pending.end();) {
+                StEv se = *it;
+                if (isExpired(se.get(), currentTime)) {  // within
+                    expired = se;
+                    it = st->pending.erase(it);
+                    continue;
+                }
+                if (waitingTimePassed(currentTime, se.get())) {
+                    it = st->pending.erase(it);
+                    const bool partnerIn = (bool)se->se[partner->stateId];
+                    if (logicalType == sql::LogicalType::OR && !partnerIn) {  // OR partner not received
+                        se->addEvent(stateId, emptyStreamEvent());
+                        ret.push_back(se);
+                    } else if (logicalType == sql::LogicalType::AND && partnerIn) {  // AND partner received
+                        ret.push_back(se);
+                    } else if (logicalType == sql::LogicalType::AND && !partnerIn) {  // let the partner proceed
+                        se->addEvent(stateId, emptyStreamEvent());
+                    }
+                    continue;
+                }
+                ++it;
+            }
+            if (expired && withinEveryPre) {
+                withinEveryPre->addEveryState(expired);
+                withinEveryPre->updateState();
+            }
+            notProcessed = ret.empty();
+            for (auto& se : ret) {
+                se->ts = currentTime;
+                sendEvent(se, st.s);
+            }
+            st->lastArrivalTime = 0;
+        }
+        if (thisPost->nextEveryStatePre || (notProcessed && isStartState)) {  // schedule again
+            const int64_t nextBreak = st->lastArrivalTime == 0 ? eng->currentTime() + waitingTime
+                                                                : st->lastArrivalTime + waitingTime;
+            scheduler->notifyAt(nextBreak);
+        }
+    }
+    Chunk processAndReturn(const SEv& ev) override {  // :262-319 (never returns matches itself)
+        Hold st(holder);
+        if (!st->active) return Chunk();
+        auto& lst = st->pending;
+        for (auto it = lst.begin(); it != lst.end();) {
+            StEv se = *it;
+            if (logicalType == sql::LogicalType::OR && se->se[partner->stateId]) {
+                it = lst.erase(it);
+                continue;
+            }
+            SEv curEv = se->se[stateId];
+            se->se[stateId] = copyStreamEvent(ev);
+            processSE(se);
+            if (waitingTime != -1 || (stateType == sql::StateType::SEQUENCE && logicalType == sql::LogicalType::AND &&
+                                      thisPost->nextEveryStatePre))
+                se->se[stateId] = curEv;  // reset to the original state after processing
+            bool removed = false;
+            if (thisLast->isEventReturned) {  // passed the filter: no longer an absence candidate
+                thisLast->isEventReturned = false;
+                it = lst.erase(it);
+                removed = true;
+                if (stateType == sql::StateType::SEQUENCE) partner->removeFromPending(se);
+            }
+            if (!st->stateChanged) {
+                se->se[stateId] = curEv;
+                if (stateType == sql::StateType::SEQUENCE) {
+                    if (removed) throw OracleError("IllegalStateException (iterator.remove twice)");
+                    it = lst.erase(it);
+                    removed = true;
+                }
+            }
+            if (!removed) ++it;
+        }
+        return Chunk();
+    }
+    void partitionCreated() override {  // :331-351
+        Hold st(holder);
+        if (!st->started) {
+            st->started = true;
+            if (isStartState && waitingTime != -1 && st->active) scheduler->notifyAt(eng->currentTime() + waitingTime);
+        }
+    }
+    bool partnerCanProceed(StateEvent* se) {  // :353-388
+        Hold st(holder);
+        if (stateType == sql::StateType::SEQUENCE && !thisPost->nextEveryStatePre && st->lastArrivalTime > 0)
+            return false;
+        if (waitingTime == -1) {
+            if (!thisPost->nextEveryStatePre) return !se->se[stateId];  // not received by the absent processor
+            if (st->lastArrivalTime > 0) {                                // every
+                st->lastArrivalTime = 0;
+                init();
+                return false;
+            }
+            return true;
+        }
+        return (bool)se->se[stateId];
+    }
+};
+
+void LogicalPost::processSE(StEv se, Chunk& c) {  // LogicalPostStateProcessor.java:59-87
+    if (type == sql::LogicalType::AND) {
+        const bool proceed = partnerPre->isAbsent() ? static_cast<AbsentLogicalPre*>(partnerPre)->partnerCanProceed(se.get())
+                                                    : se->se[partnerPre->stateId] != nullptr;
+        if (proceed) Post::processSE(se, c);
+        else thisPre->stateChanged();
+    } else {
+        Post::processSE(se, c);
+        if (partnerPost->nextProcessor && thisPre->thisLast == partnerPost) partnerPost->isEventReturned = true;
+    }
+}
+
+struct AbsentLogicalPost : LogicalPost {  // AbsentLogicalPostStateProcessor.java:37-49
+    void processSE(StEv se, Chunk&) override {
+        thisPre->stateChanged();
+        StreamEvent* s = se->se[stateId].get();
+        isEventReturned = true;
+        thisPre->updateLastArrivalTime(s->ts);
+    }
+};
 
 // ------------------------------------------------------------------------------------------------
 // selector + outputs
@@ -1598,7 +1807,7 @@ void Engine::fireTimer(Scheduler* s, int64_t t, const SSP&) { s->target->process
 void Scheduler::sendTimerEvents(const SSP& s) {
     while (!s->queue.empty() && s->queue.front() - eng->currentTime() <= 0) {
         int64_t t = s->queue.front();
-        s->queue.pop_front();
+        popHead(s);
         eng->fireTimer(this, t, s);
     }
 }
@@ -1613,6 +1822,7 @@ void Scheduler::onTimeChange(int64_t now) {
         }
         return;
     }
+    if (heads.empty() || *heads.begin() > now) return;  // nothing due: the walk below would fire nothing
     // getAllStates (activeUseCount++ on all), TreeMultimap<Long, SchedulerState> with compareTo()==0
     std::vector<SSP> all;
     map.for_each([&](const std::string&, SSP& s) { all.push_back(s); });
@@ -1900,6 +2110,7 @@ struct Builder {
             }
             pre->stateId = stateIndex;
             pre->isStartState = isStart;
+            pre->nattrs = (int)def->attrs.size();
             pre->nextProcessor = chainHead;  // setNextProcessor(singleStreamRuntime.getProcessorChain())
             if (!post) {
                 post = el->kind == StateKind::ABSENT ? (Post*)own(new AbsentPost()) : own(new Post());
@@ -1944,10 +2155,23 @@ struct Builder {
             return in;
         }
         if (el->kind == StateKind::LOGICAL) {
-            if (el->kids[0]->kind == StateKind::ABSENT || el->kids[1]->kind == StateKind::ABSENT)
-                throw OracleError("unsupported: absent inside a logical state (AbsentLogicalPreStateProcessor)");
-            auto* p1 = own(new LogicalPre());
-            auto* p2 = own(new LogicalPre());
+            // StateInputStreamParser.parse :289-378: an absent element becomes an AbsentLogicalPreStateProcessor
+            // with its own scheduler (element 1's created first), registered as a startup processor
+            auto mkPre = [&](const sql::StateP& kid) -> LogicalPre* {
+                if (kid->kind != StateKind::ABSENT) return own(new LogicalPre());
+                auto* ap = own(new AbsentLogicalPre());
+                ap->waitingTime = kid->waiting_ms;
+                q.startupPre.push_back(ap);
+                auto* sch = new Scheduler();
+                sch->eng = &rt.eng;
+                sch->target = ap;
+                sch->partitioned = partitioned;
+                rt.eng.schedulers.push_back(sch);
+                ap->scheduler = sch;
+                return ap;
+            };
+            LogicalPre* p1 = mkPre(el->kids[0]);
+            LogicalPre* p2 = mkPre(el->kids[1]);
             for (LogicalPre* p : {p1, p2}) {
                 p->kind = PreKind::LOGICAL;
                 p->logicalType = el->logical;
@@ -1956,8 +2180,8 @@ struct Builder {
                 p->holder.ctx = &rt.eng.ctx;
                 p->holder.partitioned = partitioned;
             }
-            auto* o1 = own(new LogicalPost());
-            auto* o2 = own(new LogicalPost());
+            LogicalPost* o1 = el->kids[0]->kind == StateKind::ABSENT ? own(new AbsentLogicalPost()) : own(new LogicalPost());
+            LogicalPost* o2 = el->kids[1]->kind == StateKind::ABSENT ? own(new AbsentLogicalPost()) : own(new LogicalPost());
             o1->type = o2->type = el->logical;
             o1->partnerPre = p2;
             o2->partnerPre = p1;
