@@ -120,6 +120,8 @@ class QC {
     };
     std::vector<Inner> inner_;
     std::vector<int> startup_;
+    std::vector<int> sched_;                                    // scheduler -> state id (creation order)
+    std::map<const sql::StateElement*, int> pending_sched_;     // absent logical side -> its scheduler
     int mk_inner(int kind, int a, int b, int first) {
         Inner in;
         in.kind = kind;
@@ -172,6 +174,8 @@ class QC {
         put(&p.n_update, p.update_seq, v);
         put(&p.n_expire, p.expire_seq, h_.expire_order);
         put(&p.n_startup, p.startup_seq, startup_);
+        put(&p.n_sched, p.sched_state, sched_);
+        p.playback = app_.playback;
         std::vector<std::vector<int>> per(h_.streams.size());
         tree_setup(root, per);
         for (size_t i = 0; i < per.size(); ++i) {
@@ -434,10 +438,21 @@ class QC {
                 int sid = (int)meta_.defs.size() - 1;
                 uint8_t kind = el->kind == StateKind::ABSENT ? PK_ABSENT : PK_STREAM;
                 if (kind_override >= 0) kind = (uint8_t)kind_override;
-                if (el->kind == StateKind::ABSENT && kind_override >= 0)
-                    throw CompileError(SDG_ERR_UNSUPPORTED, "absent states inside logical/count are not supported on device");
+                if (el->kind == StateKind::ABSENT && kind_override == PK_COUNT)
+                    throw CompileError(SDG_ERR_UNSUPPORTED, "a count quantifier on an absent state is not supported");
                 StateRow& r = newrow(kind, *el, is_start);
                 r.logical_or = (uint8_t)(logical_or > 0);
+                r.sched = -1;
+                if (el->kind == StateKind::ABSENT) {
+                    if (kind == PK_LOGICAL) {
+                        // AbsentLogicalPreStateProcessor: scheduler created by the logical node (pending_sched_)
+                        r.absent = 1;
+                        r.sched = (int8_t)pending_sched_.at(el.get());
+                    } else {  // AbsentStreamPreStateProcessor: scheduler created here (:181-196)
+                        r.sched = (int8_t)sched_.size();
+                        sched_.push_back(sid);
+                    }
+                }
                 // filters: FilterProcessor per [..], CURRENT default index
                 Prog pr;
                 pr.start = (int)h_.code.size();
@@ -449,6 +464,7 @@ class QC {
                 rows_[sid].filter = pr;
                 pre_list.push_back(sid);
                 if (kind == PK_ABSENT) startup_.push_back(sid);
+                if (r.absent) sched_[r.sched] = sid;
                 Sub s;
                 s.first = s.last = sid;
                 s.node = mk_inner(0, -1, -1, sid);
@@ -475,10 +491,21 @@ class QC {
             }
             case StateKind::LOGICAL: {
                 bool orr = el->logical == sql::LogicalType::OR;
-                if (el->kids[0]->kind == StateKind::ABSENT || el->kids[1]->kind == StateKind::ABSENT)
-                    throw CompileError(SDG_ERR_UNSUPPORTED, "absent inside a logical state is not supported on device yet");
+                // StateInputStreamParser :289-378: each absent side gets an AbsentLogicalPreStateProcessor whose
+                // scheduler is created here, element 1's first, and joins the startup processors in that order;
+                // its state id is assigned when the side is parsed (element 2 first)
+                for (int k = 0; k < 2; ++k) {
+                    if (el->kids[k]->kind != StateKind::ABSENT) continue;
+                    pending_sched_[el->kids[k].get()] = (int)sched_.size();
+                    sched_.push_back(-1);
+                }
+                const size_t startup_at = startup_.size();
                 Sub s2 = parse(el->kids[1], PK_LOGICAL, orr, multi, pre_list, is_start);
                 Sub s1 = parse(el->kids[0], PK_LOGICAL, orr, multi, pre_list, is_start);
+                std::vector<int> side_startup;  // element 1 before element 2
+                if (el->kids[0]->kind == StateKind::ABSENT) side_startup.push_back(s1.first);
+                if (el->kids[1]->kind == StateKind::ABSENT) side_startup.push_back(s2.first);
+                startup_.insert(startup_.begin() + (long)startup_at, side_startup.begin(), side_startup.end());
                 rows_[s1.first].partner = s2.first;
                 rows_[s2.first].partner = s1.first;
                 Sub s;

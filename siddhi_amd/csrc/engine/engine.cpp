@@ -84,37 +84,6 @@ int width_of(uint8_t kind) {
     }
 }
 
-// Java toString of a partition value (ValuePartitionExecutor.execute) -- Float/Double use the Java layout
-std::string java_real(double x, bool is_float) {
-    if (x != x) return "NaN";
-    if (std::isinf(x)) return x > 0 ? "Infinity" : "-Infinity";
-    if (x == 0) return std::signbit(x) ? "-0.0" : "0.0";
-    char buf[64];
-    for (int prec = 1; prec <= 17; ++prec) {
-        std::snprintf(buf, sizeof buf, "%.*e", prec - 1, x);
-        if (is_float ? (std::strtof(buf, nullptr) == (float)x) : (std::strtod(buf, nullptr) == x)) break;
-    }
-    std::string s(buf);
-    bool neg = s[0] == '-';
-    if (neg) s = s.substr(1);
-    size_t ep = s.find('e');
-    int e10 = std::atoi(s.c_str() + ep + 1);
-    std::string d;
-    for (size_t i = 0; i < ep; ++i) if (s[i] != '.') d += s[i];
-    while (d.size() > 1 && d.back() == '0') d.pop_back();
-    std::string o;
-    double ax = std::fabs(x);
-    if (ax >= 1e-3 && ax < 1e7) {
-        int pt = e10 + 1;
-        if (pt <= 0) o = "0." + std::string(-pt, '0') + d;
-        else if ((int)d.size() <= pt) o = d + std::string(pt - d.size(), '0') + ".0";
-        else o = d.substr(0, pt) + "." + d.substr(pt);
-    } else {
-        o = d.substr(0, 1) + "." + (d.size() > 1 ? d.substr(1) : "0") + "E" + std::to_string(e10);
-    }
-    return neg ? "-" + o : o;
-}
-
 struct PushChunk {
     int stream;
     int64_t n;
@@ -283,8 +252,8 @@ bool host_key(sdg_engine* e, QueryRt& q, int qpos, const PushChunk& c, int64_t r
     switch (kind) {
         case VK_I32: s = std::to_string(((const int32_t*)col)[row]); break;
         case VK_I64: s = std::to_string(((const int64_t*)col)[row]); break;
-        case VK_F32: s = java_real(((const float*)col)[row], true); break;
-        case VK_F64: s = java_real(((const double*)col)[row], false); break;
+        case VK_F32: s = java_real_string(((const float*)col)[row], true); break;
+        case VK_F64: s = java_real_string(((const double*)col)[row], false); break;
         case VK_BOOL: s = col[row] ? "true" : "false"; break;
         default: s = e->strings.strs[((const uint32_t*)col)[row]]; break;
     }

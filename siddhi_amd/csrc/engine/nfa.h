@@ -8,11 +8,25 @@
 //   CountPreStateProcessor.java       processAndReturn :53-95, addState :97-125, startStateReset :168-181,
 //                                     updateState :183-193;  CountPostStateProcessor.java :39-89
 //   LogicalPreStateProcessor.java     :43-178;  LogicalPostStateProcessor.java :59-87
+//   AbsentStreamPreStateProcessor     addState :80-103, addEveryState :105-124, resetState :126-148,
+//     .java                           process (TIMER) :151-227, sendEvent :238-254, processAndReturn :257-274,
+//                                     partitionCreated :291-308;  AbsentStreamPostStateProcessor.java :36-56
+//   AbsentLogicalPreStateProcessor    addState :77-97, addEveryState :99-118, process (TIMER) :121-209,
+//     .java                           sendEvent :230-250, processAndReturn :262-319, partitionCreated :331-351,
+//                                     partnerCanProceed :353-388;  AbsentLogicalPostStateProcessor.java :37-49
+//   Scheduler.java                    notifyAt :113-127 (per-key FIFO of notify times), sendTimerEvents :171-209
 //   receivers                         state/receiver/*.java (stabilizeStates), MultiProcessStreamReceiver.java
 // Object identity is kept: StateEvents and StreamEvent nodes are arena objects referenced by index, so clones
 // share StreamEvent chains exactly as StateEventCloner does (count-state aliasing, CountPatternTestCase :53-111).
 // Memory is reclaimed by a mark-sweep pass over the lists at event boundaries; running out of arena space sets
 // the key's overflow flag (reported as SDG_ERR_CAPACITY, never a silent drop).
+//
+// Timers (absent states). Each absent processor has a Scheduler; a key's notify times for it are a FIFO in the
+// arena. Which key fires at which batch position is decided by the reference's global scheduler (all keys, one
+// TreeMultimap per clock advance, Scheduler.java:71-103). A key run either derives its fires itself ("ideal"
+// mode: a due head fires at the first clock advance that reaches it -- exact for a single key, and for keys whose
+// due times never coincide with another key's) or replays an explicit fire list computed by the host scheduler
+// simulation (sched.h) from the fire/notify log every run writes. The engine iterates the two to a fixpoint.
 #pragma once
 #include <stdint.h>
 
@@ -28,8 +42,8 @@ enum : uint8_t { T_CURRENT = 0, T_EXPIRED = 1 };
 constexpr int16_t NIL = -1;
 
 struct Layout {
-    int32_t ns, nn, nr, lcap, n_states, n_cols;
-    int64_t off_ps, off_pend, off_newe, off_ret, off_se, off_nd, off_rc, bytes;
+    int32_t ns, nn, nr, lcap, n_states, n_cols, n_sched, qcap;
+    int64_t off_ps, off_pend, off_newe, off_ret, off_tq, off_tqt, off_se, off_nd, off_rc, bytes;
     int32_t se_bytes, rc_bytes;
 };
 
@@ -37,14 +51,57 @@ struct KHead {
     int32_t flags;       // bit0 overflow, bit1 key initialised
     int32_t se_free, nd_free, rc_free;
     int32_t se_used, nd_used, rc_used;
+    uint32_t kseq;       // scheduler log records written by this key in the current run
+    int32_t screate;     // scheduler states created by this key (creation order, live-mode tie break)
     int32_t pad;
 };
 
 struct PState {
     uint8_t changed, initialized, success, start_reset, active, started, returned, pad;
-    int64_t last_sched;
+    int64_t last_sched;    // AbsentStreamPreState.lastScheduledTime
     int16_t pn, nw;
     int16_t pad2[2];
+    int64_t last_arrival;  // AbsentLogicalPreStateProcessor.LogicalStreamPreState.lastArrivalTime
+};
+
+// one scheduler's notify-time FIFO of one key (Scheduler.SchedulerState.toNotifyQueue)
+struct TQ {
+    int64_t earliest;  // first batch position at which the current head may fire (ideal mode)
+    int32_t created;   // KHead::screate when this scheduler state was (re)created
+    int16_t h, n;
+};
+
+// scheduler log (device -> host scheduler simulation): every fire a key run performs and every notify time it
+// pushes, in the key's order (kseq)
+enum : uint8_t { LOG_PUSH = 0, LOG_FIRE = 1, LOG_POP = 2 };
+constexpr uint8_t ORIGIN_EVENT = 0xFF;
+struct SchedLog {
+    uint32_t key;
+    uint32_t kseq;
+    uint32_t g;       // batch position: the event being processed, or where the fire happened
+    uint8_t type;     // LOG_PUSH / LOG_FIRE / LOG_POP (a fire dequeued t)
+    uint8_t sched;    // PUSH: scheduler the time went to; FIRE / POP: scheduler that fired
+    uint8_t origin;   // PUSH: ORIGIN_EVENT (processing the event at g, incl. partitionCreated) or the scheduler
+                      //       whose fire at g pushed it
+    uint8_t pad;
+    int64_t t;        // PUSH: notify time; FIRE: the clock the fire ran with
+};
+// explicit fire (host -> device): scheduler `sched` of this key fires at position g with currentTime() = clock
+struct TimerFire {
+    uint32_t g;
+    int32_t sched;
+    int64_t clock;
+};
+// per-run timer inputs
+struct TimerIn {
+    int64_t G;                    // batch positions: every pushed event (all streams) + advance_time points
+    const int64_t* clk;           // [G] currentTime() at position g (after its clock advance)
+    const uint32_t* nadv;         // [G + 1] first clock-advance position >= g (G: none)
+    int64_t clock0;               // currentTime() before position 0
+    int32_t live;                 // wall-clock mode: fires in (time, creation) order, the fire's clock = its time
+    SchedLog* log;                // nullptr: no scheduler in this query
+    unsigned long long* log_count;
+    int64_t log_cap;
 };
 
 struct SE {
@@ -68,7 +125,7 @@ struct Rec {
     // int64_t vals[n_cols] follows
 };
 
-inline Layout make_layout(int n_states, int n_cols, int ns) {
+inline Layout make_layout(int n_states, int n_cols, int ns, int n_sched = 0) {
     Layout L;
     L.ns = ns;
     L.nn = ns * 4;
@@ -76,6 +133,8 @@ inline Layout make_layout(int n_states, int n_cols, int ns) {
     L.lcap = ns;
     L.n_states = n_states;
     L.n_cols = n_cols;
+    L.n_sched = n_sched;
+    L.qcap = n_sched ? ns : 0;
     L.se_bytes = (int32_t)((sizeof(SE) + 2 * n_states + 7) & ~7);
     L.rc_bytes = (int32_t)(sizeof(Rec) + 8 * n_cols);
     int64_t o = sizeof(KHead);
@@ -88,6 +147,10 @@ inline Layout make_layout(int n_states, int n_cols, int ns) {
     L.off_ret = o;  // StateEvents one processAndReturn call returns (emitted after its loop)
     o += (int64_t)2 * L.lcap;
     o = (o + 7) & ~7;
+    L.off_tq = o;
+    o += (int64_t)sizeof(TQ) * n_sched;
+    L.off_tqt = o;
+    o += (int64_t)8 * L.qcap * n_sched;
     L.off_se = o;
     o += (int64_t)L.se_bytes * L.ns;
     L.off_nd = o;
@@ -98,11 +161,6 @@ inline Layout make_layout(int n_states, int n_cols, int ns) {
     L.bytes = (o + 127) & ~127;
     return L;
 }
-
-// one emitted match
-struct Emit {
-    int16_t se;
-};
 
 struct Ctx;
 
@@ -133,8 +191,16 @@ struct Ctx {
     int64_t emit_cap;
     int* flags;
     uint32_t key;
+    int64_t seq_base;   // sequence number of batch position 0
     int64_t cur_seq;
     int64_t cur_sub;
+    // timers
+    TimerIn T;
+    const TimerFire* fires;  // explicit fire list of this key (nullptr: ideal mode)
+    int32_t nfires, fi;
+    int64_t clock;           // currentTime()
+    int64_t pos;             // batch position being processed (-1: before position 0)
+    int32_t fsched;          // scheduler whose fire is running (-1: event processing)
 
     // ---- arena access ------------------------------------------------------------------------------------
     SDG_HD KHead& head() { return *(KHead*)base; }
@@ -145,6 +211,8 @@ struct Ctx {
     SDG_HD int16_t* slots(int i) { return (int16_t*)((uint8_t*)&se(i) + sizeof(SE)); }
     SDG_HD Node& nd(int i) { return ((Node*)(base + L.off_nd))[i]; }
     SDG_HD Rec& rc(int i) { return *(Rec*)(base + L.off_rc + (int64_t)i * L.rc_bytes); }
+    SDG_HD TQ& tq(int s) { return ((TQ*)(base + L.off_tq))[s]; }
+    SDG_HD int64_t* tqt(int s) { return (int64_t*)(base + L.off_tqt) + (int64_t)s * L.qcap; }
     SDG_HD int64_t* vals(int i) { return (int64_t*)((uint8_t*)&rc(i) + sizeof(Rec)); }
     SDG_HD bool ovf() { return head().flags & 1; }
     SDG_HD void set_ovf() { head().flags |= 1; }
@@ -159,12 +227,20 @@ struct Ctx {
         h.se_free = 0;
         h.nd_free = 0;
         h.rc_free = 0;
+        h.kseq = 0;
+        h.screate = 0;
         for (int p = 0; p < L.n_states; ++p) {
             PState& s = ps(p);
             s.changed = s.initialized = s.success = s.start_reset = s.started = s.returned = 0;
             s.active = 1;
             s.last_sched = 0;
+            s.last_arrival = 0;
             s.pn = s.nw = 0;
+        }
+        for (int q = 0; q < L.n_sched; ++q) {
+            tq(q).h = tq(q).n = 0;
+            tq(q).created = 0;
+            tq(q).earliest = 0;
         }
     }
 
@@ -297,6 +373,72 @@ struct Ctx {
         slots(s)[pos] = NIL;
     }
 
+    // ---- scheduler ---------------------------------------------------------------------------------------
+    SDG_HD bool is_absent(int p) const {  // instanceof AbsentPreStateProcessor
+        return P->st[p].kind == PK_ABSENT || (P->st[p].kind == PK_LOGICAL && P->st[p].absent);
+    }
+    SDG_HD void log_rec(uint8_t type, int sch, uint8_t origin, int64_t t) {
+        if (!T.log) return;
+        const unsigned long long i = __atomic_fetch_add(T.log_count, 1ull, __ATOMIC_RELAXED);
+        const uint32_t kseq = head().kseq++;
+        if ((int64_t)i >= T.log_cap) {  // counted: the host grows the log and reruns
+            __atomic_fetch_or(flags + 5, 1, __ATOMIC_RELAXED);
+            return;
+        }
+        SchedLog& r = T.log[i];
+        r.key = key;
+        r.kseq = kseq;
+        r.g = (uint32_t)pos;
+        r.type = type;
+        r.sched = (uint8_t)sch;
+        r.origin = origin;
+        r.pad = 0;
+        r.t = t;
+    }
+    // Scheduler.notifyAt :113-127 for this key (SchedulerState created on demand: computeIfAbsent)
+    SDG_HD void notify_at(int sch, int64_t t) {
+        TQ& q = tq(sch);
+        if (q.n >= L.qcap) { set_ovf(); return; }
+        if (q.n == 0) {
+            q.created = ++head().screate;
+            q.h = 0;
+            // a head pushed by a fire can still fire at this position in a scheduler whose TimeChangeListener
+            // runs later (playback) / in the same live advance; one pushed while processing an event, only at
+            // the next clock advance
+            q.earliest = (fsched >= 0 && (T.live || sch > fsched)) ? pos : pos + 1;
+        }
+        tqt(sch)[(q.h + q.n) % L.qcap] = t;
+        q.n++;
+        log_rec(LOG_PUSH, sch, fsched >= 0 ? (uint8_t)fsched : ORIGIN_EVENT, t);
+    }
+    SDG_HD int64_t tq_pop(int sch) {
+        TQ& q = tq(sch);
+        const int64_t t = tqt(sch)[q.h];
+        q.h = (int16_t)((q.h + 1) % L.qcap);
+        q.n--;
+        return t;
+    }
+    // StreamEventFactory.newInstance(): timestamp -1, every attribute null
+    SDG_HD int16_t empty_node() {
+        int16_t r = rc_alloc();
+        if (r == NIL) return NIL;
+        rc(r).ts = -1;
+        rc(r).nullmask = 0xFFFFFFFFu;
+        for (int c = 0; c < L.n_cols; ++c) vals(r)[c] = 0;
+        return nd_alloc(r);
+    }
+    // an AbsentStreamPreState that is empty and not initialised is destroyed when its holder returns it
+    // (PartitionStateHolder.returnState): its lastScheduledTime restarts from 0. Only that field of a destroyed
+    // state is ever read again (start states are initialised, so never destroyed), so it is the one reset here,
+    // at the end of each event / fire (every getState/returnState scope of the reference has ended by then)
+    SDG_HD void absent_gc() {
+        for (int i = 0; i < P->n_sched; ++i) {
+            const int p = P->sched_state[i];
+            const StateRow& r = P->st[p];
+            if (r.kind == PK_ABSENT && !r.is_start && ps(p).pn == 0 && ps(p).nw == 0) ps(p).last_sched = 0;
+        }
+    }
+
     // ---- list helpers ------------------------------------------------------------------------------------
     SDG_HD void push(int16_t* lst, int16_t& n, int16_t v) {
         if (n >= L.lcap) { set_ovf(); return; }
@@ -338,6 +480,7 @@ struct Ctx {
     }
 
     SDG_HD void emit(int16_t s) {  // QuerySelector.processNoGroupBy for one StateEvent (insert current events)
+        // (timer emissions: cur_seq = the position of the fire, cur_sub negative -- before that event's own)
         if (se(s).type != T_CURRENT) return;
         unsigned long long slot = __atomic_fetch_add(emit_count, 1ull, __ATOMIC_RELAXED);
         if ((int64_t)slot >= emit_cap) {
@@ -384,6 +527,7 @@ struct Ctx {
             const StateRow& r = P->st[p];
             PState& st = ps(p);
             if (r.kind == PK_LOGICAL) {  // LogicalPreStateProcessor.addState :43-62
+                if (r.absent && !st.active) return;  // AbsentLogicalPreStateProcessor.addState :77-97
                 int q = r.partner;
                 if (r.is_start || r.seq) {
                     if (st.nw == 0) push(newe(p), st.nw, s);
@@ -391,6 +535,21 @@ struct Ctx {
                 } else {
                     push(newe(p), st.nw, s);
                     push(newe(q), ps(q).nw, s);
+                }
+                if (r.absent && !r.is_start && r.waiting_ms != -1) {
+                    notify_at(r.sched, se(s).ts + r.waiting_ms);
+                    const StateRow& pr = P->st[q];
+                    if (pr.kind == PK_LOGICAL && pr.absent) notify_at(pr.sched, se(s).ts + pr.waiting_ms);
+                }
+                return;
+            }
+            if (r.kind == PK_ABSENT) {  // AbsentStreamPreStateProcessor.addState :80-103
+                if (!st.active) return;
+                if (r.seq) st.nw = 0;
+                push(newe(p), st.nw, s);
+                if (!r.is_start) {
+                    st.last_sched = se(s).ts + r.waiting_ms;
+                    notify_at(r.sched, st.last_sched);
                 }
                 return;
             }
@@ -416,18 +575,30 @@ struct Ctx {
         int16_t c = clone(s);
         if (c == NIL) return;
         se(c).type = T_CURRENT;
+        if (r.kind == PK_LOGICAL && r.absent) {  // AbsentLogicalPreStateProcessor.addEveryState :99-118
+            if (slots(c)[p] != NIL) se(c).ts = rc(nd(slots(c)[p]).rec).ts;  // the last arrived event's time
+            slots(c)[p] = NIL;
+            slots(c)[r.partner] = NIL;
+            push(newe(p), ps(p).nw, c);
+            push(newe(r.partner), ps(r.partner).nw, c);
+            return;
+        }
         for (int i = p; i < L.n_states; ++i) slots(c)[i] = NIL;
         push(newe(p), ps(p).nw, c);
         if (r.kind == PK_LOGICAL) {  // :65-84
             slots(c)[r.partner] = NIL;
             push(newe(r.partner), ps(r.partner).nw, c);
         }
+        if (r.kind == PK_ABSENT) {  // AbsentStreamPreStateProcessor.addEveryState :105-124
+            ps(p).last_sched = se(s).ts + r.waiting_ms;
+            notify_at(r.sched, ps(p).last_sched);
+        }
     }
 
     SDG_HD void init(int p) {  // StreamPreStateProcessor.init :178-194
         const StateRow& r = P->st[p];
         PState& st = ps(p);
-        if (r.is_start && (!st.initialized || r.next_every >= 0)) {
+        if (r.is_start && (!st.initialized || r.next_every >= 0 || (r.seq && r.next >= 0 && is_absent(r.next)))) {
             int16_t s = se_alloc();
             if (s == NIL) return;
             add_state(p, s);
@@ -447,6 +618,14 @@ struct Ctx {
                     if (r.seq && r.next_every < 0 && r.next >= 0 && ps(r.next).pn != 0) return;
                     init(p);
                 }
+            }
+            return;
+        }
+        if (r.kind == PK_ABSENT) {  // AbsentStreamPreStateProcessor.resetState :126-148
+            st.pn = 0;
+            if (r.is_start) {
+                if (r.seq && r.next_every < 0 && r.next >= 0 && ps(r.next).pn != 0) return;
+                init(p);
             }
             return;
         }
@@ -536,10 +715,44 @@ struct Ctx {
             if (n == r.max_count) ps(p).changed = 1;
         }
     }
+    SDG_HD bool partner_can_proceed(int q, int16_t s) {  // AbsentLogicalPreStateProcessor.partnerCanProceed :353-388
+        const StateRow& r = P->st[q];
+        PState& st = ps(q);
+        if (r.seq && r.next_every < 0 && st.last_arrival > 0) return false;
+        if (r.waiting_ms == -1) {
+            if (r.next_every < 0) return slots(s)[q] == NIL;  // not received by the absent processor
+            if (st.last_arrival > 0) {                          // every
+                st.last_arrival = 0;
+                init(q);
+                return false;
+            }
+            return true;
+        }
+        return slots(s)[q] != NIL;
+    }
+    SDG_HD void post_absent(int p, int16_t s) {  // AbsentStreamPostStateProcessor.process :36-56
+        const StateRow& r = P->st[p];
+        ps(p).changed = 1;
+        const int64_t ts = rc(nd(slots(s)[p]).rec).ts;
+        se(s).ts = ts;
+        ps(p).returned = 1;
+        if (r.is_start && r.next_every == p) add_every_state(p, s);
+        ps(p).last_sched = ts + r.waiting_ms;  // updateLastArrivalTime :68-78
+        notify_at(r.sched, ps(p).last_sched);
+    }
     SDG_HD void post_logical(int p, int16_t s) {  // LogicalPostStateProcessor.process :59-87
         const StateRow& r = P->st[p];
+        if (r.absent) {  // AbsentLogicalPostStateProcessor.process :37-49
+            ps(p).changed = 1;
+            ps(p).returned = 1;
+            ps(p).last_arrival = rc(nd(slots(s)[p]).rec).ts;  // updateLastArrivalTime
+            return;
+        }
         if (!r.logical_or) {
-            if (slots(s)[r.partner] != NIL) post_stream(p, s);
+            const StateRow& pr = P->st[r.partner];
+            const bool proceed = (pr.kind == PK_LOGICAL && pr.absent) ? partner_can_proceed(r.partner, s)
+                                                                       : slots(s)[r.partner] != NIL;
+            if (proceed) post_stream(p, s);
             else ps(p).changed = 1;
         } else {
             post_stream(p, s);
@@ -550,6 +763,7 @@ struct Ctx {
         switch (P->st[p].kind) {
             case PK_COUNT: post_count(p, s); break;
             case PK_LOGICAL: post_logical(p, s); break;
+            case PK_ABSENT: post_absent(p, s); break;
             default: post_stream(p, s); break;
         }
     }
@@ -562,9 +776,63 @@ struct Ctx {
 
     // processAndReturn; the receiver hands the returned StateEvents to the selector after the loop
     // (StateMultiProcessStreamReceiver.processAndClear :47-68), so they are collected first
+    // AbsentLogicalPreStateProcessor.processAndReturn :262-319: a matching event removes the absence candidate; it
+    // never returns a match itself
+    SDG_HD void alogic_process_and_return(int p, int16_t rec) {
+        const StateRow& r = P->st[p];
+        PState& st = ps(p);
+        if (!st.active) return;
+        int16_t* pd = pend(p);
+        for (int j = 0; j < st.pn;) {
+            if (ovf()) return;
+            const int16_t s = pd[j];
+            if (r.logical_or && slots(s)[r.partner] != NIL) {
+                erase(pd, st.pn, j);
+                continue;
+            }
+            const int16_t cur = slots(s)[p];
+            const int16_t n = nd_alloc(rec);
+            if (n == NIL) return;
+            slots(s)[p] = n;
+            process_se(p, s);
+            if (r.waiting_ms != -1 || (r.seq && !r.logical_or && r.next_every >= 0)) slots(s)[p] = cur;
+            bool removed = false;
+            if (ps(r.last).returned) {  // passed the filter: no longer an absence candidate
+                ps(r.last).returned = 0;
+                erase(pd, st.pn, j);
+                removed = true;
+                if (r.seq) {  // partner's pending list .remove(stateEvent): first occurrence
+                    PState& qs = ps(r.partner);
+                    int16_t* qp = pend(r.partner);
+                    for (int i = 0; i < qs.pn; ++i)
+                        if (qp[i] == s) { erase(qp, qs.pn, i); break; }
+                }
+            }
+            if (!st.changed) {
+                slots(s)[p] = cur;
+                if (r.seq) {
+                    if (removed) { set_ovf(); return; }  // the reference would throw (iterator.remove twice)
+                    erase(pd, st.pn, j);
+                    removed = true;
+                }
+            }
+            if (!removed) ++j;
+        }
+    }
+
     SDG_HD void process_and_return(int p, int16_t rec, bool selector) {
         const StateRow& r = P->st[p];
         PState& st = ps(p);
+        if (r.kind == PK_LOGICAL && r.absent) {
+            alogic_process_and_return(p, rec);
+            return;
+        }
+        // AbsentStreamPreStateProcessor.processAndReturn :257-274: inactive -> nothing; otherwise the stream loop,
+        // whose returned events are discarded (an arriving event only cancels absence candidates)
+        if (r.kind == PK_ABSENT) {
+            if (!st.active) return;
+            selector = false;
+        }
         int16_t* pd = pend(p);
         const int last = r.last;
         int16_t* ret = (int16_t*)(base + L.off_ret);
@@ -616,9 +884,11 @@ struct Ctx {
                 }
             } else if (!st.changed) {
                 slots(s)[p] = NIL;
-                if (r.seq) {  // SEQUENCE: no state change -> dropped (removeOnNoStateChange)
-                    erase(pd, st.pn, j);
-                    erased = true;
+                if (r.seq) {  // SEQUENCE: no state change -> dropped (removeOnNoStateChange; false for absent)
+                    if (r.kind != PK_ABSENT) {
+                        erase(pd, st.pn, j);
+                        erased = true;
+                    }
                     if (r.kind != PK_LOGICAL && P->st[p].callback >= 0) start_state_reset(P->st[p].callback);
                 }
             }
@@ -628,9 +898,231 @@ struct Ctx {
             for (int i = 0; i < nret; ++i) emit(ret[i]);
     }
 
+    // ---- timers ------------------------------------------------------------------------------------------
+    // AbsentStreamPreStateProcessor.sendEvent :238-254
+    SDG_HD void absent_send(int p, int16_t s) {
+        const StateRow& r = P->st[p];
+        if (r.selector_after) emit(s);
+        if (r.next >= 0) add_state(r.next, s);
+        if (r.next_every >= 0) add_every_state(r.next_every, s);
+        else if (r.is_start) ps(p).active = 0;
+        if (r.callback >= 0) start_state_reset(r.callback);
+    }
+    // AbsentStreamPreStateProcessor.process(ComplexEventChunk) :151-227 for one TIMER event at time `now`
+    SDG_HD void absent_timer(int p, int64_t now) {
+        const StateRow& r = P->st[p];
+        PState& st = ps(p);
+        if (!st.active) return;
+        bool initialize = r.is_start && st.nw == 0 && st.pn == 0;
+        if (initialize && r.seq && r.next_every < 0 && st.last_sched > 0) initialize = false;
+        if (initialize) {
+            const int16_t s = se_alloc();
+            if (s == NIL) return;
+            add_state(p, s);
+        } else if (r.seq && st.nw != 0) {
+            reset_state(p);
+        }
+        update_state(p);
+        int16_t* pd = pend(p);
+        int16_t* ret = (int16_t*)(base + L.off_ret);
+        int nret = 0;
+        for (int j = 0; j < st.pn;) {
+            const int16_t s = pd[j];
+            if (is_expired(s, now)) {
+                erase(pd, st.pn, j);
+                if (r.within_every >= 0 && r.next_every != p) {
+                    if (r.next_every < 0) { set_ovf(); return; }  // the reference: NullPointerException
+                    add_every_state(r.next_every, s);
+                }
+                continue;
+            }
+            const int64_t ts = se(s).ts;
+            if ((ts == -1 && now >= st.last_sched) || (ts != -1 && now >= ts + r.waiting_ms)) {
+                erase(pd, st.pn, j);
+                se(s).ts = now;
+                if (nret >= L.lcap) { set_ovf(); return; }
+                ret[nret++] = s;
+                continue;
+            }
+            ++j;
+        }
+        if (r.within_every >= 0) update_state(r.within_every);
+        const bool not_processed = nret == 0;
+        for (int i = 0; i < nret && !ovf(); ++i) absent_send(p, ret[i]);
+        if (clock > r.waiting_ms + now) st.last_sched = clock + r.waiting_ms;
+        if (not_processed && st.last_sched < now) {
+            st.last_sched = now + r.waiting_ms;
+            notify_at(r.sched, st.last_sched);
+        }
+    }
+    // AbsentLogicalPreStateProcessor.sendEvent :230-250
+    SDG_HD void alogic_send(int p, int16_t s) {
+        const StateRow& r = P->st[p];
+        if (r.selector_after) emit(s);
+        if (r.next >= 0) add_state(r.next, s);
+        if (r.next_every >= 0) {
+            add_every_state(r.next_every, s);
+        } else if (r.is_start) {
+            ps(p).active = 0;
+            if (r.logical_or && is_absent(r.partner)) ps(r.partner).active = 0;
+        }
+        if (r.callback >= 0) start_state_reset(r.callback);
+    }
+    // AbsentLogicalPreStateProcessor.process(ComplexEventChunk) :121-209 for one TIMER event at time `now`
+    SDG_HD void alogic_timer(int p, int64_t now) {
+        const StateRow& r = P->st[p];
+        PState& st = ps(p);
+        if (!st.active) return;
+        bool not_processed = true;
+        if (now >= st.last_arrival + r.waiting_ms) {
+            if (r.is_start && r.seq && st.nw == 0 && st.pn == 0) {
+                const int16_t s = se_alloc();
+                if (s == NIL) return;
+                add_state(p, s);
+            } else if (r.seq && st.nw != 0) {
+                reset_state(p);
+            }
+            update_state(p);
+            int16_t expired = NIL;
+            int16_t* pd = pend(p);
+            int16_t* ret = (int16_t*)(base + L.off_ret);
+            int nret = 0;
+            for (int j = 0; j < st.pn;) {
+                const int16_t s = pd[j];
+                if (is_expired(s, now)) {  // within
+                    expired = s;
+                    erase(pd, st.pn, j);
+                    continue;
+                }
+                const int16_t own = slots(s)[p];
+                const bool passed = own == NIL ? now >= se(s).ts + r.waiting_ms
+                                               : now >= rc(nd(own).rec).ts + r.waiting_ms;  // waitingTimePassed
+                if (passed) {
+                    erase(pd, st.pn, j);
+                    const bool partner_in = slots(s)[r.partner] != NIL;
+                    if (r.logical_or && !partner_in) {  // OR partner not received
+                        const int16_t n = empty_node();
+                        if (n == NIL) return;
+                        add_event(s, p, n);
+                        if (nret >= L.lcap) { set_ovf(); return; }
+                        ret[nret++] = s;
+                    } else if (!r.logical_or && partner_in) {  // AND partner received
+                        if (nret >= L.lcap) { set_ovf(); return; }
+                        ret[nret++] = s;
+                    } else if (!r.logical_or) {  // AND partner not received: let it proceed
+                        const int16_t n = empty_node();
+                        if (n == NIL) return;
+                        add_event(s, p, n);
+                    }
+                    continue;
+                }
+                ++j;
+            }
+            if (expired != NIL && r.within_every >= 0) {
+                add_every_state(r.within_every, expired);
+                update_state(r.within_every);
+            }
+            not_processed = nret == 0;
+            for (int i = 0; i < nret && !ovf(); ++i) {
+                se(ret[i]).ts = now;
+                alogic_send(p, ret[i]);
+            }
+            st.last_arrival = 0;
+        }
+        if (r.next_every >= 0 || (not_processed && r.is_start)) {  // schedule again
+            const int64_t nb = st.last_arrival == 0 ? clock + r.waiting_ms : st.last_arrival + r.waiting_ms;
+            notify_at(r.sched, nb);
+        }
+    }
+    // Scheduler.sendTimerEvents :171-209 for this key: every queued time <= c, in FIFO order, each one TIMER event
+    // through the EntryValve into the absent processor
+    SDG_HD void maybe_gc() {
+        const KHead& h = head();
+        if (4 * h.se_used > 3 * L.ns || 4 * h.nd_used > 3 * L.nn || 4 * h.rc_used > 3 * L.nr) gc();
+    }
+    SDG_HD void fire(int sch, int64_t g, int64_t c) {
+        maybe_gc();  // between fires nothing but the lists holds StateEvents
+        pos = g;
+        fsched = sch;
+        clock = c;
+        cur_seq = seq_base + g;
+        cur_sub = INT64_MIN | ((int64_t)sch << 48);  // before the event at g; the host ranks fires across keys
+        log_rec(LOG_FIRE, sch, 0, c);
+        const int p = P->sched_state[sch];
+        TQ& q = tq(sch);
+        while (q.n > 0 && tqt(sch)[q.h] <= c && !ovf()) {
+            const int64_t t = tq_pop(sch);
+            log_rec(LOG_POP, sch, 0, t);
+            if (P->st[p].kind == PK_ABSENT) absent_timer(p, t);
+            else alogic_timer(p, t);
+        }
+        fsched = -1;
+        absent_gc();
+    }
+    // first position >= lo whose clock reaches t and that advances the clock (G: none in this batch)
+    SDG_HD int64_t due_at(int64_t t, int64_t lo) {
+        int64_t a = 0, b = T.G;  // lower_bound(clk, t)
+        while (a < b) {
+            const int64_t m = (a + b) >> 1;
+            if (T.clk[m] < t) a = m + 1;
+            else b = m;
+        }
+        const int64_t x = a > lo ? a : lo;
+        return x >= T.G ? T.G : (int64_t)T.nadv[x];
+    }
+    // every fire of this key at positions <= limit, in the reference's order
+    SDG_HD void fire_until(int64_t limit) {
+        if (P->n_sched == 0) return;
+        if (fires) {  // explicit list (host scheduler simulation)
+            while (fi < nfires && (int64_t)fires[fi].g <= limit && !ovf()) {
+                const TimerFire f = fires[fi++];
+                fire(f.sched, f.g, f.clock);
+            }
+            return;
+        }
+        while (!ovf()) {  // ideal: each due head at the first clock advance that reaches it
+            int64_t bg = T.G;
+            int bs = -1;
+            int64_t bt = 0;
+            int32_t bc = 0;
+            for (int i = 0; i < P->n_sched; ++i) {
+                const TQ& q = tq(i);
+                if (q.n == 0) continue;
+                const int64_t h = tqt(i)[q.h];
+                const int64_t g = due_at(h, q.earliest);
+                // playback: schedulers in listener order at one position; live: (time, creation) across them
+                const bool better = g < bg || (g == bg && bs >= 0 && T.live && (h < bt || (h == bt && q.created < bc)));
+                if (better) { bg = g; bs = i; bt = h; bc = q.created; }
+            }
+            if (bs < 0 || bg > limit || bg >= T.G) return;
+            int64_t c = T.clk[bg];
+            if (T.live) {  // liveNow = max(liveNow before this advance, the due time)
+                const int64_t before = bg > 0 ? T.clk[bg - 1] : T.clock0;
+                c = bt > before ? bt : before;
+            }
+            fire(bs, bg, c);
+        }
+    }
+
     // ---- receiver ----------------------------------------------------------------------------------------
-    SDG_HD void init_key() {  // StateStreamRuntime.initPartition
+    SDG_HD void init_key() {  // StateStreamRuntime.initPartition: init, then partitionCreated of the startups
         for (int i = 0; i < P->n_init; ++i) init(P->init_seq[i]);
+        for (int i = 0; i < P->n_startup; ++i) {
+            const int p = P->startup_seq[i];
+            const StateRow& r = P->st[p];
+            PState& st = ps(p);
+            if (st.started) continue;  // AbsentStreamPreStateProcessor :291-308 / AbsentLogical... :331-351
+            st.started = 1;
+            if (r.is_start && r.waiting_ms != -1 && st.active) {
+                if (r.kind == PK_ABSENT) {
+                    st.last_sched = clock + r.waiting_ms;
+                    notify_at(r.sched, st.last_sched);
+                } else {
+                    notify_at(r.sched, clock + r.waiting_ms);
+                }
+            }
+        }
+        absent_gc();
     }
 
     SDG_HD void on_event(int qs, int16_t rec, int64_t ts) {
@@ -678,18 +1170,41 @@ struct KeyEvents {
     int64_t b, e, seq_base;
 };
 
-// initPartition on the key's first event ever, then every row through the receiver
+// one key's batch run: initPartition on the key's first event ever (unpartitioned queries: before position 0, as
+// SiddhiAppRuntime.start does), the timer fires due before each row, every row through the receiver, and the
+// fires after the last row up to the end of the batch
 SDG_HD void run_key(Ctx& c, const KeyEvents& ev) {
     const Plan* P = c.P;
     const Layout& L = c.L;
-    if (!(c.head().flags & 2)) {
+    c.seq_base = ev.seq_base;
+    c.fsched = -1;
+    c.fi = 0;
+    c.pos = -1;
+    c.clock = c.T.clock0;
+    const bool fresh = !(c.head().flags & 2);
+    if (fresh) {
         c.arena_init();
         c.head().flags = 2;
+    }
+    c.head().kseq = 0;
+    for (int i = 0; i < L.n_sched; ++i)
+        if (c.tq(i).n > 0) c.tq(i).earliest = 0;  // positions restart with every batch
+    bool need_init = fresh;
+    if (need_init && !P->partitioned) {
         c.init_key();
+        need_init = false;
     }
     for (int64_t p = ev.b; p < ev.e && !c.ovf(); ++p) {
-        const KHead& h = c.head();
-        if (4 * h.se_used > 3 * L.ns || 4 * h.nd_used > 3 * L.nn || 4 * h.rc_used > 3 * L.nr) c.gc();
+        const int64_t g = ev.orig ? (int64_t)ev.orig[p] : p;
+        c.fire_until(g);  // TimeChangeListener.onTimeChange runs before the event is processed
+        if (c.ovf()) break;
+        c.pos = g;
+        if (P->n_sched) c.clock = c.T.clk[g];
+        if (need_init) {  // PartitionRuntimeImpl.initPartition for a first-seen key (after the clock advance)
+            c.init_key();
+            need_init = false;
+        }
+        c.maybe_gc();
         int16_t r = c.rc_alloc();
         if (r == NIL) break;
         Rec& rec = c.rc(r);
@@ -702,9 +1217,14 @@ SDG_HD void run_key(Ctx& c, const KeyEvents& ev) {
             if (ev.nulls[col] && ev.nulls[col][p]) nm |= 1u << col;
         }
         rec.nullmask = nm;
-        c.cur_seq = ev.seq_base + (ev.orig ? (int64_t)ev.orig[p] : p);
+        c.cur_seq = ev.seq_base + g;
         c.cur_sub = 0;
         c.on_event(ev.qstream ? ev.qstream[p] : 0, r, ts);
+        if (P->n_sched) c.absent_gc();
+    }
+    if (P->n_sched && c.T.G > 0 && !c.ovf()) {
+        c.fire_until(c.T.G - 1);
+        c.clock = c.T.clk[c.T.G - 1];
     }
 }
 

@@ -77,9 +77,11 @@ struct StateRow {
     int32_t callback;        // callbackPreStateProcessor (count) or -1
     int32_t last;            // thisLastProcessor's state id (own, or the query's last for the first state)
     int32_t min_count, max_count;
-    int64_t waiting_ms;      // ABSENT
+    int64_t waiting_ms;      // ABSENT / absent side of a LOGICAL (-1: no `for`)
     uint8_t selector_after;  // post.nextProcessor == selector (last state / logical partners of it)
-    uint8_t pad[7];
+    uint8_t absent;          // LOGICAL: this side is `not S[..]` (AbsentLogicalPreStateProcessor)
+    int8_t sched;            // scheduler of this absent processor (index into Plan::sched_state) or -1
+    uint8_t pad[5];
 };
 
 // per query stream: the receiver built by StateInputStreamParser (:91-110) and wired by the inner runtimes'
@@ -116,6 +118,9 @@ struct Plan {
     int32_t n_reset, reset_seq[MAX_STATES];     // innerStateRuntime.reset()
     int32_t n_update, update_seq[MAX_STATES];   // innerStateRuntime.update()
     int32_t n_startup, startup_seq[MAX_STATES]; // startupPreStateProcessors (absent partitionCreated)
+    int32_t n_sched, sched_state[MAX_STATES];   // one Scheduler per absent processor, in creation order (= the
+                                                // order its TimeChangeListener registers, SchedulerParser.parse)
+    int32_t playback;                           // @app:playback: the clock is event time (else modelled wall clock)
     // expire order (allStateProcessors), setup order per stream etc. live on the host plan
     int32_t n_code = 0, n_consts = 0;
 };

@@ -30,6 +30,8 @@ def lib():
         L.emu_string.argtypes = [P, U32]
         L.emu_send.argtypes = [P, I32, I64, ctypes.POINTER(I64), ctypes.POINTER(ctypes.c_uint8)]
         L.emu_flush.argtypes = [P]
+        L.emu_advance.argtypes = [P, I64]
+        L.emu_start.argtypes = [P, I64]
         L.emu_num_queries.argtypes = [P]
         for f in ("emu_query_name", "emu_query_target"):
             getattr(L, f).restype = ctypes.c_char_p
@@ -66,9 +68,11 @@ class EmuAdapter:
         self.records = []
 
     def start(self, ts):
-        pass
+        self.L.emu_start(self.h, ts)
 
     def send(self, sid, ts, values, now=None, mode=0):
+        if not self.playback and now is not None:
+            self.L.emu_advance(self.h, now)  # the wall clock at this send (timers due by then fire first)
         si = self.L.emu_stream_index(self.h, sid.encode())
         if si < 0:
             raise EmuError("unknown stream " + sid)
@@ -97,7 +101,7 @@ class EmuAdapter:
         self.L.emu_send(self.h, si, ts, vals, nulls)
 
     def advance(self, ts):
-        pass
+        self.L.emu_advance(self.h, ts)
 
     def flush(self):
         if self.L.emu_flush(self.h) != 0:

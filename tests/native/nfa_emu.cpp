@@ -17,6 +17,7 @@
 
 #include "../../siddhi_amd/csrc/engine/compile.h"
 #include "../../siddhi_amd/csrc/engine/nfa.h"
+#include "../../siddhi_amd/csrc/engine/sched.h"
 #include "../../siddhi_amd/csrc/siddhiql/parser.h"
 
 using namespace sdg;
@@ -34,7 +35,7 @@ int width_of(uint8_t kind) {
 }
 
 struct Ev {
-    int stream;
+    int stream;  // -1: an advance_time point
     int64_t ts;
     std::vector<int64_t> vals;
     std::vector<uint8_t> nulls;
@@ -50,8 +51,9 @@ struct EmuQuery {
     HostQuery hq;
     nfa::Layout L;
     std::map<std::string, int> keys;
+    std::vector<int32_t> key_hash;
     std::vector<std::vector<uint8_t>> arenas;
-    int64_t seq = 0;
+    SchedSim sim;
     std::vector<Out> outs;
 };
 
@@ -61,27 +63,56 @@ struct Emu {
     std::vector<std::unique_ptr<EmuQuery>> qs;
     std::vector<Ev> pending;
     int ns = 64;
+    int64_t clock = 0;  // playback: lastEventTimestamp; live: the modelled wall clock
+    int64_t seq = 0;    // positions flushed so far
 };
 
 std::string key_text(Emu* e, uint8_t kind, int64_t v) {
-    char buf[64];
     switch (kind) {
         case VK_I32: return std::to_string((int32_t)v);
         case VK_I64: return std::to_string(v);
-        case VK_F32: std::snprintf(buf, sizeof buf, "%.9g", (double)bits_f32(v)); return buf;
-        case VK_F64: std::snprintf(buf, sizeof buf, "%.17g", bits_f64(v)); return buf;
+        case VK_F32: return java_real_string(bits_f32(v), true);
+        case VK_F64: return java_real_string(bits_f64(v), false);
         case VK_BOOL: return v ? "true" : "false";
         default: return e->strings.strs[(uint32_t)v];
     }
 }
 
-int flush_query(Emu* e, EmuQuery& q) {
+// the batch clock over every pending position (TimestampGeneratorImpl.setCurrentTimestamp / live advance)
+BatchClock batch_clock(Emu* e) {
+    BatchClock bc;
+    bc.G = (int64_t)e->pending.size();
+    bc.clock0 = e->clock;
+    bc.clk.resize(bc.G);
+    bc.adv.resize(bc.G);
+    bc.nadv.resize(bc.G + 1);
+    int64_t c = e->clock;
+    for (int64_t g = 0; g < bc.G; ++g) {
+        const Ev& ev = e->pending[g];
+        if (e->app.playback) {
+            bc.adv[g] = ev.ts >= c;
+            if (ev.ts >= c) c = ev.ts;
+        } else {
+            bc.adv[g] = ev.stream < 0;
+            if (ev.stream < 0 && ev.ts > c) c = ev.ts;
+        }
+        bc.clk[g] = c;
+    }
+    bc.nadv[bc.G] = (uint32_t)bc.G;
+    for (int64_t g = bc.G - 1; g >= 0; --g) bc.nadv[g] = bc.adv[g] ? (uint32_t)g : bc.nadv[g + 1];
+    return bc;
+}
+
+int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
     HostQuery& h = q.hq;
     const Plan& P = h.plan;
     const int nc = P.n_cols;
     std::vector<const Ev*> rows;
     std::vector<int> rkey;
-    for (const Ev& ev : e->pending) {
+    std::vector<uint32_t> rpos;
+    for (int64_t g = 0; g < bc.G; ++g) {
+        const Ev& ev = e->pending[g];
+        if (ev.stream < 0) continue;
         int qpos = h.stream_pos(ev.stream);
         if (qpos < 0) continue;
         int key = 0;
@@ -90,11 +121,15 @@ int flush_query(Emu* e, EmuQuery& q) {
             if (ev.nulls[ai]) continue;  // null partition key: dropped
             std::string kt = key_text(e, h.key_kind[qpos], ev.vals[ai]);
             auto it = q.keys.find(kt);
-            if (it == q.keys.end()) it = q.keys.emplace(kt, (int)q.keys.size()).first;
+            if (it == q.keys.end()) {
+                it = q.keys.emplace(kt, (int)q.keys.size()).first;
+                q.key_hash.push_back(java_spread_hash(kt));
+            }
             key = it->second;
         }
         rows.push_back(&ev);
         rkey.push_back(key);
+        rpos.push_back((uint32_t)g);
     }
     const int64_t n = (int64_t)rows.size();
     const int K = P.partitioned ? (int)q.keys.size() : 1;
@@ -104,6 +139,7 @@ int flush_query(Emu* e, EmuQuery& q) {
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return rkey[a] < rkey[b]; });
     std::vector<int64_t> ts(std::max<int64_t>(n, 1));
     std::vector<uint8_t> qs(std::max<int64_t>(n, 1));
+    std::vector<uint32_t> gpos(std::max<int64_t>(n, 1));
     std::vector<std::vector<uint8_t>> cols(nc), nulls(nc);
     std::vector<const void*> cptr(MAX_COLS, nullptr);
     std::vector<const uint8_t*> nptr(MAX_COLS, nullptr);
@@ -119,6 +155,7 @@ int flush_query(Emu* e, EmuQuery& q) {
         int qpos = h.stream_pos(ev.stream);
         ts[p] = ev.ts;
         qs[p] = (uint8_t)qpos;
+        gpos[p] = rpos[order[p]];
         for (int k = 0; k < nc; ++k) {
             int ai = h.col_attr[qpos][k];
             int w = width_of(P.col_kind[k]);
@@ -134,14 +171,25 @@ int flush_query(Emu* e, EmuQuery& q) {
         seg_e[key] = (uint32_t)(p + 1);
     }
     while ((int)q.arenas.size() < K) q.arenas.emplace_back((size_t)q.L.bytes, 0);
-    int64_t cap = 2 * n + 4096;
-    std::vector<int64_t> o_ts(cap), o_vals((size_t)std::max(P.n_out, 1) * cap), o_seq(cap), o_sub(cap);
-    std::vector<uint32_t> o_nulls(cap), o_key(cap);
-    unsigned long long count = 0;
-    int flags[4] = {0, 0, 0, 0};
+    // keys this batch runs: rows, queued timers, the unpartitioned query's single key (initialised at start)
+    std::vector<uint32_t> run;
+    if (q.sim.active()) q.sim.queued_keys(run);
+    for (int k = 0; k < K; ++k)
+        if (seg_b[k] < seg_e[k] || !P.partitioned) run.push_back((uint32_t)k);
+    std::sort(run.begin(), run.end());
+    run.erase(std::unique(run.begin(), run.end()), run.end());
+    std::map<uint32_t, std::vector<uint8_t>> backup;
+    for (uint32_t k : run) backup[k] = q.arenas[k];
+    std::map<uint32_t, std::vector<Out>> kout;
+    std::map<uint32_t, std::vector<nfa::SchedLog>> klog;
     std::vector<int64_t> stk(STACK);
-    for (int k = 0; k < K; ++k) {
-        if (seg_b[k] >= seg_e[k]) continue;
+    auto run_one = [&](uint32_t k, const nfa::TimerFire* fires, int nfires) -> int {
+        const int64_t cap = 2 * (seg_e[k] - seg_b[k]) + 4096 + 64 * (int64_t)nfires;
+        std::vector<int64_t> o_ts(cap), o_vals((size_t)std::max(P.n_out, 1) * cap), o_seq(cap), o_sub(cap);
+        std::vector<uint32_t> o_nulls(cap), o_key(cap);
+        unsigned long long count = 0, lcount = 0;
+        std::vector<nfa::SchedLog> logs(1 << 16);
+        int flags[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         nfa::Ctx c;
         c.P = &P;
         c.code = h.code.data();
@@ -159,28 +207,83 @@ int flush_query(Emu* e, EmuQuery& q) {
         c.emit_count = &count;
         c.emit_cap = cap;
         c.flags = flags;
-        c.key = (uint32_t)k;
-        nfa::KeyEvents kev{ts.data(), qs.data(), order.data(), cptr.data(), nptr.data(), seg_b[k], seg_e[k], q.seq};
+        c.key = k;
+        c.T.G = bc.G;
+        c.T.clk = bc.clk.data();
+        c.T.nadv = bc.nadv.data();
+        c.T.clock0 = bc.clock0;
+        c.T.live = !e->app.playback;
+        c.T.log = q.sim.active() ? logs.data() : nullptr;
+        c.T.log_count = &lcount;
+        c.T.log_cap = (int64_t)logs.size();
+        c.fires = fires;
+        c.nfires = nfires;
+        nfa::KeyEvents kev{ts.data(), qs.data(), gpos.data(), cptr.data(), nptr.data(), seg_b.size() > k ? seg_b[k] : 0,
+                           seg_e.size() > k ? seg_e[k] : 0, e->seq};
+        if (kev.b > kev.e) kev.b = kev.e;
         nfa::run_key(c, kev);
         if (c.ovf()) {
             g_err = "query '" + h.name + "': partial-match arena overflow";
             return 3;
         }
+        if (flags[0] || flags[5]) {
+            g_err = "output / scheduler log overflow";
+            return 3;
+        }
+        std::vector<Out>& ko = kout[k];
+        ko.clear();
+        for (unsigned long long i = 0; i < count; ++i) {
+            Out o{o_seq[i], o_sub[i], o_ts[i], {}, o_nulls[i]};
+            for (int j = 0; j < P.n_out; ++j) o.vals.push_back(o_vals[(size_t)j * cap + i]);
+            ko.push_back(std::move(o));
+        }
+        klog[k].assign(logs.begin(), logs.begin() + (int64_t)lcount);
+        return 0;
+    };
+    for (uint32_t k : run) {
+        if (k >= seg_b.size() && P.partitioned) {  // a key of an earlier batch with queued timers only
+            seg_b.resize(k + 1, 0);
+            seg_e.resize(k + 1, 0);
+        }
+        int rc = run_one(k, nullptr, 0);
+        if (rc) return rc;
     }
-    if (flags[0]) {
-        g_err = "output overflow";
-        return 3;
+    SchedSim::Result res;
+    if (q.sim.active()) {
+        // fixpoint with the global scheduler (sched.h): rerun diverged keys with the simulated fire lists
+        for (int round = 0;; ++round) {
+            std::vector<nfa::SchedLog> all;
+            for (auto& kv : klog) all.insert(all.end(), kv.second.begin(), kv.second.end());
+            q.sim.simulate(bc, all, q.key_hash, res);
+            if (res.diverged.empty()) break;
+            if (round > 64) {
+                g_err = "scheduler fixpoint did not converge";
+                return 5;
+            }
+            for (size_t d = 0; d < res.diverged.size(); ++d) {
+                const uint32_t k = res.diverged[d];
+                q.arenas[k] = backup[k];
+                int rc = run_one(k, res.fires.data() + res.fire_off[d], (int)(res.fire_off[d + 1] - res.fire_off[d]));
+                if (rc) return rc;
+            }
+        }
+        q.sim.commit();
     }
     std::vector<Out> batch;
-    for (unsigned long long i = 0; i < count; ++i) {
-        Out o{o_seq[i], o_sub[i], o_ts[i], {}, o_nulls[i]};
-        for (int j = 0; j < P.n_out; ++j) o.vals.push_back(o_vals[(size_t)j * cap + i]);
-        batch.push_back(std::move(o));
-    }
+    for (auto& kv : kout)
+        for (Out& o : kv.second) {
+            if (o.sub < 0) {  // timer match: order among the position's fires (the scheduler's order)
+                const int sch = (int)((o.sub >> 48) & 0x7F);
+                const uint32_t g = (uint32_t)(o.seq - e->seq);
+                auto it = res.rank.find(SchedSim::rank_key(g, sch, kv.first));
+                const int64_t r = it == res.rank.end() ? 0 : it->second;
+                o.sub = INT64_MIN | (r << 24) | (o.sub & 0xFFFFFF);
+            }
+            batch.push_back(std::move(o));
+        }
     std::stable_sort(batch.begin(), batch.end(),
                      [](const Out& a, const Out& b) { return a.seq != b.seq ? a.seq < b.seq : a.sub < b.sub; });
     for (auto& o : batch) q.outs.push_back(std::move(o));
-    q.seq += n;
     return 0;
 }
 
@@ -197,11 +300,11 @@ void* emu_create(const char* text, int max_partials) {
         if (max_partials > 0) e->ns = max_partials;
         auto hqs = compile_app(e->app, e->strings);
         for (auto& h : hqs) {
-            for (int i = 0; i < h.plan.n_states; ++i)
-                if (h.plan.st[i].kind == PK_ABSENT) throw CompileError(4, "absent states not in this build");
             auto q = std::make_unique<EmuQuery>();
             q->hq = std::move(h);
-            q->L = nfa::make_layout(q->hq.plan.n_states, std::max(q->hq.plan.n_cols, 1), e->ns);
+            const Plan& P = q->hq.plan;
+            q->L = nfa::make_layout(P.n_states, std::max(P.n_cols, 1), e->ns, P.n_sched);
+            q->sim.setup(P.n_sched, P.partitioned, !e->app.playback);
             e->qs.push_back(std::move(q));
         }
         return e.release();
@@ -235,15 +338,36 @@ int emu_send(void* h, int stream, int64_t ts, const int64_t* vals, const uint8_t
     return 0;
 }
 
+// advance_time: a position of its own (playback: setCurrentTimestamp; live: the wall clock moved)
+int emu_advance(void* h, int64_t ts) {
+    Emu* e = (Emu*)h;
+    e->pending.push_back(Ev{-1, ts, {}, {}});
+    return 0;
+}
+
+// SiddhiAppRuntime.start: the live clock starts at ts (playback: the clock is event time, starting at 0)
+int emu_start(void* h, int64_t ts) {
+    Emu* e = (Emu*)h;
+    if (!e->app.playback) e->clock = ts;
+    return 0;
+}
+
 int emu_flush(void* h) {
     Emu* e = (Emu*)h;
     try {
+        BatchClock bc = batch_clock(e);
         for (auto& q : e->qs) {
-            int rc = flush_query(e, *q);
-            if (rc) return rc;
+            int rc = flush_query(e, *q, bc);
+            if (rc) {
+                e->pending.clear();
+                return rc;
+            }
         }
+        if (bc.G > 0) e->clock = bc.clk[bc.G - 1];
+        e->seq += bc.G;
     } catch (const std::exception& ex) {
         g_err = ex.what();
+        e->pending.clear();
         return 5;
     }
     e->pending.clear();
