@@ -49,10 +49,8 @@ def _rank_main(rank, world, port, out_dir):
                     dist.all_gather(allc, cnt)  # global output offsets of this batch
             finally:
                 e.close()
-            # local sequence number (over the events of the query's streams) -> global position in the trace
-            streams = {"S", "T"} if "=T[" in synth.APPS[name] else {"S"}
-            mine_q = [i for i in mine if tr[i][0] in streams]
-            part = [(mine_q[r["seq"]], r["ordinal"], (r["name"], r["ts"], tuple(r["values"]))) for r in recs]
+            # local sequence number (position among this rank's sends, all streams) -> global position in the trace
+            part = [(mine[r["seq"]], r["ordinal"], (r["name"], r["ts"], tuple(r["values"]))) for r in recs]
             parts = [None] * world
             dist.all_gather_object(parts, part)
             if rank == 0:
