@@ -11,7 +11,8 @@
  *                           (core/stream/input/InputHandler.java:59-95); events keep their call order
  *   sdg_push_device      <- the same for event columns already resident in HBM (device pointers)
  *   sdg_advance_time     <- TimestampGeneratorImpl.setCurrentTimestamp (playback clock, util/timestamp/
- *                           TimestampGeneratorImpl.java:105-122)
+ *                           TimestampGeneratorImpl.java:105-122) / the wall clock of a live app
+ *   sdg_start            <- SiddhiAppRuntime.start() (core/SiddhiAppRuntimeImpl.java:440)
  *   sdg_flush            <- the receivers' per-event processing of everything pushed so far
  *                           (core/query/input/ProcessStreamReceiver.java:98-179 -> state processors)
  *   sdg_poll             <- QueryCallback.receive(long, Event[], Event[]) / StreamCallback.receive(Event[])
@@ -72,10 +73,9 @@ typedef struct sdg_out {
     const int32_t* types;      /* [n_attrs] sdg_type */
     const int64_t* const* values; /* [n_attrs][n] 64-bit payload (float/double as bit patterns) */
     const uint8_t* const* nulls;  /* [n_attrs][n] 1 = null */
-    const int64_t* event_seq;  /* [n] sequence number of the input event whose processing emitted the row (per
-                                  query, counting the events of the query's streams from 0): consecutive rows with
-                                  equal event_seq are the one Event[] the reference hands to the callback for that
-                                  event (StateMultiProcessStreamReceiver.processAndClear :47-68) */
+    const int64_t* event_seq;  /* [n] position (from 0, over every pushed event of every stream and every
+                                  sdg_advance_time point) of the input event whose processing emitted the row; an
+                                  absent state's timer match carries the position whose clock advance fired it */
 } sdg_out;
 
 int sdg_compile(const char* siddhi_app, const sdg_opts* opts, sdg_engine** out);
@@ -97,10 +97,20 @@ const char* sdg_string(sdg_engine* e, uint32_t id);
 /* columnar host batch for ONE stream: ts[n], cols[a] (typed as above), nulls[a] may be NULL */
 int sdg_push(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const void* const* cols,
              const uint8_t* const* nulls);
+/* rows of several streams in one interleaved batch (InputHandler.send calls of different streams, in order):
+ * row i belongs to stream streams[i]; attribute a of that row is slots[a][i] as a 64-bit slot (INT/LONG the value,
+ * FLOAT/DOUBLE the bit pattern in the low bits, BOOL 0/1, STRING an sdg_intern id); nulls[a] optional */
+int sdg_push_mixed(sdg_engine* e, int64_t n, const int32_t* streams, const int64_t* ts, int32_t n_attrs,
+                   const int64_t* const* slots, const uint8_t* const* nulls);
 /* the same with device-resident columns (no copy; the caller keeps them alive until sdg_flush returns) */
 int sdg_push_device(sdg_engine* e, int stream, int64_t n, const int64_t* d_ts, const void* const* d_cols,
                     const uint8_t* const* d_nulls);
+/* the clock moves to ts (playback: TimestampGeneratorImpl.setCurrentTimestamp when ts >= clock; live: the wall
+ * clock reached ts). It is a position in the next flush: absent-state timers due by then fire there, before the
+ * events pushed after it (Scheduler.java:71-103) */
 int sdg_advance_time(sdg_engine* e, int64_t ts);
+/* SiddhiAppRuntime.start(): live (non-playback) apps start their clock at ts; before any push */
+int sdg_start(sdg_engine* e, int64_t ts);
 /* events buffered since the last flush (a push that reaches batch_capacity flushes: the count drops) */
 int64_t sdg_pending(sdg_engine* e);
 int sdg_flush(sdg_engine* e);

@@ -120,7 +120,9 @@ def load_library():
     L.sdg_string.argtypes = [P, U32]
     L.sdg_push.argtypes = [P, I32, I64, P, P, P]
     L.sdg_push_device.argtypes = [P, I32, I64, P, P, P]
+    L.sdg_push_mixed.argtypes = [P, I64, P, P, I32, P, P]
     L.sdg_advance_time.argtypes = [P, I64]
+    L.sdg_start.argtypes = [P, I64]
     L.sdg_pending.restype = I64
     L.sdg_pending.argtypes = [P]
     L.sdg_flush.argtypes = [P]
@@ -233,8 +235,12 @@ class SiddhiAppRuntime:
     def addCallback(self, name, callback):  # noqa: N802
         self._callbacks.setdefault(name, []).append(callback)
 
-    def start(self):
+    def start(self, timestamp=None):
+        """SiddhiAppRuntime.start(); a live (non-playback) app's clock starts at `timestamp` (default: now, ms)"""
         self._started = True
+        if timestamp is None:
+            timestamp = int(time.time() * 1000)
+        _check(self._L.sdg_start(self._h, int(timestamp)))
 
     def shutdown(self):
         if self._h:
@@ -319,6 +325,32 @@ class SiddhiAppRuntime:
                 nl[a] = m.ctypes.data
         self._push(idx, n, ts.ctypes.data, cols, nl)
 
+    def push_mixed(self, stream_ids, ts, slot_columns, nulls=None):
+        """Rows of several streams interleaved in one batch (in send order): stream_ids[i] names row i's stream
+        (a sequence of ids, or an int array of sdg stream indices); slot_columns[a][i] = attribute a of row i as an
+        int64 slot (int/long value, float/double bit pattern, bool 0/1, string id from intern())."""
+        import numpy as np
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        n = len(ts)
+        if len(stream_ids) and isinstance(stream_ids[0], str):
+            idx = {s: self._L.sdg_stream_index(self._h, s.encode()) for s in set(stream_ids)}
+            streams = np.array([idx[s] for s in stream_ids], dtype=np.int32)
+        else:
+            streams = np.ascontiguousarray(stream_ids, dtype=np.int32)
+        cols = [np.ascontiguousarray(c).view(np.int64) if np.asarray(c).dtype.itemsize == 8 else
+                np.ascontiguousarray(c, dtype=np.int64) for c in slot_columns]
+        cp = (ctypes.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
+        keep = list(cols)
+        nl = None
+        if nulls is not None:
+            ns = [None if m is None else np.ascontiguousarray(m, dtype=np.uint8) for m in nulls]
+            keep += [m for m in ns if m is not None]
+            nl = (ctypes.c_void_p * len(ns))(*[None if m is None else m.ctypes.data for m in ns])
+        before = self._L.sdg_pending(self._h)
+        _check(self._L.sdg_push_mixed(self._h, n, streams.ctypes.data, ts.ctypes.data, len(cols), cp, nl))
+        if self._L.sdg_pending(self._h) < before + n:
+            self._deliver()
+
     def push_device(self, stream_id, n, ts_ptr, col_ptrs):
         """Device-resident columns (e.g. torch CUDA tensors' data_ptr()); kept alive by the caller."""
         idx = self._L.sdg_stream_index(self._h, stream_id.encode())
@@ -326,7 +358,11 @@ class SiddhiAppRuntime:
         _check(self._L.sdg_push_device(self._h, idx, n, ctypes.c_void_p(ts_ptr), cols, None))
 
     def advance_time(self, ts):
-        _check(self._L.sdg_advance_time(self._h, ts))
+        """the clock reached ts (playback: event time; live: the wall clock): due absent-state timers fire at the
+        next flush, in this position of the input"""
+        if self.playback:
+            self._last_ts = max(self._last_ts, int(ts))
+        _check(self._L.sdg_advance_time(self._h, int(ts)))
 
     def flush(self, deliver=True):
         _check(self._L.sdg_flush(self._h))

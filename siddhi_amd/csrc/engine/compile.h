@@ -1,5 +1,6 @@
 // Host-side query compiler: SiddhiQL AST -> sdg::Plan (NFA table + condition bytecode).
 #pragma once
+#include <stdexcept>
 #include <string>
 #include <unordered_map>
 #include <vector>

@@ -18,6 +18,7 @@
 #include "../kernels/kernels.h"
 #include "../siddhiql/parser.h"
 #include "compile.h"
+#include "sched.h"
 
 namespace sdg {
 namespace {
@@ -85,9 +86,10 @@ int width_of(uint8_t kind) {
 }
 
 struct PushChunk {
-    int stream;
+    int stream;          // -1: an sdg_advance_time point (one position, no data); -2: mixed (rstream per row)
     int64_t n;
     bool device;
+    std::vector<int32_t> rstream;   // mixed: stream of each row; cols[a] then hold 64-bit slots of attribute a
     std::vector<int64_t> ts;
     std::vector<std::vector<uint8_t>> cols;
     std::vector<std::vector<uint8_t>> nulls;
@@ -144,7 +146,17 @@ struct QueryRt {
     HostPin h_args, h_ret;  // chain path: ChainArgs pair; counters (16 B) | flags (16 B) | overflow count (8 B)
     bool string_keys = true;                        // all partition keys are string attributes (ids used as keys)
     std::unordered_map<std::string, uint32_t> keydict;
-    int64_t seq = 0;
+    std::vector<std::string> keystr;                // keydict id -> key text (numeric keys)
+    // absent states: the scheduler simulation, per-key HashMap hashes, double-buffered arenas, the run's log
+    SchedSim sim;
+    std::vector<int32_t> key_hash;
+    DevBuf arena2, cur_bits, ran_bits, o_round, d_log, d_list, d_foff, d_fires, d_vpos;
+    int64_t log_cap = 0;
+    // timer-match ordering of the last flush (drain): fire ranks, the round each rerun key's records come from
+    bool last_timers = false;
+    int64_t last_seq_base = 0;
+    std::unordered_map<uint64_t, uint32_t> last_rank;
+    std::unordered_map<uint32_t, uint8_t> key_round;
     // batch staging
     DevBuf st_ts, st_qs, st_key, st_cols[MAX_COLS], st_nulls[MAX_COLS];
     // sorted view
@@ -197,6 +209,11 @@ struct sdg_engine {
     int64_t capacity = 1 << 24;
     int32_t max_partials = 64;
     int64_t pending_n = 0;
+    int64_t seq = 0;             // batch positions flushed so far (sequence number of the next batch's position 0)
+    int64_t clock = 0;           // currentTime(): playback = max event ts seen; live = the modelled wall clock
+    bool any_sched = false;      // some query has absent states (the batch clock is built)
+    BatchClock bc;
+    DevBuf d_clk, d_nadv;
     sdg_stats stats{};
     std::vector<std::vector<int32_t>> stream_types;
     std::vector<std::vector<int32_t>> out_types;
@@ -258,7 +275,38 @@ bool host_key(sdg_engine* e, QueryRt& q, int qpos, const PushChunk& c, int64_t r
         default: s = e->strings.strs[((const uint32_t*)col)[row]]; break;
     }
     auto it = q.keydict.find(s);
-    if (it == q.keydict.end()) it = q.keydict.emplace(s, (uint32_t)q.keydict.size()).first;
+    if (it == q.keydict.end()) {
+        it = q.keydict.emplace(s, (uint32_t)q.keydict.size()).first;
+        q.keystr.push_back(s);
+    }
+    *key = it->second;
+    if (integral) q.intkeys.insert(iv, *key);
+    return true;
+}
+
+// key of a mixed-chunk row from its 64-bit attribute slot (same toString rules as host_key)
+bool slot_key(sdg_engine* e, QueryRt& q, int qpos, int64_t slot, uint32_t* key) {
+    const uint8_t kind = q.hq.key_kind[qpos];
+    if (q.string_keys) {
+        *key = (uint32_t)slot;
+        return true;
+    }
+    const bool integral = kind == VK_I32 || kind == VK_I64;
+    const int64_t iv = kind == VK_I32 ? (int64_t)(int32_t)slot : slot;
+    if (integral && q.intkeys.find(iv, key)) return true;
+    std::string s;
+    switch (kind) {
+        case VK_I32: case VK_I64: s = std::to_string(iv); break;
+        case VK_F32: s = java_real_string(bits_f32(slot), true); break;
+        case VK_F64: s = java_real_string(bits_f64(slot), false); break;
+        case VK_BOOL: s = slot ? "true" : "false"; break;
+        default: s = e->strings.strs[(uint32_t)slot]; break;
+    }
+    auto it = q.keydict.find(s);
+    if (it == q.keydict.end()) {
+        it = q.keydict.emplace(s, (uint32_t)q.keydict.size()).first;
+        q.keystr.push_back(s);
+    }
     *key = it->second;
     if (integral) q.intkeys.insert(iv, *key);
     return true;
@@ -366,10 +414,24 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     hipStream_t st = e->stream;
     const int nc = P.n_cols;
     // ---- 1. batch view -------------------------------------------------------------------------------
+    // the query's chunks and their batch positions (every pending chunk, any stream, and every advance_time point
+    // takes positions: the clock and the sequence numbers count them all)
     std::vector<const PushChunk*> parts;
-    int64_t n = 0;
-    for (auto& c : e->pending)
-        if (h.stream_pos(c.stream) >= 0) { parts.push_back(&c); n += c.n; }
+    std::vector<int64_t> part_pos;
+    int64_t n = 0, gpos = 0;
+    for (auto& c : e->pending) {
+        bool mine = h.stream_pos(c.stream) >= 0;
+        if (c.stream == -2)
+            for (int s2 : h.streams) mine |= std::find(c.rstream.begin(), c.rstream.end(), s2) != c.rstream.end();
+        if (mine) {
+            parts.push_back(&c);
+            part_pos.push_back(gpos);
+            n += c.n;
+        }
+        gpos += c.n;
+    }
+    int64_t pos_off = 0;                  // position of view row 0 when rows map to positions contiguously
+    const uint32_t* d_vpos = nullptr;     // [nrows] view row -> batch position otherwise
     const bool partitioned = P.partitioned;
     const bool multi_stream = h.streams.size() > 1;
     const int64_t* d_ts = nullptr;
@@ -378,10 +440,11 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     const void* d_cols[MAX_COLS] = {};
     const uint8_t* d_nulls[MAX_COLS] = {};
     int64_t nrows = 0;
-    bool zero_copy = parts.size() == 1 && parts[0]->device && !multi_stream;
+    bool zero_copy = parts.size() == 1 && parts[0]->device && !multi_stream && parts[0]->stream >= 0;
     if (zero_copy) {
         const PushChunk& c = *parts[0];
         int qpos = h.stream_pos(c.stream);
+        pos_off = part_pos[0];
         d_ts = c.d_ts;
         for (int k = 0; k < nc; ++k) {
             int ai = h.col_attr[qpos][k];
@@ -403,10 +466,44 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         std::vector<uint32_t> keys;
         std::vector<std::vector<uint8_t>> cols(nc), nulls(nc);
         std::vector<bool> any_null(nc, false);
+        std::vector<uint32_t> vpos;
         ts.reserve(n);
+        vpos.reserve(n);
         for (int k = 0; k < nc; ++k) cols[k].reserve((size_t)n * width_of(P.col_kind[k]));
-        for (const PushChunk* c : parts) {
+        for (size_t pi = 0; pi < parts.size(); ++pi) {
+            const PushChunk* c = parts[pi];
             if (c->device) throw CompileError(SDG_ERR_UNSUPPORTED, "mixed / multi-stream device-resident batches");
+            if (c->stream == -2) {  // mixed chunk: row by row (attributes as 64-bit slots)
+                for (int64_t r = 0; r < c->n; ++r) {
+                    const int qpos = h.stream_pos(c->rstream[r]);
+                    if (qpos < 0) continue;
+                    uint32_t key = 0;
+                    if (partitioned) {
+                        const int ai = h.key_attr[qpos];
+                        if (!c->nulls[ai].empty() && c->nulls[ai][r]) continue;  // null partition key: dropped
+                        if (!slot_key(e, q, qpos, ((const int64_t*)c->cols[ai].data())[r], &key)) continue;
+                        keys.push_back(key);
+                    }
+                    const size_t row = ts.size();
+                    ts.push_back(c->ts[r]);
+                    vpos.push_back((uint32_t)(part_pos[pi] + r));
+                    qs.push_back((uint8_t)qpos);
+                    for (int k = 0; k < nc; ++k) {
+                        const int w = width_of(P.col_kind[k]);
+                        const int ai = h.col_attr[qpos][k];
+                        cols[k].resize((row + 1) * w, 0);
+                        nulls[k].resize(row + 1, 0);
+                        if (ai < 0) continue;
+                        const int64_t v = ((const int64_t*)c->cols[ai].data())[r];
+                        std::memcpy(&cols[k][row * w], &v, w);  // little endian: the slot's low bytes
+                        if (!c->nulls[ai].empty() && c->nulls[ai][r]) {
+                            nulls[k][row] = 1;
+                            any_null[k] = true;
+                        }
+                    }
+                }
+                continue;
+            }
             const int qpos = h.stream_pos(c->stream);
             // rows kept (null partition key: dropped), then each column appended as a whole (bulk copy when no
             // row was dropped)
@@ -432,6 +529,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             const size_t m = all ? (size_t)c->n : kept.size();
             if (all) ts.insert(ts.end(), c->ts.begin(), c->ts.begin() + c->n);
             else for (int64_t r : kept) ts.push_back(c->ts[r]);
+            if (all) for (int64_t r = 0; r < c->n; ++r) vpos.push_back((uint32_t)(part_pos[pi] + r));
+            else for (int64_t r : kept) vpos.push_back((uint32_t)(part_pos[pi] + r));
             qs.resize(base + m, (uint8_t)qpos);
             for (int k = 0; k < nc; ++k) {
                 const int w = width_of(P.col_kind[k]);
@@ -457,6 +556,14 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         }
         nrows = (int64_t)ts.size();
         size_t cnt = (size_t)std::max<int64_t>(nrows, 1);
+        bool identity = true;
+        for (int64_t i = 0; i < nrows && identity; ++i) identity = vpos[i] == (uint32_t)(vpos[0] + i);
+        if (identity) {
+            pos_off = nrows ? vpos[0] : 0;
+        } else {
+            d_vpos = (const uint32_t*)q.d_vpos.ensure(cnt * 4);
+            HIPCHECK(hipMemcpyAsync((void*)d_vpos, vpos.data(), nrows * 4, hipMemcpyHostToDevice, st));
+        }
         d_ts = (const int64_t*)q.st_ts.ensure(cnt * 8);
         if (nrows) HIPCHECK(hipMemcpyAsync((void*)d_ts, ts.data(), nrows * 8, hipMemcpyHostToDevice, st));
         if (multi_stream) {
@@ -510,7 +617,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     const uint8_t* v_qs = d_qs;
     const uint32_t* v_key = nullptr;
     const uint32_t* v_seg = nullptr;
-    const uint32_t* v_orig = nullptr;
+    const uint32_t* v_orig = d_vpos;  // partitioned: replaced by orig_sorted (positions when d_vpos is set)
     const void* v_cols[MAX_COLS];
     const uint8_t* v_nulls[MAX_COLS];
     for (int k = 0; k < nc; ++k) { v_cols[k] = d_cols[k]; v_nulls[k] = d_nulls[k]; }
@@ -527,6 +634,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         a.K = (int32_t)K;
         a.keys = d_key;
         a.key_flag = zero_copy ? flags + 4 : nullptr;  // caller-supplied device ids: range-check against K
+        a.orig_in = d_vpos;                            // orig_sorted: view rows (+ pos_off), or positions
         int c = 0;
         a.src[c] = d_ts; a.dst[c] = q.so_ts.ensure(nrows * 8); a.width[c] = 8; v_ts = (const int64_t*)a.dst[c]; ++c;
         if (d_qs) { a.src[c] = d_qs; a.dst[c] = q.so_qs.ensure(nrows); a.width[c] = 1; v_qs = (const uint8_t*)a.dst[c]; ++c; }
@@ -592,49 +700,171 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         a.seg_end = partitioned ? v_segend : nullptr;
         a.K = partitioned ? (int32_t)K : 1;
         a.orig = v_orig;
+        a.pos_off = d_vpos ? 0 : pos_off;
         for (int k = 0; k < nc; ++k) { a.cols[k] = v_cols[k]; a.nulls[k] = v_nulls[k]; }
-        a.seq_base = q.seq;
-        // arenas: grow to K keys keeping the existing keys' state, new keys zeroed (= not yet initialised)
+        a.seq_base = e->seq;
+        const bool timers = P.n_sched > 0;
+        // arenas: grow to K keys keeping the existing keys' state, new keys zeroed (= not yet initialised); with
+        // timers two copies + the per-key committed-copy bit (a key can be rerun from its batch-start state)
         const int64_t kb = q.L.bytes;
         if (q.arena_keys < a.K) {
             int64_t nk = std::max<int64_t>(a.K, q.arena_keys + q.arena_keys / 2);
-            DevBuf nb;
-            nb.ensure((size_t)(nk * kb));
-            HIPCHECK(hipMemsetAsync(nb.p, 0, (size_t)(nk * kb), st));
-            if (q.arena_keys) HIPCHECK(hipMemcpyAsync(nb.p, q.arena.p, (size_t)(q.arena_keys * kb), hipMemcpyDeviceToDevice, st));
-            HIPCHECK(hipStreamSynchronize(st));
-            std::swap(nb.p, q.arena.p);
-            std::swap(nb.cap, q.arena.cap);
+            auto grow = [&](DevBuf& buf, int64_t per) {
+                DevBuf nb;
+                nb.ensure((size_t)(nk * per));
+                HIPCHECK(hipMemsetAsync(nb.p, 0, (size_t)(nk * per), st));
+                if (q.arena_keys) HIPCHECK(hipMemcpyAsync(nb.p, buf.p, (size_t)(q.arena_keys * per), hipMemcpyDeviceToDevice, st));
+                HIPCHECK(hipStreamSynchronize(st));
+                std::swap(nb.p, buf.p);
+                std::swap(nb.cap, buf.cap);
+            };
+            grow(q.arena, kb);
+            if (timers) {
+                grow(q.arena2, kb);
+                grow(q.cur_bits, 1);
+                grow(q.ran_bits, 1);
+            }
             q.arena_keys = nk;
         }
         a.arena = q.arena.as<uint8_t>();
+        if (timers) {
+            a.arena2 = q.arena2.as<uint8_t>();
+            a.cur = q.cur_bits.as<uint8_t>();
+            a.ran = q.ran_bits.as<uint8_t>();
+            a.T.G = e->bc.G;
+            a.T.clk = e->d_clk.as<int64_t>();
+            a.T.nadv = e->d_nadv.as<uint32_t>();
+            a.T.clock0 = e->bc.clock0;
+            a.T.live = !P.playback;
+            if (q.log_cap < 1024) q.log_cap = std::max<int64_t>(1024, 4 * nrows + 1024);
+            a.T.log = (nfa::SchedLog*)q.d_log.ensure((size_t)q.log_cap * sizeof(nfa::SchedLog));
+            a.T.log_cap = q.log_cap;
+        }
         a.L = q.L;
-        int64_t cap = 2 * nrows + 4096;
-        q.out_cap = cap;
+        int64_t cap = std::max<int64_t>(q.out_cap, 2 * nrows + 4096);
         unsigned long long* counters = (unsigned long long*)q.counters.ensure(16);
-        HIPCHECK(hipMemsetAsync(counters, 0, 16, st));
-        if (!(partitioned && nrows > 0)) HIPCHECK(hipMemsetAsync(flags, 0, 32, st));
-        a.out_cap = cap;
-        a.out_count = counters;
+        if (timers) a.T.log_count = counters + 1;
         a.flags = flags;
-        a.out_ts = (int64_t*)q.o_ts.ensure(cap * 8);
-        a.out_key = (uint32_t*)q.o_key.ensure(cap * 4);
-        a.out_vals = (int64_t*)q.o_vals.ensure((size_t)std::max(P.n_out, 1) * cap * 8);
-        a.out_nulls = (uint32_t*)q.o_nulls.ensure(cap * 4);
-        a.out_emit_seq = (int64_t*)q.o_emit.ensure(cap * 8);
-        a.out_sub = (int64_t*)q.o_first.ensure(cap * 8);
+        a.out_count = counters;
         NfaArgs* h_na = (NfaArgs*)q.h_args.ensure(std::max(sizeof(NfaArgs), 2 * sizeof(ChainArgs)));
-        *h_na = a;
         NfaArgs* d_na = (NfaArgs*)q.d_args.ensure(std::max(sizeof(NfaArgs), 2 * sizeof(ChainArgs)));
-        HIPCHECK(hipMemcpyAsync(d_na, h_na, sizeof(NfaArgs), hipMemcpyHostToDevice, st));
-        HIPCHECK(hipEventRecord(e->ev[8], st));
-        nfa_run(a, d_na, st);
-        e->stats.match_launches += nrows > 0;
-        HIPCHECK(hipEventRecord(e->ev[2], st));
-        unsigned long long hc[2];
+        auto bind_out = [&]() {
+            q.out_cap = cap;
+            a.out_cap = cap;
+            a.out_ts = (int64_t*)q.o_ts.ensure(cap * 8);
+            a.out_key = (uint32_t*)q.o_key.ensure(cap * 4);
+            a.out_vals = (int64_t*)q.o_vals.ensure((size_t)std::max(P.n_out, 1) * cap * 8);
+            a.out_nulls = (uint32_t*)q.o_nulls.ensure(cap * 4);
+            a.out_emit_seq = (int64_t*)q.o_emit.ensure(cap * 8);
+            a.out_sub = (int64_t*)q.o_first.ensure(cap * 8);
+            a.out_round = timers ? (uint8_t*)q.o_round.ensure(cap) : nullptr;
+        };
         int hf[8];
-        HIPCHECK(hipMemcpyAsync(hc, counters, 16, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipMemcpyAsync(hf, flags, 32, hipMemcpyDeviceToHost, st));
+        unsigned long long hc[2];
+        // one launch; returns false when a growable buffer (outputs, scheduler log) overflowed
+        auto launch = [&](bool first) -> bool {
+            if (first) {
+                HIPCHECK(hipMemsetAsync(counters, 0, 16, st));
+                if (!(partitioned && nrows > 0)) HIPCHECK(hipMemsetAsync(flags, 0, 32, st));
+                else HIPCHECK(hipMemsetAsync(flags + 5, 0, 4, st));
+            } else {
+                HIPCHECK(hipMemsetAsync(counters + 1, 0, 8, st));  // log records of this rerun only
+            }
+            *h_na = a;
+            HIPCHECK(hipMemcpyAsync(d_na, h_na, sizeof(NfaArgs), hipMemcpyHostToDevice, st));
+            nfa_run(a, d_na, st);
+            HIPCHECK(hipMemcpyAsync(hc, counters, 16, hipMemcpyDeviceToHost, st));
+            HIPCHECK(hipMemcpyAsync(hf, flags, 32, hipMemcpyDeviceToHost, st));
+            HIPCHECK(hipStreamSynchronize(st));
+            if (hf[4]) throw CompileError(SDG_ERR_ARG, "device-resident partition key ids out of range (not from sdg_intern)");
+            if (hf[2]) {
+                e->stats.overflow += 1;
+                throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': a partition key exceeded max_partials (" +
+                                                         std::to_string(q.L.ns) + " live partial matches, or as many queued "
+                                                         "timers); raise sdg_opts.max_partials");
+            }
+            bool ok = true;
+            if (hf[0] || (int64_t)hc[0] > cap) {  // outputs: grow to what was asked for, run the batch again
+                if (!timers) {
+                    e->stats.overflow += 1;
+                    throw CompileError(SDG_ERR_CAPACITY, "match buffer overflow in query '" + h.name + "'");
+                }
+                cap = std::max<int64_t>(2 * cap, (int64_t)hc[0] + 4096);
+                ok = false;
+            }
+            if (timers && (hf[5] || (int64_t)hc[1] > q.log_cap)) {
+                q.log_cap = std::max<int64_t>(2 * q.log_cap, (int64_t)hc[1] + 1024);
+                a.T.log = (nfa::SchedLog*)q.d_log.ensure((size_t)q.log_cap * sizeof(nfa::SchedLog));
+                a.T.log_cap = q.log_cap;
+                ok = false;
+            }
+            if (!ok) {
+                bind_out();
+                HIPCHECK(hipMemsetAsync(flags, 0, 4, st));
+                HIPCHECK(hipMemsetAsync(flags + 5, 0, 4, st));
+            }
+            return ok;
+        };
+        bind_out();
+        HIPCHECK(hipEventRecord(e->ev[8], st));
+        a.list = nullptr;
+        a.round = 0;
+        for (int tries = 0; !launch(true); ++tries)  // state is double-buffered: a retry starts from the batch start
+            if (tries > 8) throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': output buffers keep overflowing");
+        e->stats.match_launches += 1;
+        q.last_timers = timers;
+        q.key_round.clear();
+        q.last_rank.clear();
+        q.last_seq_base = e->seq;
+        if (timers) {
+            // fixpoint with the global scheduler (sched.h): rerun the keys whose fires the collapse changed
+            std::vector<nfa::SchedLog> logs(hc[1]);
+            if (hc[1]) HIPCHECK(hipMemcpy(logs.data(), a.T.log, hc[1] * sizeof(nfa::SchedLog), hipMemcpyDeviceToHost));
+            auto by_key = [](const nfa::SchedLog& x, const nfa::SchedLog& y) {
+                return x.key != y.key ? x.key < y.key : x.kseq < y.kseq;
+            };
+            std::sort(logs.begin(), logs.end(), by_key);
+            while ((int64_t)q.key_hash.size() < (int64_t)K) {  // HashMap hash of each key's toString
+                const size_t k = q.key_hash.size();
+                const std::string& ks = q.string_keys ? e->strings.strs[k] : q.keystr[k];
+                q.key_hash.push_back(java_spread_hash(ks));
+            }
+            SchedSim::Result res;
+            for (int round = 1;; ++round) {
+                q.sim.simulate(e->bc, logs, q.key_hash, res);
+                if (res.diverged.empty()) break;
+                if (round > 250) throw CompileError(SDG_ERR_UNSUPPORTED, "query '" + h.name + "': scheduler fixpoint did not converge");
+                const int64_t nd = (int64_t)res.diverged.size();
+                a.list = (const uint32_t*)q.d_list.ensure(nd * 4);
+                a.fire_off = (const uint32_t*)q.d_foff.ensure((nd + 1) * 4);
+                a.fires = (const nfa::TimerFire*)q.d_fires.ensure(std::max<size_t>(1, res.fires.size()) * sizeof(nfa::TimerFire));
+                HIPCHECK(hipMemcpyAsync((void*)a.list, res.diverged.data(), nd * 4, hipMemcpyHostToDevice, st));
+                HIPCHECK(hipMemcpyAsync((void*)a.fire_off, res.fire_off.data(), (nd + 1) * 4, hipMemcpyHostToDevice, st));
+                if (!res.fires.empty())
+                    HIPCHECK(hipMemcpyAsync((void*)a.fires, res.fires.data(), res.fires.size() * sizeof(nfa::TimerFire),
+                                            hipMemcpyHostToDevice, st));
+                a.nlist = (int32_t)nd;
+                a.round = (uint8_t)round;
+                for (uint32_t k : res.diverged) q.key_round[k] = (uint8_t)round;
+                while (!launch(false))
+                    if (hf[0] || (int64_t)hc[0] > q.out_cap)  // the reruns' outputs need room next to the first run's
+                        throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': output buffer overflow in a scheduler rerun");
+                e->stats.match_launches += 1;
+                std::vector<nfa::SchedLog> fresh(hc[1]);
+                if (hc[1]) HIPCHECK(hipMemcpy(fresh.data(), a.T.log, hc[1] * sizeof(nfa::SchedLog), hipMemcpyDeviceToHost));
+                std::vector<nfa::SchedLog> kept;  // the diverged keys' old records go, the reruns' come in
+                kept.reserve(logs.size() + fresh.size());
+                for (const auto& L : logs)
+                    if (!std::binary_search(res.diverged.begin(), res.diverged.end(), L.key)) kept.push_back(L);
+                std::sort(fresh.begin(), fresh.end(), by_key);
+                logs.clear();
+                std::merge(kept.begin(), kept.end(), fresh.begin(), fresh.end(), std::back_inserter(logs), by_key);
+            }
+            q.sim.commit();
+            q.last_rank = std::move(res.rank);
+            nfa_commit(q.cur_bits.as<uint8_t>(), q.ran_bits.as<uint8_t>(), q.arena_keys, st);
+        }
+        HIPCHECK(hipEventRecord(e->ev[2], st));
         HIPCHECK(hipStreamSynchronize(st));
         float ms_kg = 0, ms_m = 0, t;
         HIPCHECK(hipEventElapsedTime(&ms_kg, e->ev[0], e->ev[1]));
@@ -652,21 +882,10 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         HIPCHECK(hipEventElapsedTime(&t, e->ev[8], e->ev[2]));
         e->stats.ms_nfa += t;
         e->stats.events += nrows;
-        if (hf[4]) throw CompileError(SDG_ERR_ARG, "device-resident partition key ids out of range (not from sdg_intern)");
-        if (hf[0]) {
-            e->stats.overflow += 1;
-            throw CompileError(SDG_ERR_CAPACITY, "match buffer overflow in query '" + h.name + "'");
-        }
-        if (hf[2]) {
-            e->stats.overflow += 1;
-            throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': a partition key exceeded max_partials (" +
-                                                     std::to_string(q.L.ns) + " live partial matches); raise sdg_opts.max_partials");
-        }
         q.out_n = (int64_t)hc[0];
         q.polled = false;
         e->stats.matches += q.out_n;
         e->stats.path = 1;
-        q.seq += nrows;
         return true;
     }
     // ---- 3. chain matcher -------------------------------------------------------------------------------
@@ -690,7 +909,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     a.K = (int32_t)K;
     a.orig = v_orig;
     for (int k = 0; k < nc; ++k) { a.cols[k] = v_cols[k]; a.nulls[k] = v_nulls[k]; }
-    a.seq_base = q.seq;
+    a.seq_base = e->seq + (d_vpos ? 0 : pos_off);  // emission seq = seq_base + orig (view row or position)
     a.s0 = h.stream_pos(P.st[0].stream);
     a.s1 = P.n_states > 1 ? h.stream_pos(P.st[1].stream) : a.s0;
     a.out_cap = cap;
@@ -864,7 +1083,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     q.polled = false;
     e->stats.matches += q.out_n;
     e->stats.path = 0;
-    q.seq += nrows;
+    q.last_timers = false;
     return true;
     };
     if (!run(try_fused)) run(false);
@@ -886,6 +1105,14 @@ void drain(sdg_engine* e, QueryRt& q) {
     int64_t* vals = first + n;
     uint32_t* nulls = (uint32_t*)(vals + (size_t)na * n);
     hipStream_t st = e->stream;
+    std::vector<uint32_t> okey;
+    std::vector<uint8_t> oround;
+    if (q.last_timers) {  // timer matches: keep each rerun key's last round, rank the fires of a position
+        okey.resize(n);
+        oround.resize(n);
+        HIPCHECK(hipMemcpyAsync(okey.data(), q.o_key.p, n * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(oround.data(), q.o_round.p, n, hipMemcpyDeviceToHost, st));
+    }
     HIPCHECK(hipMemcpyAsync(ts, q.o_ts.p, n * 8, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipMemcpyAsync(emit, q.o_emit.p, n * 8, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipMemcpyAsync(first, q.o_first.p, n * 8, hipMemcpyDeviceToHost, st));
@@ -895,21 +1122,36 @@ void drain(sdg_engine* e, QueryRt& q) {
                                 hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
     if (!q.nulls_valid) std::memset(nulls, 0, (size_t)n * 4);
-    std::vector<int64_t> ord(n);
-    std::iota(ord.begin(), ord.end(), 0);
+    std::vector<int64_t> ord;
+    ord.reserve(n);
+    for (int64_t i = 0; i < n; ++i) {
+        if (q.last_timers) {
+            auto kr = q.key_round.find(okey[i]);
+            if (oround[i] != (kr == q.key_round.end() ? 0 : kr->second)) continue;  // superseded by a rerun
+            if (first[i] < 0) {  // timer match: the fire's rank among the position's fires (scheduler order)
+                const int sch = (int)((first[i] >> 48) & 0x7F);
+                const uint32_t g = (uint32_t)(emit[i] - q.last_seq_base);
+                auto it = q.last_rank.find(SchedSim::rank_key(g, sch, okey[i]));
+                const int64_t r = it == q.last_rank.end() ? 0 : it->second;
+                first[i] = INT64_MIN | (r << 24) | (first[i] & 0xFFFFFF);
+            }
+        }
+        ord.push_back(i);
+    }
+    const int64_t nk = (int64_t)ord.size();
     std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
         return emit[x] != emit[y] ? emit[x] < emit[y] : first[x] < first[y];
     });
     const size_t b = q.acc_ts.size();
-    q.acc_ts.resize(b + n);
-    q.acc_seq.resize(b + n);
+    q.acc_ts.resize(b + nk);
+    q.acc_seq.resize(b + nk);
     q.acc_vals.resize(na);
     q.acc_nulls.resize(na);
     for (int j = 0; j < na; ++j) {
-        q.acc_vals[j].resize(b + n);
-        q.acc_nulls[j].resize(b + n);
+        q.acc_vals[j].resize(b + nk);
+        q.acc_nulls[j].resize(b + nk);
     }
-    for (int64_t i = 0; i < n; ++i) {
+    for (int64_t i = 0; i < nk; ++i) {
         const int64_t s = ord[i];
         q.acc_ts[b + i] = ts[s];
         q.acc_seq[b + i] = emit[s];
@@ -918,6 +1160,46 @@ void drain(sdg_engine* e, QueryRt& q) {
             q.acc_nulls[j][b + i] = (nulls[s] >> j) & 1u;
         }
     }
+}
+
+// the batch clock (sched.h BatchClock): playback = TimestampGeneratorImpl.setCurrentTimestamp per position (an
+// event or advance_time with ts >= clock advances it and runs the TimeChangeListeners); live = only advance_time
+// points move the modelled wall clock, each running live_fire_until
+void build_clock(sdg_engine* e, int64_t G) {
+    BatchClock& bc = e->bc;
+    const bool playback = e->app.playback;
+    bc.G = G;
+    bc.clock0 = e->clock;
+    bc.clk.resize(G);
+    bc.adv.resize(G);
+    bc.nadv.resize(G + 1);
+    int64_t c = e->clock, g = 0;
+    std::vector<int64_t> tmp;
+    for (const PushChunk& ch : e->pending) {
+        const int64_t* ts = ch.ts.data();
+        if (ch.device) {  // device-resident timestamps: read back (only apps with absent states build a clock)
+            tmp.resize(ch.n);
+            if (ch.n) HIPCHECK(hipMemcpy(tmp.data(), ch.d_ts, ch.n * 8, hipMemcpyDeviceToHost));
+            ts = tmp.data();
+        }
+        for (int64_t r = 0; r < ch.n; ++r, ++g) {
+            const int64_t t = ts[r];
+            if (playback) {
+                bc.adv[g] = t >= c;
+                if (t >= c) c = t;
+            } else {
+                bc.adv[g] = ch.stream == -1;  // advance_time points only
+                if (ch.stream == -1 && t > c) c = t;
+            }
+            bc.clk[g] = c;
+        }
+    }
+    bc.nadv[G] = (uint32_t)G;
+    for (int64_t x = G - 1; x >= 0; --x) bc.nadv[x] = bc.adv[x] ? (uint32_t)x : bc.nadv[x + 1];
+    int64_t* dc = (int64_t*)e->d_clk.ensure((size_t)std::max<int64_t>(G, 1) * 8);
+    uint32_t* dn = (uint32_t*)e->d_nadv.ensure((size_t)(G + 1) * 4);
+    if (G) HIPCHECK(hipMemcpyAsync(dc, bc.clk.data(), G * 8, hipMemcpyHostToDevice, e->stream));
+    HIPCHECK(hipMemcpyAsync(dn, bc.nadv.data(), (G + 1) * 4, hipMemcpyHostToDevice, e->stream));
 }
 
 int do_flush(sdg_engine* e) {
@@ -940,10 +1222,16 @@ int do_flush(sdg_engine* e) {
             e->pending_n = 0;
         }
     } consume{e};
+    int64_t G = 0;
+    for (auto& c : e->pending) G += c.n;
+    if (G >= (int64_t)0xFFFFFFF0) throw CompileError(SDG_ERR_CAPACITY, "a flush holds more than 2^32 - 16 events");
+    if (e->any_sched) build_clock(e, G);
     for (auto& q : e->qs) {
         drain(e, *q);  // earlier unpolled results go to the backlog first
         flush_query(e, *q);
     }
+    if (e->any_sched && G > 0) e->clock = e->bc.clk[G - 1];
+    e->seq += G;
     e->stats.ms_total = e->stats.ms_keygroup + e->stats.ms_match;
     return SDG_OK;
 }
@@ -989,11 +1277,6 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             e->max_partials = opts->max_partials;
         }
         auto hqs = compile_app(e->app, e->strings);
-        for (auto& h : hqs)
-            for (int i = 0; i < h.plan.n_states; ++i)
-                if (h.plan.st[i].kind == PK_ABSENT)
-                    throw CompileError(SDG_ERR_UNSUPPORTED, "query '" + h.name + "': absent states (not ... for) need "
-                                                                "the timer path, not in this build");
         if (!e->compile_only) {
             int ndev = 0;
             if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
@@ -1010,7 +1293,10 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             auto q = std::make_unique<QueryRt>();
             q->hq = std::move(h);
             if (e->force_generic) q->hq.plan.chain = 0;
-            q->L = nfa::make_layout(q->hq.plan.n_states, std::max(q->hq.plan.n_cols, 1), e->max_partials);
+            const Plan& P = q->hq.plan;
+            q->L = nfa::make_layout(P.n_states, std::max(P.n_cols, 1), e->max_partials, P.n_sched);
+            q->sim.setup(P.n_sched, P.partitioned, !P.playback);
+            e->any_sched |= P.n_sched > 0;
             for (size_t i = 0; i < q->hq.key_kind.size(); ++i)
                 if (q->hq.key_attr[i] >= 0 && q->hq.key_kind[i] != VK_STR) q->string_keys = false;
             if (!e->compile_only) upload_plan(e.get(), *q);
@@ -1102,6 +1388,36 @@ int sdg_push(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const void
     });
 }
 
+int sdg_push_mixed(sdg_engine* e, int64_t n, const int32_t* streams, const int64_t* ts, int32_t n_attrs,
+                   const int64_t* const* slots, const uint8_t* const* nulls) {
+    if (!e || n < 0 || (n > 0 && (!ts || !streams || !slots)) || n_attrs < 0) return fail(SDG_ERR_ARG, "bad push arguments");
+    return guarded([&]() {
+        PushChunk c;
+        c.stream = -2;
+        c.n = n;
+        c.device = false;
+        c.ts.assign(ts, ts + n);
+        c.rstream.assign(streams, streams + n);
+        int32_t na = 0;
+        for (int64_t r = 0; r < n; ++r) {
+            if (c.rstream[r] < 0 || c.rstream[r] >= (int)e->stream_types.size())
+                throw std::invalid_argument("bad stream index in a mixed push");
+            na = std::max<int32_t>(na, (int32_t)e->stream_types[c.rstream[r]].size());
+        }
+        if (na > n_attrs) throw std::invalid_argument("a row's stream has more attributes than n_attrs");
+        c.cols.resize(na);
+        c.nulls.resize(na);
+        for (int32_t a = 0; a < na; ++a) {
+            c.cols[a].assign((const uint8_t*)slots[a], (const uint8_t*)slots[a] + n * 8);
+            if (nulls && nulls[a]) c.nulls[a].assign(nulls[a], nulls[a] + n);
+        }
+        e->pending_n += n;
+        e->pending.push_back(std::move(c));
+        if (e->pending_n >= e->capacity) return do_flush(e);
+        return (int)SDG_OK;
+    });
+}
+
 int sdg_push_device(sdg_engine* e, int stream, int64_t n, const int64_t* d_ts, const void* const* d_cols,
                     const uint8_t* const* d_nulls) {
     if (!e || stream < 0 || stream >= (int)e->stream_types.size() || n < 0)
@@ -1126,9 +1442,23 @@ int sdg_push_device(sdg_engine* e, int stream, int64_t n, const int64_t* d_ts, c
 
 int64_t sdg_pending(sdg_engine* e) { return e ? e->pending_n : 0; }
 
-int sdg_advance_time(sdg_engine* e, int64_t) {
+int sdg_advance_time(sdg_engine* e, int64_t ts) {
     if (!e) return fail(SDG_ERR_ARG, "null engine");
-    return SDG_OK;  // no scheduler-driven states on the device path in this build
+    return guarded([&]() {
+        PushChunk c;  // a position of its own in the next flush
+        c.stream = -1;
+        c.n = 1;
+        c.device = false;
+        c.ts.assign(1, ts);
+        e->pending.push_back(std::move(c));
+        return (int)SDG_OK;
+    });
+}
+
+int sdg_start(sdg_engine* e, int64_t ts) {
+    if (!e) return fail(SDG_ERR_ARG, "null engine");
+    if (!e->app.playback && e->seq == 0 && e->pending.empty()) e->clock = ts;
+    return SDG_OK;
 }
 
 int sdg_flush(sdg_engine* e) {

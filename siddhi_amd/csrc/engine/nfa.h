@@ -73,13 +73,14 @@ struct TQ {
 
 // scheduler log (device -> host scheduler simulation): every fire a key run performs and every notify time it
 // pushes, in the key's order (kseq)
-enum : uint8_t { LOG_PUSH = 0, LOG_FIRE = 1, LOG_POP = 2 };
+enum : uint8_t { LOG_PUSH = 0, LOG_FIRE = 1, LOG_POP = 2, LOG_FIRE_END = 3 };
 constexpr uint8_t ORIGIN_EVENT = 0xFF;
 struct SchedLog {
     uint32_t key;
     uint32_t kseq;
     uint32_t g;       // batch position: the event being processed, or where the fire happened
-    uint8_t type;     // LOG_PUSH / LOG_FIRE / LOG_POP (a fire dequeued t)
+    uint8_t type;     // LOG_PUSH / LOG_FIRE / LOG_POP (a fire dequeued t) / LOG_FIRE_END (t: the largest clock the
+                      // fire would have behaved identically with -- the scheduler may run it later)
     uint8_t sched;    // PUSH: scheduler the time went to; FIRE / POP: scheduler that fired
     uint8_t origin;   // PUSH: ORIGIN_EVENT (processing the event at g, incl. partitionCreated) or the scheduler
                       //       whose fire at g pushed it
@@ -162,17 +163,22 @@ inline Layout make_layout(int n_states, int n_cols, int ns, int n_sched = 0) {
     return L;
 }
 
-struct Ctx;
+template <bool TM>
+struct CtxT;
 
 // bytecode accessor over a StateEvent (StateEvent.getStreamEvent(int[]) + attribute)
-struct SEAcc {
-    Ctx* c;
+template <bool TM>
+struct SEAccT {
+    CtxT<TM>* c;
     int16_t se;
     SDG_HD void load(int slot, int col, int chain, uint8_t kind, int64_t* v, bool* null);
     SDG_HD bool slot_empty(int slot, int chain);
 };
 
-struct Ctx {
+// TM: the query has absent states (timer code compiled in); without them the kernel keeps its registers for
+// the plain processors
+template <bool TM>
+struct CtxT {
     const Plan* P;
     const Instr* code;
     const int64_t* consts;
@@ -187,6 +193,8 @@ struct Ctx {
     int64_t* emit_seq;
     int64_t* emit_sub;
     uint32_t* emit_key;
+    uint8_t* emit_round;  // scheduler round of the run (nullptr: not recorded)
+    uint8_t round;
     unsigned long long* emit_count;
     int64_t emit_cap;
     int* flags;
@@ -199,6 +207,7 @@ struct Ctx {
     const TimerFire* fires;  // explicit fire list of this key (nullptr: ideal mode)
     int32_t nfires, fi;
     int64_t clock;           // currentTime()
+    int64_t clk_hi;          // during a fire: the largest clock that gives the same result (see LOG_FIRE_END)
     int64_t pos;             // batch position being processed (-1: before position 0)
     int32_t fsched;          // scheduler whose fire is running (-1: event processing)
 
@@ -375,10 +384,10 @@ struct Ctx {
 
     // ---- scheduler ---------------------------------------------------------------------------------------
     SDG_HD bool is_absent(int p) const {  // instanceof AbsentPreStateProcessor
-        return P->st[p].kind == PK_ABSENT || (P->st[p].kind == PK_LOGICAL && P->st[p].absent);
+        return TM && (P->st[p].kind == PK_ABSENT || (P->st[p].kind == PK_LOGICAL && P->st[p].absent));
     }
     SDG_HD void log_rec(uint8_t type, int sch, uint8_t origin, int64_t t) {
-        if (!T.log) return;
+        if (!TM || !T.log) return;
         const unsigned long long i = __atomic_fetch_add(T.log_count, 1ull, __ATOMIC_RELAXED);
         const uint32_t kseq = head().kseq++;
         if ((int64_t)i >= T.log_cap) {  // counted: the host grows the log and reruns
@@ -397,6 +406,7 @@ struct Ctx {
     }
     // Scheduler.notifyAt :113-127 for this key (SchedulerState created on demand: computeIfAbsent)
     SDG_HD void notify_at(int sch, int64_t t) {
+        if (!TM) return;
         TQ& q = tq(sch);
         if (q.n >= L.qcap) { set_ovf(); return; }
         if (q.n == 0) {
@@ -432,10 +442,11 @@ struct Ctx {
     // state is ever read again (start states are initialised, so never destroyed), so it is the one reset here,
     // at the end of each event / fire (every getState/returnState scope of the reference has ended by then)
     SDG_HD void absent_gc() {
+        if (!TM) return;
         for (int i = 0; i < P->n_sched; ++i) {
             const int p = P->sched_state[i];
             const StateRow& r = P->st[p];
-            if (r.kind == PK_ABSENT && !r.is_start && ps(p).pn == 0 && ps(p).nw == 0) ps(p).last_sched = 0;
+            if ((TM && r.kind == PK_ABSENT) && !r.is_start && ps(p).pn == 0 && ps(p).nw == 0) ps(p).last_sched = 0;
         }
     }
 
@@ -473,7 +484,7 @@ struct Ctx {
     SDG_HD bool filter(int p, int16_t s) {
         const StateRow& r = P->st[p];
         const FastPred& f = P->fast[p];
-        SEAcc acc{this, s};
+        SEAccT<TM> acc{this, s};
         if (f.kind == FP_TRUE) return true;
         if (f.kind != FP_NONE) return fast_pass(f, acc);
         return pass(code, r.filter, consts, acc, stk, stride);
@@ -491,8 +502,9 @@ struct Ctx {
         emit_seq[slot] = cur_seq;
         emit_sub[slot] = cur_sub++;
         emit_key[slot] = key;
+        if (emit_round) emit_round[slot] = round;
         uint32_t nm = 0;
-        SEAcc acc{this, s};
+        SEAccT<TM> acc{this, s};
         for (int j = 0; j < P->n_out; ++j) {
             int64_t v;
             bool nl;
@@ -527,7 +539,7 @@ struct Ctx {
             const StateRow& r = P->st[p];
             PState& st = ps(p);
             if (r.kind == PK_LOGICAL) {  // LogicalPreStateProcessor.addState :43-62
-                if (r.absent && !st.active) return;  // AbsentLogicalPreStateProcessor.addState :77-97
+                if ((TM && r.absent) && !st.active) return;  // AbsentLogicalPreStateProcessor.addState :77-97
                 int q = r.partner;
                 if (r.is_start || r.seq) {
                     if (st.nw == 0) push(newe(p), st.nw, s);
@@ -536,14 +548,14 @@ struct Ctx {
                     push(newe(p), st.nw, s);
                     push(newe(q), ps(q).nw, s);
                 }
-                if (r.absent && !r.is_start && r.waiting_ms != -1) {
+                if ((TM && r.absent) && !r.is_start && r.waiting_ms != -1) {
                     notify_at(r.sched, se(s).ts + r.waiting_ms);
                     const StateRow& pr = P->st[q];
-                    if (pr.kind == PK_LOGICAL && pr.absent) notify_at(pr.sched, se(s).ts + pr.waiting_ms);
+                    if (pr.kind == PK_LOGICAL && (TM && pr.absent)) notify_at(pr.sched, se(s).ts + pr.waiting_ms);
                 }
                 return;
             }
-            if (r.kind == PK_ABSENT) {  // AbsentStreamPreStateProcessor.addState :80-103
+            if ((TM && r.kind == PK_ABSENT)) {  // AbsentStreamPreStateProcessor.addState :80-103
                 if (!st.active) return;
                 if (r.seq) st.nw = 0;
                 push(newe(p), st.nw, s);
@@ -575,7 +587,7 @@ struct Ctx {
         int16_t c = clone(s);
         if (c == NIL) return;
         se(c).type = T_CURRENT;
-        if (r.kind == PK_LOGICAL && r.absent) {  // AbsentLogicalPreStateProcessor.addEveryState :99-118
+        if (r.kind == PK_LOGICAL && (TM && r.absent)) {  // AbsentLogicalPreStateProcessor.addEveryState :99-118
             if (slots(c)[p] != NIL) se(c).ts = rc(nd(slots(c)[p]).rec).ts;  // the last arrived event's time
             slots(c)[p] = NIL;
             slots(c)[r.partner] = NIL;
@@ -589,7 +601,7 @@ struct Ctx {
             slots(c)[r.partner] = NIL;
             push(newe(r.partner), ps(r.partner).nw, c);
         }
-        if (r.kind == PK_ABSENT) {  // AbsentStreamPreStateProcessor.addEveryState :105-124
+        if ((TM && r.kind == PK_ABSENT)) {  // AbsentStreamPreStateProcessor.addEveryState :105-124
             ps(p).last_sched = se(s).ts + r.waiting_ms;
             notify_at(r.sched, ps(p).last_sched);
         }
@@ -621,7 +633,7 @@ struct Ctx {
             }
             return;
         }
-        if (r.kind == PK_ABSENT) {  // AbsentStreamPreStateProcessor.resetState :126-148
+        if ((TM && r.kind == PK_ABSENT)) {  // AbsentStreamPreStateProcessor.resetState :126-148
             st.pn = 0;
             if (r.is_start) {
                 if (r.seq && r.next_every < 0 && r.next >= 0 && ps(r.next).pn != 0) return;
@@ -742,7 +754,7 @@ struct Ctx {
     }
     SDG_HD void post_logical(int p, int16_t s) {  // LogicalPostStateProcessor.process :59-87
         const StateRow& r = P->st[p];
-        if (r.absent) {  // AbsentLogicalPostStateProcessor.process :37-49
+        if ((TM && r.absent)) {  // AbsentLogicalPostStateProcessor.process :37-49
             ps(p).changed = 1;
             ps(p).returned = 1;
             ps(p).last_arrival = rc(nd(slots(s)[p]).rec).ts;  // updateLastArrivalTime
@@ -750,7 +762,7 @@ struct Ctx {
         }
         if (!r.logical_or) {
             const StateRow& pr = P->st[r.partner];
-            const bool proceed = (pr.kind == PK_LOGICAL && pr.absent) ? partner_can_proceed(r.partner, s)
+            const bool proceed = (pr.kind == PK_LOGICAL && (TM && pr.absent)) ? partner_can_proceed(r.partner, s)
                                                                        : slots(s)[r.partner] != NIL;
             if (proceed) post_stream(p, s);
             else ps(p).changed = 1;
@@ -763,7 +775,9 @@ struct Ctx {
         switch (P->st[p].kind) {
             case PK_COUNT: post_count(p, s); break;
             case PK_LOGICAL: post_logical(p, s); break;
-            case PK_ABSENT: post_absent(p, s); break;
+            case PK_ABSENT:
+                if (TM) post_absent(p, s);
+                break;
             default: post_stream(p, s); break;
         }
     }
@@ -823,13 +837,13 @@ struct Ctx {
     SDG_HD void process_and_return(int p, int16_t rec, bool selector) {
         const StateRow& r = P->st[p];
         PState& st = ps(p);
-        if (r.kind == PK_LOGICAL && r.absent) {
+        if (r.kind == PK_LOGICAL && (TM && r.absent)) {
             alogic_process_and_return(p, rec);
             return;
         }
         // AbsentStreamPreStateProcessor.processAndReturn :257-274: inactive -> nothing; otherwise the stream loop,
         // whose returned events are discarded (an arriving event only cancels absence candidates)
-        if (r.kind == PK_ABSENT) {
+        if ((TM && r.kind == PK_ABSENT)) {
             if (!st.active) return;
             selector = false;
         }
@@ -949,7 +963,12 @@ struct Ctx {
         if (r.within_every >= 0) update_state(r.within_every);
         const bool not_processed = nret == 0;
         for (int i = 0; i < nret && !ovf(); ++i) absent_send(p, ret[i]);
-        if (clock > r.waiting_ms + now) st.last_sched = clock + r.waiting_ms;
+        if (clock > r.waiting_ms + now) {
+            st.last_sched = clock + r.waiting_ms;
+            clk_hi = clock;  // the result depends on the clock itself
+        } else if (r.waiting_ms + now < clk_hi) {
+            clk_hi = r.waiting_ms + now;  // any clock up to waiting + now takes the same branch
+        }
         if (not_processed && st.last_sched < now) {
             st.last_sched = now + r.waiting_ms;
             notify_at(r.sched, st.last_sched);
@@ -1030,6 +1049,7 @@ struct Ctx {
             st.last_arrival = 0;
         }
         if (r.next_every >= 0 || (not_processed && r.is_start)) {  // schedule again
+            if (st.last_arrival == 0) clk_hi = clock;  // the next break is clock + waiting
             const int64_t nb = st.last_arrival == 0 ? clock + r.waiting_ms : st.last_arrival + r.waiting_ms;
             notify_at(r.sched, nb);
         }
@@ -1048,14 +1068,17 @@ struct Ctx {
         cur_seq = seq_base + g;
         cur_sub = INT64_MIN | ((int64_t)sch << 48);  // before the event at g; the host ranks fires across keys
         log_rec(LOG_FIRE, sch, 0, c);
+        clk_hi = INT64_MAX;
         const int p = P->sched_state[sch];
         TQ& q = tq(sch);
         while (q.n > 0 && tqt(sch)[q.h] <= c && !ovf()) {
             const int64_t t = tq_pop(sch);
             log_rec(LOG_POP, sch, 0, t);
+            if (!TM) break;
             if (P->st[p].kind == PK_ABSENT) absent_timer(p, t);
             else alogic_timer(p, t);
         }
+        log_rec(LOG_FIRE_END, sch, 0, clk_hi);
         fsched = -1;
         absent_gc();
     }
@@ -1072,7 +1095,7 @@ struct Ctx {
     }
     // every fire of this key at positions <= limit, in the reference's order
     SDG_HD void fire_until(int64_t limit) {
-        if (P->n_sched == 0) return;
+        if (!TM || P->n_sched == 0) return;
         if (fires) {  // explicit list (host scheduler simulation)
             while (fi < nfires && (int64_t)fires[fi].g <= limit && !ovf()) {
                 const TimerFire f = fires[fi++];
@@ -1107,14 +1130,14 @@ struct Ctx {
     // ---- receiver ----------------------------------------------------------------------------------------
     SDG_HD void init_key() {  // StateStreamRuntime.initPartition: init, then partitionCreated of the startups
         for (int i = 0; i < P->n_init; ++i) init(P->init_seq[i]);
-        for (int i = 0; i < P->n_startup; ++i) {
+        for (int i = 0; i < (TM ? P->n_startup : 0); ++i) {
             const int p = P->startup_seq[i];
             const StateRow& r = P->st[p];
             PState& st = ps(p);
             if (st.started) continue;  // AbsentStreamPreStateProcessor :291-308 / AbsentLogical... :331-351
             st.started = 1;
             if (r.is_start && r.waiting_ms != -1 && st.active) {
-                if (r.kind == PK_ABSENT) {
+                if ((TM && r.kind == PK_ABSENT)) {
                     st.last_sched = clock + r.waiting_ms;
                     notify_at(r.sched, st.last_sched);
                 } else {
@@ -1144,7 +1167,8 @@ struct Ctx {
     }
 };
 
-SDG_HD void SEAcc::load(int slot, int col, int chain, uint8_t kind, int64_t* v, bool* null) {
+template <bool TM>
+SDG_HD void SEAccT<TM>::load(int slot, int col, int chain, uint8_t kind, int64_t* v, bool* null) {
     (void)kind;
     *v = 0;
     *null = true;
@@ -1155,7 +1179,8 @@ SDG_HD void SEAcc::load(int slot, int col, int chain, uint8_t kind, int64_t* v, 
     *v = c->vals(r)[col];
     *null = (c->rc(r).nullmask >> col) & 1u;
 }
-SDG_HD bool SEAcc::slot_empty(int slot, int chain) {
+template <bool TM>
+SDG_HD bool SEAccT<TM>::slot_empty(int slot, int chain) {
     if (slot < 0 || slot >= c->L.n_states) return true;
     return c->chain_at(se, slot, chain) == NIL;
 }
@@ -1168,14 +1193,15 @@ struct KeyEvents {
     const void* const* cols;
     const uint8_t* const* nulls;
     int64_t b, e, seq_base;
+    int64_t pos_off;          // batch position of row 0 when orig is nullptr
 };
 
-// one key's batch run: initPartition on the key's first event ever (unpartitioned queries: before position 0, as
-// SiddhiAppRuntime.start does), the timer fires due before each row, every row through the receiver, and the
-// fires after the last row up to the end of the batch
-SDG_HD void run_key(Ctx& c, const KeyEvents& ev) {
+// one key's batch run, in steps (the device composes them in run_key; the host scheduler simulation steps a key
+// itself when it has to take it over, sched.h): initPartition on the key's first event ever (unpartitioned
+// queries: before position 0, as SiddhiAppRuntime.start does), each row through the receiver, timer fires between
+template <bool TM>
+SDG_HD bool key_begin(CtxT<TM>& c, const KeyEvents& ev) {  // returns need_init (a partitioned first-seen key)
     const Plan* P = c.P;
-    const Layout& L = c.L;
     c.seq_base = ev.seq_base;
     c.fsched = -1;
     c.fi = 0;
@@ -1187,42 +1213,53 @@ SDG_HD void run_key(Ctx& c, const KeyEvents& ev) {
         c.head().flags = 2;
     }
     c.head().kseq = 0;
-    for (int i = 0; i < L.n_sched; ++i)
+    for (int i = 0; i < c.L.n_sched; ++i)
         if (c.tq(i).n > 0) c.tq(i).earliest = 0;  // positions restart with every batch
-    bool need_init = fresh;
-    if (need_init && !P->partitioned) {
+    if (fresh && !P->partitioned) {
+        c.init_key();
+        return false;
+    }
+    return fresh;
+}
+SDG_HD int64_t key_pos(const KeyEvents& ev, int64_t p) { return ev.orig ? (int64_t)ev.orig[p] : ev.pos_off + p; }
+// row p (fires due before it have run); returns false when the key overflowed
+template <bool TM>
+SDG_HD bool key_row(CtxT<TM>& c, const KeyEvents& ev, int64_t p, bool& need_init) {
+    const Plan* P = c.P;
+    const int64_t g = key_pos(ev, p);
+    c.pos = g;
+    if (TM && P->n_sched) c.clock = c.T.clk[g];
+    if (need_init) {  // PartitionRuntimeImpl.initPartition for a first-seen key (after the clock advance)
         c.init_key();
         need_init = false;
     }
-    for (int64_t p = ev.b; p < ev.e && !c.ovf(); ++p) {
-        const int64_t g = ev.orig ? (int64_t)ev.orig[p] : p;
-        c.fire_until(g);  // TimeChangeListener.onTimeChange runs before the event is processed
-        if (c.ovf()) break;
-        c.pos = g;
-        if (P->n_sched) c.clock = c.T.clk[g];
-        if (need_init) {  // PartitionRuntimeImpl.initPartition for a first-seen key (after the clock advance)
-            c.init_key();
-            need_init = false;
-        }
-        c.maybe_gc();
-        int16_t r = c.rc_alloc();
-        if (r == NIL) break;
-        Rec& rec = c.rc(r);
-        const int64_t ts = ev.ts[p];
-        rec.ts = ts;
-        int64_t* v = c.vals(r);
-        uint32_t nm = 0;
-        for (int col = 0; col < P->n_cols; ++col) {
-            v[col] = load_col(ev.cols[col], P->col_kind[col], p);
-            if (ev.nulls[col] && ev.nulls[col][p]) nm |= 1u << col;
-        }
-        rec.nullmask = nm;
-        c.cur_seq = ev.seq_base + g;
-        c.cur_sub = 0;
-        c.on_event(ev.qstream ? ev.qstream[p] : 0, r, ts);
-        if (P->n_sched) c.absent_gc();
+    c.maybe_gc();
+    int16_t r = c.rc_alloc();
+    if (r == NIL) return false;
+    Rec& rec = c.rc(r);
+    const int64_t ts = ev.ts[p];
+    rec.ts = ts;
+    int64_t* v = c.vals(r);
+    uint32_t nm = 0;
+    for (int col = 0; col < P->n_cols; ++col) {
+        v[col] = load_col(ev.cols[col], P->col_kind[col], p);
+        if (ev.nulls[col] && ev.nulls[col][p]) nm |= 1u << col;
     }
-    if (P->n_sched && c.T.G > 0 && !c.ovf()) {
+    rec.nullmask = nm;
+    c.cur_seq = ev.seq_base + g;
+    c.cur_sub = 0;
+    c.on_event(ev.qstream ? ev.qstream[p] : 0, r, ts);
+    if (TM && P->n_sched) c.absent_gc();
+    return !c.ovf();
+}
+template <bool TM>
+SDG_HD void run_key(CtxT<TM>& c, const KeyEvents& ev) {
+    bool need_init = key_begin(c, ev);
+    for (int64_t p = ev.b; p < ev.e && !c.ovf(); ++p) {
+        c.fire_until(key_pos(ev, p));  // TimeChangeListener.onTimeChange runs before the event is processed
+        if (c.ovf() || !key_row(c, ev, p, need_init)) break;
+    }
+    if (TM && c.P->n_sched && c.T.G > 0 && !c.ovf()) {
         c.fire_until(c.T.G - 1);
         c.clock = c.T.clk[c.T.G - 1];
     }

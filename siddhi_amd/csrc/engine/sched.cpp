@@ -2,6 +2,7 @@
 #include "sched.h"
 
 #include <algorithm>
+#include <queue>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -150,78 +151,116 @@ void SchedSim::remove_if_empty(int sch, uint32_t key) {  // returnState / return
 }
 
 void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& logs,
-                        const std::vector<int32_t>& key_hash, Result& out) {
+                        const std::vector<int32_t>& key_hash, const KeyRows& rows,
+                        const std::function<KeyRun*(uint32_t)>& take_over, Result& out) {
     using nfa::SchedLog;
     work_ = cur_;
     hash_ = &key_hash;
     out = Result{};
-    // per-key cursors over the log (sorted by key, kseq); event-origin pushes by position
-    struct Cur {
-        size_t i = 0, e = 0;
-        bool div = false;
-        std::vector<nfa::TimerFire> fires;
+    constexpr size_t NONE = ~size_t(0);
+    enum : uint8_t { DEV = 0, PENDING = 1, HOST = 2 };  // the key's history so far: its device run / a device fire
+                                                      // the scheduler has not made yet / stepped on the host
+    struct KC {
+        size_t i = 0, e = 0;                 // cursor into the key's device records
+        uint8_t mode = DEV;
+        KeyRun* run = nullptr;
+        std::vector<nfa::TimerFire> fires;   // the scheduler's fires of this key so far
     };
-    std::unordered_map<uint32_t, Cur> cur;
-    std::vector<size_t> evp;
+    std::unordered_map<uint32_t, KC> kc;
+    auto posof = [&](size_t i) -> int64_t { return logs[i].g == 0xFFFFFFFFu ? -1 : (int64_t)logs[i].g; };
+    auto is_evpush = [&](size_t i) { return logs[i].type == nfa::LOG_PUSH && logs[i].origin == nfa::ORIGIN_EVENT; };
+    std::vector<size_t> evp;  // pushes made while processing events, applied at their positions
     for (size_t i = 0; i < logs.size();) {
         size_t j = i;
         while (j < logs.size() && logs[j].key == logs[i].key) ++j;
-        Cur& c = cur[logs[i].key];
+        KC& c = kc[logs[i].key];
         c.i = i;
         c.e = j;
         for (size_t x = i; x < j; ++x)
-            if (logs[x].type == nfa::LOG_PUSH && logs[x].origin == nfa::ORIGIN_EVENT) evp.push_back(x);
+            if (is_evpush(x)) evp.push_back(x);
         i = j;
     }
-    // position of a record; UINT32_MAX = before position 0 (an unpartitioned query's init at start)
-    auto posof = [&](size_t i) -> int64_t { return logs[i].g == 0xFFFFFFFFu ? -1 : (int64_t)logs[i].g; };
     std::stable_sort(evp.begin(), evp.end(), [&](size_t a, size_t b) { return posof(a) < posof(b); });
-    static const bool dbg = getenv("SDG_SCHED_DEBUG") != nullptr;
-    if (dbg) {
-        fprintf(stderr, "sim: G=%lld clock0=%lld logs=%zu\n", (long long)bc.G, (long long)bc.clock0, logs.size());
-        for (int64_t g = 0; g < bc.G; ++g)
-            fprintf(stderr, "  pos %lld clk %lld adv %d\n", (long long)g, (long long)bc.clk[g], bc.adv[g]);
-        for (const auto& L : logs)
-            fprintf(stderr, "  log key %u kseq %u g %u type %d sched %d origin %d t %lld\n", L.key, L.kseq, L.g, L.type,
-                    L.sched, L.origin, (long long)L.t);
+    auto next_fire = [&](KC& c) -> size_t {  // the key's next device fire (event pushes go by position)
+        while (c.i < c.e && is_evpush(c.i)) ++c.i;
+        return c.i < c.e && logs[c.i].type == nfa::LOG_FIRE ? c.i : NONE;
+    };
+    using HE = std::pair<int64_t, uint32_t>;
+    std::priority_queue<HE, std::vector<HE>, std::greater<HE>> fireq, rowq;
+    for (auto& kv : kc) {
+        const size_t f = next_fire(kv.second);
+        if (f != NONE) fireq.push({(int64_t)logs[f].g, kv.first});
     }
-    auto skip_events = [&](Cur& c) {
-        while (c.i < c.e && logs[c.i].type == nfa::LOG_PUSH && logs[c.i].origin == nfa::ORIGIN_EVENT) ++c.i;
+    auto first_row_at = [&](uint32_t key, int64_t g) -> int64_t {  // position of the key's first row at >= g
+        if (key >= (uint32_t)rows.K) return -1;
+        int64_t a = rows.seg_b[key], b = rows.seg_e[key];
+        while (a < b) {
+            const int64_t m = (a + b) >> 1;
+            if (rows.pos(m) < g) a = m + 1;
+            else b = m;
+        }
+        return a < (int64_t)rows.seg_e[key] ? rows.pos(a) : -1;
+    };
+    auto apply_run = [&](KC& c, uint32_t key) {  // the host run's new pops / pushes into the model
+        KeyRun* r = c.run;
+        for (; r->lread < r->lcount; ++r->lread) {
+            const SchedLog& L = r->log[r->lread];
+            if (L.type == nfa::LOG_PUSH) notify(L.sched, key, L.t);
+            else if (L.type == nfa::LOG_POP) pop(L.sched, key);
+        }
+    };
+    // replay the key on the host up to position g (its rows < g, the scheduler's fires so far except `skip_last`)
+    auto takeover = [&](uint32_t key, int64_t g, bool skip_last) {
+        KC& c = kc[key];
+        c.mode = HOST;
+        c.run = take_over(key);
+        const size_t nf = c.fires.size() - (skip_last ? 1 : 0);
+        for (size_t f = 0; f < nf; ++f) {
+            c.run->rows_before(c.fires[f].g);
+            c.run->fire(c.fires[f].sched, c.fires[f].g, c.fires[f].clock);
+        }
+        c.run->rows_before(g);
+        c.run->lread = c.run->lcount;  // what the replay pushed / popped is in the model already
+        out.taken.push_back(key);
+        const int64_t nr = c.run->next_row_pos();
+        if (nr >= 0) rowq.push({nr, key});
     };
     uint32_t rank = 0;
-    // one fire of (sch, key) at position g with currentTime() = clock: replay the run's own record of it when
-    // the run fired the same way, else model it (pops only) and mark the key for a rerun
+    // the scheduler fires (sch, key) at position g with currentTime() = clock
     auto fire = [&](int sch, uint32_t key, uint32_t g, int64_t clock) {
-        if (dbg) fprintf(stderr, "  sim fire sched %d key %u g %u clock %lld\n", sch, key, g, (long long)clock);
-        out.rank[rank_key(g, sch, key)] = rank++;
+        const uint32_t rk = rank++;
         ++out.n_fires;
-        Cur& c = cur[key];
+        KC& c = kc[key];
         c.fires.push_back(nfa::TimerFire{g, sch, clock});
-        skip_events(c);
-        if (!c.div && c.i < c.e && logs[c.i].type == nfa::LOG_FIRE && logs[c.i].g == g && logs[c.i].sched == sch &&
-            logs[c.i].t == clock) {
-            ++c.i;
-            while (c.i < c.e) {
-                const SchedLog& L = logs[c.i];
-                if (L.type == nfa::LOG_POP) {
-                    const KS& k = work_.sc[L.sched].ks[key];
-                    if (L.sched != sch || k.q.empty() || k.q.front() != L.t) {
-                        c.div = true;  // inconsistent with the model: redo this key
-                        break;
-                    }
-                    pop(sch, key);
-                } else if (L.type == nfa::LOG_PUSH && L.origin == (uint8_t)sch && L.g == g) {
-                    notify(L.sched, key, L.t);
-                } else {
-                    break;
-                }
-                ++c.i;
+        if (c.mode != HOST) {
+            const size_t f = next_fire(c);
+            bool ok = f != NONE && logs[f].sched == sch && (int64_t)logs[f].g <= (int64_t)g;
+            size_t end = NONE;
+            if (ok) {  // the fire's records end with LOG_FIRE_END (t = the largest clock it holds for)
+                for (size_t x = f + 1; x < c.e; ++x)
+                    if (logs[x].type == nfa::LOG_FIRE_END) { end = x; break; }
+                ok = end != NONE && (logs[f].g == g ? logs[f].t == clock : clock <= logs[end].t && c.mode == PENDING);
             }
-            if (!c.div) return;
+            if (ok) {
+                for (size_t x = f + 1; x < end; ++x) {
+                    const SchedLog& L = logs[x];
+                    if (L.type == nfa::LOG_POP) pop(L.sched, key);
+                    else if (L.type == nfa::LOG_PUSH) notify(L.sched, key, L.t);
+                }
+                if (logs[f].g != g) ++out.n_shifted;
+                out.rank[rank_key(logs[f].g, sch, key)] = Slot{g, rk};
+                c.i = end + 1;
+                c.mode = DEV;
+                const size_t nf = next_fire(c);
+                if (nf != NONE) fireq.push({(int64_t)logs[nf].g, key});
+                return;
+            }
+            takeover(key, g, true);
         }
-        c.div = true;
-        KS& k = work_.sc[sch].ks[key];  // sendTimerEvents: pop the FIFO while its head is due
-        while (!k.q.empty() && k.q.front() <= clock) pop(sch, key);
+        c.run->rows_before(g);
+        c.run->fire(sch, g, clock);
+        apply_run(c, key);
+        out.rank[rank_key(g, sch, key)] = Slot{g, rk};
     };
     auto next_due = [&](int64_t from) -> int64_t {
         int64_t hmin = INT64_MAX;
@@ -233,19 +272,23 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
         return x >= bc.G ? bc.G : (int64_t)bc.nadv[x];
     };
     size_t ep = 0;
-    for (; ep < evp.size() && posof(evp[ep]) < 0; ++ep) notify(logs[evp[ep]].sched, logs[evp[ep]].key, logs[evp[ep]].t);
+    for (; ep < evp.size() && posof(evp[ep]) < 0; ++ep)  // an unpartitioned query's init at start
+        if (kc[logs[evp[ep]].key].mode == DEV) notify(logs[evp[ep]].sched, logs[evp[ep]].key, logs[evp[ep]].t);
     int64_t g = 0;
-    while (g < bc.G) {
+    while (true) {
         int64_t nxt = ep < evp.size() ? posof(evp[ep]) : bc.G;
         nxt = std::min(nxt, next_due(g));
+        if (!fireq.empty()) nxt = std::min(nxt, fireq.top().first);
+        if (!rowq.empty()) nxt = std::min(nxt, rowq.top().first);
+        nxt = std::max(nxt, g);
         if (nxt >= bc.G) break;
         g = nxt;
+        // 1. the clock advance at g: TimeChangeListeners (playback) / live_fire_until
         if (bc.adv[g]) {
             rank = 0;
             const int64_t clock = bc.clk[g];
             if (!live_) {
-                // TimeChangeListeners in registration order; each: TreeMultimap of the due states, one per time
-                for (int s = 0; s < n_sched_; ++s) {
+                for (int s = 0; s < n_sched_; ++s) {  // registration order; per listener a TreeMultimap, one per time
                     SchedState& S = work_.sc[s];
                     std::vector<std::pair<int64_t, uint32_t>> W;
                     for (auto it = S.due.begin(); it != S.due.end() && it->first <= clock; ++it)
@@ -254,9 +297,8 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
                     for (auto& w : W) remove_if_empty(s, w.second);  // returnAllStates
                 }
             } else {
-                // live_fire_until: the earliest due (time, creation) across every scheduler, one at a time
                 int64_t now = g > 0 ? bc.clk[g - 1] : bc.clock0;
-                while (true) {
+                while (true) {  // the earliest due (time, creation) across every scheduler, one at a time
                     int bs = -1;
                     int64_t bt = 0;
                     OKey bk{};
@@ -274,29 +316,52 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
                 }
             }
         }
-        while (ep < evp.size() && posof(evp[ep]) == g) {  // the event's own pushes (after the fires)
-            const SchedLog& L = logs[evp[ep]];
-            notify(L.sched, L.key, L.t);
-            ++ep;
+        // 2. device fires at <= g the scheduler did not make (yet): the key waits for its delayed fire
+        while (!fireq.empty() && fireq.top().first <= g) {
+            const uint32_t key = fireq.top().second;
+            const int64_t fg = fireq.top().first;
+            fireq.pop();
+            KC& c = kc[key];
+            if (c.mode != DEV) continue;
+            const size_t f = next_fire(c);
+            if (f == NONE || (int64_t)logs[f].g != fg) continue;  // made already
+            c.mode = PENDING;
+            const int64_t r = first_row_at(key, fg);  // an event of the key before the delayed fire: diverged
+            if (r >= 0) rowq.push({r, key});
         }
+        // 3. rows at g of keys that wait for a delayed fire (diverged) or run on the host
+        while (!rowq.empty() && rowq.top().first <= g) {
+            const uint32_t key = rowq.top().second;
+            rowq.pop();
+            KC& c = kc[key];
+            if (c.mode == DEV) continue;
+            if (c.mode == PENDING) takeover(key, g, false);
+            if (c.run->next_row_pos() != g) continue;
+            c.run->row_at(g);
+            apply_run(c, key);
+            const int64_t nr = c.run->next_row_pos();
+            if (nr >= 0) rowq.push({nr, key});
+        }
+        // 4. the device keys' pushes made by the event at g
+        for (; ep < evp.size() && posof(evp[ep]) == g; ++ep)
+            if (kc[logs[evp[ep]].key].mode == DEV) notify(logs[evp[ep]].sched, logs[evp[ep]].key, logs[evp[ep]].t);
         ++g;
     }
-    // fires a run performed that the scheduler did not: diverged too
-    for (auto& kv : cur) {
-        Cur& c = kv.second;
-        if (c.div) continue;
-        for (size_t x = c.i; x < c.e; ++x)
-            if (logs[x].type != nfa::LOG_PUSH || logs[x].origin != nfa::ORIGIN_EVENT) { c.div = true; break; }
+    // device fires the scheduler never made in this batch (delayed past its end): host replay without them
+    std::vector<uint32_t> late;
+    for (auto& kv : kc)
+        if (kv.second.mode == PENDING || (kv.second.mode == DEV && next_fire(kv.second) != NONE)) late.push_back(kv.first);
+    std::sort(late.begin(), late.end());
+    for (uint32_t key : late) {
+        takeover(key, bc.G, false);
+        apply_run(kc[key], key);
     }
-    for (auto& kv : cur)
-        if (kv.second.div) out.diverged.push_back(kv.first);
-    std::sort(out.diverged.begin(), out.diverged.end());
-    out.fire_off.push_back(0);
-    for (uint32_t k : out.diverged) {
-        const Cur& c = cur[k];
-        out.fires.insert(out.fires.end(), c.fires.begin(), c.fires.end());
-        out.fire_off.push_back((uint32_t)out.fires.size());
-    }
+    for (auto& kv : kc)
+        if (kv.second.mode == HOST) {
+            kv.second.run->rows_before(bc.G);
+            apply_run(kv.second, kv.first);
+        }
+    std::sort(out.taken.begin(), out.taken.end());
 }
 
 }  // namespace sdg

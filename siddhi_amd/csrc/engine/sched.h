@@ -17,13 +17,17 @@
 // keeps as a sort key instead of walking the map. Tree bins (8+ keys in one bucket of a table >= 64) are not
 // modelled (the oracle does not model them either).
 //
-// The device runs each key's NFA (nfa.h) and logs, per key and in order, every fire it performed, every notify
-// time it pushed and every time a fire popped. simulate() replays the global scheduler over those logs: where its
-// decision for a key differs from what the key's run did (a collapse delayed a fire), the key is "diverged" and is
-// rerun with the simulated fire list. Iterating converges because everything up to the first divergence is
-// consistent, so each round moves the first divergence later; at the fixpoint the per-key runs and the global
-// scheduler agree, which is the reference's single sequential execution (both are deterministic functions of the
-// same causal prefix).
+// The device runs each key's NFA (nfa.h) firing every due timer at the first clock advance that reaches it, and
+// logs, per key and in order, every fire, every pop and every notify time pushed. simulate() then replays the
+// global scheduler once over all keys, position by position, with each key's queue taken from those logs:
+//   - a fire the scheduler makes where the key's run made it: consistent;
+//   - a fire the collapse delays to a later position: still the key's result if no event of that key lies in
+//     between and the fire's outcome does not depend on the later clock (LOG_FIRE_END carries the largest clock
+//     it holds for) -- only its position in the delivery order changes;
+//   - anything else: the key diverged. From there the simulation runs that key itself on the host (KeyRun, the
+//     same nfa.h code from the key's batch-start state, with the scheduler's fire order), in lockstep.
+// So one pass yields the reference's sequential execution: every key's history is either its own device run
+// (shown consistent with the global order) or a host replay in that order.
 #pragma once
 #include <stdint.h>
 
@@ -34,6 +38,9 @@
 #include <unordered_map>
 #include <vector>
 
+#include <functional>
+
+#include "keyrun.h"
 #include "nfa.h"
 #include "plan.h"
 
@@ -53,19 +60,28 @@ std::string java_real_string(double x, bool is_float);
 // Java String.hashCode of a UTF-8 string (as UTF-16 code units), then HashMap.hash() spreading
 int32_t java_spread_hash(const std::string& s);
 
+// a batch's rows by key (the sorted view): key k's rows are [seg_b[k], seg_e[k]), row p at batch position
+// orig ? orig[p] : pos_off + p (ascending within a key)
+struct KeyRows {
+    const uint32_t* seg_b = nullptr;
+    const uint32_t* seg_e = nullptr;
+    int64_t K = 0;
+    const uint32_t* orig = nullptr;
+    int64_t pos_off = 0;
+    int64_t n = 0;
+    int64_t pos(int64_t p) const { return orig ? (int64_t)orig[p] : pos_off + p; }
+};
+
 class SchedSim {
    public:
-    struct Fire {
-        uint32_t key;
-        nfa::TimerFire f;
+    struct Slot {
+        uint32_t g;     // position of the fire in the reference's order
+        uint32_t rank;  // order among the fires of that position
     };
     struct Result {
-        std::vector<uint32_t> diverged;                      // keys whose run must be redone with `fires`
-        std::vector<uint32_t> fire_off;                      // [diverged + 1] ranges into fires
-        std::vector<nfa::TimerFire> fires;                   // the diverged keys' simulated fire lists
-        std::unordered_map<uint64_t, uint32_t> rank;         // (position, scheduler, key) -> order among the fires
-                                                             // of that position (delivery order of timer matches)
-        int64_t n_fires = 0;
+        std::vector<uint32_t> taken;                         // keys run on the host (their device run is void)
+        std::unordered_map<uint64_t, Slot> rank;             // (position in the key's run, scheduler, key) -> slot
+        int64_t n_fires = 0, n_shifted = 0;
     };
     void setup(int n_sched, bool partitioned, bool live) {
         n_sched_ = n_sched;
@@ -76,9 +92,10 @@ class SchedSim {
     bool active() const { return n_sched_ > 0; }
     // keys with queued timers (the runs a timer-only batch must include)
     void queued_keys(std::vector<uint32_t>& out) const;
-    // one round over the batch; logs must be sorted by (key, kseq). Works on a copy of the committed state.
-    void simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& logs,
-                  const std::vector<int32_t>& key_hash, Result& out);
+    // one pass over the batch; logs sorted by (key, kseq). take_over(key) returns a started KeyRun for the key
+    // (batch-start state, its rows); the caller owns it. Works on a copy of the committed state (commit()).
+    void simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& logs, const std::vector<int32_t>& key_hash,
+                  const KeyRows& rows, const std::function<KeyRun*(uint32_t)>& take_over, Result& out);
     void commit() { cur_ = work_; }
     static uint64_t rank_key(uint32_t g, int sch, uint32_t key) {
         return ((uint64_t)g << 32) ^ ((uint64_t)sch << 27) ^ (uint64_t)key * 0x9E3779B97F4A7C15ull;

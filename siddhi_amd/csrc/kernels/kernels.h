@@ -39,6 +39,8 @@ struct KeyGroupArgs {
     void* dst[MAX_COLS + 2];
     uint8_t width[MAX_COLS + 2];      // bytes per element (1, 4 or 8)
     int* key_flag;                    // non-null: set to 1 when some key >= K (the first histogram pass checks)
+    const uint32_t* orig_in;          // [n] batch position of each input row (nullptr: the row index itself);
+                                      // orig_sorted then holds positions
 };
 // bytes of workspace for n events; fills the workspace pointers of `a` from `base`
 size_t keygroup_workspace(int64_t n, int32_t K, int32_t ncols, const uint8_t* widths);
@@ -204,11 +206,17 @@ struct NfaArgs {
     const uint32_t* seg_start;        // [K] (nullptr: unpartitioned, K == 1, one segment [0, n))
     const uint32_t* seg_end;
     int32_t K;
-    const uint32_t* orig;             // sorted -> original row (nullptr: identity)
+    const uint32_t* orig;             // sorted -> batch position (nullptr: pos_off + row)
+    int64_t pos_off;
     const void* cols[MAX_COLS];
     const uint8_t* nulls[MAX_COLS];
-    int64_t seq_base;
+    int64_t seq_base;                 // sequence number of batch position 0
     uint8_t* arena;                   // [K][L.bytes], zero-initialised on allocation, persists across batches
+    uint8_t* arena2;                  // second copy (nullptr: the run updates `arena` in place). With two, a run
+                                      // copies the key's committed state to the other copy and works there, so a
+                                      // key can be rerun from its batch-start state until nfa_commit flips it
+    uint8_t* cur;                     // [K] which copy holds the committed state (arena2 != nullptr)
+    uint8_t* ran;                     // [K] set for every key this run touched (arena2 != nullptr)
     nfa::Layout L;
     int64_t out_cap;
     unsigned long long* out_count;
@@ -217,10 +225,21 @@ struct NfaArgs {
     int64_t* out_vals;                // [n_out][out_cap]
     uint32_t* out_nulls;
     int64_t* out_emit_seq;            // sequence number of the event whose processing emitted the match
-    int64_t* out_sub;                 // emission ordinal within that event
-    int* flags;                       // [0] output overflow, [2] arena overflow (some key ran out of partial slots)
+    int64_t* out_sub;                 // emission ordinal within that event (timer matches: negative)
+    uint8_t* out_round;               // [out_cap] scheduler round that produced the record (nullptr: not written)
+    uint8_t round;
+    int* flags;                       // [0] output overflow, [2] arena overflow, [5] scheduler log overflow
+    // timers (queries with absent states)
+    nfa::TimerIn T;
+    // rerun mode: run only list[0..nlist) with the explicit fire lists fires[fire_off[i] .. fire_off[i + 1])
+    const uint32_t* list;
+    int32_t nlist;
+    const uint32_t* fire_off;
+    const nfa::TimerFire* fires;
 };
 // a: host copy (launch geometry); d_a: device copy the kernel reads
 void nfa_run(const NfaArgs& a, const NfaArgs* d_a, hipStream_t stream);
+// double-buffered arenas: flip `cur` of every key a run touched (`ran`), clearing `ran`
+void nfa_commit(uint8_t* cur, uint8_t* ran, int64_t K, hipStream_t stream);
 
 }  // namespace sdg

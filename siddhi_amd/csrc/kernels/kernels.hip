@@ -320,27 +320,56 @@ __global__ __launch_bounds__(256) void rx_segments(const uint32_t* __restrict__ 
 }
 
 // one lane per key: the key's arena is private to the lane, so the state machine runs without atomics; only
-// the output slot reservation is shared
+// the output slot and log reservations are shared
+template <bool TM>
 __global__ __launch_bounds__(256) void nfa_k(const NfaArgs* __restrict__ pa) {
     // arguments from a device copy: indexing a by-value kernel argument (cols[col]) makes the compiler copy the
     // whole struct to scratch per lane
     const NfaArgs& a = *pa;
     __shared__ int64_t stack_mem[STACK * 256];
-    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (k >= a.K) return;
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    int64_t k;
+    if (a.list) {
+        if (idx >= a.nlist) return;
+        k = a.list[idx];
+    } else {
+        if (idx >= a.K) return;
+        k = idx;
+    }
     int64_t b = 0, e = a.n;
     if (a.seg_start) {
         b = a.seg_start[k];
         e = a.seg_end[k];
     }
-    if (b >= e) return;  // initPartition happens at a key's first event
     const Plan* P = a.plan;
-    nfa::Ctx c;
+    const int64_t kb = a.L.bytes;
+    uint8_t* src = a.arena + k * kb;
+    uint8_t* dst = src;
+    if (a.arena2) {
+        if (a.cur[k]) src = a.arena2 + k * kb;
+        else dst = a.arena2 + k * kb;
+    }
+    if (!a.list && b >= e && P->partitioned) {
+        // no event of this key: it runs only for its queued timers (initPartition happens at a first event)
+        const nfa::KHead* h = (const nfa::KHead*)src;
+        if (!(h->flags & 2) || P->n_sched == 0) return;
+        bool queued = false;
+        const nfa::TQ* tq = (const nfa::TQ*)(src + a.L.off_tq);
+        for (int i = 0; i < a.L.n_sched; ++i) queued |= tq[i].n > 0;
+        if (!queued) return;
+    }
+    if (dst != src) {  // work on the other copy: the committed state stays intact until nfa_commit
+        const uint4* s4 = (const uint4*)src;
+        uint4* d4 = (uint4*)dst;
+        for (int64_t i = 0; i < kb / 16; ++i) d4[i] = s4[i];
+        a.ran[k] = 1;
+    }
+    nfa::CtxT<TM> c;
     c.P = P;
     c.code = a.code;
     c.consts = a.consts;
     c.L = a.L;
-    c.base = a.arena + k * a.L.bytes;
+    c.base = dst;
     c.stk = stack_mem + threadIdx.x;
     c.stride = 256;
     c.emit_ts = a.out_ts;
@@ -349,13 +378,29 @@ __global__ __launch_bounds__(256) void nfa_k(const NfaArgs* __restrict__ pa) {
     c.emit_seq = a.out_emit_seq;
     c.emit_sub = a.out_sub;
     c.emit_key = a.out_key;
+    c.emit_round = a.out_round;
+    c.round = a.round;
     c.emit_count = a.out_count;
     c.emit_cap = a.out_cap;
     c.flags = &a.flags[0];
     c.key = (uint32_t)k;
-    nfa::KeyEvents ev{a.ts, a.qstream, a.orig, a.cols, a.nulls, b, e, a.seq_base};
+    c.T = a.T;
+    c.fires = nullptr;
+    c.nfires = 0;
+    if (a.list) {
+        c.fires = a.fires + a.fire_off[idx];
+        c.nfires = (int32_t)(a.fire_off[idx + 1] - a.fire_off[idx]);
+    }
+    nfa::KeyEvents ev{a.ts, a.qstream, a.orig, a.cols, a.nulls, b, e, a.seq_base, a.pos_off};
     nfa::run_key(c, ev);
     if (c.ovf()) atomicOr(&a.flags[2], 1);
+}
+
+__global__ __launch_bounds__(256) void nfa_commit_k(uint8_t* __restrict__ cur, uint8_t* __restrict__ ran, int64_t K) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= K || !ran[k]) return;
+    cur[k] ^= 1;
+    ran[k] = 0;
 }
 
 }  // namespace
@@ -418,7 +463,7 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
         std::memset(&rp, 0, sizeof rp);
         rp.keys_in = kin;
         rp.keys_out = last ? a.keys_sorted : a.tmp_keys[p & 1];
-        rp.orig_in = p == 0 ? nullptr : a.tmp_orig[(p - 1) & 1];
+        rp.orig_in = p == 0 ? a.orig_in : a.tmp_orig[(p - 1) & 1];
         rp.orig_out = last ? a.orig_sorted : a.tmp_orig[p & 1];
         rp.ncols = a.ncols;
         for (int c = 0; c < a.ncols; ++c) {
@@ -492,7 +537,7 @@ void bucketize(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, uint
     std::memset(&rp, 0, sizeof rp);
     rp.keys_in = a.keys;
     rp.keys_out = a.keys_sorted;
-    rp.orig_in = nullptr;
+    rp.orig_in = a.orig_in;
     rp.orig_out = a.orig_sorted;
     rp.ncols = a.ncols;
     for (int c = 0; c < a.ncols; ++c) {
@@ -515,8 +560,15 @@ void bucketize(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, uint
 }
 
 void nfa_run(const NfaArgs& a, const NfaArgs* d_a, hipStream_t stream) {
-    if (a.K <= 0 || a.n <= 0) return;
-    hipLaunchKernelGGL(nfa_k, dim3((unsigned)((a.K + 255) / 256)), dim3(256), 0, stream, d_a);
+    const int64_t lanes = a.list ? a.nlist : a.K;
+    if (lanes <= 0) return;
+    if (a.T.log) hipLaunchKernelGGL(nfa_k<true>, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, d_a);
+    else hipLaunchKernelGGL(nfa_k<false>, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, d_a);
+}
+
+void nfa_commit(uint8_t* cur, uint8_t* ran, int64_t K, hipStream_t stream) {
+    if (K <= 0) return;
+    hipLaunchKernelGGL(nfa_commit_k, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, cur, ran, K);
 }
 
 }  // namespace sdg

@@ -3,6 +3,7 @@
 C1  every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec      (1 stream, no partition)
 C2  C1 inside `partition with (symbol of StockStream)`                                  (10k keys, 1 GPU)
 C3  partition with (key of S): every e1=S[price>20], e2=S[price>e1.price]<2:5>, e3=S[price<e2[last].price]
+C4  partition with (key of A..D): e1=A[v>10] -> (e2=B[v>20] and e3=C[v>30]) -> not D[v>40] for 5 sec
 Prices are rint((10 + 20u) * 100) / 100, u uniform in [0, 1).
 """
 import numpy as np
@@ -79,3 +80,23 @@ def c3_columns(keys, per_key=100, seed=11):
     key = (z % np.uint64(keys)).astype(np.int64)
     price = prices(seed + 1, n)
     return {"ts": ts, "id": i, "key": key, "price": price, "volume": (i % 1000).astype(np.int32)}
+
+
+C4_STREAMS = ("A", "B", "C", "D")
+C4_APP = ("@app:playback " + " ".join("define stream %s (id long, key long, v double);" % s for s in C4_STREAMS) +
+          " partition with (key of A, key of B, key of C, key of D) begin @info(name = 'query1') "
+          "from e1=A[v>10] -> (e2=B[v>20] and e3=C[v>30]) -> not D[v>40] for 5 sec "
+          "select e1.id as e1id, e2.id as e2id, e3.id as e3id insert into M; end;")
+
+
+def c4_columns(keys, per_key=20, seed=13, per_tick=10_000):
+    """C4: streams A, B, C, D round-robin by global ts, keys uniform, ts = T0 + 10 floor(i / 10^4)
+    so the 5 s timers fall due mid-run; v = rint(50 u * 100) / 100 in [0, 50) so every filter (v > 10 / 20 / 30 / 40)
+    passes part of the events. The run ends with advance_time(ts[-1] + 5000)."""
+    n = keys * per_key
+    i = np.arange(n, dtype=np.int64)
+    ts = T0 + 10 * (i // per_tick)
+    z = splitmix64(seed, n)
+    key = (z % np.uint64(keys)).astype(np.int64)
+    v = np.rint(50.0 * uniform01(splitmix64(seed + 1, n)) * 100.0) / 100.0
+    return {"ts": ts, "id": i, "key": key, "v": v, "stream": (i % 4).astype(np.int32)}

@@ -31,6 +31,7 @@ def lib():
         L.emu_send.argtypes = [P, I32, I64, ctypes.POINTER(I64), ctypes.POINTER(ctypes.c_uint8)]
         L.emu_flush.argtypes = [P]
         L.emu_advance.argtypes = [P, I64]
+        L.emu_send_batch.argtypes = [P, I64, P, P, P, P, P]
         L.emu_start.argtypes = [P, I64]
         L.emu_num_queries.argtypes = [P]
         for f in ("emu_query_name", "emu_query_target"):

@@ -17,6 +17,7 @@
 
 #include "../../siddhi_amd/csrc/engine/compile.h"
 #include "../../siddhi_amd/csrc/engine/nfa.h"
+#include "../../siddhi_amd/csrc/engine/keyrun.h"
 #include "../../siddhi_amd/csrc/engine/sched.h"
 #include "../../siddhi_amd/csrc/siddhiql/parser.h"
 
@@ -190,7 +191,7 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
         unsigned long long count = 0, lcount = 0;
         std::vector<nfa::SchedLog> logs(1 << 16);
         int flags[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        nfa::Ctx c;
+        nfa::CtxT<true> c;
         c.P = &P;
         c.code = h.code.data();
         c.consts = h.consts.data();
@@ -204,6 +205,8 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
         c.emit_seq = o_seq.data();
         c.emit_sub = o_sub.data();
         c.emit_key = o_key.data();
+        c.emit_round = nullptr;
+        c.round = 0;
         c.emit_count = &count;
         c.emit_cap = cap;
         c.flags = flags;
@@ -219,7 +222,7 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
         c.fires = fires;
         c.nfires = nfires;
         nfa::KeyEvents kev{ts.data(), qs.data(), gpos.data(), cptr.data(), nptr.data(), seg_b.size() > k ? seg_b[k] : 0,
-                           seg_e.size() > k ? seg_e[k] : 0, e->seq};
+                           seg_e.size() > k ? seg_e[k] : 0, e->seq, 0};
         if (kev.b > kev.e) kev.b = kev.e;
         nfa::run_key(c, kev);
         if (c.ovf()) {
@@ -249,35 +252,74 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
         if (rc) return rc;
     }
     SchedSim::Result res;
+    std::vector<std::unique_ptr<KeyRun>> runs;
     if (q.sim.active()) {
-        // fixpoint with the global scheduler (sched.h): rerun diverged keys with the simulated fire lists
-        for (int round = 0;; ++round) {
-            std::vector<nfa::SchedLog> all;
-            for (auto& kv : klog) all.insert(all.end(), kv.second.begin(), kv.second.end());
-            q.sim.simulate(bc, all, q.key_hash, res);
-            if (res.diverged.empty()) break;
-            if (round > 64) {
-                g_err = "scheduler fixpoint did not converge";
-                return 5;
+        // one pass of the global scheduler (sched.h) over the runs' logs; keys it takes over run here on the host
+        std::vector<nfa::SchedLog> all;
+        for (auto& kv : klog) all.insert(all.end(), kv.second.begin(), kv.second.end());
+        KeyRows kr;
+        kr.seg_b = seg_b.data();
+        kr.seg_e = seg_e.data();
+        kr.K = (int64_t)seg_b.size();
+        kr.orig = gpos.data();
+        kr.n = n;
+        nfa::TimerIn T{};
+        T.G = bc.G;
+        T.clk = bc.clk.data();
+        T.nadv = bc.nadv.data();
+        T.clock0 = bc.clock0;
+        T.live = !e->app.playback;
+        auto take = [&](uint32_t k) -> KeyRun* {
+            runs.emplace_back(new KeyRun());
+            KeyRun* r = runs.back().get();
+            r->key = k;
+            r->arena = backup[k];
+            const int64_t b = k < seg_b.size() ? seg_b[k] : 0, en = k < seg_e.size() ? seg_e[k] : 0;
+            for (int64_t p = b; p < en; ++p) {
+                r->ts.push_back(ts[p]);
+                r->qs.push_back(qs[p]);
+                r->pos.push_back(gpos[p]);
             }
-            for (size_t d = 0; d < res.diverged.size(); ++d) {
-                const uint32_t k = res.diverged[d];
-                q.arenas[k] = backup[k];
-                int rc = run_one(k, res.fires.data() + res.fire_off[d], (int)(res.fire_off[d + 1] - res.fire_off[d]));
-                if (rc) return rc;
+            r->has_qs = true;
+            r->cols.resize(nc);
+            r->nulls.resize(nc);
+            for (int c = 0; c < nc; ++c) {
+                const int w = width_of(P.col_kind[c]);
+                r->cols[c].assign(cols[c].begin() + b * w, cols[c].begin() + en * w);
+                r->nulls[c].assign(nulls[c].begin() + b, nulls[c].begin() + en);
+            }
+            r->start(&P, h.code.data(), h.consts.data(), q.L, T, e->seq);
+            return r;
+        };
+        q.sim.simulate(bc, all, q.key_hash, kr, take, res);
+        q.sim.commit();
+        for (auto& r : runs) {  // the host runs replace those keys' device results
+            if (r->overflow()) {
+                g_err = "query '" + h.name + "': partial-match arena overflow (host run)";
+                return 3;
+            }
+            q.arenas[r->key] = r->arena;
+            std::vector<Out>& ko = kout[r->key];
+            ko.clear();
+            const int64_t cap = (int64_t)r->o_ts.size();
+            for (unsigned long long i = 0; i < r->count; ++i) {
+                Out o{r->o_seq[i], r->o_sub[i], r->o_ts[i], {}, r->o_nulls[i]};
+                for (int j = 0; j < P.n_out; ++j) o.vals.push_back(r->o_vals[(size_t)j * cap + i]);
+                ko.push_back(std::move(o));
             }
         }
-        q.sim.commit();
     }
     std::vector<Out> batch;
     for (auto& kv : kout)
         for (Out& o : kv.second) {
-            if (o.sub < 0) {  // timer match: order among the position's fires (the scheduler's order)
+            if (o.sub < 0) {  // timer match: its fire's place in the scheduler's order (position, rank)
                 const int sch = (int)((o.sub >> 48) & 0x7F);
                 const uint32_t g = (uint32_t)(o.seq - e->seq);
                 auto it = res.rank.find(SchedSim::rank_key(g, sch, kv.first));
-                const int64_t r = it == res.rank.end() ? 0 : it->second;
-                o.sub = INT64_MIN | (r << 24) | (o.sub & 0xFFFFFF);
+                if (it != res.rank.end()) {
+                    o.seq = e->seq + it->second.g;
+                    o.sub = INT64_MIN | ((int64_t)it->second.rank << 24) | (o.sub & 0xFFFFFF);
+                }
             }
             batch.push_back(std::move(o));
         }
@@ -335,6 +377,20 @@ int emu_send(void* h, int stream, int64_t ts, const int64_t* vals, const uint8_t
     int na = (int)e->app.streams[stream].attrs.size();
     Ev ev{stream, ts, std::vector<int64_t>(vals, vals + na), std::vector<uint8_t>(nulls, nulls + na)};
     e->pending.push_back(std::move(ev));
+    return 0;
+}
+
+// n events (stream[i], ts[i], the row's attribute slots at slots + offsets[i]) in order
+int emu_send_batch(void* h, int64_t n, const int32_t* stream, const int64_t* ts, const int64_t* offsets,
+                   const int64_t* slots, const uint8_t* nulls) {
+    Emu* e = (Emu*)h;
+    for (int64_t i = 0; i < n; ++i) {
+        const int na = (int)e->app.streams[stream[i]].attrs.size();
+        const int64_t* v = slots + offsets[i];
+        Ev ev{stream[i], ts[i], std::vector<int64_t>(v, v + na), std::vector<uint8_t>(na, 0)};
+        if (nulls) ev.nulls.assign(nulls + offsets[i], nulls + offsets[i] + na);
+        e->pending.push_back(std::move(ev));
+    }
     return 0;
 }
 

@@ -14,7 +14,7 @@ class ProductAdapter:
         self.records = []
 
     def start(self, ts):
-        self.rt.start()
+        self.rt.start(ts)
 
     def handler(self, sid):
         if sid not in self.handlers:
@@ -22,6 +22,8 @@ class ProductAdapter:
         return self.handlers[sid]
 
     def send(self, sid, ts, values, now=None, mode=0):
+        if not self.rt.playback and now is not None:
+            self.rt.advance_time(now)  # the wall clock at this send: timers due by then fire before the event
         h = self.handler(sid)
         if mode == 1 and self.rt.playback:
             h.send(values)
@@ -29,7 +31,7 @@ class ProductAdapter:
             h.send(ts, values)
 
     def advance(self, ts):
-        pass  # no scheduler-driven states on the device path in this build
+        self.rt.advance_time(ts)
 
     def flush(self):
         self.rt.flush(deliver=False)
