@@ -139,6 +139,10 @@ typedef struct sdg_stats {
     int32_t deque;             /* chain path took the deque kernel (1 stack, 2 complete-all), 0 forward scans */
     int32_t fused;             /* chain path: 1 fused bucket matcher, 2 tried it and fell back to the radix path */
     int64_t fused_ovf;         /* fused path: partials resolved by the key-filtered bucket scan in HBM */
+    int64_t sched_fires;       /* absent-state timer fires (Scheduler.sendTimerEvents) in the last flush */
+    int64_t sched_shifted;     /* fires the reference's scheduler ran later than the key's device run did (same
+                                  result, later in the delivery order) */
+    int64_t sched_host_keys;   /* keys the scheduler simulation replayed on the host (their order changed results) */
 } sdg_stats;
 int sdg_last_stats(sdg_engine* e, sdg_stats* out);
 

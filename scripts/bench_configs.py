@@ -47,7 +47,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--c1-events", type=int, default=1_000_000)
     ap.add_argument("--c3-keys", type=int, default=1_000_000)
-    ap.add_argument("--only", default="c1,c3,c3m")
+    ap.add_argument("--only", default="c1,c3,c3m,c4")
+    ap.add_argument("--c4-keys", type=int, default=1_000_000)
     ap.add_argument("--c3-steps", type=int, default=2)
     args = ap.parse_args()
     torch.cuda.init()
@@ -99,6 +100,39 @@ def main():
                           "events_per_s_end_to_end": n * args.c3_steps / dt, "ms_per_step": dt * 1000 / args.c3_steps,
                           "device_ms_per_step": dev_ms / args.c3_steps, "events_per_s_device": n * args.c3_steps / (dev_ms / 1000),
                           "matches_per_step": m / args.c3_steps, "events_per_flush": st.events}), flush=True)
+    if "c4" in only:
+        run_c4(args.c4_keys)
+
+
+def run_c4(keys):
+    """C4: e1=A[v>10] -> (e2=B[v>20] and e3=C[v>30]) -> not D[v>40] for 5 sec over `keys` keys x 20 events, the 4
+    streams interleaved (sdg_push_mixed, host columns), then advance_time(T_end + 5000). One flush + the final
+    timer flush; device ms from sdg_stats (NFA + key grouping), end to end includes the host mixed-batch
+    assembly, the scheduler simulation and the host replays."""
+    import siddhi_amd as sa
+    from siddhi_amd import workloads as w
+    c = w.c4_columns(keys)
+    n = len(c["ts"])
+    end = int(c["ts"][-1]) + 5000
+    rt = sa.SiddhiAppRuntime(w.C4_APP, device=0, batch_capacity=n + 1)
+    idx = np.array([rt._L.sdg_stream_index(rt._h, s.encode()) for s in w.C4_STREAMS], dtype=np.int32)[c["stream"]]
+    t0 = time.perf_counter()
+    rt.push_mixed(idx, c["ts"], [c["id"], c["key"], c["v"]])
+    rt.flush(deliver=False)
+    s1 = rt.stats()
+    rt.advance_time(end)
+    rt.flush(deliver=False)
+    s2 = rt.stats()
+    ts, vals, nulls, seq = rt.poll_arrays(0)
+    dt = time.perf_counter() - t0
+    rt.shutdown()
+    dev_ms = s1.ms_keygroup + s1.ms_match + s2.ms_keygroup + s2.ms_match
+    print(json.dumps({"config": "C4 %d keys x 20 events (4 streams interleaved, host push)" % keys,
+                      "events": n, "matches": int(len(ts)), "events_per_s_end_to_end": n / dt,
+                      "device_ms": dev_ms, "ms_nfa": s1.ms_nfa + s2.ms_nfa, "events_per_s_device": n / (dev_ms / 1000),
+                      "timer_fires": s1.sched_fires + s2.sched_fires,
+                      "fires_shifted_by_collapse": s1.sched_shifted + s2.sched_shifted,
+                      "keys_replayed_on_host": s1.sched_host_keys + s2.sched_host_keys}), flush=True)
 
 
 if __name__ == "__main__":

@@ -80,7 +80,10 @@ class Stats(ctypes.Structure):
                 ("ms_chain_emit", ctypes.c_double),
                 ("deque", ctypes.c_int32),
                 ("fused", ctypes.c_int32),
-                ("fused_ovf", ctypes.c_int64)]
+                ("fused_ovf", ctypes.c_int64),
+                ("sched_fires", ctypes.c_int64),
+                ("sched_shifted", ctypes.c_int64),
+                ("sched_host_keys", ctypes.c_int64)]
 
 
 _lib = None

@@ -18,6 +18,7 @@
 #include "../kernels/kernels.h"
 #include "../siddhiql/parser.h"
 #include "compile.h"
+#include "keyrun.h"
 #include "sched.h"
 
 namespace sdg {
@@ -152,11 +153,13 @@ struct QueryRt {
     std::vector<int32_t> key_hash;
     DevBuf arena2, cur_bits, ran_bits, o_round, d_log, d_list, d_foff, d_fires, d_vpos;
     int64_t log_cap = 0;
-    // timer-match ordering of the last flush (drain): fire ranks, the round each rerun key's records come from
+    // timer-match ordering of the last flush (drain): each fire's slot in the scheduler's order; the keys the
+    // scheduler replayed on the host (their device records are void) and those replays
     bool last_timers = false;
     int64_t last_seq_base = 0;
-    std::unordered_map<uint64_t, uint32_t> last_rank;
-    std::unordered_map<uint32_t, uint8_t> key_round;
+    std::unordered_map<uint64_t, SchedSim::Slot> last_rank;
+    std::vector<uint32_t> taken;
+    std::vector<std::unique_ptr<KeyRun>> runs;
     // batch staging
     DevBuf st_ts, st_qs, st_key, st_cols[MAX_COLS], st_nulls[MAX_COLS];
     // sorted view
@@ -757,7 +760,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             a.out_nulls = (uint32_t*)q.o_nulls.ensure(cap * 4);
             a.out_emit_seq = (int64_t*)q.o_emit.ensure(cap * 8);
             a.out_sub = (int64_t*)q.o_first.ensure(cap * 8);
-            a.out_round = timers ? (uint8_t*)q.o_round.ensure(cap) : nullptr;
+            a.out_round = nullptr;
         };
         int hf[8];
         unsigned long long hc[2];
@@ -813,55 +816,97 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             if (tries > 8) throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': output buffers keep overflowing");
         e->stats.match_launches += 1;
         q.last_timers = timers;
-        q.key_round.clear();
         q.last_rank.clear();
+        q.taken.clear();
+        q.runs.clear();
         q.last_seq_base = e->seq;
         if (timers) {
-            // fixpoint with the global scheduler (sched.h): rerun the keys whose fires the collapse changed
+            // one pass of the global scheduler (sched.h) over the runs' logs; the keys it takes over are replayed
+            // on the host from their batch-start state and their results replace the device's
             std::vector<nfa::SchedLog> logs(hc[1]);
             if (hc[1]) HIPCHECK(hipMemcpy(logs.data(), a.T.log, hc[1] * sizeof(nfa::SchedLog), hipMemcpyDeviceToHost));
-            auto by_key = [](const nfa::SchedLog& x, const nfa::SchedLog& y) {
+            std::sort(logs.begin(), logs.end(), [](const nfa::SchedLog& x, const nfa::SchedLog& y) {
                 return x.key != y.key ? x.key < y.key : x.kseq < y.kseq;
-            };
-            std::sort(logs.begin(), logs.end(), by_key);
+            });
             while ((int64_t)q.key_hash.size() < (int64_t)K) {  // HashMap hash of each key's toString
                 const size_t k = q.key_hash.size();
                 const std::string& ks = q.string_keys ? e->strings.strs[k] : q.keystr[k];
                 q.key_hash.push_back(java_spread_hash(ks));
             }
+            // the batch's rows by key, on the host: segments + positions (sorted view)
+            const int64_t KR = partitioned ? (int64_t)K : 1;
+            std::vector<uint32_t> hseg_b(KR, 0), hseg_e(KR, 0), horig;
+            if (partitioned && nrows > 0) {
+                HIPCHECK(hipMemcpy(hseg_b.data(), v_seg, KR * 4, hipMemcpyDeviceToHost));
+                HIPCHECK(hipMemcpy(hseg_e.data(), v_segend, KR * 4, hipMemcpyDeviceToHost));
+            } else if (!partitioned) {
+                hseg_e[0] = (uint32_t)nrows;
+            }
+            if (v_orig && nrows > 0) {
+                horig.resize(nrows);
+                HIPCHECK(hipMemcpy(horig.data(), v_orig, nrows * 4, hipMemcpyDeviceToHost));
+            }
+            KeyRows kr;
+            kr.seg_b = hseg_b.data();
+            kr.seg_e = hseg_e.data();
+            kr.K = KR;
+            kr.orig = v_orig ? horig.data() : nullptr;
+            kr.pos_off = a.pos_off;
+            kr.n = nrows;
+            nfa::TimerIn T = a.T;  // host copy of the clock for the host runs
+            T.clk = e->bc.clk.data();
+            T.nadv = e->bc.nadv.data();
+            q.runs.clear();
+            auto take = [&](uint32_t k) -> KeyRun* {
+                q.runs.emplace_back(new KeyRun());
+                KeyRun* r = q.runs.back().get();
+                r->key = k;
+                uint8_t cur = 0;
+                HIPCHECK(hipMemcpy(&cur, q.cur_bits.as<uint8_t>() + k, 1, hipMemcpyDeviceToHost));
+                r->arena.resize(kb);
+                const uint8_t* committed = (cur ? q.arena2.as<uint8_t>() : q.arena.as<uint8_t>()) + (int64_t)k * kb;
+                HIPCHECK(hipMemcpy(r->arena.data(), committed, kb, hipMemcpyDeviceToHost));
+                const int64_t b = k < (uint32_t)KR ? hseg_b[k] : 0, en = k < (uint32_t)KR ? hseg_e[k] : 0, m = en - b;
+                r->ts.resize(m);
+                r->pos.resize(m);
+                for (int64_t p = 0; p < m; ++p) r->pos[p] = (uint32_t)kr.pos(b + p);
+                if (m) HIPCHECK(hipMemcpy(r->ts.data(), v_ts + b, m * 8, hipMemcpyDeviceToHost));
+                r->has_qs = multi_stream;
+                if (multi_stream) {
+                    r->qs.resize(m);
+                    if (m) HIPCHECK(hipMemcpy(r->qs.data(), v_qs + b, m, hipMemcpyDeviceToHost));
+                }
+                r->cols.resize(nc);
+                r->nulls.resize(nc);
+                for (int c = 0; c < nc; ++c) {
+                    const int w = width_of(P.col_kind[c]);
+                    r->cols[c].resize((size_t)std::max<int64_t>(m, 1) * w);
+                    if (m) HIPCHECK(hipMemcpy(r->cols[c].data(), (const uint8_t*)v_cols[c] + b * w, m * w, hipMemcpyDeviceToHost));
+                    if (v_nulls[c]) {
+                        r->nulls[c].resize(std::max<int64_t>(m, 1));
+                        if (m) HIPCHECK(hipMemcpy(r->nulls[c].data(), v_nulls[c] + b, m, hipMemcpyDeviceToHost));
+                    }
+                }
+                r->start(&P, h.code.data(), h.consts.data(), q.L, T, e->seq);
+                return r;
+            };
             SchedSim::Result res;
-            for (int round = 1;; ++round) {
-                q.sim.simulate(e->bc, logs, q.key_hash, res);
-                if (res.diverged.empty()) break;
-                if (round > 250) throw CompileError(SDG_ERR_UNSUPPORTED, "query '" + h.name + "': scheduler fixpoint did not converge");
-                const int64_t nd = (int64_t)res.diverged.size();
-                a.list = (const uint32_t*)q.d_list.ensure(nd * 4);
-                a.fire_off = (const uint32_t*)q.d_foff.ensure((nd + 1) * 4);
-                a.fires = (const nfa::TimerFire*)q.d_fires.ensure(std::max<size_t>(1, res.fires.size()) * sizeof(nfa::TimerFire));
-                HIPCHECK(hipMemcpyAsync((void*)a.list, res.diverged.data(), nd * 4, hipMemcpyHostToDevice, st));
-                HIPCHECK(hipMemcpyAsync((void*)a.fire_off, res.fire_off.data(), (nd + 1) * 4, hipMemcpyHostToDevice, st));
-                if (!res.fires.empty())
-                    HIPCHECK(hipMemcpyAsync((void*)a.fires, res.fires.data(), res.fires.size() * sizeof(nfa::TimerFire),
-                                            hipMemcpyHostToDevice, st));
-                a.nlist = (int32_t)nd;
-                a.round = (uint8_t)round;
-                for (uint32_t k : res.diverged) q.key_round[k] = (uint8_t)round;
-                while (!launch(false))
-                    if (hf[0] || (int64_t)hc[0] > q.out_cap)  // the reruns' outputs need room next to the first run's
-                        throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': output buffer overflow in a scheduler rerun");
-                e->stats.match_launches += 1;
-                std::vector<nfa::SchedLog> fresh(hc[1]);
-                if (hc[1]) HIPCHECK(hipMemcpy(fresh.data(), a.T.log, hc[1] * sizeof(nfa::SchedLog), hipMemcpyDeviceToHost));
-                std::vector<nfa::SchedLog> kept;  // the diverged keys' old records go, the reruns' come in
-                kept.reserve(logs.size() + fresh.size());
-                for (const auto& L : logs)
-                    if (!std::binary_search(res.diverged.begin(), res.diverged.end(), L.key)) kept.push_back(L);
-                std::sort(fresh.begin(), fresh.end(), by_key);
-                logs.clear();
-                std::merge(kept.begin(), kept.end(), fresh.begin(), fresh.end(), std::back_inserter(logs), by_key);
+            q.sim.simulate(e->bc, logs, q.key_hash, kr, take, res);
+            for (auto& r : q.runs) {
+                if (r->overflow())
+                    throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': a partition key exceeded max_partials "
+                                                         "(host replay of a key the scheduler reordered)");
+                uint8_t cur = 0;  // its state goes where the device run's went (nfa_commit makes it current)
+                HIPCHECK(hipMemcpy(&cur, q.cur_bits.as<uint8_t>() + r->key, 1, hipMemcpyDeviceToHost));
+                uint8_t* work = (cur ? q.arena.as<uint8_t>() : q.arena2.as<uint8_t>()) + (int64_t)r->key * kb;
+                HIPCHECK(hipMemcpy(work, r->arena.data(), kb, hipMemcpyHostToDevice));
             }
             q.sim.commit();
             q.last_rank = std::move(res.rank);
+            q.taken.assign(res.taken.begin(), res.taken.end());
+            e->stats.sched_fires += res.n_fires;
+            e->stats.sched_shifted += res.n_shifted;
+            e->stats.sched_host_keys += (int64_t)res.taken.size();
             nfa_commit(q.cur_bits.as<uint8_t>(), q.ran_bits.as<uint8_t>(), q.arena_keys, st);
         }
         HIPCHECK(hipEventRecord(e->ev[2], st));
@@ -1106,12 +1151,9 @@ void drain(sdg_engine* e, QueryRt& q) {
     uint32_t* nulls = (uint32_t*)(vals + (size_t)na * n);
     hipStream_t st = e->stream;
     std::vector<uint32_t> okey;
-    std::vector<uint8_t> oround;
-    if (q.last_timers) {  // timer matches: keep each rerun key's last round, rank the fires of a position
+    if (q.last_timers) {  // timer matches: drop the records of keys replayed on the host, order the fires
         okey.resize(n);
-        oround.resize(n);
         HIPCHECK(hipMemcpyAsync(okey.data(), q.o_key.p, n * 4, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipMemcpyAsync(oround.data(), q.o_round.p, n, hipMemcpyDeviceToHost, st));
     }
     HIPCHECK(hipMemcpyAsync(ts, q.o_ts.p, n * 8, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipMemcpyAsync(emit, q.o_emit.p, n * 8, hipMemcpyDeviceToHost, st));
@@ -1122,25 +1164,53 @@ void drain(sdg_engine* e, QueryRt& q) {
                                 hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
     if (!q.nulls_valid) std::memset(nulls, 0, (size_t)n * 4);
-    std::vector<int64_t> ord;
-    ord.reserve(n);
+    // the host replays' records join the device's (same layout, after them)
+    int64_t nh = 0;
+    for (auto& r : q.runs) nh += (int64_t)r->count;
+    std::vector<int64_t> hts, hemit, hfirst, hvals;
+    std::vector<uint32_t> hnulls, hkey;
+    if (nh) {
+        hts.reserve(nh); hemit.reserve(nh); hfirst.reserve(nh); hnulls.reserve(nh); hkey.reserve(nh);
+        hvals.resize((size_t)na * nh);
+        int64_t x = 0;
+        for (auto& r : q.runs) {
+            const int64_t cap = (int64_t)r->o_ts.size();
+            for (unsigned long long i = 0; i < r->count; ++i, ++x) {
+                hts.push_back(r->o_ts[i]);
+                hemit.push_back(r->o_seq[i]);
+                hfirst.push_back(r->o_sub[i]);
+                hnulls.push_back(r->o_nulls[i]);
+                hkey.push_back(r->key);
+                for (int j = 0; j < na; ++j) hvals[(size_t)j * nh + x] = r->o_vals[(size_t)j * cap + i];
+            }
+        }
+    }
+    auto slot = [&](int64_t& em, int64_t& fs, uint32_t key) {  // a timer match: its fire's slot (position, rank)
+        if (fs >= 0) return;
+        const int sch = (int)((fs >> 48) & 0x7F);
+        auto it = q.last_rank.find(SchedSim::rank_key((uint32_t)(em - q.last_seq_base), sch, key));
+        if (it == q.last_rank.end()) return;
+        em = q.last_seq_base + it->second.g;
+        fs = INT64_MIN | ((int64_t)it->second.rank << 24) | (fs & 0xFFFFFF);
+    };
+    std::vector<int64_t> ord;  // < n: device record, >= n: host record n + i
+    ord.reserve(n + nh);
     for (int64_t i = 0; i < n; ++i) {
         if (q.last_timers) {
-            auto kr = q.key_round.find(okey[i]);
-            if (oround[i] != (kr == q.key_round.end() ? 0 : kr->second)) continue;  // superseded by a rerun
-            if (first[i] < 0) {  // timer match: the fire's rank among the position's fires (scheduler order)
-                const int sch = (int)((first[i] >> 48) & 0x7F);
-                const uint32_t g = (uint32_t)(emit[i] - q.last_seq_base);
-                auto it = q.last_rank.find(SchedSim::rank_key(g, sch, okey[i]));
-                const int64_t r = it == q.last_rank.end() ? 0 : it->second;
-                first[i] = INT64_MIN | (r << 24) | (first[i] & 0xFFFFFF);
-            }
+            if (std::binary_search(q.taken.begin(), q.taken.end(), okey[i])) continue;
+            slot(emit[i], first[i], okey[i]);
         }
         ord.push_back(i);
     }
+    for (int64_t i = 0; i < nh; ++i) {
+        slot(hemit[i], hfirst[i], hkey[i]);
+        ord.push_back(n + i);
+    }
+    auto EM = [&](int64_t x) { return x < n ? emit[x] : hemit[x - n]; };
+    auto FI = [&](int64_t x) { return x < n ? first[x] : hfirst[x - n]; };
     const int64_t nk = (int64_t)ord.size();
     std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
-        return emit[x] != emit[y] ? emit[x] < emit[y] : first[x] < first[y];
+        return EM(x) != EM(y) ? EM(x) < EM(y) : FI(x) < FI(y);
     });
     const size_t b = q.acc_ts.size();
     q.acc_ts.resize(b + nk);
@@ -1153,13 +1223,17 @@ void drain(sdg_engine* e, QueryRt& q) {
     }
     for (int64_t i = 0; i < nk; ++i) {
         const int64_t s = ord[i];
-        q.acc_ts[b + i] = ts[s];
-        q.acc_seq[b + i] = emit[s];
+        const bool dev = s < n;
+        const int64_t hs = s - n;
+        q.acc_ts[b + i] = dev ? ts[s] : hts[hs];
+        q.acc_seq[b + i] = EM(s);
+        const uint32_t nm = dev ? nulls[s] : hnulls[hs];
         for (int j = 0; j < na; ++j) {
-            q.acc_vals[j][b + i] = vals[(size_t)j * n + s];
-            q.acc_nulls[j][b + i] = (nulls[s] >> j) & 1u;
+            q.acc_vals[j][b + i] = dev ? vals[(size_t)j * n + s] : hvals[(size_t)j * nh + hs];
+            q.acc_nulls[j][b + i] = (nm >> j) & 1u;
         }
     }
+    q.runs.clear();
 }
 
 // the batch clock (sched.h BatchClock): playback = TimestampGeneratorImpl.setCurrentTimestamp per position (an
@@ -1213,6 +1287,7 @@ int do_flush(sdg_engine* e) {
     e->stats.ms_chain_carry = e->stats.ms_chain_match = e->stats.ms_chain_emit = 0;
     e->stats.ms_nfa = 0;
     e->stats.fused_ovf = 0;
+    e->stats.sched_fires = e->stats.sched_shifted = e->stats.sched_host_keys = 0;
     // a flush consumes its batch whether or not it succeeds: a failing query must not make the next flush
     // replay the events onto the queries that already committed them
     struct Consume {

@@ -451,3 +451,44 @@ def test_failed_flush_consumes_its_batch(oracle_built):
     finally:
         rt.shutdown()
     assert got == ref
+
+
+# ---- absent states on the device (C4): timers, the global scheduler, host replays -----------------------------
+def product_c4(c, end, batches=3):
+    rt = sa.SiddhiAppRuntime(w.C4_APP)
+    try:
+        assert rt.query_paths() == [1]
+        idx = np.array([rt._L.sdg_stream_index(rt._h, s.encode()) for s in w.C4_STREAMS], dtype=np.int32)
+        n = len(c["ts"])
+        bounds = np.linspace(0, n, batches + 1).astype(np.int64)
+        parts, stats = [], []
+        for b in range(batches):
+            lo, hi = bounds[b], bounds[b + 1]
+            rt.push_mixed(idx[c["stream"][lo:hi]], c["ts"][lo:hi], [c["id"][lo:hi], c["key"][lo:hi], c["v"][lo:hi]])
+            rt.flush(deliver=False)
+            stats.append(rt.stats())
+            parts.append(rt.poll_arrays(0))
+        rt.advance_time(end)
+        rt.flush(deliver=False)
+        stats.append(rt.stats())
+        parts.append(rt.poll_arrays(0))
+    finally:
+        rt.shutdown()
+    ts = np.concatenate([p[0] for p in parts])
+    vals = np.concatenate([p[1] for p in parts], axis=1)
+    nulls = np.concatenate([p[2] for p in parts], axis=1)
+    return ts, vals, nulls, stats
+
+
+@pytest.mark.parametrize("keys", [10_000, 30_000])
+def test_c4_vs_oracle(keys, oracle_built):
+    """C4 at >= 10^4 keys, timers falling due mid-run and at the final advance_time: every match,
+    in the reference's delivery order (TreeMultimap collapse included)"""
+    from test_c4_host import oracle_c4
+    c = w.c4_columns(keys, per_tick=keys // 100)
+    end = int(c["ts"][-1]) + 5000
+    ots, ovals, onulls = oracle_c4(c, end)
+    gts, gvals, gnulls, stats = product_c4(c, end)
+    assert len(ots) > 1000
+    assert sum(s.sched_shifted for s in stats) > 0  # the collapse did delay fires
+    assert np.array_equal(gts, ots) and np.array_equal(gvals.T, ovals) and not gnulls.any()
