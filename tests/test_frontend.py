@@ -46,11 +46,15 @@ def test_sequence_lowers_to_generic_nfa():
     assert rt.query_paths() == [1]
 
 
-def test_absent_is_rejected_until_timer_path():
+def test_absent_states_lower_to_schedulers():
+    """absent states (plain and inside logical) compile onto the device path: one Scheduler per absent processor,
+    element 1's before element 2's (StateInputStreamParser :289-378)"""
     app = ("define stream S1 (symbol string, price float); define stream S2 (symbol string, price float); "
            "from e1=S1[price>10] -> not S2[price>e1.price] for 1 sec select e1.symbol as s insert into O;")
-    with pytest.raises(sa.OperationNotSupportedException):
-        compile_only(app)
+    assert compile_only(app).query_paths() == [1]
+    app2 = ("define stream A (x int); define stream B (x int); define stream C (x int); "
+            "from not A[x>1] for 1 sec and not B[x>2] for 2 sec -> e3=C select e3.x as x insert into O;")
+    assert compile_only(app2).query_paths() == [1]
 
 
 def test_push_needs_a_device():
