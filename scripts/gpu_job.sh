@@ -29,7 +29,7 @@ for s in "$@"; do
         bench) run bench 600 python3 bench.py ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu ;;
         pmc) i=0; for c in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_INSTS_FLAT SQ_INSTS_SMEM" "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum"; do i=$((i+1)); run pmc$i 120 rocprofv3 --pmc $c --kernel-trace -d "$OUT/pmc$i" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu; done ;;
-        c3) run c3 600 python3 scripts/bench_configs.py --only c1,c3m --c3-steps 2 ;;
+        c3) run c3 600 python3 scripts/bench_configs.py --only c1,c3m,c4 --c3-steps 2 ;;
         c3prof) run c3prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/c3prof" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3m --c3-steps 1 --warmup 1 ;;
         newtests) run newtests 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "regime or long_keys or auto_flush or consumes or many_keys or synthetic" ;;
         *) echo "unknown step $s" ;;
