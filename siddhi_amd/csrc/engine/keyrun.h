@@ -49,7 +49,7 @@ struct KeyRun {
         c_.T = T;
         c_.T.log_count = &lcount;
         c_.fires = nullptr;
-        c_.nfires = 0;
+        c_.nfires = 0;  // explicit (empty) list: the simulation calls fire() itself
         reserve(1024);
         for (int k = 0; k < ncols_; ++k) {
             cptr_[k] = cols[k].data();

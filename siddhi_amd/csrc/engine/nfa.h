@@ -204,7 +204,7 @@ struct CtxT {
     int64_t cur_sub;
     // timers
     TimerIn T;
-    const TimerFire* fires;  // explicit fire list of this key (nullptr: ideal mode)
+    const TimerFire* fires;  // explicit fire list of this key (used when nfires >= 0; -1: ideal mode)
     int32_t nfires, fi;
     int64_t clock;           // currentTime()
     int64_t clk_hi;          // during a fire: the largest clock that gives the same result (see LOG_FIRE_END)
@@ -1096,7 +1096,7 @@ struct CtxT {
     // every fire of this key at positions <= limit, in the reference's order
     SDG_HD void fire_until(int64_t limit) {
         if (!TM || P->n_sched == 0) return;
-        if (fires) {  // explicit list (host scheduler simulation)
+        if (nfires >= 0) {  // explicit list (host scheduler simulation)
             while (fi < nfires && (int64_t)fires[fi].g <= limit && !ovf()) {
                 const TimerFire f = fires[fi++];
                 fire(f.sched, f.g, f.clock);

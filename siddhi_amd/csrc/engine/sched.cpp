@@ -152,7 +152,7 @@ void SchedSim::remove_if_empty(int sch, uint32_t key) {  // returnState / return
 
 void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& logs,
                         const std::vector<int32_t>& key_hash, const KeyRows& rows,
-                        const std::function<KeyRun*(uint32_t)>& take_over, Result& out) {
+                        const std::function<KeyRun*(uint32_t)>& take_over, Result& out, bool optimistic) {
     using nfa::SchedLog;
     work_ = cur_;
     hash_ = &key_hash;
@@ -163,6 +163,7 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
     struct KC {
         size_t i = 0, e = 0;                 // cursor into the key's device records
         uint8_t mode = DEV;
+        bool reordered = false;              // optimistic pass: the scheduler's order differs from the run's
         KeyRun* run = nullptr;
         std::vector<nfa::TimerFire> fires;   // the scheduler's fires of this key so far
     };
@@ -240,6 +241,10 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
                 for (size_t x = f + 1; x < c.e; ++x)
                     if (logs[x].type == nfa::LOG_FIRE_END) { end = x; break; }
                 ok = end != NONE && (logs[f].g == g ? logs[f].t == clock : clock <= logs[end].t && c.mode == PENDING);
+                if (!ok && optimistic && end != NONE) {  // apply its records anyway; the device reruns the key
+                    ok = true;
+                    c.reordered = true;
+                }
             }
             if (ok) {
                 for (size_t x = f + 1; x < end; ++x) {
@@ -253,6 +258,13 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
                 c.mode = DEV;
                 const size_t nf = next_fire(c);
                 if (nf != NONE) fireq.push({(int64_t)logs[nf].g, key});
+                return;
+            }
+            if (optimistic) {  // no such device fire: model its pops, rerun the key on the device
+                c.reordered = true;
+                KS& k = work_.sc[sch].ks[key];
+                while (!k.q.empty() && k.q.front() <= clock) pop(sch, key);
+                out.rank[rank_key(g, sch, key)] = Slot{g, rk};
                 return;
             }
             takeover(key, g, true);
@@ -335,6 +347,10 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
             rowq.pop();
             KC& c = kc[key];
             if (c.mode == DEV) continue;
+            if (c.mode == PENDING && optimistic) {  // its event comes before the delayed fire: reorder
+                c.reordered = true;
+                continue;
+            }
             if (c.mode == PENDING) takeover(key, g, false);
             if (c.run->next_row_pos() != g) continue;
             c.run->row_at(g);
@@ -343,9 +359,24 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
             if (nr >= 0) rowq.push({nr, key});
         }
         // 4. the device keys' pushes made by the event at g
-        for (; ep < evp.size() && posof(evp[ep]) == g; ++ep)
-            if (kc[logs[evp[ep]].key].mode == DEV) notify(logs[evp[ep]].sched, logs[evp[ep]].key, logs[evp[ep]].t);
+        for (; ep < evp.size() && posof(evp[ep]) == g; ++ep) {
+            const uint8_t m = kc[logs[evp[ep]].key].mode;
+            if (m == DEV || (optimistic && m == PENDING)) notify(logs[evp[ep]].sched, logs[evp[ep]].key, logs[evp[ep]].t);
+        }
         ++g;
+    }
+    if (optimistic) {  // the reordered keys (incl. device fires never made here), with the scheduler's fire lists
+        for (auto& kv : kc)
+            if (kv.second.reordered || kv.second.mode == PENDING || next_fire(kv.second) != NONE)
+                out.reordered.push_back(kv.first);
+        std::sort(out.reordered.begin(), out.reordered.end());
+        out.fire_off.push_back(0);
+        for (uint32_t k : out.reordered) {
+            const KC& c = kc[k];
+            out.fires.insert(out.fires.end(), c.fires.begin(), c.fires.end());
+            out.fire_off.push_back((uint32_t)out.fires.size());
+        }
+        return;
     }
     // device fires the scheduler never made in this batch (delayed past its end): host replay without them
     std::vector<uint32_t> late;

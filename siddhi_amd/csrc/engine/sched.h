@@ -80,6 +80,9 @@ class SchedSim {
     };
     struct Result {
         std::vector<uint32_t> taken;                         // keys run on the host (their device run is void)
+        // optimistic pass: keys whose device run the scheduler reordered (and their fire lists in its order)
+        std::vector<uint32_t> reordered, fire_off;
+        std::vector<nfa::TimerFire> fires;
         std::unordered_map<uint64_t, Slot> rank;             // (position in the key's run, scheduler, key) -> slot
         int64_t n_fires = 0, n_shifted = 0;
     };
@@ -94,8 +97,13 @@ class SchedSim {
     void queued_keys(std::vector<uint32_t>& out) const;
     // one pass over the batch; logs sorted by (key, kseq). take_over(key) returns a started KeyRun for the key
     // (batch-start state, its rows); the caller owns it. Works on a copy of the committed state (commit()).
+    // optimistic: never take over -- a key the scheduler reorders keeps its device records where they apply (as if
+    // its events and fires commuted) and is listed in out.reordered with its fire list, to be rerun on the device
+    // in that order before the exact (non-optimistic) pass. The optimistic pass only saves host replays; the
+    // exact pass alone decides the result.
     void simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& logs, const std::vector<int32_t>& key_hash,
-                  const KeyRows& rows, const std::function<KeyRun*(uint32_t)>& take_over, Result& out);
+                  const KeyRows& rows, const std::function<KeyRun*(uint32_t)>& take_over, Result& out,
+                  bool optimistic = false);
     void commit() { cur_ = work_; }
     static uint64_t rank_key(uint32_t g, int sch, uint32_t key) {
         return ((uint64_t)g << 32) ^ ((uint64_t)sch << 27) ^ (uint64_t)key * 0x9E3779B97F4A7C15ull;

@@ -386,7 +386,7 @@ __global__ __launch_bounds__(256) void nfa_k(const NfaArgs* __restrict__ pa) {
     c.key = (uint32_t)k;
     c.T = a.T;
     c.fires = nullptr;
-    c.nfires = 0;
+    c.nfires = -1;  // ideal mode unless a rerun list gives the fires
     if (a.list) {
         c.fires = a.fires + a.fire_off[idx];
         c.nfires = (int32_t)(a.fire_off[idx + 1] - a.fire_off[idx]);

@@ -32,6 +32,8 @@ def lib():
         L.emu_flush.argtypes = [P]
         L.emu_advance.argtypes = [P, I64]
         L.emu_send_batch.argtypes = [P, I64, P, P, P, P, P]
+        L.emu_sched_stat.restype = I64
+        L.emu_sched_stat.argtypes = [I32]
         L.emu_start.argtypes = [P, I64]
         L.emu_num_queries.argtypes = [P]
         for f in ("emu_query_name", "emu_query_target"):

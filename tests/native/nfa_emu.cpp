@@ -104,6 +104,8 @@ BatchClock batch_clock(Emu* e) {
     return bc;
 }
 
+size_t reordered_ = 0, taken_ = 0;  // last flush's scheduler statistics (tests)
+
 int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
     HostQuery& h = q.hq;
     const Plan& P = h.plan;
@@ -185,7 +187,7 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
     std::map<uint32_t, std::vector<nfa::SchedLog>> klog;
     std::vector<int64_t> stk(STACK);
     auto run_one = [&](uint32_t k, const nfa::TimerFire* fires, int nfires) -> int {
-        const int64_t cap = 2 * (seg_e[k] - seg_b[k]) + 4096 + 64 * (int64_t)nfires;
+        const int64_t cap = 2 * (seg_e[k] - seg_b[k]) + 4096 + 64 * (int64_t)std::max(nfires, 0);
         std::vector<int64_t> o_ts(cap), o_vals((size_t)std::max(P.n_out, 1) * cap), o_seq(cap), o_sub(cap);
         std::vector<uint32_t> o_nulls(cap), o_key(cap);
         unsigned long long count = 0, lcount = 0;
@@ -248,7 +250,7 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
             seg_b.resize(k + 1, 0);
             seg_e.resize(k + 1, 0);
         }
-        int rc = run_one(k, nullptr, 0);
+        int rc = run_one(k, nullptr, -1);  // ideal mode
         if (rc) return rc;
     }
     SchedSim::Result res;
@@ -291,7 +293,22 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
             r->start(&P, h.code.data(), h.consts.data(), q.L, T, e->seq);
             return r;
         };
+        // optimistic pass: keys the scheduler reorders are rerun with its fire order (the device does this in one
+        // launch), then the exact pass decides, replaying on the host only what still differs
+        q.sim.simulate(bc, all, q.key_hash, kr, take, res, true);
+        if (!res.reordered.empty()) {
+            for (size_t d = 0; d < res.reordered.size(); ++d) {
+                const uint32_t k = res.reordered[d];
+                q.arenas[k] = backup[k];
+                int rc = run_one(k, res.fires.data() + res.fire_off[d], (int)(res.fire_off[d + 1] - res.fire_off[d]));
+                if (rc) return rc;
+            }
+            all.clear();
+            for (auto& kv : klog) all.insert(all.end(), kv.second.begin(), kv.second.end());
+        }
+        reordered_ = res.reordered.size();
         q.sim.simulate(bc, all, q.key_hash, kr, take, res);
+        taken_ = res.taken.size();
         q.sim.commit();
         for (auto& r : runs) {  // the host runs replace those keys' device results
             if (r->overflow()) {
@@ -430,6 +447,7 @@ int emu_flush(void* h) {
     return 0;
 }
 
+int64_t emu_sched_stat(int which) { return which == 0 ? (int64_t)reordered_ : (int64_t)taken_; }
 int emu_num_queries(void* h) { return (int)((Emu*)h)->qs.size(); }
 const char* emu_query_name(void* h, int q) { return ((Emu*)h)->qs[q]->hq.name.c_str(); }
 const char* emu_query_target(void* h, int q) { return ((Emu*)h)->qs[q]->hq.target.c_str(); }
