@@ -143,6 +143,7 @@ typedef struct sdg_stats {
     int64_t sched_shifted;     /* fires the reference's scheduler ran later than the key's device run did (same
                                   result, later in the delivery order) */
     int64_t sched_host_keys;   /* keys the scheduler simulation replayed on the host (their order changed results) */
+    int64_t sched_rerun_keys;  /* keys rerun on the device with the scheduler's fire order (optimistic pass) */
 } sdg_stats;
 int sdg_last_stats(sdg_engine* e, sdg_stats* out);
 

@@ -83,7 +83,7 @@ class Stats(ctypes.Structure):
                 ("fused_ovf", ctypes.c_int64),
                 ("sched_fires", ctypes.c_int64),
                 ("sched_shifted", ctypes.c_int64),
-                ("sched_host_keys", ctypes.c_int64)]
+                ("sched_host_keys", ctypes.c_int64), ("sched_rerun_keys", ctypes.c_int64)]
 
 
 _lib = None

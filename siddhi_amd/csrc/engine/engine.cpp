@@ -158,6 +158,7 @@ struct QueryRt {
     bool last_timers = false;
     int64_t last_seq_base = 0;
     std::unordered_map<uint64_t, SchedSim::Slot> last_rank;
+    std::vector<uint32_t> reordered;  // keys rerun with the scheduler's fire order (sorted)
     std::vector<uint32_t> taken;
     std::vector<std::unique_ptr<KeyRun>> runs;
     // batch staging
@@ -760,7 +761,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             a.out_nulls = (uint32_t*)q.o_nulls.ensure(cap * 4);
             a.out_emit_seq = (int64_t*)q.o_emit.ensure(cap * 8);
             a.out_sub = (int64_t*)q.o_first.ensure(cap * 8);
-            a.out_round = nullptr;
+            a.out_round = timers ? (uint8_t*)q.o_round.ensure(cap) : nullptr;
         };
         int hf[8];
         unsigned long long hc[2];
@@ -810,24 +811,40 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         };
         bind_out();
         HIPCHECK(hipEventRecord(e->ev[8], st));
-        a.list = nullptr;
-        a.round = 0;
-        for (int tries = 0; !launch(true); ++tries)  // state is double-buffered: a retry starts from the batch start
-            if (tries > 8) throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': output buffers keep overflowing");
-        e->stats.match_launches += 1;
+        auto first_run = [&]() {
+            a.list = nullptr;
+            a.nlist = 0;
+            a.round = 0;
+            for (int tries = 0; !launch(true); ++tries)  // state is double-buffered: a retry starts from the batch start
+                if (tries > 8) throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': output buffers keep overflowing");
+            e->stats.match_launches += 1;
+        };
+        first_run();
         q.last_timers = timers;
         q.last_rank.clear();
         q.taken.clear();
+        q.reordered.clear();
         q.runs.clear();
         q.last_seq_base = e->seq;
         if (timers) {
-            // one pass of the global scheduler (sched.h) over the runs' logs; the keys it takes over are replayed
-            // on the host from their batch-start state and their results replace the device's
-            std::vector<nfa::SchedLog> logs(hc[1]);
-            if (hc[1]) HIPCHECK(hipMemcpy(logs.data(), a.T.log, hc[1] * sizeof(nfa::SchedLog), hipMemcpyDeviceToHost));
-            std::sort(logs.begin(), logs.end(), [](const nfa::SchedLog& x, const nfa::SchedLog& y) {
-                return x.key != y.key ? x.key < y.key : x.kseq < y.kseq;
-            });
+            // the global scheduler (sched.h) over the runs' logs, in two passes: an optimistic one lists the keys
+            // whose fires it orders differently from their own runs, which rerun on the device with its fire order
+            // (round 1); the exact pass then checks every key and replays on the host, from its batch-start state,
+            // what still differs (their results replace the device's)
+            std::vector<nfa::SchedLog> logs;
+            auto read_logs = [&](bool keep_unlisted) {
+                std::vector<nfa::SchedLog> nl(hc[1]);
+                if (hc[1]) HIPCHECK(hipMemcpy(nl.data(), a.T.log, hc[1] * sizeof(nfa::SchedLog), hipMemcpyDeviceToHost));
+                if (keep_unlisted) {  // the first run's records of the keys that were not rerun
+                    for (const nfa::SchedLog& r : logs)
+                        if (!std::binary_search(q.reordered.begin(), q.reordered.end(), r.key)) nl.push_back(r);
+                }
+                logs.swap(nl);
+                std::sort(logs.begin(), logs.end(), [](const nfa::SchedLog& x, const nfa::SchedLog& y) {
+                    return x.key != y.key ? x.key < y.key : x.kseq < y.kseq;
+                });
+            };
+            read_logs(false);
             while ((int64_t)q.key_hash.size() < (int64_t)K) {  // HashMap hash of each key's toString
                 const size_t k = q.key_hash.size();
                 const std::string& ks = q.string_keys ? e->strings.strs[k] : q.keystr[k];
@@ -891,6 +908,33 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 return r;
             };
             SchedSim::Result res;
+            for (int tries = 0;; ++tries) {
+                q.sim.simulate(e->bc, logs, q.key_hash, kr, take, res, true);
+                q.reordered = res.reordered;
+                if (q.reordered.empty()) break;
+                const int64_t nl = (int64_t)q.reordered.size();
+                a.list = (const uint32_t*)q.d_list.ensure(nl * 4);
+                a.fire_off = (const uint32_t*)q.d_foff.ensure((nl + 1) * 4);
+                a.fires = (const nfa::TimerFire*)q.d_fires.ensure(std::max<size_t>(1, res.fires.size()) * sizeof(nfa::TimerFire));
+                HIPCHECK(hipMemcpyAsync((void*)a.list, q.reordered.data(), nl * 4, hipMemcpyHostToDevice, st));
+                HIPCHECK(hipMemcpyAsync((void*)a.fire_off, res.fire_off.data(), (nl + 1) * 4, hipMemcpyHostToDevice, st));
+                if (!res.fires.empty())
+                    HIPCHECK(hipMemcpyAsync((void*)a.fires, res.fires.data(), res.fires.size() * sizeof(nfa::TimerFire),
+                                            hipMemcpyHostToDevice, st));
+                a.nlist = (int32_t)nl;
+                a.round = 1;
+                e->stats.match_launches += 1;
+                if (launch(false)) {
+                    read_logs(true);
+                    break;
+                }
+                // outputs or logs overflowed in the rerun (buffers grown): everything again from the batch start
+                if (tries > 8) throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': output buffers keep overflowing");
+                first_run();
+                q.reordered.clear();
+                read_logs(false);
+            }
+            q.runs.clear();
             q.sim.simulate(e->bc, logs, q.key_hash, kr, take, res);
             for (auto& r : q.runs) {
                 if (r->overflow())
@@ -907,6 +951,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             e->stats.sched_fires += res.n_fires;
             e->stats.sched_shifted += res.n_shifted;
             e->stats.sched_host_keys += (int64_t)res.taken.size();
+            e->stats.sched_rerun_keys += (int64_t)q.reordered.size();
             nfa_commit(q.cur_bits.as<uint8_t>(), q.ran_bits.as<uint8_t>(), q.arena_keys, st);
         }
         HIPCHECK(hipEventRecord(e->ev[2], st));
@@ -1151,9 +1196,14 @@ void drain(sdg_engine* e, QueryRt& q) {
     uint32_t* nulls = (uint32_t*)(vals + (size_t)na * n);
     hipStream_t st = e->stream;
     std::vector<uint32_t> okey;
+    std::vector<uint8_t> oround;
     if (q.last_timers) {  // timer matches: drop the records of keys replayed on the host, order the fires
         okey.resize(n);
         HIPCHECK(hipMemcpyAsync(okey.data(), q.o_key.p, n * 4, hipMemcpyDeviceToHost, st));
+        if (!q.reordered.empty()) {  // and the first run's records of the keys rerun with the scheduler's order
+            oround.resize(n);
+            HIPCHECK(hipMemcpyAsync(oround.data(), q.o_round.p, n, hipMemcpyDeviceToHost, st));
+        }
     }
     HIPCHECK(hipMemcpyAsync(ts, q.o_ts.p, n * 8, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipMemcpyAsync(emit, q.o_emit.p, n * 8, hipMemcpyDeviceToHost, st));
@@ -1198,6 +1248,8 @@ void drain(sdg_engine* e, QueryRt& q) {
     for (int64_t i = 0; i < n; ++i) {
         if (q.last_timers) {
             if (std::binary_search(q.taken.begin(), q.taken.end(), okey[i])) continue;
+            if (!oround.empty() && oround[i] == 0 && std::binary_search(q.reordered.begin(), q.reordered.end(), okey[i]))
+                continue;
             slot(emit[i], first[i], okey[i]);
         }
         ord.push_back(i);
@@ -1287,7 +1339,7 @@ int do_flush(sdg_engine* e) {
     e->stats.ms_chain_carry = e->stats.ms_chain_match = e->stats.ms_chain_emit = 0;
     e->stats.ms_nfa = 0;
     e->stats.fused_ovf = 0;
-    e->stats.sched_fires = e->stats.sched_shifted = e->stats.sched_host_keys = 0;
+    e->stats.sched_fires = e->stats.sched_shifted = e->stats.sched_host_keys = e->stats.sched_rerun_keys = 0;
     // a flush consumes its batch whether or not it succeeds: a failing query must not make the next flush
     // replay the events onto the queries that already committed them
     struct Consume {
