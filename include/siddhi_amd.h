@@ -144,6 +144,9 @@ typedef struct sdg_stats {
                                   result, later in the delivery order) */
     int64_t sched_host_keys;   /* keys the scheduler simulation replayed on the host (their order changed results) */
     int64_t sched_rerun_keys;  /* keys rerun on the device with the scheduler's fire order (optimistic pass) */
+    double ms_nfa_kernel;      /* device ms inside nfa_k launches (first run + reruns); ms_nfa also counts the host
+                                  scheduler simulation, log read-back and host replays between them */
+    double ms_sched_host;      /* host ms: scheduler simulation passes, log read-back, host replays */
 } sdg_stats;
 int sdg_last_stats(sdg_engine* e, sdg_stats* out);
 

@@ -132,6 +132,8 @@ def run_c4(keys):
                       "device_ms": dev_ms, "ms_nfa": s1.ms_nfa + s2.ms_nfa, "events_per_s_device": n / (dev_ms / 1000),
                       "timer_fires": s1.sched_fires + s2.sched_fires,
                       "fires_shifted_by_collapse": s1.sched_shifted + s2.sched_shifted,
+                      "ms_nfa_kernel": s1.ms_nfa_kernel + s2.ms_nfa_kernel,
+                      "ms_sched_host": s1.ms_sched_host + s2.ms_sched_host,
                       "keys_rerun_in_scheduler_order": s1.sched_rerun_keys + s2.sched_rerun_keys,
                       "keys_replayed_on_host": s1.sched_host_keys + s2.sched_host_keys,
                       "end_to_end_s": dt}), flush=True)

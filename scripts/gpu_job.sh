@@ -33,6 +33,7 @@ for s in "$@"; do
         c3prof) run c3prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/c3prof" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3m --c3-steps 1 --warmup 1 ;;
         newtests) run newtests 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "regime or long_keys or auto_flush or consumes or many_keys or synthetic" ;;
         c4) run c4 600 python3 scripts/bench_configs.py --only c4 ;;
+        c4prof) run c4prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/c4prof" -o run --output-format csv -- python3 scripts/bench_configs.py --only c4 ;;
         c4test) run c4test 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -s --timeout 300 --timeout-method thread -p no:cacheprovider -k c4 ;;
         *) echo "unknown step $s" ;;
     esac

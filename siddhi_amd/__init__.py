@@ -83,7 +83,8 @@ class Stats(ctypes.Structure):
                 ("fused_ovf", ctypes.c_int64),
                 ("sched_fires", ctypes.c_int64),
                 ("sched_shifted", ctypes.c_int64),
-                ("sched_host_keys", ctypes.c_int64), ("sched_rerun_keys", ctypes.c_int64)]
+                ("sched_host_keys", ctypes.c_int64), ("sched_rerun_keys", ctypes.c_int64),
+                ("ms_nfa_kernel", ctypes.c_double), ("ms_sched_host", ctypes.c_double)]
 
 
 _lib = None

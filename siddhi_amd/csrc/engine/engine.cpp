@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -157,7 +158,7 @@ struct QueryRt {
     // scheduler replayed on the host (their device records are void) and those replays
     bool last_timers = false;
     int64_t last_seq_base = 0;
-    std::unordered_map<uint64_t, SchedSim::Slot> last_rank;
+    SchedSim::RankMap last_rank;
     std::vector<uint32_t> reordered;  // keys rerun with the scheduler's fire order (sorted)
     std::vector<uint32_t> taken;
     std::vector<std::unique_ptr<KeyRun>> runs;
@@ -776,10 +777,15 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             }
             *h_na = a;
             HIPCHECK(hipMemcpyAsync(d_na, h_na, sizeof(NfaArgs), hipMemcpyHostToDevice, st));
+            HIPCHECK(hipEventRecord(e->ev[10], st));
             nfa_run(a, d_na, st);
+            HIPCHECK(hipEventRecord(e->ev[11], st));
             HIPCHECK(hipMemcpyAsync(hc, counters, 16, hipMemcpyDeviceToHost, st));
             HIPCHECK(hipMemcpyAsync(hf, flags, 32, hipMemcpyDeviceToHost, st));
             HIPCHECK(hipStreamSynchronize(st));
+            float kms = 0;
+            HIPCHECK(hipEventElapsedTime(&kms, e->ev[10], e->ev[11]));
+            e->stats.ms_nfa_kernel += kms;
             if (hf[4]) throw CompileError(SDG_ERR_ARG, "device-resident partition key ids out of range (not from sdg_intern)");
             if (hf[2]) {
                 e->stats.overflow += 1;
@@ -827,6 +833,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         q.runs.clear();
         q.last_seq_base = e->seq;
         if (timers) {
+            const auto t_sched = std::chrono::steady_clock::now();
+            double k_before = e->stats.ms_nfa_kernel;
             // the global scheduler (sched.h) over the runs' logs, in two passes: an optimistic one lists the keys
             // whose fires it orders differently from their own runs, which rerun on the device with its fire order
             // (round 1); the exact pass then checks every key and replays on the host, from its batch-start state,
@@ -839,10 +847,24 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                     for (const nfa::SchedLog& r : logs)
                         if (!std::binary_search(q.reordered.begin(), q.reordered.end(), r.key)) nl.push_back(r);
                 }
-                logs.swap(nl);
-                std::sort(logs.begin(), logs.end(), [](const nfa::SchedLog& x, const nfa::SchedLog& y) {
-                    return x.key != y.key ? x.key < y.key : x.kseq < y.kseq;
-                });
+                // by (key, kseq): a stable counting sort by key (a lane appends its key's records in order); a key
+                // whose records came out of order is sorted by kseq
+                uint32_t kmax = 0;
+                for (const nfa::SchedLog& r : nl) kmax = std::max(kmax, r.key);
+                std::vector<uint32_t> cnt(nl.empty() ? 1 : (size_t)kmax + 2, 0);
+                for (const nfa::SchedLog& r : nl) ++cnt[r.key + 1];
+                for (size_t k = 1; k < cnt.size(); ++k) cnt[k] += cnt[k - 1];
+                logs.resize(nl.size());
+                for (const nfa::SchedLog& r : nl) logs[cnt[r.key]++] = r;
+                for (size_t i = 0; i < logs.size();) {
+                    size_t j = i + 1;
+                    bool sorted = true;
+                    for (; j < logs.size() && logs[j].key == logs[i].key; ++j) sorted &= logs[j - 1].kseq < logs[j].kseq;
+                    if (!sorted)
+                        std::sort(logs.begin() + i, logs.begin() + j,
+                                  [](const nfa::SchedLog& x, const nfa::SchedLog& y) { return x.kseq < y.kseq; });
+                    i = j;
+                }
             };
             read_logs(false);
             while ((int64_t)q.key_hash.size() < (int64_t)K) {  // HashMap hash of each key's toString
@@ -953,6 +975,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             e->stats.sched_host_keys += (int64_t)res.taken.size();
             e->stats.sched_rerun_keys += (int64_t)q.reordered.size();
             nfa_commit(q.cur_bits.as<uint8_t>(), q.ran_bits.as<uint8_t>(), q.arena_keys, st);
+            e->stats.ms_sched_host += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_sched).count() -
+                                      (e->stats.ms_nfa_kernel - k_before);
         }
         HIPCHECK(hipEventRecord(e->ev[2], st));
         HIPCHECK(hipStreamSynchronize(st));
@@ -1238,10 +1262,10 @@ void drain(sdg_engine* e, QueryRt& q) {
     auto slot = [&](int64_t& em, int64_t& fs, uint32_t key) {  // a timer match: its fire's slot (position, rank)
         if (fs >= 0) return;
         const int sch = (int)((fs >> 48) & 0x7F);
-        auto it = q.last_rank.find(SchedSim::rank_key((uint32_t)(em - q.last_seq_base), sch, key));
-        if (it == q.last_rank.end()) return;
-        em = q.last_seq_base + it->second.g;
-        fs = INT64_MIN | ((int64_t)it->second.rank << 24) | (fs & 0xFFFFFF);
+        const SchedSim::Slot* it = q.last_rank.find(SchedSim::rank_key((uint32_t)(em - q.last_seq_base), sch, key));
+        if (!it) return;
+        em = q.last_seq_base + it->g;
+        fs = INT64_MIN | ((int64_t)it->rank << 24) | (fs & 0xFFFFFF);
     };
     std::vector<int64_t> ord;  // < n: device record, >= n: host record n + i
     ord.reserve(n + nh);
@@ -1337,7 +1361,7 @@ int do_flush(sdg_engine* e) {
     e->stats.overflow = 0;
     e->stats.ms_kg_hist = e->stats.ms_kg_prefix = e->stats.ms_kg_scatter = 0;
     e->stats.ms_chain_carry = e->stats.ms_chain_match = e->stats.ms_chain_emit = 0;
-    e->stats.ms_nfa = 0;
+    e->stats.ms_nfa = e->stats.ms_nfa_kernel = e->stats.ms_sched_host = 0;
     e->stats.fused_ovf = 0;
     e->stats.sched_fires = e->stats.sched_shifted = e->stats.sched_host_keys = e->stats.sched_rerun_keys = 0;
     // a flush consumes its batch whether or not it succeeds: a failing query must not make the next flush

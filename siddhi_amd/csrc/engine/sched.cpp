@@ -2,6 +2,7 @@
 #include "sched.h"
 
 #include <algorithm>
+#include <chrono>
 #include <queue>
 #include <cmath>
 #include <cstdio>
@@ -69,8 +70,8 @@ int32_t java_spread_hash(const std::string& s) {  // String.hashCode over UTF-16
 
 void SchedSim::queued_keys(std::vector<uint32_t>& out) const {
     for (const SchedState& S : cur_.sc)
-        for (const auto& kv : S.ks)
-            if (!kv.second.q.empty()) out.push_back(kv.first);
+        for (size_t k = 0; k < S.ks.size(); ++k)
+            if (S.ks[k].n > 0) out.push_back((uint32_t)k);
     std::sort(out.begin(), out.end());
     out.erase(std::unique(out.begin(), out.end()), out.end());
 }
@@ -81,13 +82,67 @@ SchedSim::OKey SchedSim::okey(const SchedState& S, const KS& k, uint32_t key) co
     return OKey{(uint32_t)k.hash & (S.cap - 1), ~k.stamp, key};     // HashMap iteration order
 }
 
-void SchedSim::due_add(SchedState& S, uint32_t key, const KS& k) { S.due[k.q.front()].insert(okey(S, k, key)); }
+void SchedSim::qpush(KS& k, int64_t t) {
+    if (k.spill < 0 && k.n < (uint32_t)QI) {
+        k.a[k.n++] = t;
+        return;
+    }
+    if (k.spill < 0) {  // outgrew the inline slots
+        if (!work_.spill_free.empty()) {
+            k.spill = work_.spill_free.back();
+            work_.spill_free.pop_back();
+        } else {
+            k.spill = (int32_t)work_.spill.size();
+            work_.spill.emplace_back();
+        }
+        std::deque<int64_t>& d = work_.spill[k.spill];
+        d.assign(k.a, k.a + k.n);
+    }
+    work_.spill[k.spill].push_back(t);
+    ++k.n;
+}
 
-void SchedSim::due_del(SchedState& S, uint32_t key, const KS& k) {
-    auto it = S.due.find(k.q.front());
-    if (it == S.due.end()) return;
-    it->second.erase(okey(S, k, key));
-    if (it->second.empty()) S.due.erase(it);
+void SchedSim::qpop(KS& k) {
+    if (k.n == 0) return;
+    --k.n;
+    if (k.spill < 0) {
+        for (uint32_t i = 0; i < k.n; ++i) k.a[i] = k.a[i + 1];
+        return;
+    }
+    std::deque<int64_t>& d = work_.spill[k.spill];
+    d.pop_front();
+    if (k.n <= (uint32_t)QI) {  // back inline
+        for (uint32_t i = 0; i < k.n; ++i) k.a[i] = d[i];
+        d.clear();
+        work_.spill_free.push_back(k.spill);
+        k.spill = -1;
+    }
+}
+
+void SchedSim::due_add(SchedState& S, uint32_t key, KS& k) {
+    const DueE e{okey(S, k, key), ++k.ver};
+    std::vector<DueE>& h = S.due[qfront(k)];
+    h.push_back(e);
+    std::push_heap(h.begin(), h.end(), std::greater<DueE>());
+}
+
+bool SchedSim::due_front(SchedState& S, int64_t& t, OKey& k) {
+    while (!S.due.empty()) {
+        auto it = S.due.begin();
+        std::vector<DueE>& h = it->second;
+        while (!h.empty() && stale(S, h.front())) {
+            std::pop_heap(h.begin(), h.end(), std::greater<DueE>());
+            h.pop_back();
+        }
+        if (h.empty()) {
+            S.due.erase(it);
+            continue;
+        }
+        t = it->first;
+        k = h.front().k;
+        return true;
+    }
+    return false;
 }
 
 void SchedSim::resize(SchedState& S) {  // HashMap.resize(): 16 / 12, then doubling
@@ -100,63 +155,96 @@ void SchedSim::resize(SchedState& S) {  // HashMap.resize(): 16 / 12, then doubl
     }
     S.bin.assign(S.cap, 0);
     S.due.clear();
-    for (auto& kv : S.ks) {
-        if (!kv.second.in_map) continue;
-        S.bin[(uint32_t)kv.second.hash & (S.cap - 1)]++;
-        if (!kv.second.q.empty()) due_add(S, kv.first, kv.second);
+    for (size_t key = 0; key < S.ks.size(); ++key) {
+        KS& k = S.ks[key];
+        if (!k.in_map) continue;
+        S.bin[(uint32_t)k.hash & (S.cap - 1)]++;
+        if (k.n) {  // re-keyed by the new buckets (heaps rebuilt below)
+            S.due[qfront(k)].push_back(DueE{okey(S, k, (uint32_t)key), ++k.ver});
+        }
     }
+    for (auto& kv : S.due) std::make_heap(kv.second.begin(), kv.second.end(), std::greater<DueE>());
 }
 
 void SchedSim::notify(int sch, uint32_t key, int64_t t) {
     SchedState& S = work_.sc[sch];
-    KS& k = S.ks[key];
+    KS* k = &ks(S, key);
     if (partitioned_) {
         if (S.size > S.threshold || S.cap == 0) resize(S);  // computeIfAbsent: resize before the lookup
-        if (!k.in_map) {
-            k.hash = (*hash_)[key];
-            k.in_map = true;
-            k.stamp = ++S.stamp;
-            k.cseq = ++work_.cseq;
-            uint32_t& bc = S.bin[(uint32_t)k.hash & (S.cap - 1)];
+        if (!k->in_map) {
+            k->hash = (*hash_)[key];
+            k->in_map = true;
+            k->stamp = ++S.stamp;
+            k->cseq = ++work_.cseq;
+            uint32_t& bc = S.bin[(uint32_t)k->hash & (S.cap - 1)];
             const uint32_t before = bc++;
             ++S.size;
             if (before >= 7 && S.cap < 64) resize(S);  // treeifyBin on a table below MIN_TREEIFY_CAPACITY
         }
-    } else if (!k.in_map) {  // SingleStateHolder: created on first use, never removed
-        k.in_map = true;
-        k.cseq = ++work_.cseq;
+    } else if (!k->in_map) {  // SingleStateHolder: created on first use, never removed
+        k->in_map = true;
+        k->cseq = ++work_.cseq;
     }
-    const bool was_empty = k.q.empty();
-    k.q.push_back(t);
-    if (was_empty) due_add(S, key, k);
+    const bool was_empty = k->n == 0;
+    qpush(*k, t);
+    if (was_empty) due_add(S, key, *k);
 }
 
 void SchedSim::pop(int sch, uint32_t key) {
     SchedState& S = work_.sc[sch];
+    if (key >= S.ks.size()) return;
     KS& k = S.ks[key];
-    if (k.q.empty()) return;
-    due_del(S, key, k);
-    k.q.pop_front();
-    if (!k.q.empty()) due_add(S, key, k);
+    if (k.n == 0) return;
+    due_del(k);
+    qpop(k);
+    if (k.n) due_add(S, key, k);
 }
 
 void SchedSim::remove_if_empty(int sch, uint32_t key) {  // returnState / returnAllStates of a drained state
     if (!partitioned_) return;
     SchedState& S = work_.sc[sch];
-    auto it = S.ks.find(key);
-    if (it == S.ks.end() || !it->second.q.empty() || !it->second.in_map) return;
-    S.bin[(uint32_t)it->second.hash & (S.cap - 1)]--;
+    if (key >= S.ks.size()) return;
+    KS& k = S.ks[key];
+    if (k.n || !k.in_map) return;
+    S.bin[(uint32_t)k.hash & (S.cap - 1)]--;
     --S.size;
-    S.ks.erase(it);
+    k.in_map = false;
+    k.stamp = k.cseq = 0;
 }
+
+namespace {
+// SDG_SCHED_PROF=1: per-section host time of simulate() on stderr (diagnostics)
+struct SecProf {
+    bool on = std::getenv("SDG_SCHED_PROF") != nullptr;
+    double t[12] = {};
+    std::chrono::steady_clock::time_point last;
+    void start() { if (on) last = std::chrono::steady_clock::now(); }
+    void lap(int i) {
+        if (!on) return;
+        auto n = std::chrono::steady_clock::now();
+        t[i] += std::chrono::duration<double, std::milli>(n - last).count();
+        last = n;
+    }
+    void print(const char* tag, size_t nl, size_t ne, int64_t nf) {
+        if (!on) return;
+        std::fprintf(stderr, "[sched setup: kc %.1f scan %.1f sort %.1f heap %.1f]\n", t[8], t[9], t[10], t[11]);
+        std::fprintf(stderr, "[sched %s] logs %zu evpush %zu fires %lld; copy %.1f setup %.1f fires %.1f fireq %.1f rows %.1f pushes %.1f end %.1f next %.1f ms\n", tag, nl, ne, (long long)nf,
+                     t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7]);
+    }
+};
+}  // namespace
 
 void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& logs,
                         const std::vector<int32_t>& key_hash, const KeyRows& rows,
                         const std::function<KeyRun*(uint32_t)>& take_over, Result& out, bool optimistic) {
     using nfa::SchedLog;
+    SecProf prof;
+    prof.start();
     work_ = cur_;
+    prof.lap(0);
     hash_ = &key_hash;
     out = Result{};
+    out.rank.reserve(logs.size() / 4 + 16);
     constexpr size_t NONE = ~size_t(0);
     enum : uint8_t { DEV = 0, PENDING = 1, HOST = 2 };  // the key's history so far: its device run / a device fire
                                                       // the scheduler has not made yet / stepped on the host
@@ -164,34 +252,80 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
         size_t i = 0, e = 0;                 // cursor into the key's device records
         uint8_t mode = DEV;
         bool reordered = false;              // optimistic pass: the scheduler's order differs from the run's
+        bool touched = false;
         KeyRun* run = nullptr;
-        std::vector<nfa::TimerFire> fires;   // the scheduler's fires of this key so far
+        int32_t fh = -1, ft = -1;            // the scheduler's fires of this key so far (list in `fl`)
     };
-    std::unordered_map<uint32_t, KC> kc;
+    struct FN {
+        nfa::TimerFire f;
+        int32_t next;
+    };
+    std::vector<FN> fl;
+    // keys: dense ids; the table covers every key with records, rows or a queued state
+    size_t nkeys = (size_t)std::max<int64_t>(rows.K, 0);
+    for (const SchedState& S : work_.sc) nkeys = std::max(nkeys, S.ks.size());
+    if (!logs.empty()) nkeys = std::max(nkeys, (size_t)logs.back().key + 1);
+    std::vector<KC> kc(nkeys);
+    prof.lap(8);
+    std::vector<uint32_t> touched;
+    auto K = [&](uint32_t key) -> KC& {
+        KC& c = kc[key];
+        if (!c.touched) {
+            c.touched = true;
+            touched.push_back(key);
+        }
+        return c;
+    };
     auto posof = [&](size_t i) -> int64_t { return logs[i].g == 0xFFFFFFFFu ? -1 : (int64_t)logs[i].g; };
     auto is_evpush = [&](size_t i) { return logs[i].type == nfa::LOG_PUSH && logs[i].origin == nfa::ORIGIN_EVENT; };
     std::vector<size_t> evp;  // pushes made while processing events, applied at their positions
     for (size_t i = 0; i < logs.size();) {
         size_t j = i;
         while (j < logs.size() && logs[j].key == logs[i].key) ++j;
-        KC& c = kc[logs[i].key];
+        KC& c = K(logs[i].key);
         c.i = i;
         c.e = j;
         for (size_t x = i; x < j; ++x)
             if (is_evpush(x)) evp.push_back(x);
         i = j;
     }
-    std::stable_sort(evp.begin(), evp.end(), [&](size_t a, size_t b) { return posof(a) < posof(b); });
+    prof.lap(9);
+    {  // by position, stable: sort (position + 1, record index) packed in one word (no record loads in the sort)
+        std::vector<uint64_t> pk(evp.size());
+        for (size_t x = 0; x < evp.size(); ++x) pk[x] = ((uint64_t)(posof(evp[x]) + 1) << 32) | (uint64_t)evp[x];
+        std::sort(pk.begin(), pk.end());
+        for (size_t x = 0; x < evp.size(); ++x) evp[x] = (size_t)(pk[x] & 0xFFFFFFFFu);
+    }
+    prof.lap(10);
     auto next_fire = [&](KC& c) -> size_t {  // the key's next device fire (event pushes go by position)
         while (c.i < c.e && is_evpush(c.i)) ++c.i;
         return c.i < c.e && logs[c.i].type == nfa::LOG_FIRE ? c.i : NONE;
     };
     using HE = std::pair<int64_t, uint32_t>;
-    std::priority_queue<HE, std::vector<HE>, std::greater<HE>> fireq, rowq;
-    for (auto& kv : kc) {
-        const size_t f = next_fire(kv.second);
-        if (f != NONE) fireq.push({(int64_t)logs[f].g, kv.first});
+    struct MergeQ {  // a sorted initial run + a heap for later pushes (min first)
+        std::vector<HE> a;
+        size_t ai = 0;
+        std::priority_queue<HE, std::vector<HE>, std::greater<HE>> h;
+        bool empty() const { return ai == a.size() && h.empty(); }
+        const HE& top() const {
+            if (ai == a.size()) return h.top();
+            if (h.empty()) return a[ai];
+            return h.top() < a[ai] ? h.top() : a[ai];
+        }
+        void pop() {
+            if (ai < a.size() && (h.empty() || !(h.top() < a[ai]))) ++ai;
+            else h.pop();
+        }
+        void push(const HE& x) { h.push(x); }
+    };
+    MergeQ fireq;
+    for (uint32_t key : touched) {
+        const size_t f = next_fire(kc[key]);
+        if (f != NONE) fireq.a.push_back({(int64_t)logs[f].g, key});
     }
+    std::sort(fireq.a.begin(), fireq.a.end());
+    std::priority_queue<HE, std::vector<HE>, std::greater<HE>> rowq;
+    prof.lap(11);
     auto first_row_at = [&](uint32_t key, int64_t g) -> int64_t {  // position of the key's first row at >= g
         if (key >= (uint32_t)rows.K) return -1;
         int64_t a = rows.seg_b[key], b = rows.seg_e[key];
@@ -210,15 +344,22 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
             else if (L.type == nfa::LOG_POP) pop(L.sched, key);
         }
     };
+    auto add_fire = [&](KC& c, const nfa::TimerFire& f) {
+        fl.push_back(FN{f, -1});
+        const int32_t x = (int32_t)fl.size() - 1;
+        if (c.ft >= 0) fl[c.ft].next = x;
+        else c.fh = x;
+        c.ft = x;
+    };
     // replay the key on the host up to position g (its rows < g, the scheduler's fires so far except `skip_last`)
     auto takeover = [&](uint32_t key, int64_t g, bool skip_last) {
-        KC& c = kc[key];
+        KC& c = K(key);
         c.mode = HOST;
         c.run = take_over(key);
-        const size_t nf = c.fires.size() - (skip_last ? 1 : 0);
-        for (size_t f = 0; f < nf; ++f) {
-            c.run->rows_before(c.fires[f].g);
-            c.run->fire(c.fires[f].sched, c.fires[f].g, c.fires[f].clock);
+        for (int32_t x = c.fh; x >= 0; x = fl[x].next) {
+            if (skip_last && x == c.ft) break;
+            c.run->rows_before(fl[x].f.g);
+            c.run->fire(fl[x].f.sched, fl[x].f.g, fl[x].f.clock);
         }
         c.run->rows_before(g);
         c.run->lread = c.run->lcount;  // what the replay pushed / popped is in the model already
@@ -231,8 +372,8 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
     auto fire = [&](int sch, uint32_t key, uint32_t g, int64_t clock) {
         const uint32_t rk = rank++;
         ++out.n_fires;
-        KC& c = kc[key];
-        c.fires.push_back(nfa::TimerFire{g, sch, clock});
+        KC& c = K(key);
+        add_fire(c, nfa::TimerFire{g, sch, clock});
         if (c.mode != HOST) {
             const size_t f = next_fire(c);
             bool ok = f != NONE && logs[f].sched == sch && (int64_t)logs[f].g <= (int64_t)g;
@@ -253,7 +394,7 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
                     else if (L.type == nfa::LOG_PUSH) notify(L.sched, key, L.t);
                 }
                 if (logs[f].g != g) ++out.n_shifted;
-                out.rank[rank_key(logs[f].g, sch, key)] = Slot{g, rk};
+                out.rank.put(rank_key(logs[f].g, sch, key), Slot{g, rk});
                 c.i = end + 1;
                 c.mode = DEV;
                 const size_t nf = next_fire(c);
@@ -262,9 +403,8 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
             }
             if (optimistic) {  // no such device fire: model its pops, rerun the key on the device
                 c.reordered = true;
-                KS& k = work_.sc[sch].ks[key];
-                while (!k.q.empty() && k.q.front() <= clock) pop(sch, key);
-                out.rank[rank_key(g, sch, key)] = Slot{g, rk};
+                while (queued(sch, key) && head(sch, key) <= clock) pop(sch, key);
+                out.rank.put(rank_key(g, sch, key), Slot{g, rk});
                 return;
             }
             takeover(key, g, true);
@@ -272,27 +412,36 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
         c.run->rows_before(g);
         c.run->fire(sch, g, clock);
         apply_run(c, key);
-        out.rank[rank_key(g, sch, key)] = Slot{g, rk};
+        out.rank.put(rank_key(g, sch, key), Slot{g, rk});
     };
+    int64_t lb_t = INT64_MIN, lb_v = 0;  // last lower_bound over the clock (the earliest due time rarely changes)
     auto next_due = [&](int64_t from) -> int64_t {
-        int64_t hmin = INT64_MAX;
-        for (const SchedState& S : work_.sc)
-            if (!S.due.empty()) hmin = std::min(hmin, S.due.begin()->first);
+        int64_t hmin = INT64_MAX, t;
+        OKey k;
+        for (SchedState& S : work_.sc)
+            if (due_front(S, t, k)) hmin = std::min(hmin, t);
         if (hmin == INT64_MAX) return bc.G;
-        const int64_t lb = std::lower_bound(bc.clk.begin(), bc.clk.end(), hmin) - bc.clk.begin();
+        if (hmin != lb_t) {
+            lb_t = hmin;
+            lb_v = std::lower_bound(bc.clk.begin(), bc.clk.end(), hmin) - bc.clk.begin();
+        }
+        const int64_t lb = lb_v;
         const int64_t x = std::max(from, lb);
         return x >= bc.G ? bc.G : (int64_t)bc.nadv[x];
     };
     size_t ep = 0;
     for (; ep < evp.size() && posof(evp[ep]) < 0; ++ep)  // an unpartitioned query's init at start
-        if (kc[logs[evp[ep]].key].mode == DEV) notify(logs[evp[ep]].sched, logs[evp[ep]].key, logs[evp[ep]].t);
+        if (K(logs[evp[ep]].key).mode == DEV) notify(logs[evp[ep]].sched, logs[evp[ep]].key, logs[evp[ep]].t);
     int64_t g = 0;
+    std::vector<std::pair<int64_t, uint32_t>> W;
+    prof.lap(1);
     while (true) {
         int64_t nxt = ep < evp.size() ? posof(evp[ep]) : bc.G;
         nxt = std::min(nxt, next_due(g));
         if (!fireq.empty()) nxt = std::min(nxt, fireq.top().first);
         if (!rowq.empty()) nxt = std::min(nxt, rowq.top().first);
         nxt = std::max(nxt, g);
+        prof.lap(7);
         if (nxt >= bc.G) break;
         g = nxt;
         // 1. the clock advance at g: TimeChangeListeners (playback) / live_fire_until
@@ -302,9 +451,20 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
             if (!live_) {
                 for (int s = 0; s < n_sched_; ++s) {  // registration order; per listener a TreeMultimap, one per time
                     SchedState& S = work_.sc[s];
-                    std::vector<std::pair<int64_t, uint32_t>> W;
-                    for (auto it = S.due.begin(); it != S.due.end() && it->first <= clock; ++it)
-                        W.push_back({it->first, it->second.begin()->key});
+                    W.clear();
+                    for (auto it = S.due.begin(); it != S.due.end() && it->first <= clock;) {
+                        std::vector<DueE>& h = it->second;
+                        while (!h.empty() && stale(S, h.front())) {
+                            std::pop_heap(h.begin(), h.end(), std::greater<DueE>());
+                            h.pop_back();
+                        }
+                        if (h.empty()) {
+                            it = S.due.erase(it);
+                            continue;
+                        }
+                        W.push_back({it->first, h.front().k.key});
+                        ++it;
+                    }
                     for (auto& w : W) fire(s, w.second, (uint32_t)g, clock);
                     for (auto& w : W) remove_if_empty(s, w.second);  // returnAllStates
                 }
@@ -312,13 +472,10 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
                 int64_t now = g > 0 ? bc.clk[g - 1] : bc.clock0;
                 while (true) {  // the earliest due (time, creation) across every scheduler, one at a time
                     int bs = -1;
-                    int64_t bt = 0;
-                    OKey bk{};
+                    int64_t bt = 0, t;
+                    OKey bk{}, k;
                     for (int s = 0; s < n_sched_; ++s) {
-                        const SchedState& S = work_.sc[s];
-                        if (S.due.empty() || S.due.begin()->first > clock) continue;
-                        const int64_t t = S.due.begin()->first;
-                        const OKey& k = *S.due.begin()->second.begin();
+                        if (!due_front(work_.sc[s], t, k) || t > clock) continue;
                         if (bs < 0 || t < bt || (t == bt && k.a < bk.a)) { bs = s; bt = t; bk = k; }
                     }
                     if (bs < 0) break;
@@ -328,6 +485,7 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
                 }
             }
         }
+        prof.lap(2);
         // 2. device fires at <= g the scheduler did not make (yet): the key waits for its delayed fire
         while (!fireq.empty() && fireq.top().first <= g) {
             const uint32_t key = fireq.top().second;
@@ -341,6 +499,7 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
             const int64_t r = first_row_at(key, fg);  // an event of the key before the delayed fire: diverged
             if (r >= 0) rowq.push({r, key});
         }
+        prof.lap(3);
         // 3. rows at g of keys that wait for a delayed fire (diverged) or run on the host
         while (!rowq.empty() && rowq.top().first <= g) {
             const uint32_t key = rowq.top().second;
@@ -358,41 +517,48 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
             const int64_t nr = c.run->next_row_pos();
             if (nr >= 0) rowq.push({nr, key});
         }
+        prof.lap(4);
         // 4. the device keys' pushes made by the event at g
         for (; ep < evp.size() && posof(evp[ep]) == g; ++ep) {
             const uint8_t m = kc[logs[evp[ep]].key].mode;
             if (m == DEV || (optimistic && m == PENDING)) notify(logs[evp[ep]].sched, logs[evp[ep]].key, logs[evp[ep]].t);
         }
         ++g;
+        prof.lap(5);
     }
+    std::sort(touched.begin(), touched.end());
     if (optimistic) {  // the reordered keys (incl. device fires never made here), with the scheduler's fire lists
-        for (auto& kv : kc)
-            if (kv.second.reordered || kv.second.mode == PENDING || next_fire(kv.second) != NONE)
-                out.reordered.push_back(kv.first);
-        std::sort(out.reordered.begin(), out.reordered.end());
+        for (uint32_t k : touched) {
+            KC& c = kc[k];
+            if (c.reordered || c.mode == PENDING || next_fire(c) != NONE) out.reordered.push_back(k);
+        }
         out.fire_off.push_back(0);
         for (uint32_t k : out.reordered) {
-            const KC& c = kc[k];
-            out.fires.insert(out.fires.end(), c.fires.begin(), c.fires.end());
+            for (int32_t x = kc[k].fh; x >= 0; x = fl[x].next) out.fires.push_back(fl[x].f);
             out.fire_off.push_back((uint32_t)out.fires.size());
         }
+        prof.lap(6);
+        prof.print("optimistic", logs.size(), evp.size(), out.n_fires);
         return;
     }
     // device fires the scheduler never made in this batch (delayed past its end): host replay without them
     std::vector<uint32_t> late;
-    for (auto& kv : kc)
-        if (kv.second.mode == PENDING || (kv.second.mode == DEV && next_fire(kv.second) != NONE)) late.push_back(kv.first);
-    std::sort(late.begin(), late.end());
+    for (uint32_t k : touched) {
+        KC& c = kc[k];
+        if (c.mode == PENDING || (c.mode == DEV && next_fire(c) != NONE)) late.push_back(k);
+    }
     for (uint32_t key : late) {
         takeover(key, bc.G, false);
         apply_run(kc[key], key);
     }
-    for (auto& kv : kc)
-        if (kv.second.mode == HOST) {
-            kv.second.run->rows_before(bc.G);
-            apply_run(kv.second, kv.first);
+    for (uint32_t k : touched)
+        if (kc[k].mode == HOST) {
+            kc[k].run->rows_before(bc.G);
+            apply_run(kc[k], k);
         }
     std::sort(out.taken.begin(), out.taken.end());
+    prof.lap(6);
+    prof.print("exact", logs.size(), evp.size(), out.n_fires);
 }
 
 }  // namespace sdg

@@ -31,9 +31,9 @@
 #pragma once
 #include <stdint.h>
 
+#include <algorithm>
 #include <deque>
 #include <map>
-#include <set>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -78,12 +78,75 @@ class SchedSim {
         uint32_t g;     // position of the fire in the reference's order
         uint32_t rank;  // order among the fires of that position
     };
+    // (position in the key's run, scheduler, key) -> the fire's slot: open addressing, linear probing
+    class RankMap {
+       public:
+        void reserve(size_t n) {
+            size_t c = 16;
+            while (c < 2 * n) c <<= 1;
+            keys_.assign(c, EMPTY);
+            vals_.assign(c, Slot{0, 0});
+            n_ = 0;
+            has_empty_key_ = false;
+        }
+        void put(uint64_t k, Slot v) {
+            if (k == EMPTY) {
+                has_empty_key_ = true;
+                empty_val_ = v;
+                return;
+            }
+            if (2 * (n_ + 1) > keys_.size()) grow();
+            size_t i = at(k);
+            if (keys_[i] == EMPTY) {
+                keys_[i] = k;
+                ++n_;
+            }
+            vals_[i] = v;
+        }
+        const Slot* find(uint64_t k) const {
+            if (k == EMPTY) return has_empty_key_ ? &empty_val_ : nullptr;
+            if (keys_.empty()) return nullptr;
+            const size_t i = at(k);
+            return keys_[i] == k ? &vals_[i] : nullptr;
+        }
+        void clear() { reserve(0); }
+        bool empty() const { return n_ == 0 && !has_empty_key_; }
+
+       private:
+        static constexpr uint64_t EMPTY = ~0ull;
+        std::vector<uint64_t> keys_;
+        std::vector<Slot> vals_;
+        size_t n_ = 0;
+        bool has_empty_key_ = false;
+        Slot empty_val_{0, 0};
+        size_t at(uint64_t k) const {  // the key's slot or the empty slot where it would go
+            const size_t m = keys_.size() - 1;
+            size_t i = (size_t)((k ^ (k >> 29)) * 0xBF58476D1CE4E5B9ull >> 17) & m;
+            while (keys_[i] != EMPTY && keys_[i] != k) i = (i + 1) & m;
+            return i;
+        }
+        void grow() {
+            std::vector<uint64_t> ok;
+            std::vector<Slot> ov;
+            ok.swap(keys_);
+            ov.swap(vals_);
+            const size_t c = std::max<size_t>(16, 2 * ok.size());
+            keys_.assign(c, EMPTY);
+            vals_.assign(c, Slot{0, 0});
+            for (size_t i = 0; i < ok.size(); ++i)
+                if (ok[i] != EMPTY) {
+                    const size_t j = at(ok[i]);
+                    keys_[j] = ok[i];
+                    vals_[j] = ov[i];
+                }
+        }
+    };
     struct Result {
         std::vector<uint32_t> taken;                         // keys run on the host (their device run is void)
         // optimistic pass: keys whose device run the scheduler reordered (and their fire lists in its order)
         std::vector<uint32_t> reordered, fire_off;
         std::vector<nfa::TimerFire> fires;
-        std::unordered_map<uint64_t, Slot> rank;             // (position in the key's run, scheduler, key) -> slot
+        RankMap rank;                                        // (position in the key's run, scheduler, key) -> slot
         int64_t n_fires = 0, n_shifted = 0;
     };
     void setup(int n_sched, bool partitioned, bool live) {
@@ -104,14 +167,20 @@ class SchedSim {
     void simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& logs, const std::vector<int32_t>& key_hash,
                   const KeyRows& rows, const std::function<KeyRun*(uint32_t)>& take_over, Result& out,
                   bool optimistic = false);
-    void commit() { cur_ = work_; }
+    void commit() { std::swap(cur_, work_); }  // work_ is rebuilt from cur_ by the next simulate()
     static uint64_t rank_key(uint32_t g, int sch, uint32_t key) {
         return ((uint64_t)g << 32) ^ ((uint64_t)sch << 27) ^ (uint64_t)key * 0x9E3779B97F4A7C15ull;
     }
 
    private:
+    // one key's SchedulerState in one scheduler: its FIFO of notify times (inline up to QI, else in a spill deque),
+    // its HashMap entry (hash, insertion stamp) and creation order. Flat, indexed by dense key id.
+    static constexpr int QI = 3;
     struct KS {
-        std::deque<int64_t> q;
+        int64_t a[QI];
+        int32_t spill = -1;    // State::spill index while the queue holds more than QI times
+        uint32_t n = 0;        // queued times
+        uint32_t ver = 0;      // bumped whenever the head changes (due-heap entries of older versions are stale)
         int32_t hash = 0;
         uint64_t stamp = 0;    // insertion order into the map (iteration: newest first within a bucket)
         uint64_t cseq = 0;     // creation order (live-mode tie break)
@@ -123,16 +192,22 @@ class SchedSim {
         uint32_t key;
         bool operator<(const OKey& o) const { return a != o.a ? a < o.a : (b != o.b ? b < o.b : key < o.key); }
     };
+    struct DueE {
+        OKey k;
+        uint32_t ver;
+        bool operator>(const DueE& o) const { return o.k < k; }
+    };
     struct SchedState {
-        std::unordered_map<uint32_t, KS> ks;
-        std::map<int64_t, std::set<OKey>> due;     // head time -> states with that head
+        std::vector<KS> ks;                                 // [dense key id]
+        std::map<int64_t, std::vector<DueE>> due;           // head time -> min-heap of states (lazy deletion)
         uint64_t cap = 0, threshold = 0, size = 0, stamp = 0;
-        std::vector<uint32_t> bin;                 // keys per bucket (treeifyBin on a small table resizes)
+        std::vector<uint32_t> bin;                          // keys per bucket (treeifyBin on a small table resizes)
     };
     struct State {
         std::vector<SchedState> sc;
+        std::vector<std::deque<int64_t>> spill;             // long queues
+        std::vector<int32_t> spill_free;
         uint64_t cseq = 0;
-        int64_t live_now = 0;
     };
     int n_sched_ = 0;
     bool partitioned_ = false, live_ = false;
@@ -140,12 +215,27 @@ class SchedSim {
     const std::vector<int32_t>* hash_ = nullptr;
 
     OKey okey(const SchedState& S, const KS& k, uint32_t key) const;
-    void due_add(SchedState& S, uint32_t key, const KS& k);
-    void due_del(SchedState& S, uint32_t key, const KS& k);
+    KS& ks(SchedState& S, uint32_t key) {
+        if (key >= S.ks.size()) S.ks.resize(std::max<size_t>(key + 1, S.ks.size() + S.ks.size() / 2));
+        return S.ks[key];
+    }
+    int64_t qfront(const KS& k) const { return k.spill < 0 ? k.a[0] : work_.spill[k.spill].front(); }
+    void qpush(KS& k, int64_t t);
+    void qpop(KS& k);
+    bool stale(const SchedState& S, const DueE& e) const { return S.ks[e.k.key].ver != e.ver; }
+    // the earliest due time with a live entry (cleans stale heap tops); false when nothing is due
+    bool due_front(SchedState& S, int64_t& t, OKey& k);
+    void due_add(SchedState& S, uint32_t key, KS& k);
+    void due_del(KS& k) { ++k.ver; }
     void resize(SchedState& S);
     void notify(int sch, uint32_t key, int64_t t);  // Scheduler.notifyAt
     void pop(int sch, uint32_t key);
     void remove_if_empty(int sch, uint32_t key);
+    bool queued(int sch, uint32_t key) const {
+        const SchedState& S = work_.sc[sch];
+        return key < S.ks.size() && S.ks[key].n > 0;
+    }
+    int64_t head(int sch, uint32_t key) const { return qfront(work_.sc[sch].ks[key]); }
 };
 
 }  // namespace sdg

@@ -1,3 +1,4 @@
+#include <chrono>
 // TEST-ONLY host harness: runs the product's generic keyed-NFA code (siddhi_amd/csrc/engine/nfa.h, the same
 // __host__ __device__ functions the gfx950 kernel nfa_k executes) on the CPU, so its state-machine logic is
 // checked against the oracle on every golden fixture without a GPU. Not part of the product: the product library
@@ -104,7 +105,8 @@ BatchClock batch_clock(Emu* e) {
     return bc;
 }
 
-size_t reordered_ = 0, taken_ = 0;  // last flush's scheduler statistics (tests)
+size_t reordered_ = 0, taken_ = 0;
+double us_[3] = {0, 0, 0};  // cumulative: optimistic pass, reruns, exact pass (microseconds)  // last flush's scheduler statistics (tests)
 
 int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
     HostQuery& h = q.hq;
@@ -295,7 +297,9 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
         };
         // optimistic pass: keys the scheduler reorders are rerun with its fire order (the device does this in one
         // launch), then the exact pass decides, replaying on the host only what still differs
+        auto t0 = std::chrono::steady_clock::now();
         q.sim.simulate(bc, all, q.key_hash, kr, take, res, true);
+        auto t1 = std::chrono::steady_clock::now();
         if (!res.reordered.empty()) {
             for (size_t d = 0; d < res.reordered.size(); ++d) {
                 const uint32_t k = res.reordered[d];
@@ -307,7 +311,12 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
             for (auto& kv : klog) all.insert(all.end(), kv.second.begin(), kv.second.end());
         }
         reordered_ = res.reordered.size();
+        auto t2 = std::chrono::steady_clock::now();
         q.sim.simulate(bc, all, q.key_hash, kr, take, res);
+        auto t3 = std::chrono::steady_clock::now();
+        us_[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
+        us_[1] += std::chrono::duration<double, std::micro>(t2 - t1).count();
+        us_[2] += std::chrono::duration<double, std::micro>(t3 - t2).count();
         taken_ = res.taken.size();
         q.sim.commit();
         for (auto& r : runs) {  // the host runs replace those keys' device results
@@ -332,10 +341,10 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
             if (o.sub < 0) {  // timer match: its fire's place in the scheduler's order (position, rank)
                 const int sch = (int)((o.sub >> 48) & 0x7F);
                 const uint32_t g = (uint32_t)(o.seq - e->seq);
-                auto it = res.rank.find(SchedSim::rank_key(g, sch, kv.first));
-                if (it != res.rank.end()) {
-                    o.seq = e->seq + it->second.g;
-                    o.sub = INT64_MIN | ((int64_t)it->second.rank << 24) | (o.sub & 0xFFFFFF);
+                const SchedSim::Slot* it = res.rank.find(SchedSim::rank_key(g, sch, kv.first));
+                if (it) {
+                    o.seq = e->seq + it->g;
+                    o.sub = INT64_MIN | ((int64_t)it->rank << 24) | (o.sub & 0xFFFFFF);
                 }
             }
             batch.push_back(std::move(o));
@@ -447,7 +456,7 @@ int emu_flush(void* h) {
     return 0;
 }
 
-int64_t emu_sched_stat(int which) { return which == 0 ? (int64_t)reordered_ : (int64_t)taken_; }
+int64_t emu_sched_stat(int which) { return which == 0 ? (int64_t)reordered_ : which == 1 ? (int64_t)taken_ : (int64_t)us_[which - 2]; }
 int emu_num_queries(void* h) { return (int)((Emu*)h)->qs.size(); }
 const char* emu_query_name(void* h, int q) { return ((Emu*)h)->qs[q]->hq.name.c_str(); }
 const char* emu_query_target(void* h, int q) { return ((Emu*)h)->qs[q]->hq.target.c_str(); }
@@ -464,3 +473,46 @@ void emu_out(void* h, int q, int64_t i, int64_t* ts, int64_t* vals, uint32_t* nu
 }
 
 }  // extern "C"
+
+// ---- test-only sampling profiler for the host harness (SIGPROF, program counters of the sampled thread) ----
+#include <dlfcn.h>
+#include <signal.h>
+#include <sys/time.h>
+#include <ucontext.h>
+namespace {
+std::vector<uintptr_t> g_samples(1 << 22);
+volatile size_t g_nsamp = 0;
+void on_prof(int, siginfo_t*, void* uc) {
+    const size_t i = g_nsamp;
+    if (i < g_samples.size()) {
+        g_samples[i] = (uintptr_t)((ucontext_t*)uc)->uc_mcontext.gregs[REG_RIP];
+        g_nsamp = i + 1;
+    }
+}
+}  // namespace
+extern "C" {
+void emu_prof_start() {
+    struct sigaction sa;
+    std::memset(&sa, 0, sizeof sa);
+    sa.sa_sigaction = on_prof;
+    sa.sa_flags = SA_SIGINFO | SA_RESTART;
+    sigaction(SIGPROF, &sa, nullptr);
+    g_nsamp = 0;
+    itimerval tv{{0, 200}, {0, 200}};
+    setitimer(ITIMER_PROF, &tv, nullptr);
+}
+// writes "object offset" per sample (objects: this library's path or the hex address)
+void emu_prof_stop(const char* path) {
+    itimerval tv{{0, 0}, {0, 0}};
+    setitimer(ITIMER_PROF, &tv, nullptr);
+    FILE* f = std::fopen(path, "w");
+    for (size_t i = 0; i < g_nsamp; ++i) {
+        Dl_info di;
+        if (dladdr((void*)g_samples[i], &di) && di.dli_fname)
+            std::fprintf(f, "%s 0x%lx\n", di.dli_fname, (unsigned long)(g_samples[i] - (uintptr_t)di.dli_fbase));
+        else
+            std::fprintf(f, "? 0x%lx\n", (unsigned long)g_samples[i]);
+    }
+    std::fclose(f);
+}
+}
