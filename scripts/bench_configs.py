@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--only", default="c1,c3,c3m,c4")
     ap.add_argument("--c4-keys", type=int, default=1_000_000)
     ap.add_argument("--c3-steps", type=int, default=2)
+    ap.add_argument("--max-partials", type=int, default=0)
     args = ap.parse_args()
     torch.cuda.init()
     import siddhi_amd as sa
@@ -73,7 +74,8 @@ def main():
         c = w.c3_columns(keys)
         n = len(c["ts"])
         app = w.C3_APP if tag == "c3" else w.C3_APP.replace("<2:5>", "<1:5>")
-        rt = sa.SiddhiAppRuntime(app, device=0, batch_capacity=n + 1)  # one flush per step (no auto-flush)
+        rt = sa.SiddhiAppRuntime(app, device=0, batch_capacity=n + 1,  # one flush per step (no auto-flush)
+                                 max_partials=args.max_partials)
         ih = rt.getInputHandler("S")
         cols = [c["id"], c["key"], c["price"], c["volume"]]
         span = int(c["ts"][-1] - c["ts"][0]) + 1
@@ -97,6 +99,7 @@ def main():
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         print(json.dumps({"config": "C3 %s, %d keys x 100 events/step (host push)" % ("<2:5>" if tag == "c3" else "<1:5>", keys),
+                          "max_partials": args.max_partials or 64,
                           "events_per_s_end_to_end": n * args.c3_steps / dt, "ms_per_step": dt * 1000 / args.c3_steps,
                           "device_ms_per_step": dev_ms / args.c3_steps, "events_per_s_device": n * args.c3_steps / (dev_ms / 1000),
                           "matches_per_step": m / args.c3_steps, "events_per_flush": st.events}), flush=True)
