@@ -1060,6 +1060,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     if (fused) {
         static const char* skip = getenv("SDG_FU_SKIP");
         a.fu_skip = skip ? atoi(skip) : 0;
+        static const bool old_dq = getenv("SDG_FU_OLDDQ") != nullptr;  // A/B: the monotone-deque pass
+        if (old_dq) a.fu_skip |= 64;
         a.fu_mode = getenv("SDG_FU_NODEQUE") ? DQ_OFF : a.deque_mode;
         a.deque_mode = DQ_OFF;
         a.bstart = b_start;

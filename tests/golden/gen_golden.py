@@ -192,14 +192,25 @@ def literal(toks, i):
     raise Skip("non-literal value " + text)
 
 
-def object_array(toks, i):
-    """`new Object[]{...}` starting at `new` -> (values, next index)"""
+def object_array(toks, i, longs=None, now=None):
+    """`new Object[]{...}` starting at `new` -> (values, next index); `now`-style long expressions (++now) are
+    evaluated against `longs` (mutating it, in Java's left-to-right order)"""
     if [t[1] for t in toks[i:i + 5]] != ["new", "Object", "[", "]", "{"]:
         raise Skip("expected new Object[]{...}")
     i += 5
     vals = []
     while toks[i][1] != "}":
-        v, i = literal(toks, i)
+        if now is not None and [t[1] for t in toks[i:i + 5]] == ["System", ".", "currentTimeMillis", "(", ")"]:
+            vals.append("l:%d" % now)  # the modelled wall clock at the send
+            i += 5
+            if toks[i][1] == ",":
+                i += 1
+            continue
+        if longs is not None and (toks[i][1] in ("++", "--") or (toks[i][0] == "id" and toks[i][1] in longs)):
+            n, i = eval_int_expr(toks, i, (",", "}"), longs)
+            v = "l:%d" % n
+        else:
+            v, i = literal(toks, i)
         vals.append(v)
         if toks[i][1] == ",":
             i += 1
@@ -243,7 +254,36 @@ def parse_callback_body(toks, a, b):
     return rows
 
 
+def unroll_loops(body, limit=200_000):
+    """`for (int X = A; X < B; X++) { ... }` with literal bounds -> the body B - A times, X replaced by its value
+    (the input traces of e.g. CountPatternTestCase.testQuery16 are such loops)"""
+    out = []
+    i = 0
+    n = len(body)
+    while i < n:
+        t = [x[1] for x in body[i:i + 13]]
+        if (len(t) == 13 and t[0] == "for" and t[1] == "(" and t[2] == "int" and t[4] == "=" and t[6] == ";" and
+                t[7] == t[3] and t[8] in ("<", "<=") and t[10] == ";" and
+                ((t[11] == t[3] and t[12] == "++") or (t[11] == "++" and t[12] == t[3])) and
+                body[i + 5][0] == "num" and body[i + 9][0] == "num" and body[i + 13][1] == ")" and
+                body[i + 14][1] == "{"):
+            var = t[3]
+            lo, hi = int(t[5]), int(t[9]) + (1 if t[8] == "<=" else 0)
+            end = skip_balanced(body, i + 14)
+            inner = unroll_loops(body[i + 15:end - 1], limit)
+            if (hi - lo) * len(inner) + len(out) > limit:
+                raise Skip("loop too long to unroll")
+            for v in range(lo, hi):
+                out.extend(("num", str(v), x[2]) if x[0] == "id" and x[1] == var else x for x in inner)
+            i = end
+            continue
+        out.append(body[i])
+        i += 1
+    return out
+
+
 def extract(name, line, body, relpath, class_src):
+    body = unroll_loops(body)
     env = {}
     longs = {}
     app = None
@@ -360,17 +400,17 @@ def extract(name, line, body, relpath, class_src):
             sid = handlers[body[i - 2][1]]
             j = i + 2
             if body[j][1] == "new" and body[j + 1][1] == "Object":
-                vals, j = object_array(body, j)
+                vals, j = object_array(body, j, longs, clock)
                 trace.append({"op": "send", "stream": sid, "ts": clock, "data": vals, "explicit_ts": False})
             elif body[j][1] == "new" and body[j + 1][1] == "Event":
                 if body[j + 2][1] == "[":
                     raise Skip("Event[] batch send")
                 ts, j2 = eval_int_expr(body, j + 3, (",",), longs)
-                vals, j = object_array(body, j2 + 1)
+                vals, j = object_array(body, j2 + 1, longs)
                 trace.append({"op": "send", "stream": sid, "ts": ts, "data": vals, "explicit_ts": True})
             else:
                 ts, j2 = eval_int_expr(body, j, (",",), longs)
-                vals, j = object_array(body, j2 + 1)
+                vals, j = object_array(body, j2 + 1, longs)
                 trace.append({"op": "send", "stream": sid, "ts": ts, "data": vals, "explicit_ts": True})
             i = j
             continue
