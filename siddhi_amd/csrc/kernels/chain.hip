@@ -930,74 +930,9 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
         ChainAcc acc{&a, View{}, lo + s_row[sw(pos)], -1, -1};
         return f0.kind == FP_TRUE ? true : fast_pass(f0, acc);
     };
-    // monotone scan conditions (ordering ops, or always) take the windowed search below; == / != the deque
-    const bool ordering = m.lt != m.gt && !m.ne;  // <, <=, >, >=
-    const bool nge_ok = (K == VK_I32 || K == VK_I64 || K == VK_F32 || K == VK_F64) && !(a.fu_skip & 64) &&
-                        (ordering || sp.scan_mode == SCAN_TRUE);
-    // lockstep forward scan (monotone or always-true e2 filters). Each partial completes at the first later row
-    // of its key's run that satisfies the e2 filter while it is alive. Lanes own consecutive
-    // positions, so stepping every lane's partial one row forward per iteration reads consecutive LDS words
-    // (conflict-free) with no data-dependent control flow beyond the exec mask; a wave stops when all its partials
-    // are resolved. Where windows are short in rows (C2: ~10 rows of a key per `within 1 sec`) that is a handful
-    // of iterations; a block where some partial is still open after FU_LS rows falls back to the monotone deque
-    // (linear in the rows however long the window).
-    bool run_deque = a.fu_mode != DQ_OFF && !(a.fu_skip & 16);
-    if (a.fu_mode != DQ_OFF && nge_ok && !(a.fu_skip & 16)) {
-        constexpr int FU_LS = 32;
-        const bool always = sp.scan_mode == SCAN_TRUE;
-        const bool stack = a.fu_mode == DQ_STACK;
-        auto sat = [&](T x, T y) -> bool { return always || (left ? cmp_m(m, x, y) : cmp_m(m, y, x)); };
-        bool open = false;
-#pragma unroll 1
-        for (int k = 0; k < FU_PT; ++k) {
-            const int pos = k * FU_THREADS + t;
-            bool cand = false;
-            T y = kc;
-            uint32_t t0 = 0;
-            int end = 0;
-            if (pos < nr && s_row[sw(pos)] < own) {
-                const int64_t xr = s_x[sw(pos)];
-                const T xv = SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K));
-                cand = c0_at(pos, xr, xv);
-                if (stack) {
-                    y = xv;
-                    if (xv != xv) cand = false;  // NaN threshold: never completes (expires or runs off)
-                }
-                t0 = s_ts[sw(pos)];
-                end = (int)lend[s_lk[sw(pos)]];
-            }
-            uint16_t res = R_NONE;
-            bool un = cand;
-            int q = pos + 1;
-#pragma unroll 1
-            for (int j = 0; j < FU_LS && __ballot(un); ++j) {
-                if (un) {
-                    if (q >= end) {
-                        res = ran_res(pos);
-                        un = false;
-                    } else {
-                        const uint32_t tq = s_ts[sw(q)];
-                        const int64_t xr = s_x[sw(q)];
-                        if ((uint64_t)(tq - t0) > within_u) {  // isExpired: dead
-                            un = false;
-                        } else if (sat(SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K)), y)) {
-                            res = (uint16_t)q;
-                            un = false;
-                        }
-                        ++q;
-                    }
-                }
-            }
-            open |= un;
-            if (cand) s_res[sw(pos)] = res;
-        }
-        if (__ballot(open) && lane == 0) sb[1] = -1;  // sb[1] (the segment) is no longer read: reuse as the flag
-        __syncthreads();
-        run_deque = sb[1] == -1;
-    }
     if (a.fu_skip & 16) {
         // phase timing: no matching
-    } else if (run_deque) {
+    } else if (a.fu_mode != DQ_OFF) {
         // ---- monotone-deque pass (chain_deque_k), one lane per FU_DQ consecutive positions: the lane
         // pushes partials from its own positions only and keeps popping over the following positions of the key
         // until its deque drains. The deque is a bit mask over the lane's positions (bit i = position p0 + i
@@ -1081,7 +1016,7 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
             }
         }
         for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = ran_res(p0 + __builtin_ctz(pend));
-    } else if (a.fu_mode == DQ_OFF) {
+    } else {
         // ---- forward scans: one lane per candidate, its key's run in LDS
 #pragma unroll 1
         for (int k = 0; k < FU_PT; ++k) {
