@@ -147,6 +147,8 @@ typedef struct sdg_stats {
     double ms_nfa_kernel;      /* device ms inside nfa_k launches (first run + reruns); ms_nfa also counts the host
                                   scheduler simulation, log read-back and host replays between them */
     double ms_sched_host;      /* host ms: scheduler simulation passes, log read-back, host replays */
+    int64_t arena_growths;     /* generic NFA: times a key ran out of partial-match slots and the arenas doubled
+                                  (the batch reran from its start; max_partials is the starting size, 4096 the cap) */
 } sdg_stats;
 int sdg_last_stats(sdg_engine* e, sdg_stats* out);
 

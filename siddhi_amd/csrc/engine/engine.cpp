@@ -173,6 +173,10 @@ struct QueryRt {
         int64_t n = 0, cap = 0;
     } carry[2];
     int cur = 0;
+    // a chain query that met decreasing per-key timestamps runs on the generic NFA from then on; its carried
+    // partials are replayed into the arenas first (replay_carries)
+    bool replay_carries = false;
+    DevBuf rp_ts, rp_qs, rp_seg, rp_segend, rp_cols[MAX_COLS], rp_nulls[MAX_COLS];
     // generic NFA: per-key partial-match arenas (persist across batches)
     DevBuf arena;
     int64_t arena_keys = 0;
@@ -411,6 +415,119 @@ void chain_staging(const HostQuery& h, ChainArgs& a, bool carry_nullable) {
     const FastPred& f0 = P.fast[0];
     a.f0_on_x = f0.kind == FP_CONST && f0.sa == 0 && (f0.ia == 0 || f0.ia == -1) && f0.ca == sp.scan_col &&
                 f0.ka == sp.scan_col_kind;
+}
+
+// A chain query moving to the generic NFA: its carried partials (e1 events still pending at the end of the last
+// committed batch) are run through the NFA as events of the state-0 stream, in arrival order per key, before the
+// batch. That rebuilds exactly the pending lists the reference holds: none of them can complete or expire another
+// (each survived every later event of its key, these included, in the real history), and each re-creates its
+// partial. The replay must therefore emit nothing; it is checked.
+void replay_carries(sdg_engine* e, QueryRt& q, const NfaArgs& a0, bool multi_stream) {
+    q.replay_carries = false;
+    const Plan& P = q.hq.plan;
+    hipStream_t st = e->stream;
+    QueryRt::Carry& cin = q.carry[q.cur];
+    const int64_t n = cin.n;
+    const int nc = P.n_cols;
+    cin.n = 0;
+    if (n <= 0) return;
+    std::vector<uint32_t> key(n);
+    std::vector<int64_t> ts(n), seq(n), vals((size_t)std::max(nc, 1) * n);
+    std::vector<uint32_t> nm(n);
+    HIPCHECK(hipMemcpy(key.data(), cin.key.p, n * 4, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(ts.data(), cin.ts.p, n * 8, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(seq.data(), cin.seq.p, n * 8, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(nm.data(), cin.nulls.p, n * 4, hipMemcpyDeviceToHost));
+    for (int j = 0; j < nc; ++j)
+        HIPCHECK(hipMemcpy(vals.data() + (size_t)j * n, (const int64_t*)cin.vals.p + (size_t)j * cin.cap, n * 8,
+                           hipMemcpyDeviceToHost));
+    std::vector<int64_t> ord(n);
+    for (int64_t i = 0; i < n; ++i) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) { return key[x] != key[y] ? key[x] < key[y] : seq[x] < seq[y]; });
+    const int64_t KS = P.partitioned ? a0.K : 1;
+    std::vector<uint32_t> sb(KS, 0), se(KS, 0);
+    std::vector<int64_t> rts(n);
+    std::vector<std::vector<uint8_t>> cols(nc), nulls(nc);
+    for (int j = 0; j < nc; ++j) {
+        cols[j].resize((size_t)n * width_of(P.col_kind[j]));
+        nulls[j].assign(n, 0);
+    }
+    bool any_null[MAX_COLS] = {};
+    for (int64_t r = 0; r < n; ++r) {
+        const int64_t i = ord[r];
+        const uint32_t k = P.partitioned ? key[i] : 0;
+        if (k >= (uint32_t)KS) throw DeviceError("carried partial of an unknown key");
+        if (r == 0 || (P.partitioned && key[ord[r - 1]] != key[i])) sb[k] = (uint32_t)r;
+        se[k] = (uint32_t)(r + 1);
+        rts[r] = ts[i];
+        for (int j = 0; j < nc; ++j) {
+            const int w = width_of(P.col_kind[j]);
+            std::memcpy(&cols[j][(size_t)r * w], &vals[(size_t)j * n + i], w);  // the slot's low bytes
+            if ((nm[i] >> j) & 1u) {
+                nulls[j][r] = 1;
+                any_null[j] = true;
+            }
+        }
+    }
+    NfaArgs b = a0;
+    b.n = n;
+    b.ts = (const int64_t*)q.rp_ts.ensure(n * 8);
+    HIPCHECK(hipMemcpy((void*)b.ts, rts.data(), n * 8, hipMemcpyHostToDevice));
+    b.qstream = nullptr;
+    if (multi_stream) {
+        std::vector<uint8_t> qs(n, (uint8_t)q.hq.stream_pos(P.st[0].stream));
+        b.qstream = (const uint8_t*)q.rp_qs.ensure(n);
+        HIPCHECK(hipMemcpy((void*)b.qstream, qs.data(), n, hipMemcpyHostToDevice));
+    }
+    if (P.partitioned) {
+        b.seg_start = (const uint32_t*)q.rp_seg.ensure(KS * 4);
+        b.seg_end = (const uint32_t*)q.rp_segend.ensure(KS * 4);
+        HIPCHECK(hipMemcpy((void*)b.seg_start, sb.data(), KS * 4, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy((void*)b.seg_end, se.data(), KS * 4, hipMemcpyHostToDevice));
+    }
+    b.orig = nullptr;
+    b.pos_off = 0;
+    for (int j = 0; j < nc; ++j) {
+        b.cols[j] = q.rp_cols[j].ensure(cols[j].size());
+        HIPCHECK(hipMemcpy((void*)b.cols[j], cols[j].data(), cols[j].size(), hipMemcpyHostToDevice));
+        b.nulls[j] = nullptr;
+        if (any_null[j]) {
+            b.nulls[j] = (const uint8_t*)q.rp_nulls[j].ensure(n);
+            HIPCHECK(hipMemcpy((void*)b.nulls[j], nulls[j].data(), n, hipMemcpyHostToDevice));
+        }
+    }
+    const int64_t cap = 2 * n + 4096;
+    b.out_cap = cap;
+    b.out_ts = (int64_t*)q.o_ts.ensure(cap * 8);
+    b.out_key = (uint32_t*)q.o_key.ensure(cap * 4);
+    b.out_vals = (int64_t*)q.o_vals.ensure((size_t)std::max(P.n_out, 1) * cap * 8);
+    b.out_nulls = (uint32_t*)q.o_nulls.ensure(cap * 4);
+    b.out_emit_seq = (int64_t*)q.o_emit.ensure(cap * 8);
+    b.out_sub = (int64_t*)q.o_first.ensure(cap * 8);
+    b.out_round = nullptr;
+    unsigned long long* counters = (unsigned long long*)q.counters.ensure(16);
+    b.out_count = counters;
+    b.flags = (int*)q.flags.ensure(32);
+    b.list = nullptr;
+    b.nlist = 0;
+    HIPCHECK(hipMemsetAsync(counters, 0, 16, st));
+    HIPCHECK(hipMemsetAsync(b.flags, 0, 32, st));
+    NfaArgs* h_na = (NfaArgs*)q.h_args.ensure(std::max(sizeof(NfaArgs), 2 * sizeof(ChainArgs)));
+    NfaArgs* d_na = (NfaArgs*)q.d_args.ensure(std::max(sizeof(NfaArgs), 2 * sizeof(ChainArgs)));
+    *h_na = b;
+    HIPCHECK(hipMemcpyAsync(d_na, h_na, sizeof(NfaArgs), hipMemcpyHostToDevice, st));
+    nfa_run(b, d_na, st);
+    unsigned long long hc[2];
+    int hf[8];
+    HIPCHECK(hipMemcpyAsync(hc, counters, 16, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(hf, b.flags, 32, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    if (hf[2])
+        throw CompileError(SDG_ERR_CAPACITY, "query '" + q.hq.name + "': a partition key exceeded max_partials replaying "
+                                                                     "its carried partials");
+    if (hc[0] != 0 || hf[0]) throw DeviceError("query '" + q.hq.name + "': replaying carried partials emitted matches");
+    e->stats.match_launches += 1;
+    nfa_commit(q.cur_bits.as<uint8_t>(), q.ran_bits.as<uint8_t>(), q.arena_keys, st);  // the batch starts from it
 }
 
 void flush_query(sdg_engine* e, QueryRt& q) {
@@ -709,8 +826,9 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         for (int k = 0; k < nc; ++k) { a.cols[k] = v_cols[k]; a.nulls[k] = v_nulls[k]; }
         a.seq_base = e->seq;
         const bool timers = P.n_sched > 0;
-        // arenas: grow to K keys keeping the existing keys' state, new keys zeroed (= not yet initialised); with
-        // timers two copies + the per-key committed-copy bit (a key can be rerun from its batch-start state)
+        // arenas: grow to K keys keeping the existing keys' state, new keys zeroed (= not yet initialised); two
+        // copies + the per-key committed-copy bit, so a key can be rerun from its batch-start state (scheduler
+        // reruns, arena growth)
         const int64_t kb = q.L.bytes;
         if (q.arena_keys < a.K) {
             int64_t nk = std::max<int64_t>(a.K, q.arena_keys + q.arena_keys / 2);
@@ -724,18 +842,38 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 std::swap(nb.cap, buf.cap);
             };
             grow(q.arena, kb);
-            if (timers) {
-                grow(q.arena2, kb);
-                grow(q.cur_bits, 1);
-                grow(q.ran_bits, 1);
-            }
+            grow(q.arena2, kb);
+            grow(q.cur_bits, 1);
+            grow(q.ran_bits, 1);
             q.arena_keys = nk;
         }
         a.arena = q.arena.as<uint8_t>();
-        if (timers) {
+        a.arena2 = q.arena2.as<uint8_t>();
+        a.cur = q.cur_bits.as<uint8_t>();
+        a.ran = q.ran_bits.as<uint8_t>();
+        // a key ran out of partial-match slots: every key's committed state into a layout with twice the slots
+        // (the batch then reruns from its start)
+        auto grow_slots = [&]() {
+            const nfa::Layout Ln = nfa::make_layout(P.n_states, std::max(P.n_cols, 1), std::min(2 * q.L.ns, 4096), P.n_sched);
+            DevBuf na, na2;
+            na.ensure((size_t)(q.arena_keys * Ln.bytes));
+            na2.ensure((size_t)(q.arena_keys * Ln.bytes));
+            nfa_migrate(q.d_plan.as<Plan>(), q.arena.as<uint8_t>(), q.arena2.as<uint8_t>(), q.cur_bits.as<uint8_t>(), q.L,
+                        na.as<uint8_t>(), Ln, q.arena_keys, st);
+            HIPCHECK(hipMemsetAsync(q.cur_bits.p, 0, (size_t)q.arena_keys, st));
+            HIPCHECK(hipMemsetAsync(q.ran_bits.p, 0, (size_t)q.arena_keys, st));
+            HIPCHECK(hipStreamSynchronize(st));
+            std::swap(na.p, q.arena.p);
+            std::swap(na.cap, q.arena.cap);
+            std::swap(na2.p, q.arena2.p);
+            std::swap(na2.cap, q.arena2.cap);
+            q.L = Ln;
+            a.L = Ln;
+            a.arena = q.arena.as<uint8_t>();
             a.arena2 = q.arena2.as<uint8_t>();
-            a.cur = q.cur_bits.as<uint8_t>();
-            a.ran = q.ran_bits.as<uint8_t>();
+            e->stats.arena_growths += 1;
+        };
+        if (timers) {
             a.T.G = e->bc.G;
             a.T.clk = e->d_clk.as<int64_t>();
             a.T.nadv = e->d_nadv.as<uint32_t>();
@@ -746,6 +884,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             a.T.log_cap = q.log_cap;
         }
         a.L = q.L;
+        if (q.replay_carries) replay_carries(e, q, a, multi_stream);
         int64_t cap = std::max<int64_t>(q.out_cap, 2 * nrows + 4096);
         unsigned long long* counters = (unsigned long long*)q.counters.ensure(16);
         if (timers) a.T.log_count = counters + 1;
@@ -787,6 +926,11 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             HIPCHECK(hipEventElapsedTime(&kms, e->ev[10], e->ev[11]));
             e->stats.ms_nfa_kernel += kms;
             if (hf[4]) throw CompileError(SDG_ERR_ARG, "device-resident partition key ids out of range (not from sdg_intern)");
+            if (hf[2] && q.L.ns < 4096) {  // grow the arenas and rerun (state is double-buffered)
+                grow_slots();
+                HIPCHECK(hipMemsetAsync(flags, 0, 32, st));
+                return false;
+            }
             if (hf[2]) {
                 e->stats.overflow += 1;
                 throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': a partition key exceeded max_partials (" +
@@ -795,10 +939,6 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             }
             bool ok = true;
             if (hf[0] || (int64_t)hc[0] > cap) {  // outputs: grow to what was asked for, run the batch again
-                if (!timers) {
-                    e->stats.overflow += 1;
-                    throw CompileError(SDG_ERR_CAPACITY, "match buffer overflow in query '" + h.name + "'");
-                }
                 cap = std::max<int64_t>(2 * cap, (int64_t)hc[0] + 4096);
                 ok = false;
             }
@@ -822,7 +962,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             a.nlist = 0;
             a.round = 0;
             for (int tries = 0; !launch(true); ++tries)  // state is double-buffered: a retry starts from the batch start
-                if (tries > 8) throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': output buffers keep overflowing");
+                if (tries > 24) throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': output buffers keep overflowing");
             e->stats.match_launches += 1;
         };
         first_run();
@@ -902,9 +1042,10 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 r->key = k;
                 uint8_t cur = 0;
                 HIPCHECK(hipMemcpy(&cur, q.cur_bits.as<uint8_t>() + k, 1, hipMemcpyDeviceToHost));
-                r->arena.resize(kb);
-                const uint8_t* committed = (cur ? q.arena2.as<uint8_t>() : q.arena.as<uint8_t>()) + (int64_t)k * kb;
-                HIPCHECK(hipMemcpy(r->arena.data(), committed, kb, hipMemcpyDeviceToHost));
+                const int64_t kbn = q.L.bytes;  // (the layout may have grown during the run)
+                r->arena.resize(kbn);
+                const uint8_t* committed = (cur ? q.arena2.as<uint8_t>() : q.arena.as<uint8_t>()) + (int64_t)k * kbn;
+                HIPCHECK(hipMemcpy(r->arena.data(), committed, kbn, hipMemcpyDeviceToHost));
                 const int64_t b = k < (uint32_t)KR ? hseg_b[k] : 0, en = k < (uint32_t)KR ? hseg_e[k] : 0, m = en - b;
                 r->ts.resize(m);
                 r->pos.resize(m);
@@ -964,8 +1105,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                                                          "(host replay of a key the scheduler reordered)");
                 uint8_t cur = 0;  // its state goes where the device run's went (nfa_commit makes it current)
                 HIPCHECK(hipMemcpy(&cur, q.cur_bits.as<uint8_t>() + r->key, 1, hipMemcpyDeviceToHost));
-                uint8_t* work = (cur ? q.arena.as<uint8_t>() : q.arena2.as<uint8_t>()) + (int64_t)r->key * kb;
-                HIPCHECK(hipMemcpy(work, r->arena.data(), kb, hipMemcpyHostToDevice));
+                uint8_t* work = (cur ? q.arena.as<uint8_t>() : q.arena2.as<uint8_t>()) + (int64_t)r->key * q.L.bytes;
+                HIPCHECK(hipMemcpy(work, r->arena.data(), q.L.bytes, hipMemcpyHostToDevice));
             }
             q.sim.commit();
             q.last_rank = std::move(res.rank);
@@ -974,10 +1115,10 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             e->stats.sched_shifted += res.n_shifted;
             e->stats.sched_host_keys += (int64_t)res.taken.size();
             e->stats.sched_rerun_keys += (int64_t)q.reordered.size();
-            nfa_commit(q.cur_bits.as<uint8_t>(), q.ran_bits.as<uint8_t>(), q.arena_keys, st);
             e->stats.ms_sched_host += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_sched).count() -
                                       (e->stats.ms_nfa_kernel - k_before);
         }
+        nfa_commit(q.cur_bits.as<uint8_t>(), q.ran_bits.as<uint8_t>(), q.arena_keys, st);
         HIPCHECK(hipEventRecord(e->ev[2], st));
         HIPCHECK(hipStreamSynchronize(st));
         float ms_kg = 0, ms_m = 0, t;
@@ -1188,10 +1329,16 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         e->stats.overflow += 1;
         throw CompileError(SDG_ERR_CAPACITY, "match/carry buffer overflow in query '" + h.name + "'");
     }
-    if (hf[1])
-        throw CompileError(SDG_ERR_UNSUPPORTED, "query '" + h.name +
-                                                    "': timestamps decrease within a partition key; the chain path needs "
-                                                    "per-key non-decreasing timestamps (generic path not in this build)");
+    if (hf[1]) {
+        // timestamps decrease within a partition key: the chain path's exactness argument needs them
+        // non-decreasing. From this batch on the query runs on the generic NFA (nothing of this run is committed:
+        // the carries stay in cin and are replayed into the arenas first).
+        P.chain = 0;
+        q.replay_carries = cin.n > 0;
+        q.carry_nullable = carry_nullable0;
+        e->stats.path = 1;
+        return false;
+    }
     cout.n = (int64_t)hc[1];
     cin.n = 0;
     q.cur ^= 1;
@@ -1202,7 +1349,9 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     q.last_timers = false;
     return true;
     };
-    if (!run(try_fused)) run(false);
+    // rerun on the radix path (fused precondition broken), or on the generic NFA (chain precondition broken)
+    for (int attempt = 0; !run(try_fused && attempt == 0); ++attempt)
+        if (attempt >= 2) throw DeviceError("query '" + h.name + "': no matcher path accepted the batch");
 }
 
 // read the last flush's match records back (pinned staging) and append them to the query's delivery backlog in
@@ -1364,6 +1513,7 @@ int do_flush(sdg_engine* e) {
     e->stats.ms_kg_hist = e->stats.ms_kg_prefix = e->stats.ms_kg_scatter = 0;
     e->stats.ms_chain_carry = e->stats.ms_chain_match = e->stats.ms_chain_emit = 0;
     e->stats.ms_nfa = e->stats.ms_nfa_kernel = e->stats.ms_sched_host = 0;
+    e->stats.arena_growths = 0;
     e->stats.fused_ovf = 0;
     e->stats.sched_fires = e->stats.sched_shifted = e->stats.sched_host_keys = e->stats.sched_rerun_keys = 0;
     // a flush consumes its batch whether or not it succeeds: a failing query must not make the next flush

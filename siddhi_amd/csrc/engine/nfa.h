@@ -1167,6 +1167,41 @@ struct CtxT {
     }
 };
 
+// one key's committed arena into a larger layout (more partial-match slots, same states / columns / schedulers):
+// header, processor states, the lists (re-strided), timer queues (unrolled to start at 0) and every pool object at
+// its index; the free lists are then rebuilt by a mark-sweep in the new layout (the lists are the only roots
+// between batches), which also frees the new slots
+template <bool TM>
+SDG_HD void migrate_key(CtxT<TM>& d, const uint8_t* src, const Layout& Ls) {
+    const Layout& Ld = d.L;
+    uint8_t* dst = d.base;
+    for (int64_t i = 0; i < Ld.bytes; ++i) dst[i] = 0;
+    const KHead* sh = (const KHead*)src;
+    if (!(sh->flags & 2)) return;  // never initialised: stays zero (= fresh)
+    d.head() = *sh;
+    for (int p = 0; p < Ld.n_states; ++p) {
+        d.ps(p) = ((const PState*)(src + Ls.off_ps))[p];
+        const int16_t* sp = (const int16_t*)(src + Ls.off_pend) + (int64_t)p * Ls.lcap;
+        const int16_t* sn = (const int16_t*)(src + Ls.off_newe) + (int64_t)p * Ls.lcap;
+        for (int j = 0; j < d.ps(p).pn; ++j) d.pend(p)[j] = sp[j];
+        for (int j = 0; j < d.ps(p).nw; ++j) d.newe(p)[j] = sn[j];
+    }
+    for (int q = 0; q < Ld.n_sched; ++q) {
+        TQ t = ((const TQ*)(src + Ls.off_tq))[q];
+        const int64_t* st = (const int64_t*)(src + Ls.off_tqt) + (int64_t)q * Ls.qcap;
+        for (int j = 0; j < t.n; ++j) d.tqt(q)[j] = st[(t.h + j) % Ls.qcap];
+        t.h = 0;
+        d.tq(q) = t;
+    }
+    for (int i = 0; i < Ls.ns; ++i)
+        for (int b = 0; b < Ls.se_bytes; ++b) ((uint8_t*)&d.se(i))[b] = src[Ls.off_se + (int64_t)i * Ls.se_bytes + b];
+    for (int i = 0; i < Ls.nn; ++i) d.nd(i) = ((const Node*)(src + Ls.off_nd))[i];
+    for (int i = 0; i < Ls.nr; ++i)
+        for (int b = 0; b < Ls.rc_bytes; ++b) ((uint8_t*)&d.rc(i))[b] = src[Ls.off_rc + (int64_t)i * Ls.rc_bytes + b];
+    d.head().flags &= ~1;
+    d.gc();
+}
+
 template <bool TM>
 SDG_HD void SEAccT<TM>::load(int slot, int col, int chain, uint8_t kind, int64_t* v, bool* null) {
     (void)kind;

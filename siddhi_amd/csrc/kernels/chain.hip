@@ -157,6 +157,7 @@ __device__ int64_t scan_typed(const ChainArgs& a, const View& v, int64_t from, i
         if (filt) {  // bucket view rows are time-ordered: past the window at any row, no later row can match
             if (has_within && ts_row(a, v, q) - ts0 > within) return -1;
             if (a.key[q] != kf) continue;
+            if (ts_row(a, v, q) < ts0) atomicOr(&a.flags[1], 1);  // the key's time went back across batches
         }
         // StreamPreStateProcessor.isExpired: |start.ts - now| > within, checked before the event is processed
         if (has_within) {
@@ -205,6 +206,7 @@ __device__ __forceinline__ int64_t chain_scan(const ChainArgs& a, ChainAcc& acc,
         if (a.bstart) {  // bucket view: time-ordered rows (see scan_typed)
             if (sp.has_within && ts_row(a, acc.V, q) - ts0 > sp.within_ms) return -1;
             if (a.key[q] != kf) continue;
+            if (ts_row(a, acc.V, q) < ts0) atomicOr(&a.flags[1], 1);
         }
         if (sp.has_within) {
             int64_t d = ts0 - ts_row(a, acc.V, q);
@@ -556,6 +558,8 @@ __global__ __launch_bounds__(256) void chain_carry_k(const ChainArgs* __restrict
             b = key < (uint32_t)a.K ? (int64_t)a.seg_start[key] : 0;
             e = key < (uint32_t)a.K ? (int64_t)a.seg_end[key] : 0;
         }
+        // per-key time order across the batch boundary (within the batch the chain kernels check it)
+        if (!a.bstart && b < e && ts_row(a, v, b) < a.cin_ts[c]) atomicOr(&a.flags[1], 1);
         const int64_t r = chain_scan<true>(a, acc, b, e, a.cin_ts[c], stk, stride, key);
         if (r >= 0) { has = true; qhit = r; }
         else if (r == -2) carry = true;
@@ -610,6 +614,7 @@ __device__ int64_t wave_scan_typed(const ChainArgs& a, int64_t from, int64_t end
                 if (filt && has_within && d > within) {
                     stop = true;  // time-ordered bucket: no later row of the key is alive
                 } else if (!filt || a.key[q] == kf) {
+                    if (filt && d < 0) atomicOr(&a.flags[1], 1);  // the key's time went back across batches
                     if (has_within && (d < 0 ? -d : d) > within) stop = true;  // isExpired at this event of the key
                     else if (qs_row(a, View{}, q) == a.s1) {
                         if (always) hit = true;
@@ -701,6 +706,7 @@ __global__ __launch_bounds__(256) void chain_carry_wave_k(const ChainArgs* __res
             b = key < (uint32_t)a.K ? (int64_t)a.seg_start[key] : 0;
             e = key < (uint32_t)a.K ? (int64_t)a.seg_end[key] : 0;
         }
+        if (!a.bstart && b < e && a.ts[b] < a.cin_ts[c] && lane == 0) atomicOr(&a.flags[1], 1);  // time went back
         ChainAcc acc{&a, View{}, -1, c, -1};
         int64_t k = sp.scan_konst;
         uint8_t op = sp.scan_op;

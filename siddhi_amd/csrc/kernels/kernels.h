@@ -239,6 +239,9 @@ struct NfaArgs {
 };
 // a: host copy (launch geometry); d_a: device copy the kernel reads
 void nfa_run(const NfaArgs& a, const NfaArgs* d_a, hipStream_t stream);
+// arena growth: the committed copy of every key (arena2 && cur[k] ? arena2 : arena) into `dst` in layout Ld
+void nfa_migrate(const Plan* plan, const uint8_t* arena, const uint8_t* arena2, const uint8_t* cur,
+                 const nfa::Layout& Ls, uint8_t* dst, const nfa::Layout& Ld, int64_t K, hipStream_t stream);
 // double-buffered arenas: flip `cur` of every key a run touched (`ran`), clearing `ran`
 void nfa_commit(uint8_t* cur, uint8_t* ran, int64_t K, hipStream_t stream);
 

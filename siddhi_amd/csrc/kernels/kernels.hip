@@ -396,6 +396,20 @@ __global__ __launch_bounds__(256) void nfa_k(const NfaArgs* __restrict__ pa) {
     if (c.ovf()) atomicOr(&a.flags[2], 1);
 }
 
+// arena growth: every key's committed state into the larger layout (nfa.h migrate_key)
+__global__ __launch_bounds__(256) void nfa_migrate_k(const Plan* __restrict__ plan, const uint8_t* __restrict__ arena,
+                                                     const uint8_t* __restrict__ arena2, const uint8_t* __restrict__ cur,
+                                                     nfa::Layout Ls, uint8_t* __restrict__ dst, nfa::Layout Ld, int64_t K) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= K) return;
+    const uint8_t* src = (arena2 && cur[k] ? arena2 : arena) + k * Ls.bytes;
+    nfa::CtxT<true> c;
+    c.P = plan;
+    c.L = Ld;
+    c.base = dst + k * Ld.bytes;
+    nfa::migrate_key(c, src, Ls);
+}
+
 __global__ __launch_bounds__(256) void nfa_commit_k(uint8_t* __restrict__ cur, uint8_t* __restrict__ ran, int64_t K) {
     const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (k >= K || !ran[k]) return;
@@ -557,6 +571,13 @@ void bucketize(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, uint
     if (marks) (void)hipEventRecord(marks[2], stream);
     hipLaunchKernelGGL(bk_plan, dim3(1), dim3(256), 0, stream, a.tot, a.n, nb, seg_rows, bstart, bseg);
     if (marks) (void)hipEventRecord(marks[3], stream);
+}
+
+void nfa_migrate(const Plan* plan, const uint8_t* arena, const uint8_t* arena2, const uint8_t* cur,
+                 const nfa::Layout& Ls, uint8_t* dst, const nfa::Layout& Ld, int64_t K, hipStream_t stream) {
+    if (K <= 0) return;
+    hipLaunchKernelGGL(nfa_migrate_k, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, plan, arena, arena2, cur,
+                       Ls, dst, Ld, K);
 }
 
 void nfa_run(const NfaArgs& a, const NfaArgs* d_a, hipStream_t stream) {

@@ -106,7 +106,8 @@ BatchClock batch_clock(Emu* e) {
 }
 
 size_t reordered_ = 0, taken_ = 0;
-double us_[3] = {0, 0, 0};  // cumulative: optimistic pass, reruns, exact pass (microseconds)  // last flush's scheduler statistics (tests)
+double us_[3] = {0, 0, 0};
+int64_t growths_ = 0;  // arena doublings (all flushes)  // cumulative: optimistic pass, reruns, exact pass (microseconds)  // last flush's scheduler statistics (tests)
 
 int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
     HostQuery& h = q.hq;
@@ -188,6 +189,7 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
     std::map<uint32_t, std::vector<Out>> kout;
     std::map<uint32_t, std::vector<nfa::SchedLog>> klog;
     std::vector<int64_t> stk(STACK);
+    bool arena_ovf = false;
     auto run_one = [&](uint32_t k, const nfa::TimerFire* fires, int nfires) -> int {
         const int64_t cap = 2 * (seg_e[k] - seg_b[k]) + 4096 + 64 * (int64_t)std::max(nfires, 0);
         std::vector<int64_t> o_ts(cap), o_vals((size_t)std::max(P.n_out, 1) * cap), o_seq(cap), o_sub(cap);
@@ -231,6 +233,7 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
         nfa::run_key(c, kev);
         if (c.ovf()) {
             g_err = "query '" + h.name + "': partial-match arena overflow";
+            arena_ovf = true;
             return 3;
         }
         if (flags[0] || flags[5]) {
@@ -247,13 +250,40 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
         klog[k].assign(logs.begin(), logs.begin() + (int64_t)lcount);
         return 0;
     };
-    for (uint32_t k : run) {
-        if (k >= seg_b.size() && P.partitioned) {  // a key of an earlier batch with queued timers only
-            seg_b.resize(k + 1, 0);
-            seg_e.resize(k + 1, 0);
+    // as the engine: a key out of partial-match slots doubles every key's arena (nfa.h migrate_key from the
+    // batch-start state) and the batch reruns
+    for (bool again = true; again;) {
+        again = false;
+        for (uint32_t k : run) {
+            if (k >= seg_b.size() && P.partitioned) {  // a key of an earlier batch with queued timers only
+                seg_b.resize(k + 1, 0);
+                seg_e.resize(k + 1, 0);
+            }
+            arena_ovf = false;
+            int rc = run_one(k, nullptr, -1);  // ideal mode
+            if (rc && arena_ovf && q.L.ns < 4096) {
+                const nfa::Layout Ln = nfa::make_layout(P.n_states, std::max(nc, 1), std::min(2 * q.L.ns, 4096), P.n_sched);
+                for (size_t kk = 0; kk < q.arenas.size(); ++kk) {
+                    auto bk = backup.find((uint32_t)kk);
+                    const std::vector<uint8_t>& src = bk != backup.end() ? bk->second : q.arenas[kk];
+                    std::vector<uint8_t> dst((size_t)Ln.bytes, 0);
+                    nfa::CtxT<true> mc;
+                    mc.P = &P;
+                    mc.L = Ln;
+                    mc.base = dst.data();
+                    nfa::migrate_key(mc, src.data(), q.L);
+                    q.arenas[kk] = dst;
+                    if (bk != backup.end()) bk->second = dst;
+                }
+                q.L = Ln;
+                kout.clear();
+                klog.clear();
+                ++growths_;
+                again = true;
+                break;
+            }
+            if (rc) return rc;
         }
-        int rc = run_one(k, nullptr, -1);  // ideal mode
-        if (rc) return rc;
     }
     SchedSim::Result res;
     std::vector<std::unique_ptr<KeyRun>> runs;
@@ -456,7 +486,9 @@ int emu_flush(void* h) {
     return 0;
 }
 
-int64_t emu_sched_stat(int which) { return which == 0 ? (int64_t)reordered_ : which == 1 ? (int64_t)taken_ : (int64_t)us_[which - 2]; }
+int64_t emu_sched_stat(int which) {
+    return which == 0 ? (int64_t)reordered_ : which == 1 ? (int64_t)taken_ : which == 5 ? growths_ : (int64_t)us_[which - 2];
+}
 int emu_num_queries(void* h) { return (int)((Emu*)h)->qs.size(); }
 const char* emu_query_name(void* h, int q) { return ((Emu*)h)->qs[q]->hq.name.c_str(); }
 const char* emu_query_target(void* h, int q) { return ((Emu*)h)->qs[q]->hq.target.c_str(); }

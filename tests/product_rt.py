@@ -8,8 +8,8 @@ TAG = {sa.INT: "i", sa.LONG: "l", sa.FLOAT: "f", sa.DOUBLE: "d", sa.BOOL: "b", s
 
 
 class ProductAdapter:
-    def __init__(self, app, force_generic=False, fused=True):
-        self.rt = sa.SiddhiAppRuntime(app, force_generic=force_generic, fused=fused)
+    def __init__(self, app, force_generic=False, fused=True, max_partials=0):
+        self.rt = sa.SiddhiAppRuntime(app, force_generic=force_generic, fused=fused, max_partials=max_partials)
         self.handlers = {}
         self.records = []
 

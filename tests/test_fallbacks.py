@@ -1,0 +1,137 @@
+"""Fallbacks instead of failed flushes:
+- a key that runs out of partial-match slots doubles the arenas (nfa.h migrate_key, from the batch-start state)
+  and the batch reruns -- host NFA build on CPU, the engine on the GPU;
+- a chain-path query that meets decreasing per-key timestamps (inside a batch or across the batch boundary) moves
+  to the generic NFA, its carried partials replayed into the arenas first.
+Reference semantics for out-of-order time: StreamPreStateProcessor.isExpired uses |start.ts - now| (:118-129)."""
+import numpy as np
+import pytest
+
+import golden_util
+import synth
+from emu_rt import EmuAdapter, EmuError, lib as emu_lib, run_emu_fixture
+from oracle_rt import Oracle, OracleError, run_oracle_fixture
+
+DEEP = synth.chain_app("price>0", "price>e1.price", within="")  # no window: a descending run stays pending
+
+
+def deep_trace(depth=600, tail=300, seed=3):
+    """one key: `depth` strictly descending prices (every partial stays pending: `depth` deep), then a noisy tail
+    that completes them from the top"""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(depth):
+        out.append(("S", 1000 + i // 3, [i, "k0", float(100.0 - 0.125 * i), int(rng.integers(0, 100))]))
+    for j in range(tail):
+        i = depth + j
+        out.append(("S", 1000 + i // 3, [i, "k0", float(np.round(rng.uniform(20, 110), 2)), int(rng.integers(0, 100))]))
+    return out
+
+
+def query_rows(outs):
+    return [(o["name"], o["ts"], tuple(o["values"])) for o in outs if o["kind"] == "query" and not o["expired"]]
+
+
+def oracle_rows(app, tr, batches=1):
+    o = Oracle(app)
+    try:
+        return synth.run(o, tr, batches)
+    finally:
+        o.close()
+
+
+def test_host_nfa_grows_arenas_through_every_fixture(oracle_built, emu_built):
+    """every device-path fixture with 4 starting slots per key: growth (migration of lists, pools, timer queues)
+    must be invisible in the results"""
+    L = emu_lib()
+    g0 = L.emu_sched_stat(5)
+    bad, ran = [], 0
+    for path in golden_util.fixture_paths():
+        fx = golden_util.load(path)
+        try:
+            got = run_emu_fixture(fx, max_partials=4)
+        except EmuError:
+            continue  # not on the device path
+        try:
+            ref = run_oracle_fixture(fx)
+        except OracleError:
+            continue
+        ran += 1
+        if query_rows(got) != query_rows(ref):
+            bad.append(fx["source"])
+    assert ran > 400 and not bad, bad[:10]
+    assert L.emu_sched_stat(5) > g0  # some fixtures did outgrow 4 slots
+
+
+@pytest.mark.parametrize("batches", [1, 3])
+def test_host_nfa_500_deep_descending_run(batches, oracle_built, emu_built):
+    tr = deep_trace()
+    ref = oracle_rows(DEEP, tr, batches)
+    L = emu_lib()
+    g0 = L.emu_sched_stat(5)
+    e = EmuAdapter(DEEP, max_partials=16)
+    try:
+        got = synth.run(e, tr, batches)
+    finally:
+        e.close()
+    assert len(ref) > 100 and got == ref
+    assert L.emu_sched_stat(5) - g0 >= 5  # 16 -> 512 slots at least
+
+
+def out_of_order(tr, seed, start, jitter=6):
+    """the rows from `start` on get their timestamps jittered: per-key decreases inside the batch and across the
+    boundary with the rows before"""
+    rng = np.random.default_rng(seed)
+    out = list(tr[:start])
+    for s, ts, row in tr[start:]:
+        out.append((s, int(ts + rng.integers(-jitter, jitter + 1)), row))
+    return out
+
+
+@pytest.mark.gpu
+def test_device_arena_growth_500_deep(oracle_built):
+    from product_rt import ProductAdapter
+    tr = deep_trace()
+    ref = oracle_rows(DEEP, tr, 3)
+    p = ProductAdapter(DEEP, force_generic=True, max_partials=16)
+    try:
+        bounds = np.linspace(0, len(tr), 4).astype(int)
+        growths = 0
+        for b in range(3):
+            for s, ts, row in tr[bounds[b]:bounds[b + 1]]:
+                p.send(s, ts, row)
+            p.flush()
+            growths += p.rt.stats().arena_growths
+        got = query_rows(p.outputs())
+    finally:
+        p.close()
+    assert len(ref) > 100 and got == ref
+    assert growths >= 5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["gt", "const", "cross_col"])
+@pytest.mark.parametrize("partitioned", [True, False])
+def test_chain_query_falls_back_on_decreasing_timestamps(name, partitioned, oracle_built):
+    from product_rt import ProductAdapter
+    app = synth.CHAIN_APPS[name][0]
+    if not partitioned:
+        app = synth.flat(app.split("begin ", 1)[1].rsplit(" end;", 1)[0])
+    tr = synth.trace(3000, keys=6, seed=17, two_streams=False)
+    tr = out_of_order(tr, seed=5, start=1600)
+    ref = oracle_rows(app, tr, 3)
+    p = ProductAdapter(app)
+    try:
+        assert p.rt.query_paths() == [0]  # starts on the chain path
+        bounds = np.linspace(0, len(tr), 4).astype(int)
+        paths = []
+        for b in range(3):
+            for s, ts, row in tr[bounds[b]:bounds[b + 1]]:
+                p.send(s, ts, row)
+            p.flush()
+            paths.append(p.rt.stats().path)
+        got = query_rows(p.outputs())
+    finally:
+        p.close()
+    assert paths[0] == 0 and paths[-1] == 1  # ordered batch on the chain path, then the generic NFA
+    assert len(ref) > 50 and got == ref
