@@ -199,6 +199,58 @@ def cpu_baseline_sharded(cols, syms, sample, threads):
     return n / dt, matches, dt
 
 
+def ordered_gather_leg(rt, step_push, n, dev, dist, rank, world):
+    """C5's ordered result gather: one batch's match records exported device-to-device (sdg_export_device), sorted
+    on each rank's GPU, sent to rank 0 over RCCL (send/recv) and merged there into the single delivery order of the
+    combined stream: (event time, rank, position of the emitting event in its rank's stream, ordinal). The
+    combined stream interleaves the ranks' events by time, ties by rank. Rank 0 checks the merged order."""
+    import torch
+    from siddhi_amd import shard
+    step_push()
+    rt.flush(deliver=False)
+    cap = n + n // 4 + 4096
+    t_ts = torch.empty(cap, dtype=torch.int64, device=dev)
+    t_seq = torch.empty(cap, dtype=torch.int64, device=dev)
+    t_sub = torch.empty(cap, dtype=torch.int64, device=dev)
+    t_vals = torch.empty((2, cap), dtype=torch.int64, device=dev)
+    cnt = rt.export_device(0, cap, t_ts.data_ptr(), t_seq.data_ptr(), t_sub.data_ptr(), t_vals.data_ptr())
+    recs = {"ts": t_ts[:cnt], "seq": t_seq[:cnt], "sub": t_sub[:cnt],
+            "rank": torch.full((cnt,), rank, dtype=torch.int64, device=dev), "vals": t_vals[:, :cnt]}
+    key = ["ts", "rank", "seq", "sub"]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    if dist is None:
+        order = shard.lexsort([recs[k] for k in key])
+        merged = {k: v[..., order] for k, v in recs.items()}
+    else:
+        merged = shard.ordered_gather(dist, rank, world, recs, key)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    if rank != 0:
+        return None
+    total = int(merged["ts"].numel())
+    ok = True
+    if total > 1:  # lexicographic non-decreasing on the key (strictly increasing: records are distinct)
+        less = torch.zeros(total - 1, dtype=torch.bool, device=dev)
+        eq = torch.ones(total - 1, dtype=torch.bool, device=dev)
+        for k in key:
+            a, b = merged[k][:-1], merged[k][1:]
+            less |= eq & (a < b)
+            eq &= a == b
+        ok = bool(less.all().item())
+    if not ok:
+        raise RuntimeError("ordered gather: merged records are not in delivery order")
+    return {"records": total, "ms": dt * 1000.0, "bytes_to_rank0": int((total - cnt) * 8 * 6),
+            "key": "(event ts, rank, event position in its rank's stream, ordinal)", "ordered": True,
+            "path": "sdg_export_device -> per-rank device sort -> RCCL send/recv to rank 0 -> merge"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -212,6 +264,7 @@ def main():
                     help="events of the bench stream re-run through a fresh runtime and the oracle (bit-exact check)")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=1, help="end-to-end (host push -> poll) steps, 0 = skip")
+    ap.add_argument("--no-gather", action="store_true", help="skip the ordered result gather leg")
     args = ap.parse_args()
 
     import torch
@@ -248,7 +301,7 @@ def main():
     d_ts0 = torch.from_numpy(cols["ts"]).to(dev)
     span = int(cols["ts"][-1] - cols["ts"][0]) + 1
     nsteps = args.warmup + args.steps
-    ts_steps = [d_ts0 + s * span for s in range(nsteps)]  # consecutive batches of one stream
+    ts_steps = [d_ts0 + s * span for s in range(nsteps + 1)]  # consecutive batches of one stream (+1: gather leg)
     torch.cuda.synchronize()
 
     def step(s):
@@ -350,6 +403,12 @@ def main():
                                                  % (thr, sdt, scm)}
     else:
         out["cpu_baseline"] = None
+    if not args.no_gather:
+        log("ordered result gather (one more batch, outside the timed region)")
+        out["ordered_gather"] = ordered_gather_leg(rt, step_push=lambda: rt.push_device(
+            "StockStream", n, ts_steps[nsteps].data_ptr(), [d_id.data_ptr(), d_sym.data_ptr(), d_price.data_ptr(),
+                                                            d_vol.data_ptr()]), n=n, dev=dev, dist=dist, rank=rank,
+            world=world)
     rt.shutdown()
     if args.e2e_steps > 0 and world == 1:
         log("end-to-end (host push -> poll), %d step(s)" % args.e2e_steps)

@@ -134,6 +134,7 @@ def load_library():
     L.sdg_sync.argtypes = [P]
     L.sdg_poll.argtypes = [P, I32, ctypes.POINTER(_Out)]
     L.sdg_discard.argtypes = [P]
+    L.sdg_export_device.argtypes = [P, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), P, P, P, P]
     L.sdg_last_stats.argtypes = [P, ctypes.POINTER(Stats)]
     _lib = L
     return L
@@ -378,6 +379,13 @@ class SiddhiAppRuntime:
     def discard(self):
         """drop the unpolled results of every query (device-resident measurement only)"""
         _check(self._L.sdg_discard(self._h))
+
+    def export_device(self, q, cap, d_ts, d_seq, d_sub, d_vals):
+        """copy query q's records of the last flush into device buffers (raw pointers, `cap` records each,
+        d_vals: [n_out][cap]); unordered -- delivery order is (seq, sub). Returns the record count."""
+        n = ctypes.c_int64()
+        _check(self._L.sdg_export_device(self._h, q, cap, ctypes.byref(n), d_ts, d_seq, d_sub, d_vals))
+        return n.value
 
     def stats(self):
         s = Stats()

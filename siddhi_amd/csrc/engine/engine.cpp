@@ -1827,6 +1827,34 @@ int sdg_discard(sdg_engine* e) {
     return SDG_OK;
 }
 
+int sdg_export_device(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_t* d_ts, int64_t* d_seq,
+                      int64_t* d_sub, int64_t* d_vals) {
+    if (!e || qi < 0 || qi >= (int)e->qs.size() || !n_out) return fail(SDG_ERR_ARG, "bad export arguments");
+    return guarded([&]() {
+        QueryRt& q = *e->qs[qi];
+        if (e->compile_only) throw DeviceError("engine was compiled with SDG_COMPILE_ONLY");
+        if (!q.acc_ts.empty()) throw CompileError(SDG_ERR_ARG, "earlier results are still queued on the host: sdg_poll first");
+        if (q.last_timers) throw CompileError(SDG_ERR_UNSUPPORTED, "device export of timer (absent-state) matches");
+        const int64_t n = q.polled ? 0 : q.out_n;
+        *n_out = n;
+        if (n > cap) throw CompileError(SDG_ERR_CAPACITY, "export buffers hold " + std::to_string(cap) + " of " +
+                                                              std::to_string(n) + " records");
+        hipStream_t st = e->stream;
+        const int na = q.hq.plan.n_out;
+        if (n > 0) {
+            HIPCHECK(hipMemcpyAsync(d_ts, q.o_ts.p, n * 8, hipMemcpyDeviceToDevice, st));
+            HIPCHECK(hipMemcpyAsync(d_seq, q.o_emit.p, n * 8, hipMemcpyDeviceToDevice, st));
+            HIPCHECK(hipMemcpyAsync(d_sub, q.o_first.p, n * 8, hipMemcpyDeviceToDevice, st));
+            for (int j = 0; j < na; ++j)
+                HIPCHECK(hipMemcpyAsync(d_vals + (size_t)j * cap, (const int64_t*)q.o_vals.p + (size_t)j * q.out_cap, n * 8,
+                                        hipMemcpyDeviceToDevice, st));
+            HIPCHECK(hipStreamSynchronize(st));
+        }
+        q.polled = true;
+        return SDG_OK;
+    });
+}
+
 int sdg_last_stats(sdg_engine* e, sdg_stats* out) {
     if (!e || !out) return fail(SDG_ERR_ARG, "null argument");
     *out = e->stats;

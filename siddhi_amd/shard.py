@@ -40,3 +40,47 @@ def route(keys, world):
 def merge(parts):
     """parts: per rank, lists of (global_seq, ordinal, record) already in local order -> one ordered list"""
     return [rec for _, _, rec in heapq.merge(*parts, key=lambda t: (t[0], t[1]))]
+
+
+def lexsort(keys):
+    """permutation ordering records by `keys` (torch tensors, most significant first), stable"""
+    import torch
+    order = torch.arange(keys[0].numel(), device=keys[0].device)
+    for k in reversed(keys):
+        order = order[torch.argsort(k[order], stable=True)]
+    return order
+
+
+def ordered_gather(dist, rank, world, cols, key_names):
+    """Ordered result gather: `cols` maps names to this rank's record tensors (1-D [n], or 2-D
+    [m, n] with records along the last dim) on the communication device. Every rank sorts its records by
+    `key_names` on its device, the run lengths are all-gathered, and each rank's sorted run goes to rank 0
+    point-to-point (send/recv: RCCL over xGMI with the nccl backend, gloo on CPU), where the runs are merged by the
+    same key. Returns the merged dict on rank 0, None elsewhere."""
+    import torch
+    names = sorted(cols)
+    ref = cols[key_names[0]]
+    order = lexsort([cols[k] for k in key_names])
+    mine = {k: cols[k][..., order].contiguous() for k in names}
+    n = torch.tensor([ref.numel()], dtype=torch.int64, device=ref.device)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n)
+    counts = [int(c.item()) for c in counts]
+    if rank != 0:
+        if counts[rank] > 0:
+            for k in names:
+                dist.send(mine[k], dst=0)
+        return None
+    runs = [mine]
+    for r in range(1, world):
+        if counts[r] == 0:
+            continue
+        run = {}
+        for k in names:
+            shape = list(cols[k].shape[:-1]) + [counts[r]]
+            run[k] = torch.empty(shape, dtype=cols[k].dtype, device=ref.device)
+            dist.recv(run[k], src=r)
+        runs.append(run)
+    merged = {k: torch.cat([run[k] for run in runs], dim=-1) for k in names}
+    order = lexsort([merged[k] for k in key_names])  # the runs are sorted: a stable sort of their concatenation
+    return {k: merged[k][..., order] for k in names}

@@ -364,6 +364,37 @@ def test_c2_bench_regime_vs_oracle(oracle_built):
     assert np.all(np.diff(gseq) >= 0)  # delivery order: by emitting event
 
 
+def test_radix_path_million_keys_vs_oracle(oracle_built):
+    """C2's query over 2^20 long partition keys (past the fused path's 2^16: the full radix key sort + chain
+    kernels), 3M events in two batches at a rate that puts each key's ~3 events inside one window; every match
+    against the oracle, in delivery order"""
+    keys = 1 << 20
+    n = 3_000_000
+    app = ("@app:playback define stream S (id long, key long, price double, volume int); partition with (key of S) "
+           "begin @info(name = 'query1') from every e1=S[price>20] -> e2=S[price>e1.price] within 1 sec "
+           "select e1.id as e1id, e2.id as e2id insert into M; end;")
+    cols = w.c2_columns(n, keys=keys, per_ms=20_000)
+    rt = sa.SiddhiAppRuntime(app)
+    try:
+        assert rt.query_paths() == [0]
+        h = rt.getInputHandler("S")
+        parts = []
+        for lo, hi in ((0, n // 2), (n // 2, n)):
+            h.send_columns(cols["ts"][lo:hi], [cols["id"][lo:hi], cols["key"][lo:hi], cols["price"][lo:hi],
+                                              cols["volume"][lo:hi]])
+            rt.flush(deliver=False)
+            assert rt.stats().fused == 0 and rt.stats().path == 0
+            parts.append(rt.poll_arrays(0))
+    finally:
+        rt.shutdown()
+    gts = np.concatenate([p[0] for p in parts])
+    gvals = np.concatenate([p[1] for p in parts], axis=1)
+    ots, ovals, _ = oracle_batch_rows(app, "S", cols["ts"], [cols["id"], cols["key"], cols["price"].view(np.int64),
+                                                              cols["volume"]], 2)
+    assert len(ots) > 500_000
+    assert np.array_equal(gts, ots) and np.array_equal(gvals.T, ovals)
+
+
 @pytest.mark.parametrize("query", ["<1:5>", "<2:5>"])
 def test_c3_long_keys_vs_oracle(query, oracle_built):
     """C3 generator (long partition keys, 10^4 keys x 100 events) through the host push, generic keyed NFA; the

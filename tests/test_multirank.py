@@ -53,8 +53,16 @@ def _rank_main(rank, world, port, out_dir):
             part = [(mine[r["seq"]], r["ordinal"], (r["name"], r["ts"], tuple(r["values"]))) for r in recs]
             parts = [None] * world
             dist.all_gather_object(parts, part)
+            # the tensor path bench.py takes on the GPUs: per-rank sort, send/recv to rank 0, merge on the key
+            g = shard.ordered_gather(dist, rank, world, {
+                "gseq": torch.tensor([p[0] for p in part], dtype=torch.int64),
+                "ord": torch.tensor([p[1] for p in part], dtype=torch.int64),
+                "rank": torch.full((len(part),), rank, dtype=torch.int64),
+                "idx": torch.arange(len(part), dtype=torch.int64)}, ["gseq", "ord"])
             if rank == 0:
                 merged = shard.merge(parts)
+                tensor_merged = [parts[r][i][2] for r, i in zip(g["rank"].tolist(), g["idx"].tolist())]
+                assert tensor_merged == merged
                 with open(os.path.join(out_dir, name + ".txt"), "w") as f:
                     f.write(repr(merged))
     finally:
