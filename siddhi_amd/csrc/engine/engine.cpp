@@ -158,6 +158,11 @@ struct QueryRt {
     // scheduler replayed on the host (their device records are void) and those replays
     bool last_timers = false;
     int64_t last_seq_base = 0;
+    // delivery order on the device (order.hip): the flush's first position, and whether `sub` holds the e1 event's
+    // position (chain path) or an ordinal within the emitting event (generic NFA)
+    int64_t emit_base = 0;
+    bool sub_is_seq = false;
+    DevBuf ord_ws, g_ts, g_emit, g_vals, g_nulls;
     SchedSim::RankMap last_rank;
     std::vector<uint32_t> reordered;  // keys rerun with the scheduler's fire order (sorted)
     std::vector<uint32_t> taken;
@@ -972,6 +977,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         q.reordered.clear();
         q.runs.clear();
         q.last_seq_base = e->seq;
+        q.emit_base = e->seq;
+        q.sub_is_seq = false;
         if (timers) {
             const auto t_sched = std::chrono::steady_clock::now();
             double k_before = e->stats.ms_nfa_kernel;
@@ -1347,6 +1354,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     e->stats.matches += q.out_n;
     e->stats.path = 0;
     q.last_timers = false;
+    q.emit_base = e->seq;
+    q.sub_is_seq = true;
     return true;
     };
     // rerun on the radix path (fused precondition broken), or on the generic NFA (chain precondition broken)
@@ -1370,6 +1379,37 @@ void drain(sdg_engine* e, QueryRt& q) {
     int64_t* vals = first + n;
     uint32_t* nulls = (uint32_t*)(vals + (size_t)na * n);
     hipStream_t st = e->stream;
+    // records of queries without timers are put in delivery order on the device and read back in that order
+    const void* src_ts = q.o_ts.p;
+    const void* src_emit = q.o_emit.p;
+    const void* src_first = q.o_first.p;
+    const int64_t* src_vals = (const int64_t*)q.o_vals.p;
+    int64_t vstride = q.out_cap;
+    const void* src_nulls = q.o_nulls.p;
+    const bool dev_order = !q.last_timers && n > 1;
+    if (dev_order) {
+        const size_t wb = order_workspace(n);
+        void* work = q.ord_ws.ensure(wb);
+        uint32_t* perm = nullptr;
+        order_records((const int64_t*)q.o_emit.p, (const int64_t*)q.o_first.p, n, q.emit_base,
+                      q.sub_is_seq ? q.emit_base - (1ll << 40) : 0, work, wb, &perm, st);
+        int64_t* gts = (int64_t*)q.g_ts.ensure((size_t)n * 8);
+        int64_t* gem = (int64_t*)q.g_emit.ensure((size_t)n * 8);
+        int64_t* gv = (int64_t*)q.g_vals.ensure((size_t)std::max(na, 1) * n * 8);
+        gather_i64((const int64_t*)q.o_ts.p, perm, n, gts, st);
+        gather_i64((const int64_t*)q.o_emit.p, perm, n, gem, st);
+        for (int j = 0; j < na; ++j) gather_i64((const int64_t*)q.o_vals.p + (size_t)j * q.out_cap, perm, n, gv + (size_t)j * n, st);
+        if (q.nulls_valid) {
+            uint32_t* gn = (uint32_t*)q.g_nulls.ensure((size_t)n * 4);
+            gather_u32((const uint32_t*)q.o_nulls.p, perm, n, gn, st);
+            src_nulls = gn;
+        }
+        src_ts = gts;
+        src_emit = gem;
+        src_first = nullptr;
+        src_vals = gv;
+        vstride = n;
+    }
     std::vector<uint32_t> okey;
     std::vector<uint8_t> oround;
     if (q.last_timers) {  // timer matches: drop the records of keys replayed on the host, order the fires
@@ -1380,13 +1420,12 @@ void drain(sdg_engine* e, QueryRt& q) {
             HIPCHECK(hipMemcpyAsync(oround.data(), q.o_round.p, n, hipMemcpyDeviceToHost, st));
         }
     }
-    HIPCHECK(hipMemcpyAsync(ts, q.o_ts.p, n * 8, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipMemcpyAsync(emit, q.o_emit.p, n * 8, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipMemcpyAsync(first, q.o_first.p, n * 8, hipMemcpyDeviceToHost, st));
-    if (q.nulls_valid) HIPCHECK(hipMemcpyAsync(nulls, q.o_nulls.p, n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(ts, src_ts, n * 8, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(emit, src_emit, n * 8, hipMemcpyDeviceToHost, st));
+    if (src_first) HIPCHECK(hipMemcpyAsync(first, src_first, n * 8, hipMemcpyDeviceToHost, st));
+    if (q.nulls_valid) HIPCHECK(hipMemcpyAsync(nulls, src_nulls, n * 4, hipMemcpyDeviceToHost, st));
     for (int j = 0; j < na; ++j)
-        HIPCHECK(hipMemcpyAsync(vals + (size_t)j * n, (int64_t*)q.o_vals.p + (size_t)j * q.out_cap, n * 8,
-                                hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(vals + (size_t)j * n, src_vals + (size_t)j * vstride, n * 8, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
     if (!q.nulls_valid) std::memset(nulls, 0, (size_t)n * 4);
     // the host replays' records join the device's (same layout, after them)
@@ -1436,9 +1475,10 @@ void drain(sdg_engine* e, QueryRt& q) {
     auto EM = [&](int64_t x) { return x < n ? emit[x] : hemit[x - n]; };
     auto FI = [&](int64_t x) { return x < n ? first[x] : hfirst[x - n]; };
     const int64_t nk = (int64_t)ord.size();
-    std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
-        return EM(x) != EM(y) ? EM(x) < EM(y) : FI(x) < FI(y);
-    });
+    if (!dev_order)
+        std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
+            return EM(x) != EM(y) ? EM(x) < EM(y) : FI(x) < FI(y);
+        });
     const size_t b = q.acc_ts.size();
     q.acc_ts.resize(b + nk);
     q.acc_seq.resize(b + nk);

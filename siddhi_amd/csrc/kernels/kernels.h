@@ -245,4 +245,12 @@ void nfa_migrate(const Plan* plan, const uint8_t* arena, const uint8_t* arena2, 
 // double-buffered arenas: flip `cur` of every key a run touched (`ran`), clearing `ran`
 void nfa_commit(uint8_t* cur, uint8_t* ran, int64_t K, hipStream_t stream);
 
+// delivery order of n match records (order.hip): perm = the record indices sorted by (emit - emit_base as u32,
+// sub - sub_bias as a 48-bit key); work = order_workspace(n) bytes
+size_t order_workspace(int64_t n);
+void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t emit_base, int64_t sub_bias, void* work,
+                   size_t work_bytes, uint32_t** perm_out, hipStream_t stream);
+void gather_i64(const int64_t* src, const uint32_t* perm, int64_t n, int64_t* dst, hipStream_t stream);
+void gather_u32(const uint32_t* src, const uint32_t* perm, int64_t n, uint32_t* dst, hipStream_t stream);
+
 }  // namespace sdg
