@@ -494,6 +494,11 @@ struct MultiVarExec : Exec {
         return l;
     }
 };
+// a having-scope variable that names an output attribute (ExpressionParser.parseVariable HAVING_STATE branch)
+struct OutVarExec : Exec {
+    int j;
+    Val exec(StateEvent* e) override { return e->out[j]; }
+};
 struct AndExec : Exec {  // AndConditionExpressionExecutor.java:65-74
     ExecP l, r;
     Val exec(StateEvent* e) override {
@@ -622,6 +627,133 @@ struct MathExec : Exec {
                 }
             }
         }
+    }
+};
+
+// function executors (core/executor/function/*.java). FunctionExecutor.execute evaluates every argument first.
+struct IfThenElseExec : Exec {  // IfThenElseFunctionExecutor.execute: Boolean.TRUE.equals(data[0]) ? data[1] : data[2]
+    ExecP c, a, b;
+    Val exec(StateEvent* e) override {
+        Val cv = c->exec(e), av = a->exec(e), bv = b->exec(e);
+        return (!cv.null && cv.b()) ? av : bv;
+    }
+};
+struct CoalesceExec : Exec {  // CoalesceFunctionExecutor / DefaultFunctionExecutor: the first non-null argument
+    std::vector<ExecP> xs;
+    Val exec(StateEvent* e) override {
+        std::vector<Val> v;
+        for (auto& x : xs) v.push_back(x->exec(e));
+        for (auto& x : v)
+            if (!x.null) return x;
+        return vnull(rt);
+    }
+};
+struct InstanceOfExec : Exec {  // InstanceOf{Boolean,Double,Float,Integer,Long,String}FunctionExecutor: data instanceof T
+    ExecP x;
+    Type target;
+    Val exec(StateEvent* e) override {
+        Val v = x->exec(e);
+        return vB(!v.null && (Type)v.t == target);
+    }
+};
+static int32_t java_d2i(double d) {  // JLS 5.1.3 narrowing: NaN -> 0, saturating
+    if (d != d) return 0;
+    if (d >= 2147483647.0) return INT32_MAX;
+    if (d <= -2147483648.0) return INT32_MIN;
+    return (int32_t)d;
+}
+static int64_t java_d2l(double d) {
+    if (d != d) return 0;
+    if (d >= 9223372036854775807.0) return INT64_MAX;
+    if (d <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)d;
+}
+// MaximumFunctionExecutor / MinimumFunctionExecutor.execute(Object[]): a double running max starting at
+// Double.MIN_VALUE (the smallest POSITIVE double) / min starting at Double.MAX_VALUE; a null argument counts as
+// that start value; the result is cast back to the argument type. One argument: execute(Object) returns it as is.
+struct MaxMinExec : Exec {
+    bool is_max = true;
+    std::vector<ExecP> xs;
+    Val exec(StateEvent* e) override {
+        std::vector<Val> v;
+        for (auto& x : xs) v.push_back(x->exec(e));
+        if (v.size() == 1) return v[0];
+        const double start = is_max ? 4.9e-324 : 1.7976931348623157e308;
+        double best = start;
+        for (auto& x : v) {
+            const double value = x.null ? start : as_double(x);
+            if (is_max ? value > best : value < best) best = value;
+        }
+        switch (rt) {
+            case Type::INT: return vI(java_d2i(best));
+            case Type::LONG: return vL(java_d2l(best));
+            case Type::FLOAT: return vF((float)best);
+            default: return vD(best);
+        }
+    }
+};
+
+// attribute aggregators (core/query/selector/attribute/aggregator/*AttributeAggregatorExecutor.java) with their
+// state per partition key (the selector's state holder is partition-aware). Pattern outputs reach the selector
+// as CURRENT events only, so the states only ever add (EXPIRED: processRemove, restated for count/sum/avg).
+struct AggExec : Exec {
+    enum K { COUNT, SUM, AVG, MIN, MAX } k = COUNT;
+    ExecP arg;  // null for count()
+    Type at = Type::LONG;
+    const Ctx* ctx = nullptr;
+    bool partitioned = false;
+    struct St {
+        int64_t count = 0;
+        int64_t lsum = 0;
+        double dsum = 0;
+        bool has = false;  // MIN/MAX: minValue != null
+        Val m;
+    };
+    std::unordered_map<std::string, St> states;
+    Val exec(StateEvent* e) override {
+        St& s = states[partitioned ? ctx->key : std::string()];
+        const bool add = e->type != EXPIRED;
+        if (k == COUNT) {  // CountAttributeAggregatorExecutor.processAdd / processRemove
+            s.count += add ? 1 : -1;
+            return vL(s.count);
+        }
+        Val v = arg->exec(e);
+        const bool integral = at == Type::INT || at == Type::LONG;
+        if (k == SUM) {  // SumAttributeAggregatorExecutor: AggregatorState{Int->Long, Long, Float->Double, Double}
+            if (!v.null) {
+                if (integral) s.lsum = (int64_t)((uint64_t)s.lsum + (uint64_t)(add ? as_long(v) : -as_long(v)));
+                else s.dsum = add ? s.dsum + as_double(v) : s.dsum - as_double(v);
+                s.count += add ? 1 : -1;
+            }
+            if (s.count == 0) return vnull(rt);  // currentValue / processRemove at count 0
+            return integral ? vL(s.lsum) : vD(s.dsum);
+        }
+        if (k == AVG) {  // AvgAttributeAggregatorExecutor: double value, long count
+            if (!v.null) {
+                s.count += add ? 1 : -1;
+                s.dsum = add ? s.dsum + as_double(v) : s.dsum - as_double(v);
+            }
+            if (s.count == 0) return vnull(rt);
+            return vD(s.dsum / (double)s.count);
+        }
+        // Min/MaxAttributeAggregatorExecutor (and the *Forever variants): minValue == null || minValue > value
+        if (!add) throw OracleError("unsupported: min/max of expired events on the pattern path");
+        if (!v.null) {
+            bool take = !s.has;
+            if (s.has) {
+                switch (at) {
+                    case Type::INT: take = k == MIN ? s.m.i() > v.i() : s.m.i() < v.i(); break;
+                    case Type::LONG: take = k == MIN ? s.m.l() > v.l() : s.m.l() < v.l(); break;
+                    case Type::FLOAT: take = k == MIN ? s.m.f() > v.f() : s.m.f() < v.f(); break;
+                    default: take = k == MIN ? s.m.d() > v.d() : s.m.d() < v.d(); break;
+                }
+            }
+            if (take) {
+                s.m = v;
+                s.has = true;
+            }
+        }
+        return s.has ? s.m : vnull(rt);
     }
 };
 
@@ -1478,6 +1610,7 @@ struct Selector : Processor {
         MultiVarExec* mv = nullptr;
     };
     std::vector<Attr> attrs;
+    ExecP having;  // QuerySelector.havingConditionExecutor
     bool currentOn = true, expiredOn = false;
     QueryRt* q = nullptr;
     void process(Chunk& c) override;  // QuerySelector.process -> processNoGroupBy
@@ -1697,7 +1830,9 @@ void Selector::process(Chunk& c) {  // QuerySelector.processNoGroupBy :161-205
                         ev->out_list[i] = nullptr;
                     }
                 }
-                if ((ev->type != CURRENT || !currentOn) && (ev->type != EXPIRED || !expiredOn)) c.remove();
+                if (((ev->type != CURRENT || !currentOn) && (ev->type != EXPIRED || !expiredOn)) ||
+                    (having && [&]() { Val h = having->exec(ev.get()); return h.null || !h.b(); }()))
+                    c.remove();
                 break;
             }
             case RESET:
@@ -1880,6 +2015,9 @@ struct Builder {
     std::map<std::string, Receiver*> recv;  // processStreamReceiverMap
     bool partitioned;
 
+    bool having_scope = false;           // parsing the having condition: output names resolve first
+    std::vector<std::string> out_names;  // the selector's output attributes
+    std::vector<Type> out_types;
     Builder(AppRt& r, QueryRt& qq, const sql::Query& a, bool part) : rt(r), q(qq), qa(a), partitioned(part) {}
 
     template <class T>
@@ -1983,9 +2121,91 @@ struct Builder {
                 x->idx = idx;
                 return x;
             }
+            case ExprKind::FUNC: return func(e, currentState, defaultIdx);
             default:
-                throw OracleError("OperationNotSupportedException: functions are not supported");
+                throw OracleError("OperationNotSupportedException: expression kind not supported");
         }
+    }
+    // ExpressionParser.parseExpression AttributeFunction: core functions (executor/function) and, in the selector
+    // / having scope only, attribute aggregators (query/selector/attribute/aggregator)
+    ExecP func(const sql::ExprP& e, int cs, int di) {
+        const std::string& n = e->fn_name;
+        auto bad = [&](const std::string& m) { return OracleError("SiddhiAppValidationException: " + n + "(): " + m); };
+        if (!e->fn_ns.empty())
+            throw OracleError("OperationNotSupportedException: function '" + e->fn_ns + ":" + n + "' is not supported");
+        std::vector<ExecP> args;
+        for (auto& k : e->kids) args.push_back(expr(k, cs, di));
+        auto same_types = [&]() {
+            for (auto& a : args)
+                if (a->rt != args[0]->rt) throw bad("all parameters should be of the same type");
+        };
+        if (n == "ifThenElse") {
+            if (args.size() != 3) throw bad("required 3 arguments");
+            if (args[0]->rt != Type::BOOL) throw bad("the condition must be bool");
+            if (args[1]->rt != args[2]->rt) throw bad("then / else types differ");
+            auto x = std::make_unique<IfThenElseExec>();
+            x->rt = args[1]->rt;
+            x->c = std::move(args[0]); x->a = std::move(args[1]); x->b = std::move(args[2]);
+            return x;
+        }
+        if (n == "coalesce" || n == "default") {
+            if (args.empty()) throw bad("needs arguments");
+            if (n == "default" && (args.size() != 2 || e->kids[1]->kind != sql::ExprKind::CONST))
+                throw bad("takes (attribute, constant default)");
+            same_types();
+            auto x = std::make_unique<CoalesceExec>();
+            x->rt = args[0]->rt;
+            x->xs = std::move(args);
+            return x;
+        }
+        static const std::pair<const char*, Type> inst[] = {
+            {"instanceOfBoolean", Type::BOOL}, {"instanceOfDouble", Type::DOUBLE}, {"instanceOfFloat", Type::FLOAT},
+            {"instanceOfInteger", Type::INT},  {"instanceOfLong", Type::LONG},     {"instanceOfString", Type::STRING}};
+        for (auto& p : inst)
+            if (n == p.first) {
+                if (args.size() != 1) throw bad("required 1 argument");
+                auto x = std::make_unique<InstanceOfExec>();
+                x->rt = Type::BOOL;
+                x->target = p.second;
+                x->x = std::move(args[0]);
+                return x;
+            }
+        if (n == "maximum" || n == "minimum") {
+            if (args.empty()) throw bad("needs arguments");
+            for (auto& a : args)
+                if (!sql::is_numeric(a->rt)) throw bad("numeric parameters required");
+            same_types();
+            auto x = std::make_unique<MaxMinExec>();
+            x->rt = args[0]->rt;
+            x->is_max = n == "maximum";
+            x->xs = std::move(args);
+            return x;
+        }
+        static const std::pair<const char*, AggExec::K> aggs[] = {
+            {"count", AggExec::COUNT}, {"sum", AggExec::SUM}, {"avg", AggExec::AVG}, {"min", AggExec::MIN},
+            {"max", AggExec::MAX}, {"minForever", AggExec::MIN}, {"maxForever", AggExec::MAX}};
+        for (auto& p : aggs)
+            if (n == p.first) {
+                if (cs != -1) throw OracleError("SiddhiAppCreationException: aggregator " + n + "() outside the selector");
+                auto x = std::make_unique<AggExec>();
+                x->k = p.second;
+                x->ctx = &rt.eng.ctx;
+                x->partitioned = partitioned;
+                if (x->k == AggExec::COUNT) {
+                    if (!args.empty()) throw bad("takes no arguments");
+                    x->rt = Type::LONG;
+                    return x;
+                }
+                if (args.size() != 1 || !sql::is_numeric(args[0]->rt))
+                    throw OracleError("OperationNotSupportedException: " + n + "() needs one numeric argument");
+                x->at = args[0]->rt;
+                x->arg = std::move(args[0]);
+                if (x->k == AggExec::SUM) x->rt = (x->at == Type::INT || x->at == Type::LONG) ? Type::LONG : Type::DOUBLE;
+                else if (x->k == AggExec::AVG) x->rt = Type::DOUBLE;
+                else x->rt = x->at;
+                return x;
+            }
+        throw OracleError("OperationNotSupportedException: function '" + n + "' is not supported");
     }
     ExecP cond(const sql::ExprP& e, int cs, int di) {
         ExecP x = expr(e, cs, di);
@@ -1994,6 +2214,15 @@ struct Builder {
     }
     // ExpressionParser.parseVariable, MetaStateEvent branch :1302-1438
     ExecP var(const sql::ExprP& e, int currentState, int defaultIdx, bool* multiOut = nullptr) {
+        if (having_scope && e->stream_ref.empty()) {  // :1310-1318: the output definition first
+            for (size_t j = 0; j < out_names.size(); ++j)
+                if (out_names[j] == e->attr) {
+                    auto x = std::make_unique<OutVarExec>();
+                    x->j = (int)j;
+                    x->rt = out_types[j];
+                    return x;
+                }
+        }
         int idx = defaultIdx;
         if (e->has_index) idx = e->index <= sql::IDX_LAST ? e->index + 1 : e->index;
         int chain = -1;
@@ -2272,8 +2501,26 @@ struct Builder {
         sel->q = &q;
         sel->currentOn = qa.out_type != sql::OutputEventType::EXPIRED;
         sel->expiredOn = qa.out_type != sql::OutputEventType::CURRENT;
-        if (qa.select_all) throw OracleError("unsupported: select * on a pattern query");
-        for (auto& oa : qa.select) {
+        // select *: every attribute of every state's stream, unqualified (SelectorParser.getAttributeProcessors
+        // :182-209; a name in two streams is a DuplicateAttributeException)
+        std::vector<sql::OutputAttribute> sel_list = qa.select;
+        if (qa.select_all) {
+            sel_list.clear();
+            for (auto* d : meta.defs)
+                for (auto& at : d->attrs) {
+                    for (auto& o : sel_list)
+                        if (o.rename == at.name) throw OracleError("DuplicateAttributeException: '" + at.name + "'");
+                    sql::OutputAttribute o;
+                    o.rename = at.name;
+                    o.expr = std::make_shared<sql::Expr>();
+                    o.expr->kind = sql::ExprKind::VAR;
+                    o.expr->attr = at.name;
+                    sel_list.push_back(o);
+                }
+        }
+        out_names.clear();
+        for (auto& oa : sel_list) out_names.push_back(oa.rename);
+        for (auto& oa : sel_list) {
             Selector::Attr a;
             bool mv = false;
             if (oa.expr->kind == sql::ExprKind::VAR) {
@@ -2283,6 +2530,12 @@ struct Builder {
                 a.ex = expr(oa.expr, -1, 0);
             }
             sel->attrs.push_back(std::move(a));
+        }
+        for (auto& a : sel->attrs) out_types.push_back(a.ex->rt);
+        if (qa.having) {  // HAVING_STATE, default chain index 0 (SelectorParser.generateHavingExecutor)
+            having_scope = true;
+            sel->having = cond(qa.having, -1, 0);
+            having_scope = false;
         }
         q.selector = sel;
         for (PreProc* p : preList) {

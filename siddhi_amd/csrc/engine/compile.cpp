@@ -54,12 +54,35 @@ class QC {
         rows_[root.first].last = root.last;  // the first processor's thisLastProcessor
         set_selector(q_.root, root);
         h_.expire_order = pre_list;
-        // selector
-        if (q_.select_all) throw CompileError(SDG_ERR_UNSUPPORTED, "select * on a pattern query is not supported");
-        if ((int)q_.select.size() > MAX_OUT) throw CompileError(SDG_ERR_UNSUPPORTED, "too many output attributes");
-        p.n_out = (int)q_.select.size();
-        for (size_t i = 0; i < q_.select.size(); ++i) {
-            const auto& oa = q_.select[i];
+        // selector (SelectorParser.getAttributeProcessors): select * = every attribute of every state's stream,
+        // unqualified (:182-209; a name in two streams is a DuplicateAttributeException)
+        std::vector<sql::OutputAttribute> sel = q_.select;
+        if (q_.select_all) {
+            sel.clear();
+            for (auto* d : meta_.defs)
+                for (auto& at : d->attrs) {
+                    for (auto& o : sel)
+                        if (o.rename == at.name)
+                            throw CompileError(SDG_ERR_VALIDATION, "select *: duplicate attribute '" + at.name + "'");
+                    sql::OutputAttribute o;
+                    o.rename = at.name;
+                    o.expr = std::make_shared<sql::Expr>();
+                    o.expr->kind = sql::ExprKind::VAR;
+                    o.expr->attr = at.name;
+                    sel.push_back(o);
+                }
+        }
+        if ((int)sel.size() > MAX_OUT) throw CompileError(SDG_ERR_UNSUPPORTED, "too many output attributes");
+        p.n_user_out = p.n_out = (int)sel.size();
+        for (auto& oa : sel) user_names_.push_back(oa.rename);
+        // items without aggregators are evaluated at emission; items over aggregators by the post pass, whose
+        // input references become hidden emission columns (pending_)
+        for (size_t i = 0; i < sel.size(); ++i) {
+            const auto& oa = sel[i];
+            p.out_multi[i] = 0;
+            p.out_post[i] = 0;
+            p.out_prog[i] = Prog{};
+            if (has_agg(oa.expr)) continue;
             Prog pr;
             pr.start = (int)h_.code.size();
             bool multi = false;
@@ -68,11 +91,48 @@ class QC {
             if (multi)
                 throw CompileError(SDG_ERR_UNSUPPORTED,
                                    "multi-value selection of a count state (no [index]) is not supported on device");
+            check_stack(pr);
             p.out_prog[i] = pr;
             p.out_kind[i] = k;
-            p.out_multi[i] = 0;
-            h_.out_names.push_back(oa.rename);
-            h_.out_types.push_back(k);
+        }
+        post_ = true;
+        for (size_t i = 0; i < sel.size(); ++i) {
+            if (!has_agg(sel[i].expr)) continue;
+            Prog pr;
+            pr.start = (int)h_.code.size();
+            p.out_kind[i] = expr(sel[i].expr, -1, 0, nullptr);
+            pr.len = (int)h_.code.size() - pr.start;
+            check_stack(pr);
+            p.out_post[i] = 1;
+            p.post_prog[i] = pr;
+        }
+        p.having = Prog{};
+        if (q_.having) {  // HAVING_STATE (SelectorParser.generateHavingExecutor: default chain index 0)
+            having_ = true;
+            Prog pr;
+            pr.start = (int)h_.code.size();
+            cond(q_.having, -1, 0);
+            pr.len = (int)h_.code.size() - pr.start;
+            check_stack(pr);
+            p.having = pr;
+            having_ = false;
+        }
+        post_ = false;
+        for (size_t i = 0; i < pending_.size(); ++i) {  // hidden emission columns
+            Prog pr;
+            pr.start = (int)h_.code.size();
+            bool multi = false;
+            const uint8_t k = expr(pending_[i].e, -1, pending_[i].defidx, &multi);
+            pr.len = (int)h_.code.size() - pr.start;
+            if (multi) throw CompileError(SDG_ERR_UNSUPPORTED, "multi-value operand of an aggregator / having");
+            check_stack(pr);
+            p.out_prog[pending_[i].col] = pr;
+            if (k != p.out_kind[pending_[i].col]) throw CompileError(SDG_ERR_ARG, "hidden column kind mismatch");
+        }
+        p.has_post = p.n_agg > 0 || p.having.len > 0;
+        for (size_t i = 0; i < sel.size(); ++i) {
+            h_.out_names.push_back(sel[i].rename);
+            h_.out_types.push_back(p.out_kind[i]);
         }
         for (int s = 0; s < p.n_states; ++s) {
             p.st[s] = rows_[s];
@@ -95,6 +155,10 @@ class QC {
         partition_keys();
         p.partitioned = q_.partition_index >= 0;
         detect_chain(root);
+        if (p.has_post) {  // the selector's post pass reads every record's key: the generic NFA writes it
+            p.chain = 0;
+            h_.chain_reason = "aggregators / having in the selector";
+        }
         runtime_tables(root.node);
         p.n_code = (int)h_.code.size();
         p.n_consts = (int)h_.consts.size();
@@ -282,9 +346,166 @@ class QC {
         return k;
     }
 
+    // ---- selector post pass ------------------------------------------------------------------------------
+    bool post_ = false, having_ = false;
+    std::vector<std::string> user_names_;
+    struct Pending {
+        sql::ExprP e;
+        int col, defidx;
+    };
+    std::vector<Pending> pending_;
+    static bool is_agg_name(const std::string& n) {
+        return n == "count" || n == "sum" || n == "avg" || n == "min" || n == "max" || n == "minForever" ||
+               n == "maxForever";
+    }
+    static bool has_agg(const sql::ExprP& e) {
+        if (e->kind == sql::ExprKind::FUNC && e->fn_ns.empty() && is_agg_name(e->fn_name)) return true;
+        for (auto& k : e->kids)
+            if (has_agg(k)) return true;
+        return false;
+    }
+    int new_col(uint8_t kind) {
+        Plan& p = h_.plan;
+        if (p.n_out >= MAX_OUT) throw CompileError(SDG_ERR_UNSUPPORTED, "too many output + hidden selector columns");
+        p.out_kind[p.n_out] = kind;
+        p.out_prog[p.n_out] = Prog{};
+        p.out_post[p.n_out] = 0;
+        p.out_multi[p.n_out] = 0;
+        return p.n_out++;
+    }
+    // the kind of an emission-scope expression, without keeping its code
+    uint8_t dry_kind(const sql::ExprP& e, int defidx) {
+        const size_t nc = h_.code.size(), nk = h_.consts.size();
+        const bool post = post_, hav = having_;
+        post_ = having_ = false;
+        const uint8_t k = expr(e, -1, defidx, nullptr);
+        post_ = post;
+        having_ = hav;
+        h_.code.resize(nc);
+        h_.consts.resize(nk);
+        return k;
+    }
+    // evaluation stack depth of a program (eval.h: STACK entries per lane)
+    void check_stack(const Prog& pr) {
+        int sp = 0, mx = 0;
+        for (int i = pr.start; i < pr.start + pr.len; ++i) {
+            const Instr& in = h_.code[i];
+            switch (in.op) {
+                case OP_LOAD: case OP_CONST: case OP_SLOTNULL: case OP_AGG: ++sp; break;
+                case OP_CMP: case OP_ARITH: case OP_AND: case OP_OR: --sp; break;
+                case OP_IFELSE: sp -= 2; break;
+                case OP_COALESCE: case OP_MAXMIN: sp -= in.a - 1; break;
+                default: break;
+            }
+            mx = std::max(mx, sp);
+        }
+        if (mx > STACK) throw CompileError(SDG_ERR_UNSUPPORTED, "expression too deep for the device evaluator");
+    }
+    // ExpressionParser.parseExpression AttributeFunction: core functions (executor/function/*.java), attribute
+    // aggregators in the selector / having scope (query/selector/attribute/aggregator/*.java)
+    uint8_t func(const sql::ExprP& e, int cur, int defidx) {
+        const std::string& n = e->fn_name;
+        auto bad = [&](const std::string& m) { return CompileError(SDG_ERR_VALIDATION, n + "(): " + m); };
+        if (!e->fn_ns.empty())
+            throw CompileError(SDG_ERR_UNSUPPORTED, "function '" + e->fn_ns + ":" + n + "' is not supported");
+        const size_t na = e->kids.size();
+        if (is_agg_name(n)) {
+            if (!post_) throw CompileError(SDG_ERR_VALIDATION, "aggregator " + n + "() outside the selector");
+            Plan& p = h_.plan;
+            if (p.n_agg >= MAX_AGG) throw CompileError(SDG_ERR_UNSUPPORTED, "too many aggregators");
+            AggSpec a;
+            std::memset(&a, 0, sizeof a);
+            a.arg_col = -1;
+            if (n == "count") {
+                if (na != 0) throw bad("takes no arguments");
+                a.kind = AG_COUNT;
+                a.out_kind = VK_I64;
+            } else {
+                if (na != 1) throw bad("takes one argument");
+                if (has_agg(e->kids[0])) throw bad("nested aggregators");
+                const uint8_t k = dry_kind(e->kids[0], defidx);
+                if (k > VK_F64) throw CompileError(SDG_ERR_UNSUPPORTED, n + "() needs a numeric argument");
+                a.arg_kind = k;
+                a.arg_col = new_col(k);
+                pending_.push_back({e->kids[0], a.arg_col, defidx});
+                if (n == "sum") a.kind = AG_SUM, a.out_kind = (k == VK_I32 || k == VK_I64) ? VK_I64 : VK_F64;
+                else if (n == "avg") a.kind = AG_AVG, a.out_kind = VK_F64;
+                else a.kind = (n == "min" || n == "minForever") ? AG_MIN : AG_MAX, a.out_kind = k;
+            }
+            a.out_col = -1;
+            emit(OP_AGG, a.out_kind, (uint8_t)p.n_agg);
+            p.agg[p.n_agg++] = a;
+            return a.out_kind;
+        }
+        if (n == "ifThenElse") {
+            if (na != 3) throw bad("required 3 arguments");
+            if (cond(e->kids[0], cur, defidx) != VK_BOOL) throw bad("the condition must be bool");
+            const uint8_t a = expr(e->kids[1], cur, defidx, nullptr), b = expr(e->kids[2], cur, defidx, nullptr);
+            if (a != b) throw bad("then / else types differ");
+            emit(OP_IFELSE, a);
+            return a;
+        }
+        if (n == "coalesce" || n == "default") {
+            if (na == 0 || na > STACK) throw bad("argument count");
+            if (n == "default" && (na != 2 || e->kids[1]->kind != sql::ExprKind::CONST))
+                throw bad("takes (attribute, constant default)");
+            uint8_t k0 = 0;
+            for (size_t i = 0; i < na; ++i) {
+                const uint8_t k = expr(e->kids[i], cur, defidx, nullptr);
+                if (i == 0) k0 = k;
+                else if (k != k0) throw bad("all parameters should be of the same type");
+            }
+            emit(OP_COALESCE, k0, (uint8_t)na);
+            return k0;
+        }
+        static const std::pair<const char*, uint8_t> inst[] = {
+            {"instanceOfBoolean", VK_BOOL}, {"instanceOfDouble", VK_F64}, {"instanceOfFloat", VK_F32},
+            {"instanceOfInteger", VK_I32},  {"instanceOfLong", VK_I64},   {"instanceOfString", VK_STR}};
+        for (auto& it : inst)
+            if (n == it.first) {  // data instanceof T: the static kind decides, then null-ness
+                if (na != 1) throw bad("required 1 argument");
+                const uint8_t k = expr(e->kids[0], cur, defidx, nullptr);
+                emit(OP_ISNULL, VK_BOOL);
+                if (k == it.second) {
+                    emit(OP_NOT, VK_BOOL);
+                } else {  // (x is null) and false
+                    emit(OP_CONST, VK_BOOL, 0, 0, 0, konst(0));
+                    emit(OP_AND, VK_BOOL);
+                }
+                return VK_BOOL;
+            }
+        if (n == "maximum" || n == "minimum") {
+            if (na == 0 || na > STACK) throw bad("argument count");
+            uint8_t k0 = 0;
+            for (size_t i = 0; i < na; ++i) {
+                const uint8_t k = expr(e->kids[i], cur, defidx, nullptr);
+                if (k > VK_F64) throw bad("numeric parameters required");
+                if (i == 0) k0 = k;
+                else if (k != k0) throw bad("all parameters should be of the same type");
+            }
+            emit(OP_MAXMIN, k0, (uint8_t)na, 0, n == "maximum" ? 1 : 0);
+            return k0;
+        }
+        throw CompileError(SDG_ERR_UNSUPPORTED, "function '" + n + "' is not supported in pattern queries");
+    }
+
     uint8_t expr(const sql::ExprP& e, int cur, int defidx, bool* multi_out) {
         using sql::ExprKind;
         if (multi_out) *multi_out = false;
+        if (post_ && (e->kind == ExprKind::VAR || e->kind == ExprKind::IS_NULL_STREAM)) {
+            Plan& p = h_.plan;
+            if (having_ && e->kind == ExprKind::VAR && e->stream_ref.empty())  // the output definition first
+                for (size_t j = 0; j < user_names_.size(); ++j)
+                    if (user_names_[j] == e->attr) {
+                        emit(OP_LOAD, p.out_kind[j], OUT_SLOT, (int32_t)j, 0);
+                        return p.out_kind[j];
+                    }
+            const uint8_t k = dry_kind(e, defidx);  // an input reference: a hidden emission column
+            const int col = new_col(k);
+            pending_.push_back({e, col, defidx});
+            emit(OP_LOAD, k, OUT_SLOT, col, 0);
+            return k;
+        }
         switch (e->kind) {
             case ExprKind::CONST: {
                 const auto& c = e->c;
@@ -303,11 +524,17 @@ class QC {
             }
             case ExprKind::VAR: return var(e, cur, defidx, multi_out);
             case ExprKind::AND:
-            case ExprKind::OR:
+            case ExprKind::OR: {
                 cond(e->kids[0], cur, defidx);
+                // post scope: short-circuit (a skipped operand's aggregators must not update); a relative jump,
+                // so a CVT the enclosing compare inserts before this code does not move its target
+                const size_t j = h_.code.size();
+                if (post_) emit(e->kind == ExprKind::AND ? OP_JAND : OP_JOR, VK_BOOL);
                 cond(e->kids[1], cur, defidx);
                 emit(e->kind == ExprKind::AND ? OP_AND : OP_OR, VK_BOOL);
+                if (post_) h_.code[j].imm = (int32_t)(h_.code.size() - j);
                 return VK_BOOL;
+            }
             case ExprKind::NOT:
                 cond(e->kids[0], cur, defidx);
                 emit(OP_NOT, VK_BOOL);
@@ -393,8 +620,9 @@ class QC {
                 emit(OP_SLOTNULL, VK_BOOL, (uint8_t)chain, 0, idx);
                 return VK_BOOL;
             }
+            case ExprKind::FUNC: return func(e, cur, defidx);
             default:
-                throw CompileError(SDG_ERR_UNSUPPORTED, "function '" + e->fn_name + "' is not supported in pattern queries");
+                throw CompileError(SDG_ERR_UNSUPPORTED, "expression kind not supported in pattern queries");
         }
     }
 

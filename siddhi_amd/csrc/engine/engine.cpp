@@ -162,7 +162,10 @@ struct QueryRt {
     // position (chain path) or an ordinal within the emitting event (generic NFA)
     int64_t emit_base = 0;
     bool sub_is_seq = false;
-    DevBuf ord_ws, g_ts, g_emit, g_vals, g_nulls;
+    DevBuf ord_ws, g_ts, g_emit, g_vals, g_nulls, g_key;
+    // the selector's post pass (aggregators / having): per-key aggregator state, persistent; staging
+    DevBuf agg_state, ps_key, ps_vals, ps_nulls, ps_pass, ps_ws;
+    int64_t agg_keys = 0;
     SchedSim::RankMap last_rank;
     std::vector<uint32_t> reordered;  // keys rerun with the scheduler's fire order (sorted)
     std::vector<uint32_t> taken;
@@ -1371,7 +1374,8 @@ void drain(sdg_engine* e, QueryRt& q) {
     q.polled = true;
     const int64_t n = q.out_n;
     if (n <= 0) return;
-    const int na = q.hq.plan.n_out;
+    const int na = q.hq.plan.n_out;  // every column of the records (hidden selector columns included)
+    const bool post = q.hq.plan.has_post;
     uint8_t* hb = (uint8_t*)q.h_rb.ensure((size_t)n * (28 + 8 * (size_t)na));
     int64_t* ts = (int64_t*)hb;
     int64_t* emit = ts + n;
@@ -1386,6 +1390,7 @@ void drain(sdg_engine* e, QueryRt& q) {
     const int64_t* src_vals = (const int64_t*)q.o_vals.p;
     int64_t vstride = q.out_cap;
     const void* src_nulls = q.o_nulls.p;
+    const void* src_key = q.o_key.p;
     const bool dev_order = !q.last_timers && n > 1;
     if (dev_order) {
         const size_t wb = order_workspace(n);
@@ -1404,6 +1409,11 @@ void drain(sdg_engine* e, QueryRt& q) {
             gather_u32((const uint32_t*)q.o_nulls.p, perm, n, gn, st);
             src_nulls = gn;
         }
+        if (post) {
+            uint32_t* gk = (uint32_t*)q.g_key.ensure((size_t)n * 4);
+            gather_u32((const uint32_t*)q.o_key.p, perm, n, gk, st);
+            src_key = gk;
+        }
         src_ts = gts;
         src_emit = gem;
         src_first = nullptr;
@@ -1412,9 +1422,11 @@ void drain(sdg_engine* e, QueryRt& q) {
     }
     std::vector<uint32_t> okey;
     std::vector<uint8_t> oround;
-    if (q.last_timers) {  // timer matches: drop the records of keys replayed on the host, order the fires
-        okey.resize(n);
-        HIPCHECK(hipMemcpyAsync(okey.data(), q.o_key.p, n * 4, hipMemcpyDeviceToHost, st));
+    if (q.last_timers || post) {  // keys: the aggregators' state, and for timer matches: drop the records of keys
+        okey.resize(n);            // replayed on the host, order the fires
+        HIPCHECK(hipMemcpyAsync(okey.data(), src_key, n * 4, hipMemcpyDeviceToHost, st));
+    }
+    if (q.last_timers) {
         if (!q.reordered.empty()) {  // and the first run's records of the keys rerun with the scheduler's order
             oround.resize(n);
             HIPCHECK(hipMemcpyAsync(oround.data(), q.o_round.p, n, hipMemcpyDeviceToHost, st));
@@ -1479,26 +1491,91 @@ void drain(sdg_engine* e, QueryRt& q) {
         std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
             return EM(x) != EM(y) ? EM(x) < EM(y) : FI(x) < FI(y);
         });
-    const size_t b = q.acc_ts.size();
-    q.acc_ts.resize(b + nk);
-    q.acc_seq.resize(b + nk);
-    q.acc_vals.resize(na);
-    q.acc_nulls.resize(na);
-    for (int j = 0; j < na; ++j) {
-        q.acc_vals[j].resize(b + nk);
-        q.acc_nulls[j].resize(b + nk);
+    // the selector's post pass on the device over the records in delivery order (aggregators per key, select items
+    // over them, having), then the user's columns of the records that pass join the backlog
+    std::vector<int64_t> fv;
+    std::vector<uint32_t> fn;
+    std::vector<uint8_t> fpass;
+    if (post && nk > 0) {
+        const Plan& P = q.hq.plan;
+        std::vector<uint32_t> fk(nk);
+        fv.resize((size_t)na * nk);
+        fn.resize(nk);
+        uint32_t kmax = 0;
+        for (int64_t i = 0; i < nk; ++i) {
+            const int64_t s = ord[i];
+            const bool dev = s < n;
+            fk[i] = dev ? okey[s] : hkey[s - n];
+            kmax = std::max(kmax, fk[i]);
+            fn[i] = dev ? nulls[s] : hnulls[s - n];
+            for (int j = 0; j < na; ++j) fv[(size_t)j * nk + i] = dev ? vals[(size_t)j * n + s] : hvals[(size_t)j * nh + (s - n)];
+        }
+        const int64_t K = (int64_t)kmax + 1;
+        const size_t per = (size_t)std::max(P.n_agg, 1) * 16;
+        if (K > q.agg_keys) {  // grow the per-key aggregator state, keeping the existing keys' states
+            const int64_t nkeys = std::max<int64_t>(K, q.agg_keys * 2);
+            void* nb = nullptr;
+            HIPCHECK(hipMalloc(&nb, (size_t)nkeys * per));
+            HIPCHECK(hipMemsetAsync(nb, 0, (size_t)nkeys * per, st));
+            if (q.agg_keys) HIPCHECK(hipMemcpyAsync(nb, q.agg_state.p, (size_t)q.agg_keys * per, hipMemcpyDeviceToDevice, st));
+            HIPCHECK(hipStreamSynchronize(st));
+            if (q.agg_state.p) HIPCHECK(hipFree(q.agg_state.p));
+            q.agg_state.p = nb;
+            q.agg_state.cap = (size_t)nkeys * per;
+            q.agg_keys = nkeys;
+        }
+        int kbits = 0;
+        while ((1ll << kbits) < K) ++kbits;
+        uint32_t* dk = (uint32_t*)q.ps_key.ensure((size_t)nk * 4);
+        int64_t* dv = (int64_t*)q.ps_vals.ensure((size_t)na * nk * 8);
+        uint32_t* dn = (uint32_t*)q.ps_nulls.ensure((size_t)nk * 4);
+        uint8_t* dp = (uint8_t*)q.ps_pass.ensure((size_t)nk);
+        HIPCHECK(hipMemcpyAsync(dk, fk.data(), (size_t)nk * 4, hipMemcpyHostToDevice, st));
+        HIPCHECK(hipMemcpyAsync(dv, fv.data(), (size_t)na * nk * 8, hipMemcpyHostToDevice, st));
+        HIPCHECK(hipMemcpyAsync(dn, fn.data(), (size_t)nk * 4, hipMemcpyHostToDevice, st));
+        SelPostArgs pa;
+        std::memset(&pa, 0, sizeof pa);
+        pa.plan = q.d_plan.as<Plan>();
+        pa.code = q.d_code.as<Instr>();
+        pa.consts = q.d_consts.as<int64_t>();
+        pa.n = nk;
+        pa.vals = dv;
+        pa.vstride = nk;
+        pa.nulls = dn;
+        pa.pass = dp;
+        pa.agg_state = (int64_t*)q.agg_state.p;
+        select_post(pa, q.hq.plan.partitioned ? dk : nullptr, kbits, q.ps_ws.ensure(select_post_workspace(nk)), st);
+        fpass.resize(nk);
+        HIPCHECK(hipMemcpyAsync(fv.data(), dv, (size_t)P.n_user_out * nk * 8, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(fn.data(), dn, (size_t)nk * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(fpass.data(), dp, (size_t)nk, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
     }
-    for (int64_t i = 0; i < nk; ++i) {
+    const int nu = q.hq.plan.n_user_out;
+    int64_t keep = nk;
+    if (post) keep = (int64_t)std::count(fpass.begin(), fpass.end(), (uint8_t)1);
+    const size_t b = q.acc_ts.size();
+    q.acc_ts.resize(b + keep);
+    q.acc_seq.resize(b + keep);
+    q.acc_vals.resize(nu);
+    q.acc_nulls.resize(nu);
+    for (int j = 0; j < nu; ++j) {
+        q.acc_vals[j].resize(b + keep);
+        q.acc_nulls[j].resize(b + keep);
+    }
+    for (int64_t i = 0, o = (int64_t)b; i < nk; ++i) {
+        if (post && !fpass[i]) continue;
         const int64_t s = ord[i];
         const bool dev = s < n;
         const int64_t hs = s - n;
-        q.acc_ts[b + i] = dev ? ts[s] : hts[hs];
-        q.acc_seq[b + i] = EM(s);
-        const uint32_t nm = dev ? nulls[s] : hnulls[hs];
-        for (int j = 0; j < na; ++j) {
-            q.acc_vals[j][b + i] = dev ? vals[(size_t)j * n + s] : hvals[(size_t)j * nh + hs];
-            q.acc_nulls[j][b + i] = (nm >> j) & 1u;
+        q.acc_ts[o] = dev ? ts[s] : hts[hs];
+        q.acc_seq[o] = EM(s);
+        const uint32_t nm = post ? fn[i] : dev ? nulls[s] : hnulls[hs];
+        for (int j = 0; j < nu; ++j) {
+            q.acc_vals[j][o] = post ? fv[(size_t)j * nk + i] : dev ? vals[(size_t)j * n + s] : hvals[(size_t)j * nh + hs];
+            q.acc_nulls[j][o] = (nm >> j) & 1u;
         }
+        ++o;
     }
     q.runs.clear();
 }
@@ -1821,7 +1898,7 @@ int sdg_poll(sdg_engine* e, int qi, sdg_out* out) {
     if (!e || qi < 0 || qi >= (int)e->qs.size() || !out) return fail(SDG_ERR_ARG, "bad poll arguments");
     return guarded([&]() {
         QueryRt& q = *e->qs[qi];
-        const int na = q.hq.plan.n_out;
+        const int na = q.hq.plan.n_user_out;
         if (!e->compile_only) drain(e, q);
         const int64_t n = (int64_t)q.acc_ts.size();
         q.h_ts.swap(q.acc_ts);
@@ -1875,12 +1952,13 @@ int sdg_export_device(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_
         if (e->compile_only) throw DeviceError("engine was compiled with SDG_COMPILE_ONLY");
         if (!q.acc_ts.empty()) throw CompileError(SDG_ERR_ARG, "earlier results are still queued on the host: sdg_poll first");
         if (q.last_timers) throw CompileError(SDG_ERR_UNSUPPORTED, "device export of timer (absent-state) matches");
+        if (q.hq.plan.has_post) throw CompileError(SDG_ERR_UNSUPPORTED, "device export of aggregated / having outputs");
         const int64_t n = q.polled ? 0 : q.out_n;
         *n_out = n;
         if (n > cap) throw CompileError(SDG_ERR_CAPACITY, "export buffers hold " + std::to_string(cap) + " of " +
                                                               std::to_string(n) + " records");
         hipStream_t st = e->stream;
-        const int na = q.hq.plan.n_out;
+        const int na = q.hq.plan.n_user_out;
         if (n > 0) {
             HIPCHECK(hipMemcpyAsync(d_ts, q.o_ts.p, n * 8, hipMemcpyDeviceToDevice, st));
             HIPCHECK(hipMemcpyAsync(d_seq, q.o_emit.p, n * 8, hipMemcpyDeviceToDevice, st));

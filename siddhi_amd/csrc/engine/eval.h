@@ -144,6 +144,7 @@ SDG_FN int64_t arith(uint8_t op, uint8_t k, int64_t a, int64_t b, bool* null) {
 // Acc must provide:
 //   void load(int slot, int col, int chain, uint8_t kind, int64_t* v, bool* null);
 //   bool slot_empty(int slot, int chain);
+//   void agg(int g, int64_t* v, bool* null);   (selector post pass; never reached elsewhere)
 // stk: this lane's LDS stack base, entries at stk[i * stride]
 template <class Acc>
 SDG_FN void run(const Instr* __restrict__ code, Prog p, const int64_t* __restrict__ consts,
@@ -224,6 +225,75 @@ SDG_FN void run(const Instr* __restrict__ code, Prog p, const int64_t* __restric
                 bool n = nulls & (1u << (sp - 1));
                 if (n) stk[(sp - 1) * stride] = 0;
                 nulls &= ~(1u << (sp - 1));
+                break;
+            }
+            case OP_IFELSE: {  // IfThenElseFunctionExecutor: Boolean.TRUE.equals(cond) ? then : else
+                const int b0 = sp - 3;
+                const bool c = !(nulls & (1u << b0)) && stk[b0 * stride] != 0;
+                const int pick = c ? b0 + 1 : b0 + 2;
+                const int64_t v = stk[pick * stride];
+                const bool n = nulls & (1u << pick);
+                stk[b0 * stride] = v;
+                nulls = (nulls & ~(7u << b0)) | (n ? 1u << b0 : 0u);
+                sp = b0 + 1;
+                break;
+            }
+            case OP_COALESCE: {  // the first non-null argument
+                const int na = in.a, b0 = sp - na;
+                int64_t v = 0;
+                bool n = true;
+                for (int i = 0; i < na && n; ++i)
+                    if (!(nulls & (1u << (b0 + i)))) {
+                        v = stk[(b0 + i) * stride];
+                        n = false;
+                    }
+                stk[b0 * stride] = v;
+                nulls = (nulls & ~(((1u << na) - 1u) << b0)) | (n ? 1u << b0 : 0u);
+                sp = b0 + 1;
+                break;
+            }
+            case OP_MAXMIN: {  // Maximum/MinimumFunctionExecutor.execute(Object[]) (one argument: returned as is)
+                const int na = in.a, b0 = sp - na;
+                if (na > 1) {
+                    const bool mx = in.c != 0;
+                    const double start = mx ? 4.9406564584124654e-324 : 1.7976931348623157e308;
+                    double best = start;
+                    for (int i = 0; i < na; ++i) {
+                        const int64_t r = stk[(b0 + i) * stride];
+                        double x = start;
+                        if (!(nulls & (1u << (b0 + i))))
+                            x = in.k == VK_I32 ? (double)(int32_t)r : in.k == VK_I64 ? (double)r
+                                : in.k == VK_F32 ? (double)bits_f32(r) : bits_f64(r);
+                        if (mx ? x > best : x < best) best = x;
+                    }
+                    int64_t v;
+                    if (in.k == VK_I32) v = best >= 2147483647.0 ? INT32_MAX : best <= -2147483648.0 ? INT32_MIN : (int64_t)(int32_t)best;
+                    else if (in.k == VK_I64) v = best >= 9223372036854775807.0 ? INT64_MAX : best <= -9223372036854775808.0 ? INT64_MIN : (int64_t)best;
+                    else if (in.k == VK_F32) v = f32_bits((float)best);
+                    else v = f64_bits(best);
+                    stk[b0 * stride] = v;
+                    nulls &= ~(((1u << na) - 1u) << b0);
+                    sp = b0 + 1;
+                }
+                break;
+            }
+            case OP_AGG: {
+                int64_t v;
+                bool n;
+                acc.agg(in.a, &v, &n);
+                stk[sp * stride] = v;
+                nulls = n ? (nulls | (1u << sp)) : (nulls & ~(1u << sp));
+                ++sp;
+                break;
+            }
+            case OP_JAND:
+            case OP_JOR: {
+                const bool t = !(nulls & (1u << (sp - 1))) && stk[(sp - 1) * stride] != 0;
+                if (t == (in.op == OP_JOR)) {
+                    stk[(sp - 1) * stride] = t;
+                    nulls &= ~(1u << (sp - 1));
+                    pc += in.imm - 1;
+                }
                 break;
             }
             default:

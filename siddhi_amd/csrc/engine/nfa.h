@@ -173,6 +173,7 @@ struct SEAccT {
     int16_t se;
     SDG_HD void load(int slot, int col, int chain, uint8_t kind, int64_t* v, bool* null);
     SDG_HD bool slot_empty(int slot, int chain);
+    SDG_HD void agg(int, int64_t* v, bool* n) { *v = 0; *n = true; }  // aggregators: the post pass only
 };
 
 // TM: the query has absent states (timer code compiled in); without them the kernel keeps its registers for
@@ -1077,7 +1078,10 @@ struct CtxT {
             if (!TM) break;
             if (P->st[p].kind == PK_ABSENT) absent_timer(p, t);
             else alogic_timer(p, t);
+            absent_gc();  // each TIMER event is its own getState / returnState scope (process() :150-227)
         }
+        // at a later clock the same fire would also pop the next queued time: the outcome holds below it only
+        if (q.n > 0 && tqt(sch)[q.h] - 1 < clk_hi) clk_hi = tqt(sch)[q.h] - 1;
         log_rec(LOG_FIRE_END, sch, 0, clk_hi);
         fsched = -1;
         absent_gc();

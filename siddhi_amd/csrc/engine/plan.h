@@ -26,7 +26,17 @@ enum OpCode : uint8_t {
     OP_ISNULL,     // pop 1 push bool
     OP_SLOTNULL,   // push bool: state slot a, chain index c is empty (IsNullStreamConditionExpressionExecutor)
     OP_COND,       // pop 1 push bool: null -> false (BoolConditionExpressionExecutor)
+    OP_IFELSE,     // pop 3 (cond, then, else) push: cond non-null and true ? then : else (IfThenElseFunctionExecutor)
+    OP_COALESCE,   // a = n: pop n push the first non-null one, else null (Coalesce / DefaultFunctionExecutor)
+    OP_MAXMIN,     // a = n, c = 1 maximum / 0 minimum, k = kind (Maximum / MinimumFunctionExecutor)
+    // selector post pass only (aggregators are stateful, so And/Or must short-circuit exactly as Java does):
+    OP_AGG,        // push aggregator a's value after this record (its state updates only when this runs)
+    OP_JAND,       // top not true: replace it by false and jump imm instructions ahead (past the right operand
+                   // and its OP_AND); else fall through (AndConditionExpressionExecutor :65-74)
+    OP_JOR,        // top true: replace it by true and jump imm ahead (OrConditionExpressionExecutor :65-76)
 };
+// OP_LOAD slot of the selector's post pass (aggregates, having): column b of the output record being selected
+constexpr uint8_t OUT_SLOT = 0xFF;
 enum CmpOp : uint8_t { CMP_EQ = 0, CMP_NE, CMP_GT, CMP_GE, CMP_LT, CMP_LE };
 enum ArithOp : uint8_t { AR_ADD = 0, AR_SUB, AR_MUL, AR_DIV, AR_MOD };
 
@@ -59,6 +69,19 @@ constexpr int MAX_STATES = 16;
 constexpr int MAX_OUT = 32;
 constexpr int MAX_COLS = 32;
 constexpr int STACK = 8;
+constexpr int MAX_AGG = 8;
+
+// attribute aggregators in a pattern query's selector (query/selector/attribute/aggregator/*), running per
+// partition key over the query's output records in delivery order (the selector's post pass)
+enum AggKind : uint8_t { AG_COUNT = 0, AG_SUM, AG_AVG, AG_MIN, AG_MAX };
+struct AggSpec {
+    uint8_t kind;       // AggKind
+    uint8_t arg_kind;   // kind of the argument column
+    uint8_t out_kind;   // result kind (count/sum of int,long: long; sum of float,double / avg: double; min/max: arg)
+    uint8_t pad;
+    int32_t arg_col;    // output-record column holding the argument (evaluated at emission), -1 for count()
+    int32_t out_col;    // unused (-1): the value is pushed by OP_AGG where the expression reads it
+};
 
 // processor kinds of the generic NFA (one per PreStateProcessor)
 enum ProcKind : uint8_t { PK_STREAM = 0, PK_COUNT = 1, PK_LOGICAL = 2, PK_ABSENT = 3 };
@@ -102,10 +125,18 @@ struct Plan {
     int64_t within_ms = 0;
     int32_t partitioned = 0;
     int32_t chain = 0;             // 1: the independent-partial fast path applies
-    int32_t n_out = 0;
+    int32_t n_out = 0;             // columns of an output record: the user's select list, then hidden columns
+                                   // (aggregator arguments and results, having operands)
+    int32_t n_user_out = 0;        // the select list (what sdg_poll returns)
     uint8_t out_kind[MAX_OUT];
-    Prog out_prog[MAX_OUT];
+    Prog out_prog[MAX_OUT];        // evaluated at emission (len 0: filled by the post pass)
     uint8_t out_multi[MAX_OUT];    // multi-value (count state, no index) -> unsupported on device for now
+    uint8_t out_post[MAX_OUT];     // 1: a select item over aggregates, evaluated by the post pass (post_prog)
+    Prog post_prog[MAX_OUT];
+    int32_t n_agg = 0;
+    AggSpec agg[MAX_AGG];
+    Prog having;                   // post pass; len 0: no having clause
+    int32_t has_post = 0;          // aggregates or having: the selector's post pass runs
     int32_t n_cols = 0;            // physical columns of this query's batch view
     uint8_t col_kind[MAX_COLS];
     int32_t n_streams = 0;         // streams this query reads, in receiver order

@@ -259,6 +259,7 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
     struct FN {
         nfa::TimerFire f;
         int32_t next;
+        uint32_t rank;  // the fire's rank among the fires of its position
     };
     std::vector<FN> fl;
     // keys: dense ids; the table covers every key with records, rows or a queued state
@@ -344,8 +345,8 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
             else if (L.type == nfa::LOG_POP) pop(L.sched, key);
         }
     };
-    auto add_fire = [&](KC& c, const nfa::TimerFire& f) {
-        fl.push_back(FN{f, -1});
+    auto add_fire = [&](KC& c, const nfa::TimerFire& f, uint32_t rk) {
+        fl.push_back(FN{f, -1, rk});
         const int32_t x = (int32_t)fl.size() - 1;
         if (c.ft >= 0) fl[c.ft].next = x;
         else c.fh = x;
@@ -360,6 +361,9 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
             if (skip_last && x == c.ft) break;
             c.run->rows_before(fl[x].f.g);
             c.run->fire(fl[x].f.sched, fl[x].f.g, fl[x].f.clock);
+            // the replay's records of this fire sit at the scheduler's position (a device fire accepted as
+            // shifted was ranked under the device's position)
+            out.rank.put(rank_key(fl[x].f.g, fl[x].f.sched, key), Slot{fl[x].f.g, fl[x].rank});
         }
         c.run->rows_before(g);
         c.run->lread = c.run->lcount;  // what the replay pushed / popped is in the model already
@@ -373,7 +377,7 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
         const uint32_t rk = rank++;
         ++out.n_fires;
         KC& c = K(key);
-        add_fire(c, nfa::TimerFire{g, sch, clock});
+        add_fire(c, nfa::TimerFire{g, sch, clock}, rk);
         if (c.mode != HOST) {
             const size_t f = next_fire(c);
             bool ok = f != NONE && logs[f].sched == sch && (int64_t)logs[f].g <= (int64_t)g;
@@ -393,6 +397,11 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
                     if (L.type == nfa::LOG_POP) pop(L.sched, key);
                     else if (L.type == nfa::LOG_PUSH) notify(L.sched, key, L.t);
                 }
+                // Scheduler.sendTimerEvents pops every queued time <= currentTime in this one fire. A device fire
+                // made at an earlier clock may have left some of them (only the optimistic pass accepts such a
+                // fire, c.reordered): without this the model would fire the key again at the next advance -- a
+                // fire the reference never makes, which the rerun would then execute
+                while (queued(sch, key) && head(sch, key) <= clock) pop(sch, key);
                 if (logs[f].g != g) ++out.n_shifted;
                 out.rank.put(rank_key(logs[f].g, sch, key), Slot{g, rk});
                 c.i = end + 1;

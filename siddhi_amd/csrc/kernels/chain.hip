@@ -76,6 +76,7 @@ struct ChainAcc {
         *v = col_row(*A, V, col, kind, row);
         *null = null_row(*A, col, row);
     }
+    __device__ void agg(int, int64_t* v, bool* n) { *v = 0; *n = true; }  // aggregators: the post pass only
     __device__ bool slot_empty(int slot, int chain) {
         if (!(chain == 0 || chain == -1)) return true;
         if (slot == 0) return !(c0 >= 0 || r0 >= 0);

@@ -253,4 +253,22 @@ void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t e
 void gather_i64(const int64_t* src, const uint32_t* perm, int64_t n, int64_t* dst, hipStream_t stream);
 void gather_u32(const uint32_t* src, const uint32_t* perm, int64_t n, uint32_t* dst, hipStream_t stream);
 
+// the selector's post pass (order.hip): aggregators per key in delivery order, select items over them, having
+struct SelPostArgs {
+    const Plan* plan;                 // device copy
+    const Instr* code;
+    const int64_t* consts;
+    int64_t n;                        // records, in delivery order
+    int64_t* vals;                    // [n_out][vstride]: emission columns in, aggregate / post columns out
+    int64_t vstride;
+    uint32_t* nulls;                  // [n] null bits (updated)
+    uint8_t* pass;                    // [n] having result
+    int64_t* agg_state;               // [K][n_agg][2], persistent per partition key
+    const uint32_t* perm;             // set by select_post
+    const uint32_t* key_sorted;
+};
+size_t select_post_workspace(int64_t n);
+// key: [n] partition key ids < 2^kbits (nullptr / kbits 0: unpartitioned, one run)
+void select_post(SelPostArgs a, const uint32_t* key, int kbits, void* work, hipStream_t stream);
+
 }  // namespace sdg

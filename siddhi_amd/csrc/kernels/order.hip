@@ -9,6 +9,7 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 
+#include "../engine/eval.h"
 #include "kernels.h"
 
 namespace sdg {
@@ -80,6 +81,161 @@ void gather_i64(const int64_t* src, const uint32_t* perm, int64_t n, int64_t* ds
 }
 void gather_u32(const uint32_t* src, const uint32_t* perm, int64_t n, uint32_t* dst, hipStream_t stream) {
     if (n > 0) hipLaunchKernelGGL(gather_k<uint32_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, src, perm, n, dst);
+}
+
+// ---- the selector's post pass (QuerySelector.processNoGroupBy :161-205 for aggregators and having) ------------
+// Records arrive in delivery order. Attribute aggregators keep their state per partition key and see that key's
+// records in delivery order, so the records are stably sorted by key (a record index, rocPRIM) and one lane walks
+// each key's run sequentially -- float sums must add in the reference's order to be bit-exact. Per record: the
+// aggregators (arguments were evaluated at emission into hidden columns), then the select items over them, then
+// the having condition.
+namespace {
+
+__device__ __forceinline__ double as_f64(int64_t v, uint8_t k) {
+    return k == VK_I32 ? (double)(int32_t)v : k == VK_I64 ? (double)v : k == VK_F32 ? (double)bits_f32(v) : bits_f64(v);
+}
+
+// state per (key, aggregator): {count, value}; value = long sum | double sum bits | min/max payload
+__device__ __forceinline__ void agg_step(const AggSpec& g, int64_t* st, int64_t arg, bool arg_null, int64_t* out,
+                                         bool* out_null) {
+    int64_t& cnt = st[0];
+    int64_t& v = st[1];
+    switch (g.kind) {
+        case AG_COUNT:  // CountAttributeAggregatorExecutor.processAdd
+            ++cnt;
+            *out = cnt;
+            *out_null = false;
+            return;
+        case AG_SUM:  // SumAttributeAggregatorExecutor: Int -> Long state, Float -> Double state; null -> currentValue
+            if (!arg_null) {
+                if (g.out_kind == VK_I64) v = (int64_t)((uint64_t)v + (uint64_t)(g.arg_kind == VK_I32 ? (int64_t)(int32_t)arg : arg));
+                else v = f64_bits(bits_f64(v) + as_f64(arg, g.arg_kind));
+                ++cnt;
+            }
+            *out = v;
+            *out_null = cnt == 0;
+            return;
+        case AG_AVG: {  // AvgAttributeAggregatorExecutor: double value / long count
+            if (!arg_null) {
+                ++cnt;
+                v = f64_bits(bits_f64(v) + as_f64(arg, g.arg_kind));
+            }
+            *out = f64_bits(bits_f64(v) / (double)cnt);
+            *out_null = cnt == 0;
+            return;
+        }
+        default: {  // Min/MaxAttributeAggregatorExecutor: minValue == null || minValue > value
+            if (!arg_null) {
+                bool take = cnt == 0;
+                if (!take) {
+                    const bool mn = g.kind == AG_MIN;
+                    switch (g.arg_kind) {
+                        case VK_I32: take = mn ? (int32_t)v > (int32_t)arg : (int32_t)v < (int32_t)arg; break;
+                        case VK_I64: take = mn ? v > arg : v < arg; break;
+                        case VK_F32: take = mn ? bits_f32(v) > bits_f32(arg) : bits_f32(v) < bits_f32(arg); break;
+                        default: take = mn ? bits_f64(v) > bits_f64(arg) : bits_f64(v) < bits_f64(arg); break;
+                    }
+                }
+                if (take) {
+                    v = arg;
+                    cnt = 1;
+                }
+            }
+            *out = v;
+            *out_null = cnt == 0;
+            return;
+        }
+    }
+}
+
+// the post pass's view of one record: its columns, and its key's aggregator states
+struct PostAcc {
+    const Plan* P;
+    const int64_t* vals;
+    int64_t vstride;
+    int64_t i;
+    uint32_t nm;
+    int64_t* st;
+    __device__ void load(int, int col, int, uint8_t, int64_t* v, bool* null) {
+        *v = vals[(int64_t)col * vstride + i];
+        *null = (nm >> col) & 1u;
+    }
+    __device__ bool slot_empty(int, int) { return false; }
+    __device__ void agg(int g, int64_t* v, bool* n) {
+        const AggSpec& s = P->agg[g];
+        int64_t arg = 0;
+        bool an = true;
+        if (s.arg_col >= 0) {
+            arg = vals[(int64_t)s.arg_col * vstride + i];
+            an = (nm >> s.arg_col) & 1u;
+        }
+        agg_step(s, st + 2 * g, arg, an, v, n);
+    }
+};
+
+__global__ __launch_bounds__(256) void sel_post_k(SelPostArgs a) {
+    __shared__ int64_t stk_mem[STACK * 256];
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= a.n) return;
+    const uint32_t k = a.key_sorted ? a.key_sorted[p] : 0u;
+    if (p > 0 && a.key_sorted && a.key_sorted[p - 1] == k) return;  // not the head of its key's run
+    if (p > 0 && !a.key_sorted) return;                               // one run: lane 0
+    const Plan* P = a.plan;
+    const int na = P->n_agg;
+    int64_t* st = a.agg_state + (int64_t)k * na * 2;
+    int64_t* stk = stk_mem + threadIdx.x;
+    for (int64_t q = p; q < a.n && (!a.key_sorted || a.key_sorted[q] == k); ++q) {
+        const int64_t i = a.perm ? (int64_t)a.perm[q] : q;
+        const uint32_t nm0 = a.nulls[i];
+        PostAcc acc{P, a.vals, a.vstride, i, nm0, st};
+        for (int j = 0; j < P->n_user_out; ++j) {  // select items over aggregators, in order, then having
+            if (!P->out_post[j]) continue;
+            int64_t v;
+            bool nl;
+            run(a.code, P->post_prog[j], a.consts, acc, stk, 256, &v, &nl);
+            a.vals[(int64_t)j * a.vstride + i] = v;
+            acc.nm = nl ? (acc.nm | (1u << j)) : (acc.nm & ~(1u << j));
+        }
+        a.nulls[i] = acc.nm;
+        a.pass[i] = P->having.len == 0 ? 1 : (uint8_t)pass(a.code, P->having, a.consts, acc, stk, 256);
+    }
+}
+
+__global__ __launch_bounds__(256) void iota_k(uint32_t* __restrict__ x, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) x[i] = (uint32_t)i;
+}
+
+}  // namespace
+
+size_t select_post_workspace(int64_t n) {
+    size_t t = 0;
+    uint32_t* k = nullptr;
+    rocprim::radix_sort_pairs(nullptr, t, k, k, k, k, (size_t)n, 0, 32);
+    return ((t + 255) & ~size_t(255)) + (size_t)n * 12 + 1024;
+}
+
+void select_post(SelPostArgs a, const uint32_t* key, int kbits, void* work, hipStream_t stream) {
+    if (a.n <= 0) return;
+    const unsigned grid = (unsigned)((a.n + 255) / 256);
+    a.perm = nullptr;
+    a.key_sorted = nullptr;
+    if (key && kbits > 0) {  // stable sort of the record index by key: each key's records stay in delivery order
+        size_t t = 0;
+        uint32_t* kk = nullptr;
+        rocprim::radix_sort_pairs(nullptr, t, kk, kk, kk, kk, (size_t)a.n, 0, kbits);
+        uint8_t* p = (uint8_t*)work;
+        void* tmp = p;
+        p += (t + 255) & ~size_t(255);
+        uint32_t* ks = (uint32_t*)p; p += (size_t)a.n * 4;
+        uint32_t* ix0 = (uint32_t*)p; p += (size_t)a.n * 4;
+        uint32_t* ix1 = (uint32_t*)p;
+        hipLaunchKernelGGL(iota_k, dim3(grid), dim3(256), 0, stream, ix0, a.n);
+        rocprim::radix_sort_pairs(tmp, t, key, ks, ix0, ix1, (size_t)a.n, 0, kbits, stream);
+        a.perm = ix1;
+        a.key_sorted = ks;
+    }
+    hipLaunchKernelGGL(sel_post_k, dim3(a.key_sorted ? grid : 1u), dim3(256), 0, stream, a);
 }
 
 }  // namespace sdg

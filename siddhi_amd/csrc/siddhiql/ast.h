@@ -66,7 +66,7 @@ enum class ExprKind : uint8_t {
     ADD, SUB, MUL, DIV, MOD,
     IS_NULL,      // <expr> is null
     IS_NULL_STREAM,  // e1 is null / e1[2] is null
-    FUNC,         // function call (rejected by the lowering for now)
+    FUNC,         // function call: ifThenElse / coalesce / default / instanceOf* / maximum / minimum, aggregators
 };
 enum class CmpOp : uint8_t { EQ, NE, GT, GE, LT, LE };
 
@@ -127,6 +127,7 @@ struct Query {
     int64_t within_ms = 0;
     bool select_all = false;
     std::vector<OutputAttribute> select;
+    ExprP having;               // `having <expr>` (QuerySelector.havingConditionExecutor) or null
     std::string target;         // insert into <target>
     bool target_inner = false;
     OutputEventType out_type = OutputEventType::CURRENT;

@@ -370,8 +370,13 @@ class Parser {
                     break;
                 }
             }
-            if (kw("group") || kw("having") || kw("order") || kw("limit") || kw("offset"))
-                throw Unsupported("group by / having / order by / limit are out of scope on the pattern path");
+            if (kw("group")) throw Unsupported("group by is out of scope on the pattern path");
+            if (kw("having")) {
+                ++p_;
+                q.having = parse_expr();
+            }
+            if (kw("order") || kw("limit") || kw("offset"))
+                throw Unsupported("order by / limit / offset are out of scope on the pattern path");
         } else {
             q.select_all = true;
         }

@@ -401,6 +401,8 @@ void* emu_create(const char* text, int max_partials) {
             auto q = std::make_unique<EmuQuery>();
             q->hq = std::move(h);
             const Plan& P = q->hq.plan;
+            if (P.has_post)  // the selector's post pass runs on the device only (order.hip select_post)
+                throw std::runtime_error("selector post pass (aggregators / having) is device-only");
             q->L = nfa::make_layout(P.n_states, std::max(P.n_cols, 1), e->ns, P.n_sched);
             q->sim.setup(P.n_sched, P.partitioned, !e->app.playback);
             e->qs.push_back(std::move(q));

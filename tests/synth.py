@@ -120,3 +120,50 @@ def nan_trace(n, keys=4, seed=0, nan_rate=0.05, null_rate=0.05):
             price = None
         out.append(("S", int(ts[i]), [i, "k%d" % rng.integers(0, keys), price, int(rng.integers(0, 100))]))
     return out
+
+
+# ---- the selector: functions, attribute aggregators per partition key, having, select * ----
+SELECT_APPS = {
+    "agg_all": part("@info(name='q') from every e1=S[price>30] -> e2=T[price>e1.price] select e1.id as a, "
+                    "count() as n, sum(e2.volume) as sv, sum(e2.price) as sp, avg(e1.price) as ap, "
+                    "min(e2.price) as mn, max(e1.volume) as mx, minForever(e2.volume) as mf insert into O;"),
+    "agg_expr": part("@info(name='q') from every e1=S[price>30] -> e2=T[price>e1.price] select e2.id as b, "
+                     "sum(e2.price) / count() as mean, count() + 1 as n1, maxForever(e1.price) - min(e2.price) as r "
+                     "insert into O;"),
+    "agg_flat": flat("@info(name='q') from every e1=S[price>20] -> e2=T[price>e1.price] select count() as n, "
+                     "avg(e2.price) as a, sum(e1.volume) as s insert into O;"),
+    "having_count": part("@info(name='q') from every e1=S[price>20] -> e2=T[price>e1.price] "
+                         "select e1.id as a, e2.id as b, count() as n having n % 3 == 0 insert into O;"),
+    "having_inputs": part("@info(name='q') from every e1=S[price>20]<1:3> -> e2=T[price>e1[0].price] "
+                          "select e1[0].id as a, e2.id as b having instanceOfDouble(e1[1].price) and "
+                          "not (e1[2] is null) and e2.volume > 10 insert into O;"),
+    "having_agg": part("@info(name='q') from every e1=S[price>40] -> e2=T[price>e1.price] "
+                       "select e1.id as a, e2.price as p having avg(e2.price) > 70.0 or count() < 3 insert into O;"),
+    "functions": part("@info(name='q') from every e1=S[price>20] -> e2=T[price>e1.price] "
+                      "select ifThenElse(e2.volume > 50, e1.id, e2.id) as a, coalesce(e1.price, e2.price) as b, "
+                      "maximum(e1.price, e2.price, 55.0) as c, minimum(e1.volume, e2.volume) as d, "
+                      "instanceOfLong(e1.id) as e, default(e2.price, -1.0) as f, instanceOfString(e1.price) as g "
+                      "insert into O;"),
+    "select_star": part("@info(name='q') from every e1=S[price>90] select * insert into O;"),
+    "agg_absent": part("@info(name='q') from every e1=S[price>60] -> not T[price>e1.price] for 20 milliseconds "
+                       "select e1.id as a, count() as n, max(e1.price) as m insert into O;"),
+}
+
+
+# ---- absent states under heavy timer collisions (few keys, many equal due times): the scheduler's
+# TreeMultimap collapse, multi-pop fires and destroyed-state re-arms (Scheduler.java:71-127,
+# AbsentStreamPreStateProcessor.process :150-227) ----
+ABSENT_APPS = {
+    "absent_every_20": part("@info(name='q') from every e1=S[price>60] -> not T[price>e1.price] for 20 milliseconds "
+                            "select e1.id as a, e1.key as k insert into O;"),
+    "absent_every_7": part("@info(name='q') from every e1=S[price>60] -> not T[price>e1.price] for 7 milliseconds "
+                           "select e1.id as a, e1.key as k insert into O;"),
+    "absent_once": part("@info(name='q') from e1=S[price>30] -> not T[price>e1.price] for 15 milliseconds "
+                        "select e1.id as a, e1.key as k insert into O;"),
+    "absent_start": part("@info(name='q') from every not S[price>90] for 10 milliseconds -> e2=T[price>50] "
+                         "select e2.id as a insert into O;"),
+    "absent_and": part("@info(name='q') from every e1=S[price>50] -> (not T[price>e1.price] for 12 milliseconds "
+                       "and e3=S[price>80]) select e1.id as a, e3.id as b insert into O;"),
+    "absent_mid": part("@info(name='q') from every e1=S[price>50] -> not T[price>e1.price] for 9 milliseconds -> "
+                       "e3=S[price>e1.price] select e1.id as a, e3.id as b insert into O;"),
+}

@@ -4,6 +4,7 @@ due time, so Scheduler.onTimeChange's TreeMultimap collapse (one key per due tim
 HashMap order) delays fires and the per-key fixpoint has to reproduce it. The GPU run of the same trace is
 test_gpu_parity.py::test_c4_vs_oracle."""
 import numpy as np
+import pytest
 
 from siddhi_amd import workloads as w
 
@@ -68,3 +69,28 @@ def test_c4_host_nfa_matches_oracle(oracle_built, emu_built):
     assert len(ots) > 1000 and not onulls.any()
     gts, gvals = emu_c4(c, end, batches=3)
     assert np.array_equal(gts, ots) and np.array_equal(gvals, ovals)
+
+
+# ---- timer collisions on few keys: the host build of the device path (nfa.h + the scheduler simulation) ----
+import synth as _synth  # noqa: E402
+
+
+@pytest.mark.parametrize("name", sorted(_synth.ABSENT_APPS))
+@pytest.mark.parametrize("seed", [100, 102, 104, 106])
+def test_absent_collisions_host(name, seed, oracle_built, emu_built):
+    from emu_rt import EmuAdapter
+    from oracle_rt import Oracle
+    app = _synth.ABSENT_APPS[name]
+    tr = _synth.trace(3000, keys=6, seed=seed, null_rate=0.05)
+    o = Oracle(app)
+    try:
+        ref = _synth.run(o, tr)
+    finally:
+        o.close()
+    for batches in (1, 3):
+        e = EmuAdapter(app)
+        try:
+            got = _synth.run(e, tr, batches)
+        finally:
+            e.close()
+        assert got == ref, (name, seed, batches)

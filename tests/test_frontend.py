@@ -61,3 +61,33 @@ def test_push_needs_a_device():
     rt = compile_only(w.C1_APP)
     with pytest.raises(sa.DeviceError):
         rt.flush()
+
+
+# ---- the selector: every synthetic selector app compiles for the device and runs in the oracle
+import synth as _synth  # noqa: E402
+
+
+@pytest.mark.parametrize("name", sorted(_synth.SELECT_APPS))
+def test_selector_apps_compile_and_run_in_oracle(name, oracle_built):
+    from oracle_rt import Oracle
+    app = _synth.SELECT_APPS[name]
+    sa.SiddhiAppRuntime(app, compile_only=True)
+    o = Oracle(app)
+    try:
+        rows = _synth.run(o, _synth.trace(800, keys=3, seed=1, null_rate=0.05))
+    finally:
+        o.close()
+    assert rows, name
+
+
+@pytest.mark.parametrize("sel,err", [
+    ("count(e1.price) as n", "count"),            # count() takes no arguments
+    ("ifThenElse(e1.price, 1, 2) as x", "bool"),  # condition must be bool
+    ("coalesce(e1.price, e1.id) as x", "same type"),
+    ("sum(e1.key) as x", "numeric"),
+])
+def test_selector_validation_errors(sel, err):
+    app = _synth.part("@info(name='q') from every e1=S[price>30] -> e2=T[price>e1.price] select %s insert into O;" % sel)
+    with pytest.raises(Exception) as ei:
+        sa.SiddhiAppRuntime(app, compile_only=True)
+    assert err in str(ei.value)
