@@ -7,8 +7,9 @@
  *                           (modules/siddhi-core/src/main/java/io/siddhi/core/SiddhiManager.java:93-96)
  *   sdg_stream_index /   <- SiddhiAppRuntime.getInputHandler(String) + the stream definition
  *   sdg_stream_schema       (core/SiddhiAppRuntimeImpl.java:414)
- *   sdg_push             <- InputHandler.send(long, Object[]) / send(Event[]) for one stream, columnar
- *                           (core/stream/input/InputHandler.java:59-95); events keep their call order
+ *   sdg_push             <- InputHandler.send(long, Object[]) for one stream, columnar, one call per row
+ *                           (core/stream/input/InputHandler.java:59-70); events keep their call order
+ *   sdg_push_events      <- InputHandler.send(Event[]) (:85-95: the clock moves to the last event first)
  *   sdg_push_device      <- the same for event columns already resident in HBM (device pointers)
  *   sdg_advance_time     <- TimestampGeneratorImpl.setCurrentTimestamp (playback clock, util/timestamp/
  *                           TimestampGeneratorImpl.java:105-122) / the wall clock of a live app
@@ -18,6 +19,8 @@
  *   sdg_poll             <- QueryCallback.receive(long, Event[], Event[]) / StreamCallback.receive(Event[])
  *                           (core/query/output/callback/QueryCallback.java:60-105,
  *                            core/stream/output/StreamCallback.java:93-129), columnar
+ *   sdg_snapshot /       <- SiddhiAppRuntime.snapshot() / restore(byte[]), persist() / restoreRevision()
+ *   sdg_restore             (core/SiddhiAppRuntimeImpl.java:677-737)
  *   sdg_destroy          <- SiddhiAppRuntime.shutdown()
  *
  * Conventions (mirroring the reference): compile errors are returned as status codes with a thread-local
@@ -97,6 +100,11 @@ const char* sdg_string(sdg_engine* e, uint32_t id);
 /* columnar host batch for ONE stream: ts[n], cols[a] (typed as above), nulls[a] may be NULL */
 int sdg_push(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const void* const* cols,
              const uint8_t* const* nulls);
+/* InputHandler.send(Event[]) (core/stream/input/InputHandler.java:85-95): the same columns as sdg_push, but a
+ * playback app's clock first moves to the LAST event's timestamp (absent-state timers due by then fire before the
+ * first event) and the events themselves do not move it; sdg_push is a sequence of send(long, Object[]) calls */
+int sdg_push_events(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const void* const* cols,
+                    const uint8_t* const* nulls);
 /* rows of several streams in one interleaved batch (InputHandler.send calls of different streams, in order):
  * row i belongs to stream streams[i]; attribute a of that row is slots[a][i] as a 64-bit slot (INT/LONG the value,
  * FLOAT/DOUBLE the bit pattern in the low bits, BOOL 0/1, STRING an sdg_intern id); nulls[a] optional */
@@ -126,6 +134,13 @@ int sdg_discard(sdg_engine* e);
  * states (their timer matches are ordered on the host). */
 int sdg_export_device(sdg_engine* e, int query, int64_t cap, int64_t* n_out, int64_t* d_ts, int64_t* d_seq,
                       int64_t* d_sub, int64_t* d_vals);
+
+/* SiddhiAppRuntime.snapshot() / restore(byte[]) (core/SiddhiAppRuntimeImpl.java:677-737): every partial match,
+ * carried partial, timer queue, aggregator and key dictionary of the engine, after flushing what was pushed. The
+ * bytes stay valid until the next sdg_snapshot / sdg_destroy. sdg_restore takes a snapshot of an engine compiled
+ * from the same app text (else SDG_ERR_ARG, CannotRestoreSiddhiAppStateException) and nothing pending. */
+int sdg_snapshot(sdg_engine* e, const uint8_t** data, int64_t* len);
+int sdg_restore(sdg_engine* e, const uint8_t* data, int64_t len);
 
 /* introspection for measurement: device time of the last flush per kernel family, algorithmic bytes,
  * match count, and which kernel path each query took (0 = chain, 1 = generic). */

@@ -1286,6 +1286,15 @@ struct Scheduler {
         if (!s->queue.empty()) heads.insert(s->queue.front());
     }
     void sendTimerEvents(const SSP& s);
+    void purgeKey(const std::string& k) {  // partition purge: the key's SchedulerState is destroyed
+        SSP found;
+        map.for_each([&](const std::string& kk, SSP& st) {
+            if (kk == k) found = st;
+        });
+        if (!found) return;
+        if (!found->queue.empty()) heads.erase(heads.find(found->queue.front()));
+        map.remove(k);
+    }
     void onTimeChange(int64_t now);  // playback TimeChangeListener
     bool nextDue(int64_t upto, int64_t& t, SSP& st);  // live mode
 };
@@ -1635,6 +1644,8 @@ struct QueryRt {
     std::vector<std::vector<StEv>> pendingOut;
     bool buffering = false;
     void sendToCallBacks(std::vector<StEv>& evs);
+    std::vector<AggExec*> aggs;            // the selector's aggregators (partition purge cleans their key states)
+    void purgeKey(const std::string& key);
 };
 
 // InnerStateRuntime tree (query/input/stream/state/runtime/*.java)
@@ -1760,7 +1771,10 @@ void Receiver::receive(const SEv& in) {
 struct PartitionRt {
     int index = 0;
     std::vector<int> queries;
-    std::unordered_map<std::string, bool> keys;  // PartitionState.partitionKeys
+    std::unordered_map<std::string, int64_t> keys;  // PartitionState.partitionKeys: key -> currentTime at its last event
+    bool purge = false;
+    int64_t purge_interval = 0, purge_idle = 0;
+    int64_t first_init = INT64_MIN;                 // currentTime of the partition's first initPartition
     struct With {
         int stream;
         ExecP expr;
@@ -1793,6 +1807,13 @@ struct AppRt {
     void emitStreamOutput(const std::string& streamId, int64_t ts, bool expired, const std::vector<Val>& vals,
                           const std::vector<std::shared_ptr<std::vector<Val>>>& lists);
 };
+
+void QueryRt::purgeKey(const std::string& key) {  // cleanGroupByStates of every StateHolder of the query
+    for (PreProc* p : allPre) p->holder.map.erase(key);
+    for (Scheduler* s : app->eng.schedulers)
+        if (std::find(allPre.begin(), allPre.end(), s->target) != allPre.end()) s->purgeKey(key);
+    for (AggExec* a : aggs) a->states.erase(key);
+}
 
 void QueryRt::sendToCallBacks(std::vector<StEv>& evs) {
     // OutputRateLimiter.sendToCallBacks :64-108 -> QueryCallback.receiveStreamEvent, InsertIntoStreamCallback
@@ -2191,6 +2212,7 @@ struct Builder {
                 x->k = p.second;
                 x->ctx = &rt.eng.ctx;
                 x->partitioned = partitioned;
+                q.aggs.push_back(x.get());
                 if (x->k == AggExec::COUNT) {
                     if (!args.empty()) throw bad("takes no arguments");
                     x->rt = Type::LONG;
@@ -2597,10 +2619,27 @@ void AppRt::deliverStream(int stream, const SEv& ev) {
                 Ctx saved = eng.ctx;
                 eng.ctx.has_key = true;
                 eng.ctx.key = key;
+                const int64_t now = eng.currentTime();
+                if (p->purge) {
+                    // @purge (PartitionRuntimeImpl.initPartition :368-401): a task every `interval` ms destroys the
+                    // states of keys idle for more than idle.period (by currentTime). The reference runs it on a
+                    // scheduled executor in wall-clock time -- and registers one more such task on every
+                    // initPartition call, so passes are near-continuous once the first interval has elapsed.
+                    // Modelling assumption: a pass at every clock reading from first_init + interval on; a key's
+                    // state is destroyed before its next event when that event's clock exceeds its last activity
+                    // by idle.period (equivalent for every key with no pending timer).
+                    auto it = p->keys.find(key);
+                    if (it != p->keys.end() && p->first_init != INT64_MIN && now >= p->first_init + p->purge_interval &&
+                        it->second + p->purge_idle < now) {
+                        p->keys.erase(it);
+                        for (int qi : p->queries) queries[qi]->purgeKey(key);
+                    }
+                }
                 if (!p->keys.count(key)) {  // PartitionRuntimeImpl.initPartition
                     for (int qi : p->queries) queries[qi]->initPartition();
-                    p->keys[key] = true;
+                    if (p->first_init == INT64_MIN) p->first_init = now;
                 }
+                p->keys[key] = now;
                 auto it = innerSubs.find({p->index, stream});
                 if (it != innerSubs.end())
                     for (Receiver* r : it->second) r->receive(ev);
@@ -2634,6 +2673,9 @@ static void build_app(orc_engine* e, const char* text) {
         p->index = (int)pi;
         rt.partitions.emplace_back(p);
         p->queries = rt.app.partitions[pi].queries;
+        p->purge = rt.app.partitions[pi].purge;
+        p->purge_interval = rt.app.partitions[pi].purge_interval_ms;
+        p->purge_idle = rt.app.partitions[pi].purge_idle_ms;
     }
     for (size_t qi = 0; qi < rt.app.queries.size(); ++qi) {
         const sql::Query& qa = rt.app.queries[qi];
@@ -2790,7 +2832,9 @@ static void advance(orc_engine* e, int64_t ts) {
     }
 }
 
-// mode 0: InputHandler.send(ts, data); mode 1: InputHandler.send(data) (timestamp = currentTime()).
+// mode 0: InputHandler.send(ts, data); mode 1: InputHandler.send(data) (timestamp = currentTime()); mode 2: one
+// event of an InputHandler.send(Event[]) (:85-95): the caller moved the clock once for the array (orc_advance_time
+// to the last event's timestamp), the event itself does not move it.
 // now: the modelled wall clock (live mode); ignored in playback.
 static void send_one(orc_engine* e, int stream, int64_t ts, int64_t now, int mode, const int64_t* slots,
                      const uint8_t* nulls) {
@@ -2799,9 +2843,9 @@ static void send_one(orc_engine* e, int stream, int64_t ts, int64_t now, int mod
     start_app(e, g.playback ? ts : now);
     if (g.playback) {
         if (mode == 0) advance(e, ts);
-        else ts = g.currentTime();
+        else if (mode == 1) ts = g.currentTime();
     } else {
-        advance(e, now);
+        if (mode != 2) advance(e, now);
         if (mode == 1) ts = now;
     }
     const auto& def = rt.app.streams[stream];

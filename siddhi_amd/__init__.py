@@ -124,6 +124,7 @@ def load_library():
     L.sdg_string.restype = ctypes.c_char_p
     L.sdg_string.argtypes = [P, U32]
     L.sdg_push.argtypes = [P, I32, I64, P, P, P]
+    L.sdg_push_events.argtypes = [P, I32, I64, P, P, P]
     L.sdg_push_device.argtypes = [P, I32, I64, P, P, P]
     L.sdg_push_mixed.argtypes = [P, I64, P, P, I32, P, P]
     L.sdg_advance_time.argtypes = [P, I64]
@@ -134,6 +135,8 @@ def load_library():
     L.sdg_sync.argtypes = [P]
     L.sdg_poll.argtypes = [P, I32, ctypes.POINTER(_Out)]
     L.sdg_discard.argtypes = [P]
+    L.sdg_snapshot.argtypes = [P, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(I64)]
+    L.sdg_restore.argtypes = [P, ctypes.c_char_p, I64]
     L.sdg_export_device.argtypes = [P, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), P, P, P, P]
     L.sdg_last_stats.argtypes = [P, ctypes.POINTER(Stats)]
     _lib = L
@@ -195,7 +198,8 @@ class InputHandler:
         elif isinstance(args[0], Event):
             self._rt._send(self._idx, self._types, [(args[0].timestamp, args[0].data)])
         elif args and isinstance(args[0], (list, tuple)) and args[0] and isinstance(args[0][0], Event):
-            self._rt._send(self._idx, self._types, [(ev.timestamp, ev.data) for ev in args[0]])
+            # send(Event[]): the clock moves to the last event's timestamp first (InputHandler.java:85-95)
+            self._rt._send(self._idx, self._types, [(ev.timestamp, ev.data) for ev in args[0]], events=True)
         else:
             self._rt._send(self._idx, self._types, [(None, list(args[0]))])
 
@@ -215,6 +219,10 @@ class SiddhiAppRuntime:
         _check(L.sdg_compile(app_text.encode(), ctypes.byref(opts), ctypes.byref(h)))
         self._h = h
         self.playback = "@app:playback" in app_text.replace(" ", "").lower()
+        import re as _re
+        m = _re.search(r"@app:name\(\s*['\"]([^'\"]*)['\"]", app_text)
+        self.name = m.group(1) if m else "siddhi_app"
+        self._store = None
         self._last_ts = 0
         self._callbacks = {}  # name -> [callback]
         self._queries = []
@@ -289,7 +297,7 @@ class SiddhiAppRuntime:
             return int(v)
         return float(v)
 
-    def _send(self, idx, types, rows):
+    def _send(self, idx, types, rows, events=False):
         n = len(rows)
         ts = (ctypes.c_int64 * n)()
         for i, (t, _) in enumerate(rows):
@@ -306,11 +314,12 @@ class SiddhiAppRuntime:
             keep += [arr, nl]
             cols[a] = ctypes.cast(arr, ctypes.c_void_p)
             nulls[a] = ctypes.cast(nl, ctypes.c_void_p) if any(r[1][a] is None for r in rows) else None
-        self._push(idx, n, ts, cols, nulls)
+        self._push(idx, n, ts, cols, nulls, events)
 
-    def _push(self, idx, n, ts, cols, nulls):
+    def _push(self, idx, n, ts, cols, nulls, events=False):
         before = self._L.sdg_pending(self._h)
-        _check(self._L.sdg_push(self._h, idx, n, ts, cols, nulls))
+        push = self._L.sdg_push_events if events else self._L.sdg_push
+        _check(push(self._h, idx, n, ts, cols, nulls))
         if self._L.sdg_pending(self._h) < before + n:  # the push filled the batch and flushed it
             self._deliver()
 
@@ -370,6 +379,45 @@ class SiddhiAppRuntime:
         if self.playback:
             self._last_ts = max(self._last_ts, int(ts))
         _check(self._L.sdg_advance_time(self._h, int(ts)))
+
+    # --- persistence (core/SiddhiAppRuntimeImpl.java:677-737) ------------------------------------------------
+    def snapshot(self):
+        """every partial match / timer / aggregator state, after processing what was sent; results produced by
+        then are delivered to the callbacks"""
+        data = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_int64()
+        _check(self._L.sdg_snapshot(self._h, ctypes.byref(data), ctypes.byref(n)))
+        blob = ctypes.string_at(data, n.value)
+        self._deliver()
+        return blob
+
+    def restore(self, snapshot):
+        try:
+            _check(self._L.sdg_restore(self._h, bytes(snapshot), len(snapshot)))
+        except (SiddhiAppCreationException, ValueError) as ex:
+            raise CannotRestoreSiddhiAppStateException(str(ex))
+
+    def persist(self):
+        """snapshot into the manager's persistence store; returns the revision"""
+        if getattr(self, "_store", None) is None:
+            raise SiddhiAppCreationException("NoPersistenceStoreException: no persistence store assigned")
+        rev = "%d_%s" % (int(time.time() * 1e6), self.name)
+        self._store.save(self.name, rev, self.snapshot())
+        return rev
+
+    def restoreRevision(self, revision):  # noqa: N802
+        blob = self._store.load(self.name, revision) if getattr(self, "_store", None) else None
+        if blob is None:
+            raise CannotRestoreSiddhiAppStateException("no revision %s of %s" % (revision, self.name))
+        self.restore(blob)
+
+    def restoreLastRevision(self):  # noqa: N802
+        if getattr(self, "_store", None) is None:
+            raise SiddhiAppCreationException("NoPersistenceStoreException: no persistence store assigned")
+        rev = self._store.getLastRevision(self.name)
+        if rev is not None:
+            self.restoreRevision(rev)
+        return rev
 
     def flush(self, deliver=True):
         _check(self._L.sdg_flush(self._h))
@@ -461,12 +509,45 @@ class SiddhiAppRuntime:
             [[out.nulls[j][i] for i in range(n)] for j in range(len(types))]
 
 
+class InMemoryPersistenceStore:
+    """PersistenceStore (core/util/persistence/PersistenceStore.java) kept in memory: revisions per app"""
+
+    def __init__(self):
+        self._revs = {}
+
+    def save(self, app_name, revision, snapshot):
+        self._revs.setdefault(app_name, []).append((revision, bytes(snapshot)))
+
+    def load(self, app_name, revision):
+        for r, b in self._revs.get(app_name, []):
+            if r == revision:
+                return b
+        return None
+
+    def getLastRevision(self, app_name):  # noqa: N802
+        revs = self._revs.get(app_name, [])
+        return revs[-1][0] if revs else None
+
+    def clearAllRevisions(self, app_name):  # noqa: N802
+        self._revs.pop(app_name, None)
+
+
+class CannotRestoreSiddhiAppStateException(SiddhiAppCreationException):
+    pass
+
+
 class SiddhiManager:
     def __init__(self, device=0):
         self.device = device
+        self._store = None
+
+    def setPersistenceStore(self, store):  # noqa: N802
+        self._store = store
 
     def createSiddhiAppRuntime(self, app, batch_capacity=0):  # noqa: N802
-        return SiddhiAppRuntime(app, device=self.device, batch_capacity=batch_capacity)
+        rt = SiddhiAppRuntime(app, device=self.device, batch_capacity=batch_capacity)
+        rt._store = self._store
+        return rt
 
     def shutdown(self):
         pass

@@ -160,6 +160,20 @@ class QC {
             h_.chain_reason = "aggregators / having in the selector";
         }
         runtime_tables(root.node);
+        p.purge = 0;
+        if (q_.partition_index >= 0 && app_.partitions[q_.partition_index].purge) {
+            const sql::Partition& pt = app_.partitions[q_.partition_index];
+            if (p.n_sched > 0 || p.n_agg > 0)
+                throw CompileError(SDG_ERR_UNSUPPORTED, "@purge with absent states or aggregators is not on the device path");
+            for (const auto& w : pt.with)  // the partition's keys are refreshed by any of its streams' events
+                if (std::find(h_.streams.begin(), h_.streams.end(), app_.stream_index(w.stream_id)) == h_.streams.end())
+                    throw CompileError(SDG_ERR_UNSUPPORTED, "@purge: every query of the partition must read all its streams");
+            p.purge = 1;
+            p.purge_interval_ms = pt.purge_interval_ms;
+            p.purge_idle_ms = pt.purge_idle_ms;
+            p.chain = 0;  // per-key state lifetimes: the generic NFA
+            h_.chain_reason = "@purge partition";
+        }
         p.n_code = (int)h_.code.size();
         p.n_consts = (int)h_.consts.size();
     }

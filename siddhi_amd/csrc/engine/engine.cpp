@@ -91,6 +91,7 @@ struct PushChunk {
     int stream;          // -1: an sdg_advance_time point (one position, no data); -2: mixed (rstream per row)
     int64_t n;
     bool device;
+    bool no_adv = false; // rows of an InputHandler.send(Event[]): they do not move the playback clock
     std::vector<int32_t> rstream;   // mixed: stream of each row; cols[a] then hold 64-bit slots of attribute a
     std::vector<int64_t> ts;
     std::vector<std::vector<uint8_t>> cols;
@@ -166,6 +167,10 @@ struct QueryRt {
     // the selector's post pass (aggregators / having): per-key aggregator state, persistent; staging
     DevBuf agg_state, ps_key, ps_vals, ps_nulls, ps_pass, ps_ws;
     int64_t agg_keys = 0;
+    // @purge: per-key clock reading at the key's last event (stored XOR INT64_MIN: zero bytes = never seen), its
+    // copy at the batch start (a rerun starts from it), the partition's first initPartition reading
+    DevBuf last_seen, last_seen_bak;
+    int64_t purge_first = INT64_MIN;
     SchedSim::RankMap last_rank;
     std::vector<uint32_t> reordered;  // keys rerun with the scheduler's fire order (sorted)
     std::vector<uint32_t> taken;
@@ -229,6 +234,7 @@ struct sdg_engine {
     int64_t seq = 0;             // batch positions flushed so far (sequence number of the next batch's position 0)
     int64_t clock = 0;           // currentTime(): playback = max event ts seen; live = the modelled wall clock
     bool any_sched = false;      // some query has absent states (the batch clock is built)
+    bool any_purge = false;      // some query's partition purges idle keys (the batch clock is built)
     BatchClock bc;
     DevBuf d_clk, d_nadv;
     sdg_stats stats{};
@@ -238,6 +244,8 @@ struct sdg_engine {
     bool compile_only = false;
     bool force_generic = false;
     bool no_fused = false;
+    uint64_t app_hash = 0;       // FNV-1a of the app text: a snapshot restores only into the app it came from
+    std::vector<uint8_t> snap;   // the last sdg_snapshot's bytes (valid until the next snapshot / destroy)
 };
 
 namespace {
@@ -853,6 +861,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             grow(q.arena2, kb);
             grow(q.cur_bits, 1);
             grow(q.ran_bits, 1);
+            if (P.purge) grow(q.last_seen, 8);
             q.arena_keys = nk;
         }
         a.arena = q.arena.as<uint8_t>();
@@ -892,6 +901,14 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             a.T.log_cap = q.log_cap;
         }
         a.L = q.L;
+        if (P.purge) {  // a rerun of the batch (arena growth, output regrowth) starts from the batch-start readings
+            a.last_seen = q.last_seen.as<int64_t>();
+            a.purge_clk = e->d_clk.as<int64_t>();
+            a.purge_from = q.purge_first == INT64_MIN ? INT64_MAX : q.purge_first + P.purge_interval_ms;
+            a.purge_idle = P.purge_idle_ms;
+            HIPCHECK(hipMemcpyAsync(q.last_seen_bak.ensure((size_t)q.arena_keys * 8), q.last_seen.p, (size_t)q.arena_keys * 8,
+                                    hipMemcpyDeviceToDevice, st));
+        }
         if (q.replay_carries) replay_carries(e, q, a, multi_stream);
         int64_t cap = std::max<int64_t>(q.out_cap, 2 * nrows + 4096);
         unsigned long long* counters = (unsigned long long*)q.counters.ensure(16);
@@ -915,6 +932,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         unsigned long long hc[2];
         // one launch; returns false when a growable buffer (outputs, scheduler log) overflowed
         auto launch = [&](bool first) -> bool {
+            if (first && P.purge)
+                HIPCHECK(hipMemcpyAsync(q.last_seen.p, q.last_seen_bak.p, (size_t)q.arena_keys * 8, hipMemcpyDeviceToDevice, st));
             if (first) {
                 HIPCHECK(hipMemsetAsync(counters, 0, 16, st));
                 if (!(partitioned && nrows > 0)) HIPCHECK(hipMemsetAsync(flags, 0, 32, st));
@@ -1603,8 +1622,8 @@ void build_clock(sdg_engine* e, int64_t G) {
         for (int64_t r = 0; r < ch.n; ++r, ++g) {
             const int64_t t = ts[r];
             if (playback) {
-                bc.adv[g] = t >= c;
-                if (t >= c) c = t;
+                bc.adv[g] = !ch.no_adv && t >= c;
+                if (bc.adv[g]) c = t;
             } else {
                 bc.adv[g] = ch.stream == -1;  // advance_time points only
                 if (ch.stream == -1 && t > c) c = t;
@@ -1645,15 +1664,223 @@ int do_flush(sdg_engine* e) {
     int64_t G = 0;
     for (auto& c : e->pending) G += c.n;
     if (G >= (int64_t)0xFFFFFFF0) throw CompileError(SDG_ERR_CAPACITY, "a flush holds more than 2^32 - 16 events");
-    if (e->any_sched) build_clock(e, G);
+    if (e->any_sched || e->any_purge) build_clock(e, G);
     for (auto& q : e->qs) {
         drain(e, *q);  // earlier unpolled results go to the backlog first
+        if (q->hq.plan.purge && q->purge_first == INT64_MIN) {  // the partition's first event: its clock reading
+            int64_t g = 0;
+            for (const PushChunk& ch : e->pending) {
+                const auto& ss = q->hq.streams;
+                if (ch.stream >= 0 && std::find(ss.begin(), ss.end(), ch.stream) != ss.end() && ch.n > 0) {
+                    q->purge_first = e->bc.clk[g];
+                    break;
+                }
+                if (ch.stream == -2) {
+                    int64_t r = 0;
+                    while (r < ch.n && std::find(ss.begin(), ss.end(), ch.rstream[r]) == ss.end()) ++r;
+                    if (r < ch.n) {
+                        q->purge_first = e->bc.clk[g + r];
+                        break;
+                    }
+                }
+                g += ch.n;
+            }
+        }
         flush_query(e, *q);
     }
-    if (e->any_sched && G > 0) e->clock = e->bc.clk[G - 1];
+    if ((e->any_sched || e->any_purge) && G > 0) e->clock = e->bc.clk[G - 1];
     e->seq += G;
     e->stats.ms_total = e->stats.ms_keygroup + e->stats.ms_match;
     return SDG_OK;
+}
+
+// ---- snapshot / restore ------------------------------------------------------------------------------------
+// SiddhiAppRuntime.snapshot() / restore(byte[]) (core/SiddhiAppRuntimeImpl.java:677-737) collect every
+// StateHolder's state (StreamPreStateProcessor.java:450-469, CountPreStateProcessor.java:206-219,
+// AbsentStreamPreStateProcessor.java:328-341, the schedulers, the selector's aggregators). Here that state is what
+// outlives a flush: the chain queries' carried partials, the generic NFA's per-key arenas (the StreamPreStates,
+// committed copies), the scheduler model, the per-key aggregator states, the key dictionaries, the string table,
+// the position counter and the clock. The format is this engine's own (the reference's is Java serialisation);
+// restore is behavioural: the restored engine continues exactly as the one snapshotted would have.
+struct SnapW {
+    std::vector<uint8_t>& o;
+    template <class T>
+    void put(const T& v) {
+        const uint8_t* b = (const uint8_t*)&v;
+        o.insert(o.end(), b, b + sizeof(T));
+    }
+    void bytes(const void* p, size_t n) {
+        put<uint64_t>(n);
+        o.insert(o.end(), (const uint8_t*)p, (const uint8_t*)p + n);
+    }
+    template <class T>
+    void vec(const std::vector<T>& v) { bytes(v.data(), v.size() * sizeof(T)); }
+    void str(const std::string& s) { bytes(s.data(), s.size()); }
+    void dev(const void* d, size_t n, hipStream_t st) {  // a device buffer's first n bytes
+        put<uint64_t>(n);
+        const size_t at = o.size();
+        o.resize(at + n);
+        if (n) HIPCHECK(hipMemcpyAsync(o.data() + at, d, n, hipMemcpyDeviceToHost, st));
+        if (n) HIPCHECK(hipStreamSynchronize(st));
+    }
+};
+struct SnapR {
+    const uint8_t* p;
+    const uint8_t* end;
+    template <class T>
+    T get() {
+        if (p + sizeof(T) > end) throw CompileError(SDG_ERR_ARG, "snapshot is truncated");
+        T v;
+        std::memcpy(&v, p, sizeof(T));
+        p += sizeof(T);
+        return v;
+    }
+    const uint8_t* bytes(size_t* n) {
+        *n = get<uint64_t>();
+        if (*n > (size_t)(end - p)) throw CompileError(SDG_ERR_ARG, "snapshot is truncated");
+        const uint8_t* r = p;
+        p += *n;
+        return r;
+    }
+    template <class T>
+    void vec(std::vector<T>& v) {
+        size_t n;
+        const uint8_t* b = bytes(&n);
+        v.resize(n / sizeof(T));
+        std::memcpy(v.data(), b, v.size() * sizeof(T));
+    }
+    std::string str() {
+        size_t n;
+        const uint8_t* b = bytes(&n);
+        return std::string((const char*)b, n);
+    }
+    void dev(DevBuf& d, hipStream_t st) {  // into a device buffer (allocated to at least the size)
+        size_t n;
+        const uint8_t* b = bytes(&n);
+        void* x = d.ensure(n);
+        if (n) HIPCHECK(hipMemcpyAsync(x, b, n, hipMemcpyHostToDevice, st));
+        if (n) HIPCHECK(hipStreamSynchronize(st));
+    }
+};
+constexpr uint64_t SNAP_MAGIC = 0x31504e5347445353ull;  // "SSDGSNP1"
+
+void snapshot(sdg_engine* e, std::vector<uint8_t>& out) {
+    out.clear();
+    SnapW w{out};
+    hipStream_t st = e->stream;
+    w.put(SNAP_MAGIC);
+    w.put(e->app_hash);
+    w.put(e->seq);
+    w.put(e->clock);
+    w.put<uint64_t>(e->strings.strs.size());
+    for (auto& x : e->strings.strs) w.str(x);
+    w.put<uint32_t>((uint32_t)e->qs.size());
+    for (auto& qp : e->qs) {
+        QueryRt& q = *qp;
+        const Plan& P = q.hq.plan;
+        w.put<int32_t>(P.chain);
+        w.put<uint8_t>(q.replay_carries);
+        w.put<uint8_t>(q.carry_nullable);
+        // carried partials (chain path): the committed buffer's n records, SoA
+        const QueryRt::Carry& c = q.carry[q.cur];
+        const int nc = std::max(P.n_cols, 1);
+        w.put<int64_t>(c.n);
+        if (c.n > 0) {
+            w.dev(c.key.p, (size_t)c.n * 4, st);
+            w.dev(c.ts.p, (size_t)c.n * 8, st);
+            w.dev(c.seq.p, (size_t)c.n * 8, st);
+            for (int k = 0; k < nc; ++k) w.dev((const int64_t*)c.vals.p + (size_t)k * c.cap, (size_t)c.n * 8, st);
+            w.dev(c.nulls.p, (size_t)c.n * 4, st);
+        }
+        // key dictionaries (numeric partition values; string keys use the string table)
+        w.vec(q.intkeys.k);
+        w.vec(q.intkeys.v);
+        w.put<uint64_t>(q.intkeys.n);
+        w.put<uint64_t>(q.keystr.size());
+        for (auto& x : q.keystr) w.str(x);
+        w.vec(q.key_hash);
+        // generic NFA: layout + both arena copies + the committed-copy bits
+        w.put(q.L);
+        w.put<int64_t>(q.arena_keys);
+        if (q.arena_keys > 0) {
+            w.dev(q.arena.p, (size_t)(q.arena_keys * q.L.bytes), st);
+            w.dev(q.arena2.p, (size_t)(q.arena_keys * q.L.bytes), st);
+            w.dev(q.cur_bits.p, (size_t)q.arena_keys, st);
+        }
+        w.put<int64_t>(q.purge_first);
+        if (P.purge && q.arena_keys > 0) w.dev(q.last_seen.p, (size_t)q.arena_keys * 8, st);
+        // selector aggregators per key
+        w.put<int64_t>(q.agg_keys);
+        if (q.agg_keys > 0) w.dev(q.agg_state.p, (size_t)q.agg_keys * (size_t)std::max(P.n_agg, 1) * 16, st);
+        q.sim.save(out);
+    }
+}
+
+void restore(sdg_engine* e, const uint8_t* data, size_t len) {
+    SnapR r{data, data + len};
+    if (r.get<uint64_t>() != SNAP_MAGIC) throw CompileError(SDG_ERR_ARG, "not an engine snapshot");
+    if (r.get<uint64_t>() != e->app_hash)
+        throw CompileError(SDG_ERR_ARG, "the snapshot was taken from a different Siddhi app");  // CannotRestoreSiddhiAppStateException
+    hipStream_t st = e->stream;
+    const int64_t seq = r.get<int64_t>();
+    const int64_t clock = r.get<int64_t>();
+    Interner strings;
+    const uint64_t ns = r.get<uint64_t>();
+    for (uint64_t i = 0; i < ns; ++i) strings.get(r.str());
+    if (r.get<uint32_t>() != e->qs.size()) throw CompileError(SDG_ERR_ARG, "snapshot query count differs");
+    for (auto& qp : e->qs) {
+        QueryRt& q = *qp;
+        Plan& P = q.hq.plan;
+        P.chain = r.get<int32_t>();
+        q.replay_carries = r.get<uint8_t>() != 0;
+        q.carry_nullable = r.get<uint8_t>() != 0;
+        const int nc = std::max(P.n_cols, 1);
+        q.cur = 0;
+        q.carry[1].n = 0;
+        QueryRt::Carry& c = q.carry[0];
+        c.n = r.get<int64_t>();
+        if (c.n > 0) {
+            c.cap = c.n;
+            r.dev(c.key, st);
+            r.dev(c.ts, st);
+            r.dev(c.seq, st);
+            c.vals.ensure((size_t)nc * c.n * 8);
+            for (int k = 0; k < nc; ++k) {
+                size_t n;
+                const uint8_t* b = r.bytes(&n);
+                HIPCHECK(hipMemcpy((int64_t*)c.vals.p + (size_t)k * c.cap, b, n, hipMemcpyHostToDevice));
+            }
+            r.dev(c.nulls, st);
+        }
+        r.vec(q.intkeys.k);
+        r.vec(q.intkeys.v);
+        q.intkeys.n = (size_t)r.get<uint64_t>();
+        q.keystr.resize(r.get<uint64_t>());
+        q.keydict.clear();
+        for (size_t i = 0; i < q.keystr.size(); ++i) {
+            q.keystr[i] = r.str();
+            q.keydict[q.keystr[i]] = (uint32_t)i;
+        }
+        r.vec(q.key_hash);
+        q.L = r.get<nfa::Layout>();
+        q.arena_keys = r.get<int64_t>();
+        if (q.arena_keys > 0) {
+            r.dev(q.arena, st);
+            r.dev(q.arena2, st);
+            r.dev(q.cur_bits, st);
+            q.ran_bits.ensure((size_t)q.arena_keys);
+            HIPCHECK(hipMemset(q.ran_bits.p, 0, (size_t)q.arena_keys));
+        }
+        q.purge_first = r.get<int64_t>();
+        if (P.purge && q.arena_keys > 0) r.dev(q.last_seen, st);
+        q.agg_keys = r.get<int64_t>();
+        if (q.agg_keys > 0) r.dev(q.agg_state, st);
+        r.p = q.sim.load(r.p, r.end);
+    }
+    if (r.p != r.end) throw CompileError(SDG_ERR_ARG, "snapshot has trailing bytes");
+    e->seq = seq;
+    e->clock = clock;
+    e->strings = std::move(strings);
 }
 
 template <class F>
@@ -1685,6 +1912,8 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
     return guarded([&]() {
         auto e = std::make_unique<sdg_engine>();
         e->app = sql::parse_app(text);
+        e->app_hash = 1469598103934665603ull;
+        for (const char* c = text; *c; ++c) e->app_hash = (e->app_hash ^ (uint8_t)*c) * 1099511628211ull;
         if (opts) {
             e->device = opts->device;
             if (opts->batch_capacity > 0) e->capacity = opts->batch_capacity;
@@ -1717,6 +1946,7 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             q->L = nfa::make_layout(P.n_states, std::max(P.n_cols, 1), e->max_partials, P.n_sched);
             q->sim.setup(P.n_sched, P.partitioned, !P.playback);
             e->any_sched |= P.n_sched > 0;
+            e->any_purge |= P.purge != 0;
             for (size_t i = 0; i < q->hq.key_kind.size(); ++i)
                 if (q->hq.key_attr[i] >= 0 && q->hq.key_kind[i] != VK_STR) q->string_keys = false;
             if (!e->compile_only) upload_plan(e.get(), *q);
@@ -1753,6 +1983,31 @@ void sdg_destroy(sdg_engine* e) {
     delete e;
 }
 
+int sdg_snapshot(sdg_engine* e, const uint8_t** data, int64_t* len) {
+    if (!e || !data || !len) return fail(SDG_ERR_ARG, "bad snapshot arguments");
+    return guarded([&]() {
+        if (e->compile_only) throw DeviceError("engine was compiled with SDG_COMPILE_ONLY");
+        HIPCHECK(hipSetDevice(e->device));
+        if (!e->pending.empty()) do_flush(e);  // persist(): what was sent before is processed first
+        for (auto& q : e->qs) drain(e, *q);     // results produced so far stay queued for sdg_poll
+        snapshot(e, e->snap);
+        *data = e->snap.data();
+        *len = (int64_t)e->snap.size();
+        return (int)SDG_OK;
+    });
+}
+
+int sdg_restore(sdg_engine* e, const uint8_t* data, int64_t len) {
+    if (!e || !data || len < 0) return fail(SDG_ERR_ARG, "bad restore arguments");
+    return guarded([&]() {
+        if (e->compile_only) throw DeviceError("engine was compiled with SDG_COMPILE_ONLY");
+        if (!e->pending.empty()) throw CompileError(SDG_ERR_ARG, "events are pending: flush before restoring");
+        HIPCHECK(hipSetDevice(e->device));
+        restore(e, data, (size_t)len);
+        return (int)SDG_OK;
+    });
+}
+
 int sdg_stream_index(sdg_engine* e, const char* sid) { return e && sid ? e->app.stream_index(sid) : -1; }
 
 int sdg_stream_schema(sdg_engine* e, int s, int32_t* n, const int32_t** types) {
@@ -1782,15 +2037,25 @@ const char* sdg_string(sdg_engine* e, uint32_t id) {
     return id < e->strings.strs.size() ? e->strings.strs[id].c_str() : nullptr;
 }
 
-int sdg_push(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const void* const* cols,
-             const uint8_t* const* nulls) {
+namespace {
+int push_host(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const void* const* cols,
+              const uint8_t* const* nulls, bool event_array) {
     if (!e || stream < 0 || stream >= (int)e->stream_types.size() || n < 0 || (n > 0 && !ts))
         return fail(SDG_ERR_ARG, "bad push arguments");
     return guarded([&]() {
+        if (event_array && n > 0 && e->app.playback) {  // InputHandler.send(Event[]) :85-95: the clock first
+            PushChunk a;                                  // moves to the last event's timestamp
+            a.stream = -1;
+            a.n = 1;
+            a.device = false;
+            a.ts.assign(1, ts[n - 1]);
+            e->pending.push_back(std::move(a));
+        }
         PushChunk c;
         c.stream = stream;
         c.n = n;
         c.device = false;
+        c.no_adv = event_array;
         c.ts.assign(ts, ts + n);
         const auto& types = e->stream_types[stream];
         c.cols.resize(types.size());
@@ -1806,6 +2071,17 @@ int sdg_push(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const void
         if (e->pending_n >= e->capacity) return do_flush(e);
         return (int)SDG_OK;
     });
+}
+}  // namespace
+
+int sdg_push(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const void* const* cols,
+             const uint8_t* const* nulls) {
+    return push_host(e, stream, n, ts, cols, nulls, false);
+}
+
+int sdg_push_events(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const void* const* cols,
+                    const uint8_t* const* nulls) {
+    return push_host(e, stream, n, ts, cols, nulls, true);
 }
 
 int sdg_push_mixed(sdg_engine* e, int64_t n, const int32_t* streams, const int64_t* ts, int32_t n_attrs,

@@ -105,6 +105,16 @@ struct TimerIn {
     int64_t log_cap;
 };
 
+// @purge of the key's partition (PartitionRuntimeImpl.java:368-401, modelled as in the oracle): before an event
+// whose clock reading exceeds the key's last activity by idle.period (from the partition's first initPartition +
+// interval on), the key's states are destroyed and initPartition runs again
+struct PurgeIn {
+    const int64_t* clk;           // [G] currentTime() at position g; nullptr: no purge
+    int64_t from;                 // first clock reading a purge pass can see
+    int64_t idle;                 // idle.period (ms)
+    int64_t last;                 // the key's currentTime at its last event (INT64_MIN: none yet); updated by the run
+};
+
 struct SE {
     int16_t free_next;
     uint8_t type, mark;
@@ -205,6 +215,7 @@ struct CtxT {
     int64_t cur_sub;
     // timers
     TimerIn T;
+    PurgeIn purge{};
     const TimerFire* fires;  // explicit fire list of this key (used when nfires >= 0; -1: ideal mode)
     int32_t nfires, fi;
     int64_t clock;           // currentTime()
@@ -1268,6 +1279,15 @@ SDG_HD bool key_row(CtxT<TM>& c, const KeyEvents& ev, int64_t p, bool& need_init
     const int64_t g = key_pos(ev, p);
     c.pos = g;
     if (TM && P->n_sched) c.clock = c.T.clk[g];
+    if (c.purge.clk) {
+        const int64_t now = c.purge.clk[g];
+        if (!need_init && c.purge.last != INT64_MIN && now >= c.purge.from && c.purge.last + c.purge.idle < now) {
+            c.arena_init();  // the key's states destroyed (cleanGroupByStates); its partition key is new again
+            c.head().flags = 2;
+            need_init = true;
+        }
+        c.purge.last = now;  // partitionKeys.put(key, currentTime)
+    }
     if (need_init) {  // PartitionRuntimeImpl.initPartition for a first-seen key (after the clock advance)
         c.init_key();
         need_init = false;

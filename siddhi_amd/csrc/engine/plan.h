@@ -152,6 +152,8 @@ struct Plan {
     int32_t n_sched, sched_state[MAX_STATES];   // one Scheduler per absent processor, in creation order (= the
                                                 // order its TimeChangeListener registers, SchedulerParser.parse)
     int32_t playback;                           // @app:playback: the clock is event time (else modelled wall clock)
+    int32_t purge;                              // the partition has @purge(enable='true')
+    int64_t purge_interval_ms, purge_idle_ms;
     // expire order (allStateProcessors), setup order per stream etc. live on the host plan
     int32_t n_code = 0, n_consts = 0;
 };

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <stdexcept>
 
 namespace sdg {
 
@@ -568,6 +569,88 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
     std::sort(out.taken.begin(), out.taken.end());
     prof.lap(6);
     prof.print("exact", logs.size(), evp.size(), out.n_fires);
+}
+
+namespace {
+template <class T>
+void put(std::vector<uint8_t>& o, const T& v) {
+    const uint8_t* b = (const uint8_t*)&v;
+    o.insert(o.end(), b, b + sizeof(T));
+}
+template <class T>
+void put_vec(std::vector<uint8_t>& o, const std::vector<T>& v) {
+    put<uint64_t>(o, v.size());
+    const uint8_t* b = (const uint8_t*)v.data();
+    o.insert(o.end(), b, b + v.size() * sizeof(T));
+}
+template <class T>
+T get(const uint8_t*& p, const uint8_t* end) {
+    if (p + sizeof(T) > end) throw std::runtime_error("snapshot: truncated scheduler state");
+    T v;
+    std::memcpy(&v, p, sizeof(T));
+    p += sizeof(T);
+    return v;
+}
+template <class T>
+void get_vec(const uint8_t*& p, const uint8_t* end, std::vector<T>& v) {
+    const uint64_t n = get<uint64_t>(p, end);
+    if (n > (uint64_t)(end - p) / sizeof(T)) throw std::runtime_error("snapshot: truncated scheduler state");
+    v.resize(n);
+    std::memcpy(v.data(), p, n * sizeof(T));
+    p += n * sizeof(T);
+}
+}  // namespace
+
+void SchedSim::save(std::vector<uint8_t>& o) const {
+    put<uint32_t>(o, (uint32_t)cur_.sc.size());
+    for (const SchedState& S : cur_.sc) {
+        put_vec(o, S.ks);
+        put<uint64_t>(o, S.due.size());
+        for (const auto& kv : S.due) {
+            put<int64_t>(o, kv.first);
+            put_vec(o, kv.second);
+        }
+        put<uint64_t>(o, S.cap);
+        put<uint64_t>(o, S.threshold);
+        put<uint64_t>(o, S.size);
+        put<uint64_t>(o, S.stamp);
+        put_vec(o, S.bin);
+    }
+    put<uint64_t>(o, cur_.spill.size());
+    for (const auto& d : cur_.spill) put_vec(o, std::vector<int64_t>(d.begin(), d.end()));
+    put_vec(o, cur_.spill_free);
+    put<uint64_t>(o, cur_.cseq);
+}
+
+const uint8_t* SchedSim::load(const uint8_t* p, const uint8_t* end) {
+    State st;
+    const uint32_t ns = get<uint32_t>(p, end);
+    if ((int)ns != n_sched_) throw std::runtime_error("snapshot: scheduler count differs from the app's");
+    st.sc.resize(ns);
+    for (SchedState& S : st.sc) {
+        get_vec(p, end, S.ks);
+        const uint64_t nd = get<uint64_t>(p, end);
+        for (uint64_t i = 0; i < nd; ++i) {
+            const int64_t t = get<int64_t>(p, end);
+            get_vec(p, end, S.due[t]);
+        }
+        S.cap = get<uint64_t>(p, end);
+        S.threshold = get<uint64_t>(p, end);
+        S.size = get<uint64_t>(p, end);
+        S.stamp = get<uint64_t>(p, end);
+        get_vec(p, end, S.bin);
+    }
+    const uint64_t nsp = get<uint64_t>(p, end);
+    st.spill.resize(nsp);
+    for (auto& d : st.spill) {
+        std::vector<int64_t> v;
+        get_vec(p, end, v);
+        d.assign(v.begin(), v.end());
+    }
+    get_vec(p, end, st.spill_free);
+    st.cseq = get<uint64_t>(p, end);
+    cur_ = std::move(st);
+    return p;
 }
 
 }  // namespace sdg

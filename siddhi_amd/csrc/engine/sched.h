@@ -168,6 +168,9 @@ class SchedSim {
                   const KeyRows& rows, const std::function<KeyRun*(uint32_t)>& take_over, Result& out,
                   bool optimistic = false);
     void commit() { std::swap(cur_, work_); }  // work_ is rebuilt from cur_ by the next simulate()
+    // snapshot / restore of the committed scheduler states (sdg_snapshot): every key's queue and HashMap entry
+    void save(std::vector<uint8_t>& out) const;
+    const uint8_t* load(const uint8_t* p, const uint8_t* end);  // returns the end of what it read (throws on a bad blob)
     static uint64_t rank_key(uint32_t g, int sch, uint32_t key) {
         return ((uint64_t)g << 32) ^ ((uint64_t)sch << 27) ^ (uint64_t)key * 0x9E3779B97F4A7C15ull;
     }

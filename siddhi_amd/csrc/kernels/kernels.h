@@ -231,6 +231,10 @@ struct NfaArgs {
     int* flags;                       // [0] output overflow, [2] arena overflow, [5] scheduler log overflow
     // timers (queries with absent states)
     nfa::TimerIn T;
+    // @purge: per-key last activity (persistent, INT64_MIN = never), the clock, the purge window
+    int64_t* last_seen;               // nullptr: the query's partition does not purge
+    const int64_t* purge_clk;
+    int64_t purge_from, purge_idle;
     // rerun mode: run only list[0..nlist) with the explicit fire lists fires[fire_off[i] .. fire_off[i + 1])
     const uint32_t* list;
     int32_t nlist;

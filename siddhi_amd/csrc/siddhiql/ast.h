@@ -142,6 +142,10 @@ struct PartitionWith {
 struct Partition {
     std::vector<PartitionWith> with;
     std::vector<int> queries;   // indices into App::queries
+    // @purge(enable, interval, idle.period) (PartitionRuntimeImpl.java:120-150): idle keys' states are destroyed
+    bool purge = false;
+    int64_t purge_interval_ms = 300000;
+    int64_t purge_idle_ms = 0;
 };
 
 struct App {

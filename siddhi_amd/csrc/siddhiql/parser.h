@@ -267,7 +267,12 @@ class Parser {
     void check_definition_annotations(const std::vector<Ann>& anns) {
         for (auto& a : anns) {
             std::string n = lower(a.name);
-            if (n == "async" || n == "source" || n == "sink" || n == "store" || n == "onerror")
+            // @Async(buffer.size, workers, batch.size.max): StreamJunction hands events to a disruptor ring
+            // (StreamJunction.java:101-131, 276-305) -- same per-stream order, consumed on another thread. The engine
+            // consumes every pushed event in push order at its flush, which is one valid schedule of that
+            // asynchronous hand-off, so the annotation is accepted and has no further effect.
+            if (n == "async") continue;
+            if (n == "source" || n == "sink" || n == "store" || n == "onerror")
                 throw Unsupported("@" + a.name + " on a stream definition is not supported by the pattern engine");
         }
     }
@@ -331,9 +336,17 @@ class Parser {
             app.queries.push_back(std::move(q));
         }
         expect_kw("end");
-        for (auto& a : pending) {
-            std::string n = lower(a.name);
-            if (n == "purge") throw Unsupported("@purge partitions are out of scope for v1 (SURVEY 8(f) next #4)");
+        for (auto& a : pending) {  // PartitionRuntimeImpl constructor :120-150
+            if (lower(a.name) != "purge") continue;
+            const std::string en = lower(a.get("enable"));
+            if (en.empty()) throw ParseError("Annotation @purge is missing element 'enable'");
+            if (en != "true" && en != "false") throw ParseError("Invalid value for enable: " + en + ". Please use 'true' or 'false'");
+            part.purge = en == "true";
+            const std::string idle = a.get("idle.period");
+            if (idle.empty()) throw ParseError("Annotation @purge is missing element 'idle.period'");
+            part.purge_idle_ms = annotation_time(idle);
+            const std::string iv = a.get("interval");
+            if (!iv.empty()) part.purge_interval_ms = annotation_time(iv);
         }
         app.partitions.push_back(part);
     }
@@ -587,6 +600,31 @@ class Parser {
         if (l == "sec" || l == "second" || l == "seconds") { mult = 1000; return true; }
         if (l == "millisec" || l == "millisecond" || l == "milliseconds") { mult = 1; return true; }
         return false;
+    }
+
+    // Expression.Time.timeToLong (siddhi-query-api .../expression/Expression.java:250-290): the first digit run and
+    // the first non-digit run of an annotation value ("1 sec", "2 min")
+    static int64_t annotation_time(const std::string& v) {
+        size_t i = 0;
+        while (i < v.size() && !std::isdigit((unsigned char)v[i])) ++i;
+        size_t j = i;
+        while (j < v.size() && std::isdigit((unsigned char)v[j])) ++j;
+        size_t a = 0;
+        while (a < v.size() && std::isdigit((unsigned char)v[a])) ++a;
+        size_t b = a;
+        while (b < v.size() && !std::isdigit((unsigned char)v[b])) ++b;
+        std::string unit = lower(v.substr(a, b - a));
+        while (!unit.empty() && std::isspace((unsigned char)unit.back())) unit.pop_back();
+        while (!unit.empty() && std::isspace((unsigned char)unit.front())) unit.erase(unit.begin());
+        if (i == j || unit.empty()) throw ParseError("Provided retention value cannot be identified: " + v);
+        const int64_t n = std::atoll(v.substr(i, j - i).c_str());
+        if (unit == "sec" || unit == "seconds" || unit == "second") return n * 1000;
+        if (unit == "min" || unit == "minutes" || unit == "minute") return n * 60000;
+        if (unit == "h" || unit == "hour" || unit == "hours") return n * 3600000;
+        if (unit == "day" || unit == "days") return n * 86400000;
+        if (unit == "year" || unit == "years") return n * 31556900000LL;
+        if (unit == "month" || unit == "months") return n * 2630000000LL;
+        throw ParseError("Provided retention value cannot be identified: " + v);
     }
 
     int64_t parse_time_value() {

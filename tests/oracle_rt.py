@@ -78,6 +78,7 @@ def bits_f64(u):
 
 class Oracle:
     def __init__(self, app_text):
+        self.playback = "@app:playback" in app_text.replace(" ", "").lower()
         L = lib()
         err = ctypes.create_string_buffer(2048)
         self.h = L.orc_create(app_text.encode(), err, 2048)
@@ -135,6 +136,14 @@ class Oracle:
         rc = self.L.orc_send_ex(self.h, si, ts, ts if now is None else now, mode, slots, nulls)
         if rc != 0:
             raise OracleError(self.L.orc_last_error().decode())
+
+    def send_events(self, sid, rows):
+        """InputHandler.send(Event[]) with rows [(ts, values), ...]: the clock moves to the last event's timestamp,
+        then each event is processed without moving it (InputHandler.java:85-95)"""
+        if rows and self.playback:
+            self.advance(rows[-1][0])
+        for ts, values in rows:
+            self.send(sid, ts, values, mode=2)
 
     def advance(self, ts):
         if self.L.orc_advance_time(self.h, ts) != 0:

@@ -30,6 +30,10 @@ class ProductAdapter:
         else:
             h.send(ts, values)
 
+    def send_events(self, sid, rows):
+        """InputHandler.send(Event[]) with rows [(ts, values), ...]"""
+        self.handler(sid).send([sa.Event(ts, values) for ts, values in rows])
+
     def advance(self, ts):
         self.rt.advance_time(ts)
 

@@ -7,6 +7,10 @@ DEFS = ("define stream S (id long, key string, price double, volume int); "
         "define stream T (id long, key string, price double, volume int); ")
 
 
+DEFS_NUM = ("@app:playback define stream S (id long, k long, price double, volume int); "
+            "define stream T (id long, k long, price double, volume int); ")
+
+
 def part(q):
     return "@app:playback " + DEFS + "partition with (key of S, key of T) begin " + q + " end;"
 
@@ -167,3 +171,55 @@ ABSENT_APPS = {
     "absent_mid": part("@info(name='q') from every e1=S[price>50] -> not T[price>e1.price] for 9 milliseconds -> "
                        "e3=S[price>e1.price] select e1.id as a, e3.id as b insert into O;"),
 }
+
+
+def run_events(adapter, tr, chunk=7, batches=1):
+    """the trace through InputHandler.send(Event[]): consecutive rows of one stream in arrays of <= chunk events
+    (InputHandler.java:85-95 -- the playback clock moves to each array's last timestamp first)"""
+    groups, cur = [], []
+    for s, ts, row in tr:
+        if cur and (cur[0][0] != s or len(cur) == chunk):
+            groups.append(cur)
+            cur = []
+        cur.append((s, ts, row))
+    if cur:
+        groups.append(cur)
+    bounds = np.linspace(0, len(groups), batches + 1).astype(int)
+    for b in range(batches):
+        for g in groups[bounds[b]:bounds[b + 1]]:
+            adapter.send_events(g[0][0], [(ts, row) for _, ts, row in g])
+        if hasattr(adapter, "flush"):
+            adapter.flush()
+    return [(o["name"], o["ts"], tuple(o["values"])) for o in adapter.outputs()
+            if o["kind"] == "query" and not o["expired"]]
+
+
+# ---- @purge (SURVEY 8(f) 4): keys active in bursts, idle in between (PartitionRuntimeImpl.java:368-401) ----
+def purge_part(q, idle="1 sec", interval="1 sec"):
+    return ("@app:playback " + DEFS + "@purge(enable='true', interval='%s', idle.period='%s') "
+            "partition with (key of S, key of T) begin %s end;" % (interval, idle, q))
+
+
+PURGE_APPS = {
+    "purge_pattern": purge_part("@info(name='q') from every e1=S[price>60] -> e2=T[price>e1.price] "
+                                "select e1.id as a, e2.id as b insert into O;"),
+    "purge_count": purge_part("@info(name='q') from every e1=S[price>40]<2:4> -> e2=T[price>e1[0].price] "
+                              "select e1[0].id as a, e1[last].id as b, e2.id as c insert into O;"),
+    "purge_non_every": purge_part("@info(name='q') from e1=S[price>80] -> e2=T[price>e1.price] "
+                                  "select e1.id as a, e2.id as b insert into O;", idle="2 sec"),
+    "purge_sequence": purge_part("@info(name='q') from every e1=S[price>30], e2=T[price>e1.price]+, "
+                                 "e3=S[price>e2[0].price] select e1.id as a, e2[0].id as b, e3.id as c insert into O;"),
+}
+
+
+def purge_trace(n, keys=8, burst=120, seed=0):
+    """every key is active for `burst` consecutive events, then idle while the other keys take their turns;
+    ts steps of 0-24 ms, so a key's idle gaps span seconds"""
+    rng = np.random.default_rng(seed)
+    ts = 1000 + np.cumsum(rng.integers(0, 25, size=n))
+    out = []
+    for i in range(n):
+        s = "T" if rng.random() < 0.4 else "S"
+        k = (i // burst) % keys if rng.random() < 0.9 else int(rng.integers(0, keys))
+        out.append((s, int(ts[i]), [i, "k%d" % k, float(np.round(rng.uniform(0, 100), 1)), int(rng.integers(0, 100))]))
+    return out

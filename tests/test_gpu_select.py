@@ -66,3 +66,50 @@ def test_absent_collisions_on_gpu(name, seed, oracle_built):
         finally:
             p.close()
         assert got == ref, batches
+
+
+@pytest.mark.parametrize("name", ["absent_every_20", "absent_start", "absent_mid"])
+@pytest.mark.parametrize("chunk", [3, 11])
+def test_send_event_arrays_on_gpu(name, chunk, oracle_built):
+    """InputHandler.send(Event[]): the clock moves to the array's last timestamp before its first event"""
+    app = synth.ABSENT_APPS[name]
+    tr = synth.trace(2000, keys=5, seed=7, null_rate=0.02)
+    o = Oracle(app)
+    try:
+        ref = synth.run_events(o, tr, chunk)
+        per_event = synth.run(Oracle(app), tr)
+    finally:
+        o.close()
+    assert ref != per_event, "the workload does not tell Event[] from per-event sends"
+    p = ProductAdapter(app)
+    try:
+        got = synth.run_events(p, tr, chunk, batches=2)
+    finally:
+        p.close()
+    assert got == ref
+
+
+@pytest.mark.parametrize("name", sorted(synth.PURGE_APPS))
+@pytest.mark.parametrize("batches", [1, 4])
+def test_purge_on_gpu(name, batches, oracle_built):
+    """@purge: idle keys' states destroyed, initPartition again at their next event (the oracle's model of the
+    purge task); non-vacuous: the output differs from the same app without @purge"""
+    import re
+    app = synth.PURGE_APPS[name]
+    tr = synth.purge_trace(6000, seed=3)
+    o = Oracle(app)
+    try:
+        ref = synth.run(o, tr)
+    finally:
+        o.close()
+    o2 = Oracle(re.sub(r"@purge\([^)]*\)", "", app))
+    try:
+        assert synth.run(o2, tr) != ref
+    finally:
+        o2.close()
+    p = ProductAdapter(app)
+    try:
+        got = synth.run(p, tr, batches)
+    finally:
+        p.close()
+    assert got == ref
