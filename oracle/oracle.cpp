@@ -1777,8 +1777,9 @@ struct PartitionRt {
     int64_t first_init = INT64_MIN;                 // currentTime of the partition's first initPartition
     struct With {
         int stream;
-        ExecP expr;
+        ExecP expr;                                           // value partition (null for ranges)
         Type t;
+        std::vector<std::pair<ExecP, std::string>> ranges;  // RangePartitionExecutor per range, in order
     };
     std::vector<With> with;
 };
@@ -2600,22 +2601,31 @@ void AppRt::deliverStream(int stream, const SEv& ev) {
             PartitionRt* p = sub.p;
             for (auto& w : p->with) {
                 if (w.stream != stream) continue;
-                // ValuePartitionExecutor: expr.execute(event).toString(); null -> dropped
                 StEv holder(new StateEvent());
                 holder->se.resize(1);
                 holder->se[0] = ev;
-                Val v = w.expr->exec(holder.get());
-                if (v.null) continue;
-                std::string key;
-                switch ((Type)v.t) {
-                    case Type::STRING: key = eng.strings.strs[(uint32_t)v.raw]; break;
-                    case Type::INT: key = std::to_string(v.i()); break;
-                    case Type::LONG: key = std::to_string(v.l()); break;
-                    case Type::FLOAT: key = java_real_to_string(v.f(), true); break;
-                    case Type::DOUBLE: key = java_real_to_string(v.d(), false); break;
-                    case Type::BOOL: key = v.b() ? "true" : "false"; break;
-                    default: break;
+                std::vector<std::string> keys;
+                if (!w.expr) {  // RangePartitionExecutor.execute: the label when the condition holds, else null
+                    for (auto& r : w.ranges) {
+                        Val c = r.first->exec(holder.get());
+                        if (!c.null && c.b()) keys.push_back(r.second);
+                    }
+                } else {  // ValuePartitionExecutor: expr.execute(event).toString(); null -> dropped
+                    Val v = w.expr->exec(holder.get());
+                    if (v.null) continue;
+                    std::string key;
+                    switch ((Type)v.t) {
+                        case Type::STRING: key = eng.strings.strs[(uint32_t)v.raw]; break;
+                        case Type::INT: key = std::to_string(v.i()); break;
+                        case Type::LONG: key = std::to_string(v.l()); break;
+                        case Type::FLOAT: key = java_real_to_string(v.f(), true); break;
+                        case Type::DOUBLE: key = java_real_to_string(v.d(), false); break;
+                        case Type::BOOL: key = v.b() ? "true" : "false"; break;
+                        default: break;
+                    }
+                    keys.push_back(key);
                 }
+                for (const std::string& key : keys) {  // PartitionStreamReceiver.send(key, event) per executor
                 Ctx saved = eng.ctx;
                 eng.ctx.has_key = true;
                 eng.ctx.key = key;
@@ -2644,6 +2654,7 @@ void AppRt::deliverStream(int stream, const SEv& ev) {
                 if (it != innerSubs.end())
                     for (Receiver* r : it->second) r->receive(ev);
                 eng.ctx = saved;
+                }
             }
         }
     }
@@ -2726,8 +2737,13 @@ static void build_app(orc_engine* e, const char* text) {
             b.meta.defs.push_back(&rt.app.streams[si]);
             b.meta.refs.push_back("");
             b.meta.multi.push_back(false);
-            pw.expr = b.expr(w.expr, 0, sql::IDX_CURRENT);
-            pw.t = pw.expr->rt;
+            if (w.ranges.empty()) {
+                pw.expr = b.expr(w.expr, 0, sql::IDX_CURRENT);
+                pw.t = pw.expr->rt;
+            } else {
+                for (auto& r : w.ranges) pw.ranges.push_back({b.cond(r.first, 0, sql::IDX_CURRENT), r.second});
+                pw.t = Type::STRING;
+            }
             p->with.push_back(std::move(pw));
             if (std::find(streamsSeen.begin(), streamsSeen.end(), si) == streamsSeen.end()) {
                 streamsSeen.push_back(si);

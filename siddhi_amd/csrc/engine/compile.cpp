@@ -155,6 +155,11 @@ class QC {
         partition_keys();
         p.partitioned = q_.partition_index >= 0;
         detect_chain(root);
+        for (int ka : h_.key_attr)
+            if (ka == -2) {  // an event may go to several keys (one view row each): the generic NFA
+                p.chain = 0;
+                h_.chain_reason = "range partition";
+            }
         if (p.has_post) {  // the selector's post pass reads every record's key: the generic NFA writes it
             p.chain = 0;
             h_.chain_reason = "aggregators / having in the selector";
@@ -885,6 +890,7 @@ class QC {
     void partition_keys() {
         h_.key_attr.assign(h_.streams.size(), -1);
         h_.key_kind.assign(h_.streams.size(), 0);
+        h_.key_ranges.assign(h_.streams.size(), {});
         if (q_.partition_index < 0) return;
         const sql::Partition& part = app_.partitions[q_.partition_index];
         for (size_t i = 0; i < h_.streams.size(); ++i) {
@@ -893,6 +899,28 @@ class QC {
             for (const auto& w : part.with) {
                 if (w.stream_id != def.id) continue;
                 if (found) throw CompileError(SDG_ERR_UNSUPPORTED, "a stream partitioned twice is not supported");
+                if (!w.ranges.empty()) {  // RangePartitionExecutor per range: condition over the stream's event
+                    Meta saved = meta_;
+                    meta_.defs = {&def};
+                    meta_.refs = {""};
+                    meta_.multi = {false};
+                    for (const auto& r : w.ranges) {
+                        HostQuery::RangeKey rk;
+                        rk.cond.start = (int)h_.code.size();
+                        cond(r.first, 0, sql::IDX_CURRENT);
+                        rk.cond.len = (int)h_.code.size() - rk.cond.start;
+                        check_stack(rk.cond);
+                        rk.label = strings_.get(r.second);
+                        h_.key_ranges[i].push_back(rk);
+                    }
+                    meta_ = saved;
+                    if (h_.key_ranges[i].size() > 255) throw CompileError(SDG_ERR_UNSUPPORTED, "more than 255 partition ranges");
+                    h_.key_attr[i] = -2;
+                    h_.key_kind[i] = VK_STR;
+                    h_.plan.chain = 0;
+                    found = true;
+                    continue;
+                }
                 if (w.expr->kind != sql::ExprKind::VAR || !w.expr->stream_ref.empty() || w.expr->has_index)
                     throw CompileError(SDG_ERR_UNSUPPORTED, "value partitions must be a plain attribute of the stream");
                 int ai = def.index_of(w.expr->attr);

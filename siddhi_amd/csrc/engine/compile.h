@@ -37,7 +37,12 @@ struct HostQuery {
     std::vector<int> streams;                          // app stream index, receiver (first appearance) order
     std::vector<std::pair<std::string, uint8_t>> cols; // physical column (attribute name, kind)
     std::vector<std::vector<int>> col_attr;            // [query stream][column] -> attribute index or -1
-    std::vector<int> key_attr;                         // [query stream] partition key attribute (-1: none)
+    std::vector<int> key_attr;                         // [query stream] partition key attribute (-1: none, -2: ranges)
+    struct RangeKey {
+        Prog cond;                                     // over the stream's event (OP_LOAD slot 0, physical columns)
+        uint32_t label;                                // interned label: the partition key when cond holds
+    };
+    std::vector<std::vector<RangeKey>> key_ranges;     // [query stream] range partition executors, in order
     std::vector<uint8_t> key_kind;                     // [query stream] kind of that attribute
     std::vector<std::string> out_names;
     std::vector<int32_t> out_types;

@@ -176,9 +176,9 @@ struct QueryRt {
     std::vector<uint32_t> taken;
     std::vector<std::unique_ptr<KeyRun>> runs;
     // batch staging
-    DevBuf st_ts, st_qs, st_key, st_cols[MAX_COLS], st_nulls[MAX_COLS];
+    DevBuf st_ts, st_qs, st_key, st_vrank, st_cols[MAX_COLS], st_nulls[MAX_COLS];
     // sorted view
-    DevBuf so_ts, so_qs, so_key, so_orig, so_cols[MAX_COLS], so_nulls[MAX_COLS], seg, kg_counts, kg_gsum;
+    DevBuf so_ts, so_qs, so_key, so_orig, so_vrank, so_cols[MAX_COLS], so_nulls[MAX_COLS], seg, kg_counts, kg_gsum;
     DevBuf bk_plan;                                 // fused path: bstart[257] + bseg[257]
     // carries (double buffered)
     struct Carry {
@@ -335,6 +335,33 @@ bool slot_key(sdg_engine* e, QueryRt& q, int qpos, int64_t slot, uint32_t* key) 
     *key = it->second;
     if (integral) q.intkeys.insert(iv, *key);
     return true;
+}
+
+// RangePartitionExecutor.execute (core/partition/executor/RangePartitionExecutor.java): the range condition over
+// one pushed row (the same bytecode interpreter as the device, eval.h, on the row's attributes). Keys are computed
+// on the host for host pushes, like the value partitions' toString keys.
+struct RowAcc {
+    const HostQuery* h;
+    int qpos;
+    const PushChunk* c;
+    int64_t r;
+    bool mixed;  // attribute a of row r is the 64-bit slot cols[a][r]
+    void load(int, int col, int, uint8_t kind, int64_t* v, bool* null) {
+        const int ai = h->col_attr[qpos][col];
+        *v = 0;
+        *null = true;
+        if (ai < 0) return;
+        *null = !c->nulls[ai].empty() && c->nulls[ai][r];
+        if (mixed) *v = ((const int64_t*)c->cols[ai].data())[r];
+        else *v = load_col(c->cols[ai].data(), kind, r);
+    }
+    bool slot_empty(int, int) { return false; }
+    void agg(int, int64_t* v, bool* n) { *v = 0; *n = true; }
+};
+int64_t range_stack[STACK];
+bool range_holds(const HostQuery& h, const HostQuery::RangeKey& rk, int qpos, const PushChunk& c, int64_t r, bool mixed) {
+    RowAcc acc{&h, qpos, &c, r, mixed};
+    return pass(h.code.data(), rk.cond, h.consts.data(), acc, range_stack, 1);
 }
 
 // chain_match_k's LDS tile: the columns the state-1 filter reads from its own event (the scanned rows), and
@@ -578,6 +605,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     const void* d_cols[MAX_COLS] = {};
     const uint8_t* d_nulls[MAX_COLS] = {};
     int64_t nrows = 0;
+    const bool ranged = std::find(h.key_attr.begin(), h.key_attr.end(), -2) != h.key_attr.end();
+    const uint8_t* d_vrank = nullptr;
     bool zero_copy = parts.size() == 1 && parts[0]->device && !multi_stream && parts[0]->stream >= 0;
     if (zero_copy) {
         const PushChunk& c = *parts[0];
@@ -591,6 +620,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             if (!d_cols[k]) d_cols[k] = q.st_cols[k].ensure((size_t)std::max<int64_t>(n, 1) * width_of(P.col_kind[k]));
         }
         if (partitioned) {
+            if (ranged) throw CompileError(SDG_ERR_UNSUPPORTED, "device-resident batches of a range partition");
             if (!q.string_keys) throw CompileError(SDG_ERR_UNSUPPORTED, "device-resident batches need string partition keys");
             int ai = h.key_attr[qpos];
             if (c.d_nulls[ai]) throw CompileError(SDG_ERR_UNSUPPORTED, "null partition keys in device-resident batches");
@@ -605,6 +635,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         std::vector<std::vector<uint8_t>> cols(nc), nulls(nc);
         std::vector<bool> any_null(nc, false);
         std::vector<uint32_t> vpos;
+        std::vector<uint8_t> vrank;  // range partitions: the range each view row came from (its delivery sub-order)
         ts.reserve(n);
         vpos.reserve(n);
         for (int k = 0; k < nc; ++k) cols[k].reserve((size_t)n * width_of(P.col_kind[k]));
@@ -616,12 +647,21 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                     const int qpos = h.stream_pos(c->rstream[r]);
                     if (qpos < 0) continue;
                     uint32_t key = 0;
-                    if (partitioned) {
+                    int copies = 1;
+                    std::vector<uint32_t> rkeys;
+                    if (partitioned && h.key_attr[qpos] == -2) {
+                        const auto& rs = h.key_ranges[qpos];
+                        for (size_t x = 0; x < rs.size(); ++x)
+                            if (range_holds(h, rs[x], qpos, *c, r, true)) rkeys.push_back((uint32_t)x);
+                        copies = (int)rkeys.size();
+                    } else if (partitioned) {
                         const int ai = h.key_attr[qpos];
                         if (!c->nulls[ai].empty() && c->nulls[ai][r]) continue;  // null partition key: dropped
                         if (!slot_key(e, q, qpos, ((const int64_t*)c->cols[ai].data())[r], &key)) continue;
-                        keys.push_back(key);
                     }
+                    for (int cp = 0; cp < copies; ++cp) {
+                    if (partitioned) keys.push_back(rkeys.empty() ? key : h.key_ranges[qpos][rkeys[cp]].label);
+                    if (ranged) vrank.push_back(rkeys.empty() ? 0 : (uint8_t)rkeys[cp]);
                     const size_t row = ts.size();
                     ts.push_back(c->ts[r]);
                     vpos.push_back((uint32_t)(part_pos[pi] + r));
@@ -639,6 +679,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                             any_null[k] = true;
                         }
                     }
+                    }
                 }
                 continue;
             }
@@ -648,7 +689,17 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             std::vector<int64_t> kept;
             bool all = true;
             const size_t base = ts.size();
-            if (partitioned) {
+            if (partitioned && h.key_attr[qpos] == -2) {  // one view row per range that holds (in range order)
+                all = false;
+                const auto& rs = h.key_ranges[qpos];
+                for (int64_t r = 0; r < c->n; ++r)
+                    for (size_t x = 0; x < rs.size(); ++x)
+                        if (range_holds(h, rs[x], qpos, *c, r, false)) {
+                            keys.push_back(rs[x].label);
+                            kept.push_back(r);
+                            vrank.push_back((uint8_t)x);
+                        }
+            } else if (partitioned) {
                 keys.reserve(keys.size() + (size_t)c->n);
                 for (int64_t r = 0; r < c->n; ++r) {
                     uint32_t key = 0;
@@ -665,6 +716,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 }
             }
             const size_t m = all ? (size_t)c->n : kept.size();
+            if (ranged && h.key_attr[qpos] != -2) vrank.resize(base + m, 0);
             if (all) ts.insert(ts.end(), c->ts.begin(), c->ts.begin() + c->n);
             else for (int64_t r : kept) ts.push_back(c->ts[r]);
             if (all) for (int64_t r = 0; r < c->n; ++r) vpos.push_back((uint32_t)(part_pos[pi] + r));
@@ -712,6 +764,10 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             d_key = (const uint32_t*)q.st_key.ensure(cnt * 4);
             if (nrows) HIPCHECK(hipMemcpyAsync((void*)d_key, keys.data(), nrows * 4, hipMemcpyHostToDevice, st));
         }
+        if (ranged) {
+            d_vrank = (const uint8_t*)q.st_vrank.ensure(cnt);
+            if (nrows) HIPCHECK(hipMemcpyAsync((void*)d_vrank, vrank.data(), nrows, hipMemcpyHostToDevice, st));
+        }
         for (int k = 0; k < nc; ++k) {
             int w = width_of(P.col_kind[k]);
             d_cols[k] = q.st_cols[k].ensure(cnt * w);
@@ -753,6 +809,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     // ---- 2. key grouping ---------------------------------------------------------------------------------
     const int64_t* v_ts = d_ts;
     const uint8_t* v_qs = d_qs;
+    const uint8_t* v_vrank = d_vrank;
     const uint32_t* v_key = nullptr;
     const uint32_t* v_seg = nullptr;
     const uint32_t* v_orig = d_vpos;  // partitioned: replaced by orig_sorted (positions when d_vpos is set)
@@ -776,6 +833,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         int c = 0;
         a.src[c] = d_ts; a.dst[c] = q.so_ts.ensure(nrows * 8); a.width[c] = 8; v_ts = (const int64_t*)a.dst[c]; ++c;
         if (d_qs) { a.src[c] = d_qs; a.dst[c] = q.so_qs.ensure(nrows); a.width[c] = 1; v_qs = (const uint8_t*)a.dst[c]; ++c; }
+        if (d_vrank) { a.src[c] = d_vrank; a.dst[c] = q.so_vrank.ensure(nrows); a.width[c] = 1; v_vrank = (const uint8_t*)a.dst[c]; ++c; }
         for (int k = 0; k < nc; ++k) {
             if (c >= MAX_COLS + 2) throw CompileError(SDG_ERR_UNSUPPORTED, "too many columns");
             int w = width_of(P.col_kind[k]);
@@ -834,6 +892,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         a.n = nrows;
         a.ts = v_ts;
         a.qstream = multi_stream ? v_qs : nullptr;
+        a.vrank = v_vrank;
         a.seg_start = partitioned ? v_seg : nullptr;
         a.seg_end = partitioned ? v_segend : nullptr;
         a.K = partitioned ? (int32_t)K : 1;

@@ -1244,6 +1244,8 @@ struct KeyEvents {
     const uint8_t* const* nulls;
     int64_t b, e, seq_base;
     int64_t pos_off;          // batch position of row 0 when orig is nullptr
+    const uint8_t* vrank = nullptr;  // range partitions: the range a row came from -- one event sent to several keys
+                                     // is processed key after key in range order (PartitionStreamReceiver.receive)
 };
 
 // one key's batch run, in steps (the device composes them in run_key; the host scheduler simulation steps a key
@@ -1306,7 +1308,7 @@ SDG_HD bool key_row(CtxT<TM>& c, const KeyEvents& ev, int64_t p, bool& need_init
     }
     rec.nullmask = nm;
     c.cur_seq = ev.seq_base + g;
-    c.cur_sub = 0;
+    c.cur_sub = ev.vrank ? (int64_t)ev.vrank[p] << 40 : 0;
     c.on_event(ev.qstream ? ev.qstream[p] : 0, r, ts);
     if (TM && P->n_sched) c.absent_gc();
     return !c.ovf();

@@ -393,7 +393,7 @@ __global__ __launch_bounds__(256) void nfa_k(const NfaArgs* __restrict__ pa) {
     }
     // last_seen is stored XOR INT64_MIN, so the zero-filled array reads as "never seen"
     if (a.last_seen) c.purge = nfa::PurgeIn{a.purge_clk, a.purge_from, a.purge_idle, a.last_seen[k] ^ INT64_MIN};
-    nfa::KeyEvents ev{a.ts, a.qstream, a.orig, a.cols, a.nulls, b, e, a.seq_base, a.pos_off};
+    nfa::KeyEvents ev{a.ts, a.qstream, a.orig, a.cols, a.nulls, b, e, a.seq_base, a.pos_off, a.vrank};
     nfa::run_key(c, ev);
     if (a.last_seen) a.last_seen[k] = c.purge.last ^ INT64_MIN;
     if (c.ovf()) atomicOr(&a.flags[2], 1);

@@ -135,8 +135,11 @@ struct Query {
 };
 
 struct PartitionWith {
-    ExprP expr;                 // value partition expression
+    ExprP expr;                 // value partition expression (null for a range partition)
     std::string stream_id;
+    // range partition `c1 as 'l1' or c2 as 'l2' of S` (RangePartitionType): one RangePartitionExecutor per range,
+    // each sends the event to partition key `label` when its condition holds (an event may go to several keys)
+    std::vector<std::pair<ExprP, std::string>> ranges;
 };
 
 struct Partition {

@@ -314,8 +314,21 @@ class Parser {
         int pidx = (int)app.partitions.size();
         while (true) {
             PartitionWith w;
-            w.expr = parse_expr();
-            if (kw("as")) throw Unsupported("range partitions are out of scope (value partitions only)");
+            ExprP first = parse_expr();
+            if (kw("as")) {  // condition_ranges: condition_range (or condition_range)*, condition_range: expr as 'label'
+                auto range = [&](ExprP cond) {
+                    expect_kw("as");
+                    if (cur().kind != Tok::STR) throw ParseError("range partition label must be a string at " + std::to_string(cur().pos));
+                    w.ranges.push_back({cond, t_[p_++].text});
+                };
+                range(first);
+                while (kw("or")) {
+                    ++p_;
+                    range(parse_expr());
+                }
+            } else {
+                w.expr = first;
+            }
             expect_kw("of");
             w.stream_id = name();
             part.with.push_back(w);

@@ -403,6 +403,9 @@ void* emu_create(const char* text, int max_partials) {
             const Plan& P = q->hq.plan;
             if (P.has_post)  // the selector's post pass runs on the device only (order.hip select_post)
                 throw std::runtime_error("selector post pass (aggregators / having) is device-only");
+            for (int ka : q->hq.key_attr)
+                if (ka == -2) throw std::runtime_error("range partitions: the engine's batch assembly only");
+            if (P.purge) throw std::runtime_error("@purge: the engine's kernel arguments only");
             q->L = nfa::make_layout(P.n_states, std::max(P.n_cols, 1), e->ns, P.n_sched);
             q->sim.setup(P.n_sched, P.partitioned, !e->app.playback);
             e->qs.push_back(std::move(q));

@@ -223,3 +223,20 @@ def purge_trace(n, keys=8, burst=120, seed=0):
         k = (i // burst) % keys if rng.random() < 0.9 else int(rng.integers(0, keys))
         out.append((s, int(ts[i]), [i, "k%d" % k, float(np.round(rng.uniform(0, 100), 1)), int(rng.integers(0, 100))]))
     return out
+
+
+# ---- range partitions (RangePartitionExecutor): overlapping ranges send one event to several keys ----
+RANGE_APPS = {
+    "range_disjoint": flat("partition with (price < 30 as 'low' or price >= 30 and price < 70 as 'mid' or "
+                           "price >= 70 as 'high' of S, volume < 50 as 'low' or volume >= 50 as 'high' of T) begin "
+                           "@info(name='q') from every e1=S[volume>40] -> e2=T[price>e1.price] "
+                           "select e1.id as a, e2.id as b insert into O; end;"),
+    "range_overlap": flat("partition with (price < 60 as 'a' or price > 40 as 'b' or volume > 80 as 'c' of S, "
+                          "price < 60 as 'a' or price > 40 as 'b' of T) begin "
+                          "@info(name='q') from every e1=S[volume>30] -> e2=T[volume>e1.volume] "
+                          "select e1.id as a, e2.id as b insert into O; end;"),
+    "range_sequence": flat("partition with (price < 50 as 'lo' or price >= 50 as 'hi' of S, "
+                           "price < 50 as 'lo' or price >= 50 as 'hi' of T) begin "
+                           "@info(name='q') from every e1=S[volume>20], e2=T[volume>e1.volume]+, e3=S[volume<e2[0].volume] "
+                           "select e1.id as a, e2[0].id as b, e3.id as c insert into O; end;"),
+}

@@ -113,3 +113,22 @@ def test_purge_on_gpu(name, batches, oracle_built):
     finally:
         p.close()
     assert got == ref
+
+
+@pytest.mark.parametrize("name", sorted(synth.RANGE_APPS))
+@pytest.mark.parametrize("batches", [1, 3])
+def test_range_partitions_on_gpu(name, batches, oracle_built):
+    """range partitions: one view row per range that holds, processed in range order within the event"""
+    app = synth.RANGE_APPS[name]
+    tr = synth.trace(3000, keys=1, seed=21, null_rate=0.03)
+    o = Oracle(app)
+    try:
+        ref = synth.run(o, tr)
+    finally:
+        o.close()
+    p = ProductAdapter(app)
+    try:
+        got = synth.run(p, tr, batches)
+    finally:
+        p.close()
+    assert len(ref) > 50 and got == ref
