@@ -124,6 +124,12 @@ int64_t sdg_pending(sdg_engine* e);
 int sdg_flush(sdg_engine* e);
 int sdg_sync(sdg_engine* e);
 int sdg_poll(sdg_engine* e, int query, sdg_out* out);
+/* a multi-value selection (`e1.price` of a count state e1 without [index]: MultiValueVariableFunctionExecutor,
+ * ExpressionParser.java:1430-1436) in the last sdg_poll: values[attr][i] is record i's list length; its elements are
+ * items[0..cap)[i] / item_nulls[0..cap)[i] (elements past the length are null), typed *elem_type. *cap = 0: attr is
+ * not a list. Valid until the next sdg_poll. */
+int sdg_poll_list(sdg_engine* e, int query, int attr, int32_t* cap, int32_t* elem_type, const int64_t* const** items,
+                  const uint8_t* const** item_nulls);
 /* drop every query's unpolled results without reading them back (measurement of the device-resident path; an
  * application that wants its matches polls instead) */
 int sdg_discard(sdg_engine* e);

@@ -135,6 +135,9 @@ def load_library():
     L.sdg_sync.argtypes = [P]
     L.sdg_poll.argtypes = [P, I32, ctypes.POINTER(_Out)]
     L.sdg_discard.argtypes = [P]
+    L.sdg_poll_list.argtypes = [P, I32, I32, ctypes.POINTER(I32), ctypes.POINTER(I32),
+                                ctypes.POINTER(ctypes.POINTER(ctypes.POINTER(I64))),
+                                ctypes.POINTER(ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)))]
     L.sdg_snapshot.argtypes = [P, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(I64)]
     L.sdg_restore.argtypes = [P, ctypes.c_char_p, I64]
     L.sdg_export_device.argtypes = [P, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), P, P, P, P]
@@ -440,14 +443,45 @@ class SiddhiAppRuntime:
         _check(self._L.sdg_last_stats(self._h, ctypes.byref(s)))
         return s
 
+    def _lists(self, q, n_attrs):
+        """multi-value selections of the last poll: {attr: (cap, items, item_nulls)}"""
+        res = {}
+        for j in range(n_attrs):
+            cap, et = ctypes.c_int32(), ctypes.c_int32()
+            items = ctypes.POINTER(ctypes.POINTER(ctypes.c_int64))()
+            nls = ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8))()
+            _check(self._L.sdg_poll_list(self._h, q, j, ctypes.byref(cap), ctypes.byref(et), ctypes.byref(items),
+                                         ctypes.byref(nls)))
+            if cap.value:
+                res[j] = (cap.value, items, nls)
+        return res
+
+    def _decode(self, t, v):
+        if t == INT:
+            return ctypes.c_int32(v).value
+        if t == LONG:
+            return v
+        if t == FLOAT:
+            return struct.unpack("<f", struct.pack("<I", v & 0xffffffff))[0]
+        if t == DOUBLE:
+            return struct.unpack("<d", struct.pack("<q", v))[0]
+        if t == BOOL:
+            return bool(v)
+        return self.string(v)
+
     def poll(self, q):
         out = _Out()
         _check(self._L.sdg_poll(self._h, q, ctypes.byref(out)))
         name, target, types, names = self._queries[q]
+        lists = self._lists(q, len(types))
         evs = []
         for i in range(out.n):
             data = []
             for j, t in enumerate(types):
+                if j in lists:  # a multi-value selection: the list of the count state's values
+                    _, items, nls = lists[j]
+                    data.append([None if nls[e][i] else self._decode(t, items[e][i]) for e in range(out.values[j][i])])
+                    continue
                 if out.nulls[j][i]:
                     data.append(None)
                     continue
@@ -504,9 +538,16 @@ class SiddhiAppRuntime:
         _check(self._L.sdg_poll(self._h, q, ctypes.byref(out)))
         n = out.n
         types = self._queries[q][2]
-        return types, [out.ts[i] for i in range(n)], \
-            [[out.values[j][i] for i in range(n)] for j in range(len(types))], \
-            [[out.nulls[j][i] for i in range(n)] for j in range(len(types))]
+        lists = self._lists(q, len(types))
+        vals = []
+        for j in range(len(types)):
+            if j in lists:  # multi-value selection: a list of payloads (None = null element) per record
+                _, items, nls = lists[j]
+                vals.append([[None if nls[e][i] else items[e][i] for e in range(out.values[j][i])] for i in range(n)])
+            else:
+                vals.append([out.values[j][i] for i in range(n)])
+        return types, [out.ts[i] for i in range(n)], vals, \
+            [[0 if j in lists else out.nulls[j][i] for i in range(n)] for j in range(len(types))]
 
 
 class InMemoryPersistenceStore:

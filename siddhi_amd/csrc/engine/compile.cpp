@@ -88,9 +88,29 @@ class QC {
             bool multi = false;
             uint8_t k = expr(oa.expr, -1, 0, &multi);
             pr.len = (int)h_.code.size() - pr.start;
-            if (multi)
-                throw CompileError(SDG_ERR_UNSUPPORTED,
-                                   "multi-value selection of a count state (no [index]) is not supported on device");
+            if (multi) {
+                // MultiValueVariableFunctionExecutor (ExpressionParser.java:1430-1436): the attribute over the count
+                // state's whole chain. The column holds the chain length; element e is the hidden column
+                // out_list_col + e, `slot[e].attr` evaluated at emission (null past the end)
+                const Instr ld = h_.code.back();
+                h_.code.resize(pr.start);
+                const int mc = rows_[ld.a].max_count;
+                const int cap = (mc > 0 && mc <= 16) ? mc : 16;  // unbounded counts: 16, longer lists fail the flush
+                emit(OP_SLOTLEN, VK_I64, ld.a, 0, cap + 1);
+                pr.len = 1;
+                p.out_multi[i] = 1;
+                p.out_list_cap[i] = cap;
+                p.out_list_col[i] = p.n_out;
+                for (int el = 0; el < cap; ++el) {
+                    const int col = new_col(k);
+                    Prog ep;
+                    ep.start = (int)h_.code.size();
+                    emit(OP_LOAD, k, ld.a, ld.b, el);
+                    ep.len = 1;
+                    p.out_prog[col] = ep;
+                }
+                p.n_list_cols += cap;
+            }
             check_stack(pr);
             p.out_prog[i] = pr;
             p.out_kind[i] = k;
@@ -138,6 +158,7 @@ class QC {
             p.st[s] = rows_[s];
             p.fast[s] = fast_pred(rows_[s].filter);
         }
+        partition_keys();  // range conditions may reference attributes nothing else reads: before the column table
         // physical columns
         if ((int)h_.cols.size() > MAX_COLS) throw CompileError(SDG_ERR_UNSUPPORTED, "too many referenced attributes");
         p.n_cols = (int)h_.cols.size();
@@ -152,7 +173,6 @@ class QC {
                 if (ai >= 0 && (uint8_t)def.attrs[ai].type == h_.cols[c].second) h_.col_attr[i][c] = ai;
             }
         }
-        partition_keys();
         p.partitioned = q_.partition_index >= 0;
         detect_chain(root);
         for (int ka : h_.key_attr)
@@ -383,7 +403,7 @@ class QC {
             if (has_agg(k)) return true;
         return false;
     }
-    int new_col(uint8_t kind) {
+    int new_col(uint8_t kind) {  // (list element columns first: they follow the select list directly)
         Plan& p = h_.plan;
         if (p.n_out >= MAX_OUT) throw CompileError(SDG_ERR_UNSUPPORTED, "too many output + hidden selector columns");
         p.out_kind[p.n_out] = kind;

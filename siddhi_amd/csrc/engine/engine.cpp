@@ -1624,12 +1624,12 @@ void drain(sdg_engine* e, QueryRt& q) {
         pa.agg_state = (int64_t*)q.agg_state.p;
         select_post(pa, q.hq.plan.partitioned ? dk : nullptr, kbits, q.ps_ws.ensure(select_post_workspace(nk)), st);
         fpass.resize(nk);
-        HIPCHECK(hipMemcpyAsync(fv.data(), dv, (size_t)P.n_user_out * nk * 8, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(fv.data(), dv, (size_t)(P.n_user_out + P.n_list_cols) * nk * 8, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipMemcpyAsync(fn.data(), dn, (size_t)nk * 4, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipMemcpyAsync(fpass.data(), dp, (size_t)nk, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
     }
-    const int nu = q.hq.plan.n_user_out;
+    const int nu = q.hq.plan.n_user_out + q.hq.plan.n_list_cols;  // the select list, then list elements
     int64_t keep = nk;
     if (post) keep = (int64_t)std::count(fpass.begin(), fpass.end(), (uint8_t)1);
     const size_t b = q.acc_ts.size();
@@ -1653,6 +1653,10 @@ void drain(sdg_engine* e, QueryRt& q) {
             q.acc_vals[j][o] = post ? fv[(size_t)j * nk + i] : dev ? vals[(size_t)j * n + s] : hvals[(size_t)j * nh + hs];
             q.acc_nulls[j][o] = (nm >> j) & 1u;
         }
+        for (int j = 0; j < q.hq.plan.n_user_out; ++j)  // OP_SLOTLEN counted to cap + 1: a longer chain
+            if (q.hq.plan.out_multi[j] && q.acc_vals[j][o] > q.hq.plan.out_list_cap[j])
+                throw CompileError(SDG_ERR_CAPACITY, "query '" + q.hq.name + "': a multi-value selection holds more than " +
+                                                         std::to_string(q.hq.plan.out_list_cap[j]) + " events");
         ++o;
     }
     q.runs.clear();
@@ -2233,7 +2237,7 @@ int sdg_poll(sdg_engine* e, int qi, sdg_out* out) {
     if (!e || qi < 0 || qi >= (int)e->qs.size() || !out) return fail(SDG_ERR_ARG, "bad poll arguments");
     return guarded([&]() {
         QueryRt& q = *e->qs[qi];
-        const int na = q.hq.plan.n_user_out;
+        const int na = q.hq.plan.n_user_out + q.hq.plan.n_list_cols;  // list elements kept for sdg_poll_list
         if (!e->compile_only) drain(e, q);
         const int64_t n = (int64_t)q.acc_ts.size();
         q.h_ts.swap(q.acc_ts);
@@ -2258,7 +2262,7 @@ int sdg_poll(sdg_engine* e, int qi, sdg_out* out) {
         out->n = n;
         out->ts = q.h_ts.data();
         out->expired = q.h_expired.data();
-        out->n_attrs = na;
+        out->n_attrs = q.hq.plan.n_user_out;
         out->types = e->out_types[qi].data();
         out->values = q.h_vptr.data();
         out->nulls = q.h_nptr.data();
@@ -2276,6 +2280,20 @@ int sdg_discard(sdg_engine* e) {
         q->acc_vals.clear();
         q->acc_nulls.clear();
     }
+    return SDG_OK;
+}
+
+int sdg_poll_list(sdg_engine* e, int qi, int attr, int32_t* cap, int32_t* elem_type, const int64_t* const** items,
+                  const uint8_t* const** item_nulls) {
+    if (!e || qi < 0 || qi >= (int)e->qs.size() || !cap) return fail(SDG_ERR_ARG, "bad poll_list arguments");
+    QueryRt& q = *e->qs[qi];
+    const Plan& P = q.hq.plan;
+    if (attr < 0 || attr >= P.n_user_out) return fail(SDG_ERR_ARG, "bad attribute index");
+    *cap = P.out_multi[attr] ? P.out_list_cap[attr] : 0;
+    if (elem_type) *elem_type = P.out_kind[attr];
+    const size_t c0 = (size_t)P.out_list_col[attr];
+    if (items) *items = *cap && q.h_vptr.size() >= c0 + *cap ? q.h_vptr.data() + c0 : nullptr;
+    if (item_nulls) *item_nulls = *cap && q.h_nptr.size() >= c0 + *cap ? q.h_nptr.data() + c0 : nullptr;
     return SDG_OK;
 }
 

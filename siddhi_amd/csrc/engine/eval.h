@@ -277,6 +277,14 @@ SDG_FN void run(const Instr* __restrict__ code, Prog p, const int64_t* __restric
                 }
                 break;
             }
+            case OP_SLOTLEN: {  // MultiValueVariableFunctionExecutor's list size (ExpressionParser.java:1430-1436)
+                int n = 0;
+                while (n < in.c && !acc.slot_empty(in.a, n)) ++n;
+                stk[sp * stride] = n;
+                nulls &= ~(1u << sp);
+                ++sp;
+                break;
+            }
             case OP_AGG: {
                 int64_t v;
                 bool n;

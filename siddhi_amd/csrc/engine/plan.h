@@ -34,6 +34,7 @@ enum OpCode : uint8_t {
     OP_JAND,       // top not true: replace it by false and jump imm instructions ahead (past the right operand
                    // and its OP_AND); else fall through (AndConditionExpressionExecutor :65-74)
     OP_JOR,        // top true: replace it by true and jump imm ahead (OrConditionExpressionExecutor :65-76)
+    OP_SLOTLEN,    // push the length of state slot a's event chain, counting at most c (a multi-value selection)
 };
 // OP_LOAD slot of the selector's post pass (aggregates, having): column b of the output record being selected
 constexpr uint8_t OUT_SLOT = 0xFF;
@@ -130,7 +131,10 @@ struct Plan {
     int32_t n_user_out = 0;        // the select list (what sdg_poll returns)
     uint8_t out_kind[MAX_OUT];
     Prog out_prog[MAX_OUT];        // evaluated at emission (len 0: filled by the post pass)
-    uint8_t out_multi[MAX_OUT];    // multi-value (count state, no index) -> unsupported on device for now
+    uint8_t out_multi[MAX_OUT];    // multi-value selection (a count state without [index]): the column holds the
+                                   // list length, elements in out_list_cap hidden columns from out_list_col
+    int32_t out_list_col[MAX_OUT], out_list_cap[MAX_OUT];
+    int32_t n_list_cols = 0;       // hidden element columns, right after the select list
     uint8_t out_post[MAX_OUT];     // 1: a select item over aggregates, evaluated by the post pass (post_prog)
     Prog post_prog[MAX_OUT];
     int32_t n_agg = 0;

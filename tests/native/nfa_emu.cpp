@@ -406,6 +406,7 @@ void* emu_create(const char* text, int max_partials) {
             for (int ka : q->hq.key_attr)
                 if (ka == -2) throw std::runtime_error("range partitions: the engine's batch assembly only");
             if (P.purge) throw std::runtime_error("@purge: the engine's kernel arguments only");
+            if (P.n_list_cols) throw std::runtime_error("multi-value selections: the engine's poll only");
             q->L = nfa::make_layout(P.n_states, std::max(P.n_cols, 1), e->ns, P.n_sched);
             q->sim.setup(P.n_sched, P.partitioned, !e->app.playback);
             e->qs.push_back(std::move(q));

@@ -41,10 +41,24 @@ class ProductAdapter:
         self.rt.flush(deliver=False)
         for q, (name, target, types, names) in enumerate(self.rt._queries):
             types, ts, vals, nulls = self.rt.raw_outputs(q)
+            def dec(t, v):
+                if v is None:
+                    return None
+                if t == sa.INT:
+                    return ("i", ctypes.c_int32(v).value)
+                if t == sa.FLOAT:
+                    return ("f", v & 0xffffffff)
+                if t == sa.BOOL:
+                    return ("b", bool(v))
+                if t == sa.STRING:
+                    return ("s", self.rt.string(v))
+                return (TAG[t], v)
             for i in range(len(ts)):
                 row = []
                 for j, t in enumerate(types):
-                    if nulls[j][i]:
+                    if isinstance(vals[j][i], list):  # multi-value selection
+                        row.append(("list", tuple(dec(t, x) for x in vals[j][i])))
+                    elif nulls[j][i]:
                         row.append(None)
                     elif t == sa.INT:
                         row.append(("i", ctypes.c_int32(vals[j][i]).value))

@@ -240,3 +240,10 @@ RANGE_APPS = {
                            "@info(name='q') from every e1=S[volume>20], e2=T[volume>e1.volume]+, e3=S[volume<e2[0].volume] "
                            "select e1.id as a, e2[0].id as b, e3.id as c insert into O; end;"),
 }
+
+SELECT_APPS["multi_value"] = part(
+    "@info(name='q') from every e1=S[price>40]<1:4> -> e2=T[price>e1[0].price] "
+    "select e1.id as ids, e1.price as prices, e2.id as b, e1[0].volume as v0 insert into O;")
+SELECT_APPS["multi_value_seq"] = part(
+    "@info(name='q') from every e1=S[price>20], e2=T[price>e1.price]+, e3=S[price<e2[last].price] "
+    "select e1.id as a, e2.volume as vols, e3.id as c insert into O;")
