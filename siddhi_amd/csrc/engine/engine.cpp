@@ -573,7 +573,34 @@ void replay_carries(sdg_engine* e, QueryRt& q, const NfaArgs& a0, bool multi_str
     nfa_commit(q.cur_bits.as<uint8_t>(), q.ran_bits.as<uint8_t>(), q.arena_keys, st);  // the batch starts from it
 }
 
+// per-kernel HIP event timing (sdg_stats); SDG_NO_EVENTS=1 drops the event records (measuring their cost)
+const bool g_no_events = getenv("SDG_NO_EVENTS") != nullptr;
+void ev_record(hipEvent_t ev, hipStream_t st) {
+    if (!g_no_events) HIPCHECK(hipEventRecord(ev, st));
+}
+void ev_elapsed(float* ms, hipEvent_t a, hipEvent_t b) {
+    *ms = 0;
+    if (!g_no_events) HIPCHECK(hipEventElapsedTime(ms, a, b));
+}
+
+// SDG_HOST_PROF: host timestamps of a flush's phases (where the host, not the device, sets the pace)
+struct HostProf {
+    bool on = getenv("SDG_HOST_PROF") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), last = t0;
+    std::string s;
+    void mark(const char* what) {
+        if (!on) return;
+        auto t = std::chrono::steady_clock::now();
+        s += std::string(" ") + what + "=" + std::to_string(std::chrono::duration<double, std::micro>(t - last).count());
+        last = t;
+    }
+    ~HostProf() {
+        if (on) std::fprintf(stderr, "[host us]%s\n", s.c_str());
+    }
+};
+
 void flush_query(sdg_engine* e, QueryRt& q) {
+    HostProf hp;
     HostQuery& h = q.hq;
     Plan& P = h.plan;
     hipStream_t st = e->stream;
@@ -816,7 +843,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     const void* v_cols[MAX_COLS];
     const uint8_t* v_nulls[MAX_COLS];
     for (int k = 0; k < nc; ++k) { v_cols[k] = d_cols[k]; v_nulls[k] = d_nulls[k]; }
-    HIPCHECK(hipEventRecord(e->ev[0], st));
+    hp.mark("view");
+    ev_record(e->ev[0], st);
     const uint32_t* v_segend = nullptr;
     int* flags = (int*)q.flags.ensure(32);  // [0] output overflow [1] decreasing ts [2] bounds [3] mono [4] key range
     int bbits = 0;
@@ -857,7 +885,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             b_start = (uint32_t*)q.bk_plan.ensure(2 * 257 * 4);
             b_seg = b_start + 257;
             HIPCHECK(hipMemsetAsync(flags, 0, 32, st));
-            bucketize(a, bbits, 0 /* ts is payload column 0 */, flags + 3, b_start, b_seg, FU_OWN, st, &e->ev[4]);
+            bucketize(a, bbits, 0 /* ts is payload column 0 */, flags + 3, b_start, b_seg, FU_OWN, st, g_no_events ? nullptr : &e->ev[4]);
             if (getenv("SDG_DEBUG")) {  // validate the bucket plan on the host before the matcher reads it
                 std::vector<uint32_t> hp(2 * 257);
                 HIPCHECK(hipMemcpyAsync(hp.data(), b_start, 2 * 257 * 4, hipMemcpyDeviceToHost, st));
@@ -869,7 +897,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             }
         } else {
             HIPCHECK(hipMemsetAsync(flags, 0, 32, st));
-            keygroup(a, st, &e->ev[4]);
+            keygroup(a, st, g_no_events ? nullptr : &e->ev[4]);
         }
         v_key = a.keys_sorted;
         v_seg = a.seg_start;
@@ -882,7 +910,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         HIPCHECK(hipMemsetAsync((void*)v_seg, 0, (size_t)K * 4, st));
         HIPCHECK(hipMemsetAsync((void*)v_segend, 0, (size_t)K * 4, st));
     }
-    HIPCHECK(hipEventRecord(e->ev[1], st));
+    hp.mark("keygroup_enqueue");
+    ev_record(e->ev[1], st);
     if (!P.chain) {
         NfaArgs a;
         std::memset(&a, 0, sizeof a);
@@ -1002,14 +1031,14 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             }
             *h_na = a;
             HIPCHECK(hipMemcpyAsync(d_na, h_na, sizeof(NfaArgs), hipMemcpyHostToDevice, st));
-            HIPCHECK(hipEventRecord(e->ev[10], st));
+            ev_record(e->ev[10], st);
             nfa_run(a, d_na, st);
-            HIPCHECK(hipEventRecord(e->ev[11], st));
+            ev_record(e->ev[11], st);
             HIPCHECK(hipMemcpyAsync(hc, counters, 16, hipMemcpyDeviceToHost, st));
             HIPCHECK(hipMemcpyAsync(hf, flags, 32, hipMemcpyDeviceToHost, st));
             HIPCHECK(hipStreamSynchronize(st));
             float kms = 0;
-            HIPCHECK(hipEventElapsedTime(&kms, e->ev[10], e->ev[11]));
+            ev_elapsed(&kms, e->ev[10], e->ev[11]);
             e->stats.ms_nfa_kernel += kms;
             if (hf[4]) throw CompileError(SDG_ERR_ARG, "device-resident partition key ids out of range (not from sdg_intern)");
             if (hf[2] && q.L.ns < 4096) {  // grow the arenas and rerun (state is double-buffered)
@@ -1042,7 +1071,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             return ok;
         };
         bind_out();
-        HIPCHECK(hipEventRecord(e->ev[8], st));
+        ev_record(e->ev[8], st);
         auto first_run = [&]() {
             a.list = nullptr;
             a.nlist = 0;
@@ -1207,22 +1236,22 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                                       (e->stats.ms_nfa_kernel - k_before);
         }
         nfa_commit(q.cur_bits.as<uint8_t>(), q.ran_bits.as<uint8_t>(), q.arena_keys, st);
-        HIPCHECK(hipEventRecord(e->ev[2], st));
+        ev_record(e->ev[2], st);
         HIPCHECK(hipStreamSynchronize(st));
         float ms_kg = 0, ms_m = 0, t;
-        HIPCHECK(hipEventElapsedTime(&ms_kg, e->ev[0], e->ev[1]));
-        HIPCHECK(hipEventElapsedTime(&ms_m, e->ev[1], e->ev[2]));
+        ev_elapsed(&ms_kg, e->ev[0], e->ev[1]);
+        ev_elapsed(&ms_m, e->ev[1], e->ev[2]);
         e->stats.ms_keygroup += ms_kg;
         e->stats.ms_match += ms_m;
         if (partitioned && nrows > 0) {
-            HIPCHECK(hipEventElapsedTime(&t, e->ev[4], e->ev[5]));
+            ev_elapsed(&t, e->ev[4], e->ev[5]);
             e->stats.ms_kg_hist += t;
-            HIPCHECK(hipEventElapsedTime(&t, e->ev[6], e->ev[7]));
+            ev_elapsed(&t, e->ev[6], e->ev[7]);
             e->stats.ms_kg_prefix += t;
-            HIPCHECK(hipEventElapsedTime(&t, e->ev[5], e->ev[6]));
+            ev_elapsed(&t, e->ev[5], e->ev[6]);
             e->stats.ms_kg_scatter += t;
         }
-        HIPCHECK(hipEventElapsedTime(&t, e->ev[8], e->ev[2]));
+        ev_elapsed(&t, e->ev[8], e->ev[2]);
         e->stats.ms_nfa += t;
         e->stats.events += nrows;
         q.out_n = (int64_t)hc[0];
@@ -1321,7 +1350,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     dbg_sync("bucketize / staging");
     chain_carry(a, d_a, st);
     dbg_sync("chain_carry_k");
-    HIPCHECK(hipEventRecord(e->ev[8], st));
+    ev_record(e->ev[8], st);
     if (fused) {
         const int64_t grid = chain_fused_grid(nrows, a.nb);
         static int64_t* trace = nullptr;
@@ -1338,7 +1367,9 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             a.dbg = (volatile int64_t*)dp;
             HIPCHECK(hipMemcpyAsync(d_a, &a, sizeof a, hipMemcpyHostToDevice, st));
         }
+        hp.mark("chain_setup+carry");
         chain_fused(a, d_a, grid, st);
+        hp.mark("fused_enqueue");
         if (dbg) {
             hipError_t err = hipStreamSynchronize(st);
             if (err != hipSuccess) {
@@ -1359,19 +1390,19 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 throw DeviceError(m);
             }
         }
-        HIPCHECK(hipEventRecord(e->ev[9], st));
+        ev_record(e->ev[9], st);
         chain_fovf(a, d_a, st);
         dbg_sync("chain_fovf_k");
     } else if (a.deque_mode != DQ_OFF && nrows > 0) {
         chain_deque(a, d_a, st);
-        HIPCHECK(hipEventRecord(e->ev[9], st));
+        ev_record(e->ev[9], st);
         chain_match(h_a[1], d_a + 1, st);
     } else {
-        HIPCHECK(hipEventRecord(e->ev[9], st));
+        ev_record(e->ev[9], st);
         chain_match(a, d_a, st);
     }
     e->stats.match_launches += (cin.n > 0) + (nrows > 0);
-    HIPCHECK(hipEventRecord(e->ev[2], st));
+    ev_record(e->ev[2], st);
     uint8_t* ret = (uint8_t*)q.h_ret.ensure(56);
     unsigned long long* hc = (unsigned long long*)ret;
     int* hf = (int*)(ret + 16);
@@ -1380,7 +1411,9 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     HIPCHECK(hipMemcpyAsync(hc, counters, 16, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipMemcpyAsync(hf, flags, 32, hipMemcpyDeviceToHost, st));
     if (fused) HIPCHECK(hipMemcpyAsync(&hovf, a.ovf_count, 8, hipMemcpyDeviceToHost, st));
+    hp.mark("tail_enqueue");
     HIPCHECK(hipStreamSynchronize(st));
+    hp.mark("sync_wait");
     if (hf[4]) throw CompileError(SDG_ERR_ARG, "device-resident partition key ids out of range (not from sdg_intern)");
     if (fused && hf[2]) throw DeviceError("fused matcher bounds check failed: bits " + std::to_string(hf[2]));
     if (fused && hf[3]) {  // batch timestamps not in arrival order (or a block's span over 2^32 ms): radix path
@@ -1391,25 +1424,25 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     e->stats.fused = fused ? 1 : e->stats.fused;
     e->stats.fused_ovf += (int64_t)hovf;
     float ms_kg = 0, ms_m = 0;
-    HIPCHECK(hipEventElapsedTime(&ms_kg, e->ev[0], e->ev[1]));
-    HIPCHECK(hipEventElapsedTime(&ms_m, e->ev[1], e->ev[2]));
+    ev_elapsed(&ms_kg, e->ev[0], e->ev[1]);
+    ev_elapsed(&ms_m, e->ev[1], e->ev[2]);
     e->stats.ms_keygroup += ms_kg;
     e->stats.ms_match += ms_m;
     float t;
     if (partitioned && nrows > 0) {
         // radix: [4]..[5] first hist+prefix, [5]..[6] scatter passes (+ later hist/prefix), [6]..[7] segments
-        HIPCHECK(hipEventElapsedTime(&t, e->ev[4], e->ev[5]));
+        ev_elapsed(&t, e->ev[4], e->ev[5]);
         e->stats.ms_kg_hist += t;
-        HIPCHECK(hipEventElapsedTime(&t, e->ev[6], e->ev[7]));
+        ev_elapsed(&t, e->ev[6], e->ev[7]);
         e->stats.ms_kg_prefix += t;
-        HIPCHECK(hipEventElapsedTime(&t, e->ev[5], e->ev[6]));
+        ev_elapsed(&t, e->ev[5], e->ev[6]);
         e->stats.ms_kg_scatter += t;
     }
-    HIPCHECK(hipEventElapsedTime(&t, e->ev[1], e->ev[8]));
+    ev_elapsed(&t, e->ev[1], e->ev[8]);
     e->stats.ms_chain_carry += t;
-    HIPCHECK(hipEventElapsedTime(&t, e->ev[8], e->ev[9]));
+    ev_elapsed(&t, e->ev[8], e->ev[9]);
     e->stats.ms_chain_match += t;
-    HIPCHECK(hipEventElapsedTime(&t, e->ev[9], e->ev[2]));
+    ev_elapsed(&t, e->ev[9], e->ev[2]);
     e->stats.ms_chain_emit += t;
     e->stats.deque = a.deque_mode;
     e->stats.events += nrows;
