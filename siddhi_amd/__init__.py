@@ -100,10 +100,11 @@ def load_library():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
+    path = os.environ.get("SDG_LIB", LIB_PATH)  # an alternative build of the same library (A/B measurements)
+    if not os.path.exists(path):
         raise DeviceError("siddhi_amd native library missing at %s — run __graft_entry__.build() "
                           "(make -C siddhi_amd); there is no CPU fallback" % LIB_PATH)
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     P, I32, I64, U32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint32
     L.sdg_compile.argtypes = [ctypes.c_char_p, ctypes.POINTER(_Opts), ctypes.POINTER(P)]
     L.sdg_destroy.argtypes = [P]

@@ -319,10 +319,16 @@ __global__ __launch_bounds__(256) void rx_segments(const uint32_t* __restrict__ 
     if (p == n - 1 || keys[p + 1] != k) seg_end[k] = (uint32_t)(p + 1);
 }
 
+// blocks per CU the generic NFA without timers is compiled for. 4 (4 waves/SIMD, <= 128 VGPRs, a few spills) measured
+// no faster than 1 (150 VGPRs, 3 waves/SIMD) on C3 (175 vs 171 ms per 10^8 events, r2ab): the kernel is bound by its
+// uncoalesced per-key arena traffic (each lane walks its own key's arena), not by latency hiding
+#ifndef SDG_NFA_MINB
+#define SDG_NFA_MINB 1
+#endif
 // one lane per key: the key's arena is private to the lane, so the state machine runs without atomics; only
 // the output slot and log reservations are shared
 template <bool TM>
-__global__ __launch_bounds__(256) void nfa_k(const NfaArgs* __restrict__ pa) {
+__global__ __launch_bounds__(256, TM ? 1 : SDG_NFA_MINB) void nfa_k(const NfaArgs* __restrict__ pa) {
     // arguments from a device copy: indexing a by-value kernel argument (cols[col]) makes the compiler copy the
     // whole struct to scratch per lane
     const NfaArgs& a = *pa;
