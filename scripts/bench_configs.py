@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--c4-keys", type=int, default=1_000_000)
     ap.add_argument("--c3-steps", type=int, default=2)
     ap.add_argument("--max-partials", type=int, default=0)
+    ap.add_argument("--c2-events", type=int, default=100_000_000)
     args = ap.parse_args()
     torch.cuda.init()
     import siddhi_amd as sa
@@ -67,6 +68,22 @@ def main():
         ev, ms, m = run(rt, "StockStream", n, torch.from_numpy(c["ts"]).to(dev), cols, args.steps, args.warmup)
         print(json.dumps({"config": "C1 unpartitioned, %d events/step" % n, "events_per_s": ev, "ms_per_step": ms,
                           "matches_per_step": m}), flush=True)
+    # C2 on the paths a query that just misses the fused envelope takes: the radix key sort + chain matcher, and the
+    # generic keyed NFA (one lane per key) -- the cost of falling outside each kernel's shape
+    for tag, kw, n in (("c2radix", {"fused": False}, args.c2_events), ("c2generic", {"force_generic": True}, args.c2_events // 10)):
+        if tag not in only:
+            continue
+        c = w.c2_columns(n)
+        rt = sa.SiddhiAppRuntime(w.C2_APP, device=0, **kw)
+        syms = w.symbols(10_000)
+        sym_ids = np.array([rt.intern(x) for x in syms], dtype=np.uint32)
+        cols = [torch.from_numpy(c["id"]).to(dev), torch.from_numpy(sym_ids[c["key"]].view(np.int32)).to(dev),
+                torch.from_numpy(c["price"]).to(dev), torch.from_numpy(c["volume"]).to(dev)]
+        ev, ms, m = run(rt, "StockStream", n, torch.from_numpy(c["ts"]).to(dev), cols, args.steps, args.warmup)
+        st = rt.stats()
+        print(json.dumps({"config": "C2 on the %s path, %d events/step, 10k keys" % (tag[2:], n), "events_per_s": ev,
+                          "ms_per_step": ms, "matches_per_step": m, "path": st.path, "fused": st.fused,
+                          "ms_keygroup": st.ms_keygroup, "ms_match": st.ms_match}), flush=True)
     for tag in ("c3", "c3m"):
         if tag not in only:
             continue
