@@ -32,6 +32,7 @@ for s in "$@"; do
         c3) run c3 600 python3 scripts/bench_configs.py --only c1,c3m,c4 --c3-steps 2 ;;
         c3prof) run c3prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/c3prof" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3m --c3-steps 1 --warmup 1 ;;
         newtests) run newtests 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "regime or long_keys or auto_flush or consumes or many_keys or synthetic" ;;
+        dq) run dqtests 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider && run dqcfg 300 python3 scripts/bench_configs.py --only c1,c2radix ;;
         c4) run c4 600 python3 scripts/bench_configs.py --only c4 ;;
         c3pmc) i=0; for c in "FETCH_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_INSTS_FLAT SQ_INST_CYCLES_VMEM_RD SQ_WAIT_INST_LDS" "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum"; do i=$((i+1)); run c3pmc$i 180 rocprofv3 --pmc $c --kernel-trace -d "$OUT/c3pmc$i" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3m --c3-steps 1 --warmup 0; done ;;
         c3ns) for ns in 8 16 32 64; do run c3ns$ns 300 python3 scripts/bench_configs.py --only c3m --c3-steps 1 --warmup 1 --max-partials $ns; done ;;

@@ -145,7 +145,7 @@ struct IntKeyCache {
 struct QueryRt {
     HostQuery hq;
     IntKeyCache intkeys;
-    DevBuf d_plan, d_code, d_consts, d_args, o_mq, o_ovf, o_ovfc;
+    DevBuf d_plan, d_code, d_consts, d_args, o_mq, o_ovf, o_ovfc, o_dqs;
     HostPin h_args, h_ret;  // chain path: ChainArgs pair; counters (16 B) | flags (16 B) | overflow count (8 B)
     bool string_keys = true;                        // all partition keys are string attributes (ids used as keys)
     std::unordered_map<std::string, uint32_t> keydict;
@@ -1335,6 +1335,18 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         a.ovf_count = (unsigned long long*)q.o_ovfc.ensure(8);
         HIPCHECK(hipMemsetAsync(a.ovf_count, 0, 8, st));
     }
+    // one-key batch on the deque path: 64-row chunk summaries let a lane's continuation skip the chunks that cannot
+    // complete its deque's top (ordering comparisons on a numeric scan column only; chain_dq_summ_k)
+    const bool numeric = a.sp.scan_t == VK_I32 || a.sp.scan_t == VK_I64 || a.sp.scan_t == VK_F32 || a.sp.scan_t == VK_F64;
+    const bool ord_op = a.sp.scan_op == CMP_GT || a.sp.scan_op == CMP_GE || a.sp.scan_op == CMP_LT || a.sp.scan_op == CMP_LE;
+    if (a.deque_mode != DQ_OFF && !fused && nrows > 0 && !a.key && numeric && ord_op && a.sp.scan_mode != SCAN_TRUE &&
+        !getenv("SDG_DQ_NOSKIP")) {
+        const int64_t nch = (nrows + DQ_CHUNK - 1) / DQ_CHUNK;
+        uint8_t* b = (uint8_t*)q.o_dqs.ensure((size_t)nch * 17);
+        a.dq_hi = (int64_t*)b;
+        a.dq_lo = (int64_t*)(b + nch * 8);
+        a.dq_any = b + nch * 16;
+    }
     ChainArgs* d_a = (ChainArgs*)q.d_args.ensure(std::max(sizeof(NfaArgs), 2 * sizeof(ChainArgs)));
     ChainArgs* h_a = (ChainArgs*)q.h_args.ensure(std::max(sizeof(NfaArgs), 2 * sizeof(ChainArgs)));  // pinned
     h_a[0] = a;
@@ -1470,6 +1482,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     q.last_timers = false;
     q.emit_base = e->seq;
     q.sub_is_seq = true;
+    hp.mark("post_sync");
     return true;
     };
     // rerun on the radix path (fused precondition broken), or on the generic NFA (chain precondition broken)

@@ -512,13 +512,91 @@ __global__ __launch_bounds__(DQ_THREADS) void chain_deque_k(const ChainArgs* __r
             step(q, ts[j], xr[j], xn[j], true);
         }
     }
-    // continuation: pop over the key's following rows until the deque drains
+    // continuation: pop over the key's following rows until the deque drains, DQ_GROUP rows per round of loads.
+    // With chunk summaries (one-key batches), a whole 64-row chunk none of whose rows can complete the deque's top
+    // (stack: a completion pops from the top, so nothing below it goes first; all-mode: any passing row completes
+    // everything) only ages the deque: the entries whose window ends inside it expire, exactly as row by row.
+    // Without it the lanes whose highest partial waits ~a window of rows (C1: 1000) set the pace of the flush.
     const int64_t end = a.key ? (int64_t)a.seg_end[min(cur_key, (uint32_t)a.K - 1u)] : a.n;
-    for (int64_t q = c1; q < end && cnt > 0; ++q) {
-        const int64_t tq = a.ts[q];
-        step(q, tq, load_col(a.cols[col], kind, q), xnull ? xnull[q] != 0 : false, false);
+    const bool summ = a.dq_any != nullptr;
+    for (int64_t g = c1; g < end && cnt > 0;) {
+        if (summ && (g & (DQ_CHUNK - 1)) == 0 && g + DQ_CHUNK <= end) {
+            const int64_t ch = g / DQ_CHUNK;
+            bool may = false;
+            if (a.dq_any[ch]) {
+                const T hi = C::get(a.dq_hi[ch]), lo = C::get(a.dq_lo[ch]);
+                const T y = stack ? C::get(dq_y[(head + cnt - 1) & (DQ_DEPTH - 1)][tid]) : kc;
+                may = left ? (cmp_m(m, hi, y) || cmp_m(m, lo, y)) : (cmp_m(m, y, hi) || cmp_m(m, y, lo));
+            }
+            if (!may) {
+                if (has_within) {
+                    const int64_t tl = a.ts[g + DQ_CHUNK - 1];
+                    while (cnt > 0) {
+                        int64_t d = dq_ts[head][tid] - tl;
+                        if (d < 0) d = -d;
+                        if (d <= within) break;
+                        a.mq[dq_row[head][tid]] = MQ_NONE;
+                        head = (head + 1) & (DQ_DEPTH - 1);
+                        --cnt;
+                    }
+                }
+                g += DQ_CHUNK;
+                continue;
+            }
+        }
+        int64_t ts[DQ_GROUP], xr[DQ_GROUP];
+        bool xn[DQ_GROUP];
+#pragma unroll
+        for (int j = 0; j < DQ_GROUP; ++j) {
+            const int64_t q = min(g + j, end - 1);
+            ts[j] = a.ts[q];
+            xr[j] = load_col(a.cols[col], kind, q);
+            xn[j] = xnull ? xnull[q] != 0 : false;
+        }
+#pragma unroll
+        for (int j = 0; j < DQ_GROUP; ++j) {
+            if (g + j >= end || cnt == 0) break;
+            step(g + j, ts[j], xr[j], xn[j], false);
+        }
+        g += DQ_GROUP;
     }
     carry_all();  // reached the end of the key's segment in this batch
+}
+
+// chunk summaries for chain_deque_k's continuation: one wave per DQ_CHUNK = 64 rows, the largest and smallest
+// converted scan value among the rows whose comparison can hold (not null, not NaN)
+static_assert(DQ_CHUNK == 64, "chain_dq_summ_k: one wave per chunk");
+template <int K>
+__global__ __launch_bounds__(256) void chain_dq_summ_k(const ChainArgs* __restrict__ pa) {
+    using C = KT<K>;
+    const ChainArgs& a = *pa;
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int col = a.sp.scan_col;
+    const uint8_t kind = a.sp.scan_col_kind;
+    int64_t r = 0;
+    bool ok = false;
+    if (q < a.n) {
+        r = cvt(load_col(a.cols[col], kind, q), kind, (uint8_t)K);
+        const typename C::T x = C::get(r);
+        ok = !(a.nulls[col] && a.nulls[col][q]) && x == x;
+    }
+    int64_t hi = r, lo = r;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t h2 = __shfl_xor((long long)hi, o), l2 = __shfl_xor((long long)lo, o);
+        const bool ok2 = __shfl_xor((int)ok, o) != 0;
+        if (ok2) {
+            if (!ok || C::get(h2) > C::get(hi)) hi = h2;
+            if (!ok || C::get(l2) < C::get(lo)) lo = l2;
+            ok = true;
+        }
+    }
+    if (lane_id() == 0 && q < a.n) {
+        const int64_t ch = q / DQ_CHUNK;
+        a.dq_hi[ch] = hi;
+        a.dq_lo[ch] = lo;
+        a.dq_any[ch] = ok;
+    }
 }
 
 // rows evicted from a lane's deque: the forward scan of the generic path
@@ -1248,6 +1326,16 @@ void chain_match(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
 
 void chain_deque(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
     if (a.n <= 0) return;
+    if (a.dq_any) {
+        const dim3 sg((unsigned)((a.n + 255) / 256));
+        switch (a.sp.scan_t) {
+            case VK_I32: hipLaunchKernelGGL(chain_dq_summ_k<VK_I32>, sg, dim3(256), 0, stream, d_a); break;
+            case VK_I64: hipLaunchKernelGGL(chain_dq_summ_k<VK_I64>, sg, dim3(256), 0, stream, d_a); break;
+            case VK_F32: hipLaunchKernelGGL(chain_dq_summ_k<VK_F32>, sg, dim3(256), 0, stream, d_a); break;
+            case VK_F64: hipLaunchKernelGGL(chain_dq_summ_k<VK_F64>, sg, dim3(256), 0, stream, d_a); break;
+            default: break;  // engine.cpp sets dq_any for numeric scans only
+        }
+    }
     const dim3 grid((unsigned)((a.n + (int64_t)DQ_THREADS * DQ_CHUNK - 1) / ((int64_t)DQ_THREADS * DQ_CHUNK)));
     switch (a.sp.scan_t) {
         case VK_I32: hipLaunchKernelGGL(chain_deque_k<VK_I32>, grid, dim3(DQ_THREADS), 0, stream, d_a); break;

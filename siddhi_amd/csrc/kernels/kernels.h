@@ -145,6 +145,12 @@ struct ChainArgs {
     uint32_t* mq;                     // [n]
     unsigned long long* ovf_count;
     uint32_t* ovf_rows;               // [n]
+    // one-key batches (unpartitioned): per 64-row chunk, the largest / smallest converted scan value of its rows that
+    // can compare true (not null, not NaN) and whether there is one; a lane's continuation skips the chunks that
+    // cannot complete its deque's top (chain_dq_summ_k). nullptr: no summaries
+    int64_t* dq_hi;
+    int64_t* dq_lo;
+    uint8_t* dq_any;
     const uint32_t* mq_in;            // chain_match_k: results to emit (nullptr: scan itself)
     int32_t write_nulls;              // 0: no output can be null (out_nulls is not written)
     // fused bucket path (chain_fused_k): the view is bucket-ordered (bucketize), not key-sorted. bstart != nullptr

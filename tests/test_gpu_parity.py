@@ -86,6 +86,38 @@ def test_c1_matches_oracle(adversarial, oracle_built):
     assert got == ref
 
 
+# one-key (unpartitioned) deque shapes: the continuation skips 64-row chunks by their min / max summaries
+# (chain_dq_summ_k), so cover both stack directions, e2 on either side, ties (>= / <=), constant (all-mode) scans, an
+# int column and no `within`, on random and on long descending / ascending runs (partials waiting ~a window)
+DQ_APPS = [
+    "every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec",
+    "every e1=StockStream[price>12] -> e2=StockStream[price<e1.price] within 2 sec",
+    "every e1=StockStream[price>12] -> e2=StockStream[e1.price<=price] within 500 millisec",
+    "every e1=StockStream[price>12] -> e2=StockStream[price>=e1.price]",
+    "every e1=StockStream[volume>10] -> e2=StockStream[price>29.5] within 1 sec",
+    "every e1=StockStream[price>20] -> e2=StockStream[29.0 > price] within 3 sec",
+    "every e1=StockStream[volume>=0] -> e2=StockStream[volume>e1.volume] within 2 sec",
+]
+
+
+@pytest.mark.parametrize("data", ["random", "runs"])
+@pytest.mark.parametrize("qi", range(len(DQ_APPS)))
+def test_one_key_deque_shapes(qi, data, oracle_built):
+    n = 12_000
+    cols = w.c1_columns(n)
+    i = np.arange(n)
+    if data == "runs":  # descending and ascending runs of ~1500 rows, prices rounded to 0.5 (ties)
+        saw = np.where((i // 1500) % 2 == 0, 30.0 - (i % 1500) * 0.012, 12.0 + (i % 1500) * 0.012)
+        cols["price"] = np.rint(saw * 2.0) / 2.0
+        cols["volume"] = np.where((i // 1500) % 2 == 0, 1000 - (i % 1500) // 3, (i % 1500) // 3).astype(np.int32)
+    app = "@app:playback " + w.STOCK_STREAM + " @info(name = 'query1') from " + DQ_APPS[qi] + \
+        " select e1.id as e1id, e2.id as e2id insert into M;"
+    ref = oracle_c_rows(app, cols)
+    got = product_c_rows(app, cols, batches=2)
+    assert got == ref
+    assert len(ref) > 10
+
+
 @pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("batches", [1, 7])
 def test_c2_matches_oracle(batches, fused, oracle_built):
