@@ -1341,11 +1341,19 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     const bool ord_op = a.sp.scan_op == CMP_GT || a.sp.scan_op == CMP_GE || a.sp.scan_op == CMP_LT || a.sp.scan_op == CMP_LE;
     if (a.deque_mode != DQ_OFF && !fused && nrows > 0 && !a.key && numeric && ord_op && a.sp.scan_mode != SCAN_TRUE &&
         !getenv("SDG_DQ_NOSKIP")) {
-        const int64_t nch = (nrows + DQ_CHUNK - 1) / DQ_CHUNK;
-        uint8_t* b = (uint8_t*)q.o_dqs.ensure((size_t)nch * 17);
+        const int64_t nch = (nrows + DQ_CHUNK - 1) / DQ_CHUNK, ngr = nch * (DQ_CHUNK / DQ_GROUP);
+        uint8_t* b = (uint8_t*)q.o_dqs.ensure((size_t)(nch + ngr) * 17);
         a.dq_hi = (int64_t*)b;
-        a.dq_lo = (int64_t*)(b + nch * 8);
-        a.dq_any = b + nch * 16;
+        a.dq_lo = a.dq_hi + nch;
+        a.dq_hi8 = a.dq_lo + nch;
+        a.dq_lo8 = a.dq_hi8 + ngr;
+        a.dq_any = (uint8_t*)(a.dq_lo8 + ngr);
+        a.dq_any8 = a.dq_any + nch;
+        // with skipping, a lane's own rows are most of its serial work: fewer per lane, more lanes (C1: 244 waves
+        // of 64 rows left 3/4 of the SIMDs idle)
+        static const char* lane = getenv("SDG_DQ_LANE");
+        a.dq_lane = lane ? atoi(lane) : 16;
+        if (a.dq_lane < DQ_GROUP || a.dq_lane % DQ_GROUP) a.dq_lane = DQ_CHUNK;
     }
     ChainArgs* d_a = (ChainArgs*)q.d_args.ensure(std::max(sizeof(NfaArgs), 2 * sizeof(ChainArgs)));
     ChainArgs* h_a = (ChainArgs*)q.h_args.ensure(std::max(sizeof(NfaArgs), 2 * sizeof(ChainArgs)));  // pinned

@@ -411,9 +411,10 @@ __global__ __launch_bounds__(DQ_THREADS) void chain_deque_k(const ChainArgs* __r
     __shared__ int64_t dq_ts[DQ_DEPTH][DQ_THREADS];
     __shared__ uint32_t dq_row[DQ_DEPTH][DQ_THREADS];
     const int tid = threadIdx.x;
-    const int64_t c0 = ((int64_t)blockIdx.x * DQ_THREADS + tid) * DQ_CHUNK;
+    const int64_t lane_rows = a.dq_lane > 0 ? a.dq_lane : DQ_CHUNK;
+    const int64_t c0 = ((int64_t)blockIdx.x * DQ_THREADS + tid) * lane_rows;
     if (c0 >= a.n) return;
-    const int64_t c1 = min(a.n, c0 + DQ_CHUNK);
+    const int64_t c1 = min(a.n, c0 + lane_rows);
     const int col = sp.scan_col;
     const uint8_t kind = sp.scan_col_kind;
     const uint8_t* xnull = a.nulls[col];
@@ -520,17 +521,21 @@ __global__ __launch_bounds__(DQ_THREADS) void chain_deque_k(const ChainArgs* __r
     const int64_t end = a.key ? (int64_t)a.seg_end[min(cur_key, (uint32_t)a.K - 1u)] : a.n;
     const bool summ = a.dq_any != nullptr;
     for (int64_t g = c1; g < end && cnt > 0;) {
-        if (summ && (g & (DQ_CHUNK - 1)) == 0 && g + DQ_CHUNK <= end) {
-            const int64_t ch = g / DQ_CHUNK;
+        // a whole 64-row chunk, else a whole 8-row group (g stays a multiple of DQ_GROUP: lane_rows is one)
+        const bool whole64 = (g & (DQ_CHUNK - 1)) == 0 && g + DQ_CHUNK <= end;
+        if (summ && (whole64 || g + DQ_GROUP <= end)) {
+            const int64_t span = whole64 ? DQ_CHUNK : DQ_GROUP;
+            const int64_t ch = g / span;
             bool may = false;
-            if (a.dq_any[ch]) {
-                const T hi = C::get(a.dq_hi[ch]), lo = C::get(a.dq_lo[ch]);
+            if (whole64 ? a.dq_any[ch] : a.dq_any8[ch]) {
+                const T hi = C::get(whole64 ? a.dq_hi[ch] : a.dq_hi8[ch]);
+                const T lo = C::get(whole64 ? a.dq_lo[ch] : a.dq_lo8[ch]);
                 const T y = stack ? C::get(dq_y[(head + cnt - 1) & (DQ_DEPTH - 1)][tid]) : kc;
                 may = left ? (cmp_m(m, hi, y) || cmp_m(m, lo, y)) : (cmp_m(m, y, hi) || cmp_m(m, y, lo));
             }
             if (!may) {
                 if (has_within) {
-                    const int64_t tl = a.ts[g + DQ_CHUNK - 1];
+                    const int64_t tl = a.ts[g + span - 1];
                     while (cnt > 0) {
                         int64_t d = dq_ts[head][tid] - tl;
                         if (d < 0) d = -d;
@@ -540,7 +545,7 @@ __global__ __launch_bounds__(DQ_THREADS) void chain_deque_k(const ChainArgs* __r
                         --cnt;
                     }
                 }
-                g += DQ_CHUNK;
+                g += span;
                 continue;
             }
         }
@@ -589,6 +594,12 @@ __global__ __launch_bounds__(256) void chain_dq_summ_k(const ChainArgs* __restri
             if (!ok || C::get(h2) > C::get(hi)) hi = h2;
             if (!ok || C::get(l2) < C::get(lo)) lo = l2;
             ok = true;
+        }
+        if (o == DQ_GROUP / 2 && (lane_id() & (DQ_GROUP - 1)) == 0 && q < a.n) {  // the 8-row group's summary
+            const int64_t gi = q / DQ_GROUP;
+            a.dq_hi8[gi] = hi;
+            a.dq_lo8[gi] = lo;
+            a.dq_any8[gi] = ok;
         }
     }
     if (lane_id() == 0 && q < a.n) {
@@ -1326,6 +1337,7 @@ void chain_match(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
 
 void chain_deque(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
     if (a.n <= 0) return;
+    const int64_t lane_rows = a.dq_lane > 0 ? a.dq_lane : DQ_CHUNK;
     if (a.dq_any) {
         const dim3 sg((unsigned)((a.n + 255) / 256));
         switch (a.sp.scan_t) {
@@ -1336,7 +1348,7 @@ void chain_deque(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
             default: break;  // engine.cpp sets dq_any for numeric scans only
         }
     }
-    const dim3 grid((unsigned)((a.n + (int64_t)DQ_THREADS * DQ_CHUNK - 1) / ((int64_t)DQ_THREADS * DQ_CHUNK)));
+    const dim3 grid((unsigned)((a.n + DQ_THREADS * lane_rows - 1) / (DQ_THREADS * lane_rows)));
     switch (a.sp.scan_t) {
         case VK_I32: hipLaunchKernelGGL(chain_deque_k<VK_I32>, grid, dim3(DQ_THREADS), 0, stream, d_a); break;
         case VK_I64: hipLaunchKernelGGL(chain_deque_k<VK_I64>, grid, dim3(DQ_THREADS), 0, stream, d_a); break;

@@ -151,6 +151,10 @@ struct ChainArgs {
     int64_t* dq_hi;
     int64_t* dq_lo;
     uint8_t* dq_any;
+    int64_t* dq_hi8;                  // the same per DQ_GROUP = 8 rows
+    int64_t* dq_lo8;
+    uint8_t* dq_any8;
+    int32_t dq_lane;                  // rows each lane owns (0: DQ_CHUNK); a multiple of DQ_GROUP
     const uint32_t* mq_in;            // chain_match_k: results to emit (nullptr: scan itself)
     int32_t write_nulls;              // 0: no output can be null (out_nulls is not written)
     // fused bucket path (chain_fused_k): the view is bucket-ordered (bucketize), not key-sorted. bstart != nullptr
