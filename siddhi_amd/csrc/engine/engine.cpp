@@ -148,6 +148,12 @@ struct QueryRt {
     DevBuf d_plan, d_code, d_consts, d_args, o_mq, o_ovf, o_ovfc, o_dqs;
     HostPin h_args, h_ret;  // chain path: ChainArgs pair; counters (16 B) | flags (16 B) | overflow count (8 B)
     bool string_keys = true;                        // all partition keys are string attributes (ids used as keys)
+    bool int_keys = false;                          // all partition keys are int / long attributes (device key table)
+    // device key table (keytab.hip) for device-resident batches of int / long keys: a mirror of keydict's ids
+    DevBuf kt_keys, kt_ids, kt_first, kt_cnt, kt_pairs, kt_vals, kt_slots;
+    uint64_t kt_cap = 0;
+    size_t kt_synced = 0;                           // keydict ids [0, kt_synced) are in the table
+    HostPin kt_ret;
     std::unordered_map<std::string, uint32_t> keydict;
     std::vector<std::string> keystr;                // keydict id -> key text (numeric keys)
     // absent states: the scheduler simulation, per-key HashMap hashes, double-buffered arenas, the run's log
@@ -599,6 +605,102 @@ struct HostProf {
     }
 };
 
+KeyTab kt_view(QueryRt& q) {
+    return KeyTab{q.kt_keys.as<int64_t>(), q.kt_ids.as<uint32_t>(), q.kt_first.as<uint32_t>(), q.kt_cap - 1, q.kt_cap};
+}
+
+// the host dictionary's ids [kt_synced, K) into the device key table (keys the host path assigned)
+void kt_sync(sdg_engine* e, QueryRt& q) {
+    const size_t K = q.keystr.size();
+    if (q.kt_synced >= K) return;
+    std::vector<int64_t> vals(K - q.kt_synced);
+    for (size_t i = q.kt_synced; i < K; ++i) vals[i - q.kt_synced] = std::stoll(q.keystr[i]);  // int / long keys only
+    int64_t* d_vals = (int64_t*)q.kt_vals.ensure(vals.size() * 8);
+    int* d_flags = (int*)((uint8_t*)q.kt_cnt.ensure(32) + 8);
+    HIPCHECK(hipMemcpy(d_vals, vals.data(), vals.size() * 8, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemsetAsync(d_flags, 0, 8, e->stream));
+    kt_load(kt_view(q), d_vals, (uint32_t)q.kt_synced, (int64_t)vals.size(), d_flags, e->stream);
+    int hf = 0;
+    HIPCHECK(hipMemcpyAsync(&hf, d_flags, 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHECK(hipStreamSynchronize(e->stream));
+    if (hf) throw DeviceError("device key table: probe limit while loading the dictionary");
+    q.kt_synced = K;
+}
+
+void kt_rebuild(sdg_engine* e, QueryRt& q, uint64_t cap) {
+    uint64_t c = 1;
+    while (c < cap) c <<= 1;
+    q.kt_cap = c;
+    q.kt_keys.ensure((size_t)(c + 1) * 8);
+    q.kt_ids.ensure((size_t)(c + 1) * 4);
+    q.kt_first.ensure((size_t)(c + 1) * 4);
+    kt_clear(kt_view(q), e->stream);
+    q.kt_synced = 0;
+    kt_sync(e, q);
+}
+
+// dense key ids of a device-resident batch keyed by an int / long attribute: looked up (and new keys inserted) in
+// the device key table; new keys get the next ids in order of their first row, as host_key assigns them, and
+// enter the host dictionary too (snapshots, scheduler hashes, later host pushes)
+const uint32_t* device_key_ids(sdg_engine* e, QueryRt& q, const void* col, int kind, int64_t n) {
+    hipStream_t st = e->stream;
+    uint32_t* out = (uint32_t*)q.st_key.ensure((size_t)std::max<int64_t>(n, 1) * 4);
+    if (n <= 0) return out;
+    uint64_t want = 0;
+    for (int attempt = 0;; ++attempt) {
+        if (attempt > 8) throw DeviceError("device key table: could not size the table");
+        const size_t K0 = q.keystr.size();
+        want = std::max<uint64_t>(want, std::max<uint64_t>(1u << 16, 4 * (uint64_t)K0));
+        if (q.kt_cap < want) kt_rebuild(e, q, want);
+        else kt_sync(e, q);
+        const KeyTab t = kt_view(q);
+        uint8_t* d_c = (uint8_t*)q.kt_cnt.ensure(32);
+        unsigned long long* d_cnt = (unsigned long long*)d_c;
+        int* d_flags = (int*)(d_c + 8);
+        HIPCHECK(hipMemsetAsync(d_c, 0, 32, st));
+        kt_probe(t, col, kind, n, out, d_cnt, d_flags, st);
+        uint8_t* hr = (uint8_t*)q.kt_ret.ensure(16);
+        HIPCHECK(hipMemcpyAsync(hr, d_c, 16, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        const uint64_t cnt = *(unsigned long long*)hr;
+        const int flags = *(int*)(hr + 8);
+        if (flags || K0 + cnt > t.cap / 2) {  // probe limit / over half full: a larger table, the batch again
+            want = 4 * (K0 + std::max<uint64_t>(cnt, flags ? t.cap : 0));
+            q.kt_cap = 0;
+            continue;
+        }
+        if (cnt == 0) return out;
+        unsigned long long* d_pairs = (unsigned long long*)q.kt_pairs.ensure(cnt * 8);
+        int64_t* d_vals = (int64_t*)q.kt_vals.ensure(cnt * 8);
+        unsigned long long* d_n2 = (unsigned long long*)(d_c + 16);
+        kt_collect(t, d_pairs, d_vals, d_n2, (int64_t)cnt, st);
+        std::vector<unsigned long long> pairs(cnt);
+        std::vector<int64_t> vals(cnt);
+        HIPCHECK(hipMemcpyAsync(pairs.data(), d_pairs, cnt * 8, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(vals.data(), d_vals, cnt * 8, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        std::vector<uint32_t> order(cnt);
+        for (uint32_t i = 0; i < cnt; ++i) order[i] = i;
+        std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return pairs[a] < pairs[b]; });
+        std::vector<uint32_t> slots(cnt);
+        for (uint64_t j = 0; j < cnt; ++j) {
+            const uint32_t i = order[j];
+            const uint32_t id = (uint32_t)(K0 + j);
+            slots[j] = (uint32_t)(pairs[i] & 0xFFFFFFFFull);
+            std::string ks = std::to_string(vals[i]);
+            if (!q.keydict.emplace(ks, id).second) throw DeviceError("device key table out of step with the dictionary");
+            q.keystr.push_back(std::move(ks));
+            q.intkeys.insert(vals[i], id);
+        }
+        uint32_t* d_slots = (uint32_t*)q.kt_slots.ensure(cnt * 4);
+        HIPCHECK(hipMemcpy(d_slots, slots.data(), cnt * 4, hipMemcpyHostToDevice));
+        kt_assign(t, d_slots, (uint32_t)K0, (int64_t)cnt, st);
+        kt_fix(t, col, kind, n, out, st);
+        q.kt_synced = q.keystr.size();
+        return out;
+    }
+}
+
 void flush_query(sdg_engine* e, QueryRt& q) {
     HostProf hp;
     HostQuery& h = q.hq;
@@ -648,10 +750,12 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         }
         if (partitioned) {
             if (ranged) throw CompileError(SDG_ERR_UNSUPPORTED, "device-resident batches of a range partition");
-            if (!q.string_keys) throw CompileError(SDG_ERR_UNSUPPORTED, "device-resident batches need string partition keys");
+            if (!q.string_keys && !q.int_keys)
+                throw CompileError(SDG_ERR_UNSUPPORTED, "device-resident batches need string or int / long partition keys");
             int ai = h.key_attr[qpos];
             if (c.d_nulls[ai]) throw CompileError(SDG_ERR_UNSUPPORTED, "null partition keys in device-resident batches");
-            d_key = (const uint32_t*)c.d_cols[ai];
+            if (q.string_keys) d_key = (const uint32_t*)c.d_cols[ai];
+            else d_key = device_key_ids(e, q, c.d_cols[ai], h.key_kind[qpos], n);
         }
         nrows = n;
     } else {
@@ -1974,6 +2078,8 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
         q.intkeys.n = (size_t)r.get<uint64_t>();
         q.keystr.resize(r.get<uint64_t>());
         q.keydict.clear();
+        q.kt_cap = 0;  // the device key table is rebuilt from the dictionary on the next device-resident batch
+        q.kt_synced = 0;
         for (size_t i = 0; i < q.keystr.size(); ++i) {
             q.keystr[i] = r.str();
             q.keydict[q.keystr[i]] = (uint32_t)i;
@@ -2066,6 +2172,9 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             e->any_purge |= P.purge != 0;
             for (size_t i = 0; i < q->hq.key_kind.size(); ++i)
                 if (q->hq.key_attr[i] >= 0 && q->hq.key_kind[i] != VK_STR) q->string_keys = false;
+            q->int_keys = P.partitioned && !q->hq.key_kind.empty();
+            for (size_t i = 0; i < q->hq.key_kind.size(); ++i)
+                q->int_keys &= q->hq.key_attr[i] >= 0 && (q->hq.key_kind[i] == VK_I32 || q->hq.key_kind[i] == VK_I64);
             if (!e->compile_only) upload_plan(e.get(), *q);
             e->qs.push_back(std::move(q));
         }

@@ -286,4 +286,21 @@ size_t select_post_workspace(int64_t n);
 // key: [n] partition key ids < 2^kbits (nullptr / kbits 0: unpartitioned, one run)
 void select_post(SelPostArgs a, const uint32_t* key, int kbits, void* work, hipStream_t stream);
 
+// device partition key table for integral partition attributes (keytab.hip): value -> dense key id
+struct KeyTab {
+    int64_t* keys;    // [cap + 1]
+    uint32_t* ids;    // [cap + 1] id + 1 (0: new in this batch)
+    uint32_t* first;  // [cap + 1] a new key's first row
+    uint64_t mask;    // cap - 1 (cap a power of two)
+    uint64_t cap;
+};
+void kt_clear(const KeyTab& t, hipStream_t st);
+void kt_load(const KeyTab& t, const int64_t* vals, uint32_t id0, int64_t n, int* flags, hipStream_t st);
+void kt_probe(const KeyTab& t, const void* col, int kind, int64_t n, uint32_t* out, unsigned long long* new_count,
+              int* flags, hipStream_t st);
+void kt_collect(const KeyTab& t, unsigned long long* pairs, int64_t* vals, unsigned long long* cnt, int64_t cap_out,
+                hipStream_t st);
+void kt_assign(const KeyTab& t, const uint32_t* slots, uint32_t id0, int64_t m, hipStream_t st);
+void kt_fix(const KeyTab& t, const void* col, int kind, int64_t n, uint32_t* out, hipStream_t st);
+
 }  // namespace sdg

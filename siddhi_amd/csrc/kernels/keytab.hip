@@ -1,0 +1,149 @@
+// Device-resident partition key table for integral (int / long) partition attributes: an open-addressed HBM hash
+// table from the key value to the dense key id the rest of the engine indexes its per-key state with (arenas,
+// carries, segments). ValuePartitionExecutor keys a partition by the attribute's toString (reference:
+// core/partition/executor/ValuePartitionExecutor.java, PartitionStreamReceiver.java:262-272); Java's toString is
+// injective on int / long and prints equal values of either type alike, so the sign-extended 64-bit value stands
+// for the key. Ids are dense and assigned in order of a key's first row, as the host dictionary assigns them
+// (engine.cpp host_key), so a batch maps to the same ids whichever side it was pushed from.
+//
+// Slots: keys[cap] (KT_EMPTY = free; the value KT_EMPTY itself lives in the extra slot keys[cap], used = 1),
+// ids[cap + 1] (id + 1, 0 = new in this batch), first[cap + 1] (smallest row of a new key). Linear probing; a
+// probe sequence longer than KT_MAX_PROBE sets the overflow flag (the host grows the table and runs again).
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace sdg {
+namespace {
+
+constexpr int64_t KT_EMPTY = INT64_MIN;
+constexpr uint32_t KT_MAX_PROBE = 4096;
+constexpr uint32_t KT_NEW = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint64_t kt_mix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ int64_t kt_value(const void* col, int kind, int64_t r) {
+    return kind == VK_I32 ? (int64_t)((const int32_t*)col)[r] : ((const int64_t*)col)[r];
+}
+
+// the slot of v, inserting it when absent (winner counts a new key); -1: probe limit hit
+__device__ __forceinline__ int64_t kt_slot(const KeyTab& t, int64_t v, unsigned long long* new_count) {
+    if (v == KT_EMPTY) {
+        const unsigned long long was = atomicCAS((unsigned long long*)&t.keys[t.cap], 0ull, 1ull);
+        if (was == 0ull && new_count) atomicAdd(new_count, 1ull);
+        return t.cap;
+    }
+    uint64_t h = kt_mix((uint64_t)v) & t.mask;
+    for (uint32_t i = 0; i < KT_MAX_PROBE && i <= t.mask; ++i) {
+        int64_t cur = t.keys[h];
+        if (cur == KT_EMPTY) {  // a stale read can only show a slot as still free: the CAS decides
+            cur = (int64_t)atomicCAS((unsigned long long*)&t.keys[h], (unsigned long long)KT_EMPTY, (unsigned long long)v);
+            if (cur == KT_EMPTY) {
+                if (new_count) atomicAdd(new_count, 1ull);
+                return (int64_t)h;
+            }
+        }
+        if (cur == v) return (int64_t)h;
+        h = (h + 1) & t.mask;
+    }
+    return -1;
+}
+
+__global__ __launch_bounds__(256) void kt_clear_k(KeyTab t) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i > (int64_t)t.cap) return;
+    t.keys[i] = i == (int64_t)t.cap ? 0 : KT_EMPTY;
+    t.ids[i] = 0;
+    t.first[i] = 0xFFFFFFFFu;
+}
+
+// known keys (the host dictionary's, id order)
+__global__ __launch_bounds__(256) void kt_load_k(KeyTab t, const int64_t* __restrict__ vals, uint32_t id0, int64_t n,
+                                                 int* __restrict__ flags) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int64_t s = kt_slot(t, vals[i], nullptr);
+    if (s < 0) {
+        atomicOr(&flags[0], 1);
+        return;
+    }
+    t.ids[s] = id0 + (uint32_t)i + 1u;
+}
+
+// per row: the key id, or KT_NEW (first sighting in this batch: the row's index competes for the key's first row)
+__global__ __launch_bounds__(256) void kt_probe_k(KeyTab t, const void* __restrict__ col, int kind, int64_t n,
+                                                  uint32_t* __restrict__ out, unsigned long long* __restrict__ new_count,
+                                                  int* __restrict__ flags) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= n) return;
+    const int64_t s = kt_slot(t, kt_value(col, kind, r), new_count);
+    if (s < 0) {
+        atomicOr(&flags[0], 1);
+        out[r] = 0;
+        return;
+    }
+    const uint32_t id = t.ids[s];
+    if (id) {
+        out[r] = id - 1u;
+    } else {
+        out[r] = KT_NEW;
+        atomicMin(&t.first[s], (uint32_t)r);
+    }
+}
+
+// the slots of the batch's new keys: (first row << 32 | slot) and the key values
+__global__ __launch_bounds__(256) void kt_collect_k(KeyTab t, unsigned long long* __restrict__ pairs,
+                                                    int64_t* __restrict__ vals, unsigned long long* __restrict__ cnt,
+                                                    int64_t cap_out) {
+    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s > (int64_t)t.cap) return;
+    const bool used = s == (int64_t)t.cap ? t.keys[s] != 0 : t.keys[s] != KT_EMPTY;
+    if (!used || t.ids[s] != 0) return;
+    const unsigned long long o = atomicAdd(cnt, 1ull);
+    if ((int64_t)o >= cap_out) return;  // the host sized pairs by the probe's count
+    pairs[o] = ((unsigned long long)t.first[s] << 32) | (unsigned long long)s;
+    vals[o] = s == (int64_t)t.cap ? KT_EMPTY : t.keys[s];
+}
+
+__global__ __launch_bounds__(256) void kt_assign_k(KeyTab t, const uint32_t* __restrict__ slots, uint32_t id0, int64_t m) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    t.ids[slots[i]] = id0 + (uint32_t)i + 1u;
+}
+
+__global__ __launch_bounds__(256) void kt_fix_k(KeyTab t, const void* __restrict__ col, int kind, int64_t n,
+                                                uint32_t* __restrict__ out) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= n || out[r] != KT_NEW) return;
+    const int64_t s = kt_slot(t, kt_value(col, kind, r), nullptr);  // present: inserted by the probe
+    out[r] = s >= 0 ? t.ids[s] - 1u : 0u;
+}
+
+dim3 blocks(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+}  // namespace
+
+void kt_clear(const KeyTab& t, hipStream_t st) { hipLaunchKernelGGL(kt_clear_k, blocks((int64_t)t.cap + 1), dim3(256), 0, st, t); }
+void kt_load(const KeyTab& t, const int64_t* vals, uint32_t id0, int64_t n, int* flags, hipStream_t st) {
+    if (n > 0) hipLaunchKernelGGL(kt_load_k, blocks(n), dim3(256), 0, st, t, vals, id0, n, flags);
+}
+void kt_probe(const KeyTab& t, const void* col, int kind, int64_t n, uint32_t* out, unsigned long long* new_count,
+              int* flags, hipStream_t st) {
+    if (n > 0) hipLaunchKernelGGL(kt_probe_k, blocks(n), dim3(256), 0, st, t, col, kind, n, out, new_count, flags);
+}
+void kt_collect(const KeyTab& t, unsigned long long* pairs, int64_t* vals, unsigned long long* cnt, int64_t cap_out,
+                hipStream_t st) {
+    hipLaunchKernelGGL(kt_collect_k, blocks((int64_t)t.cap + 1), dim3(256), 0, st, t, pairs, vals, cnt, cap_out);
+}
+void kt_assign(const KeyTab& t, const uint32_t* slots, uint32_t id0, int64_t m, hipStream_t st) {
+    if (m > 0) hipLaunchKernelGGL(kt_assign_k, blocks(m), dim3(256), 0, st, t, slots, id0, m);
+}
+void kt_fix(const KeyTab& t, const void* col, int kind, int64_t n, uint32_t* out, hipStream_t st) {
+    if (n > 0) hipLaunchKernelGGL(kt_fix_k, blocks(n), dim3(256), 0, st, t, col, kind, n, out);
+}
+
+}  // namespace sdg
