@@ -120,6 +120,35 @@ def main():
                           "events_per_s_end_to_end": n * args.c3_steps / dt, "ms_per_step": dt * 1000 / args.c3_steps,
                           "device_ms_per_step": dev_ms / args.c3_steps, "events_per_s_device": n * args.c3_steps / (dev_ms / 1000),
                           "matches_per_step": m / args.c3_steps, "events_per_flush": st.events}), flush=True)
+    if "c3md" in only:  # C3 <1:5> device-resident: long keys through the device key table (keytab.hip)
+        keys = args.c3_keys
+        c = w.c3_columns(keys)
+        n = len(c["ts"])
+        rt = sa.SiddhiAppRuntime(w.C3_APP.replace("<2:5>", "<1:5>"), device=0, batch_capacity=n + 1,
+                                 max_partials=args.max_partials)
+        d = [torch.from_numpy(c[k]).to(dev) for k in ("id", "key", "price", "volume")]
+        d_ts0 = torch.from_numpy(c["ts"]).to(dev)
+        span = int(c["ts"][-1] - c["ts"][0]) + 1
+        ts_steps = [d_ts0 + s * span for s in range(args.warmup + args.c3_steps)]
+        torch.cuda.synchronize()
+
+        def step(s):
+            rt.push_device("S", n, ts_steps[s].data_ptr(), [x.data_ptr() for x in d])
+            rt.flush(deliver=False)
+            rt.discard()
+            return rt.stats()
+        for s in range(args.warmup):
+            step(s)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        m = 0
+        for s in range(args.warmup, args.warmup + args.c3_steps):
+            m += step(s).matches
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        print(json.dumps({"config": "C3 <1:5>, %d keys x 100 events/step, device-resident (device key table)" % keys,
+                          "events_per_s": n * args.c3_steps / dt, "ms_per_step": dt * 1000 / args.c3_steps,
+                          "matches_per_step": m / args.c3_steps}), flush=True)
     if "c4" in only:
         run_c4(args.c4_keys)
 

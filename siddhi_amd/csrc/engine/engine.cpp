@@ -658,14 +658,14 @@ const uint32_t* device_key_ids(sdg_engine* e, QueryRt& q, const void* col, int k
         unsigned long long* d_cnt = (unsigned long long*)d_c;
         int* d_flags = (int*)(d_c + 8);
         HIPCHECK(hipMemsetAsync(d_c, 0, 32, st));
-        kt_probe(t, col, kind, n, out, d_cnt, d_flags, st);
+        kt_probe(t, col, kind, n, out, d_cnt, t.cap / 2 - K0, d_flags, st);  // (cap >= 4 K0)
         uint8_t* hr = (uint8_t*)q.kt_ret.ensure(16);
         HIPCHECK(hipMemcpyAsync(hr, d_c, 16, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
         const uint64_t cnt = *(unsigned long long*)hr;
-        const int flags = *(int*)(hr + 8);
-        if (flags || K0 + cnt > t.cap / 2) {  // probe limit / over half full: a larger table, the batch again
-            want = 4 * (K0 + std::max<uint64_t>(cnt, flags ? t.cap : 0));
+        const int flags = *(int*)(hr + 8) | *(int*)(hr + 12);
+        if (flags || K0 + cnt > t.cap / 2) {  // probe limit / over half full (pass stopped): larger table, again
+            want = std::max<uint64_t>(4 * (K0 + cnt), 8 * t.cap);
             q.kt_cap = 0;
             continue;
         }

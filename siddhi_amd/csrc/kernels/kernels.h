@@ -297,7 +297,7 @@ struct KeyTab {
 void kt_clear(const KeyTab& t, hipStream_t st);
 void kt_load(const KeyTab& t, const int64_t* vals, uint32_t id0, int64_t n, int* flags, hipStream_t st);
 void kt_probe(const KeyTab& t, const void* col, int kind, int64_t n, uint32_t* out, unsigned long long* new_count,
-              int* flags, hipStream_t st);
+              unsigned long long limit, int* flags, hipStream_t st);
 void kt_collect(const KeyTab& t, unsigned long long* pairs, int64_t* vals, unsigned long long* cnt, int64_t cap_out,
                 hipStream_t st);
 void kt_assign(const KeyTab& t, const uint32_t* slots, uint32_t id0, int64_t m, hipStream_t st);

@@ -8,7 +8,8 @@
 //
 // Slots: keys[cap] (KT_EMPTY = free; the value KT_EMPTY itself lives in the extra slot keys[cap], used = 1),
 // ids[cap + 1] (id + 1, 0 = new in this batch), first[cap + 1] (smallest row of a new key). Linear probing; a
-// probe sequence longer than KT_MAX_PROBE sets the overflow flag (the host grows the table and runs again).
+// probe sequence longer than KT_MAX_PROBE, or a batch whose new keys would fill the table over half, stops the pass
+// early (flags) and the host grows the table (at least 8x) and probes again.
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
@@ -30,20 +31,28 @@ __device__ __forceinline__ int64_t kt_value(const void* col, int kind, int64_t r
     return kind == VK_I32 ? (int64_t)((const int32_t*)col)[r] : ((const int64_t*)col)[r];
 }
 
-// the slot of v, inserting it when absent (winner counts a new key); -1: probe limit hit
-__device__ __forceinline__ int64_t kt_slot(const KeyTab& t, int64_t v, unsigned long long* new_count) {
+// a new key: counted; once the table would be over half full, flags[1] stops the pass (the host grows the table)
+__device__ __forceinline__ void kt_count_new(unsigned long long* new_count, unsigned long long limit, int* flags) {
+    if (!new_count) return;
+    if (atomicAdd(new_count, 1ull) >= limit) atomicOr(&flags[1], 1);
+}
+
+// the slot of v, inserting it when absent; -1: probe limit hit, or the pass was stopped
+__device__ __forceinline__ int64_t kt_slot(const KeyTab& t, int64_t v, unsigned long long* new_count,
+                                           unsigned long long limit, int* flags) {
     if (v == KT_EMPTY) {
         const unsigned long long was = atomicCAS((unsigned long long*)&t.keys[t.cap], 0ull, 1ull);
-        if (was == 0ull && new_count) atomicAdd(new_count, 1ull);
+        if (was == 0ull) kt_count_new(new_count, limit, flags);
         return t.cap;
     }
     uint64_t h = kt_mix((uint64_t)v) & t.mask;
     for (uint32_t i = 0; i < KT_MAX_PROBE && i <= t.mask; ++i) {
+        if ((i & 31) == 31 && flags && *(volatile int*)&flags[1]) return -1;
         int64_t cur = t.keys[h];
         if (cur == KT_EMPTY) {  // a stale read can only show a slot as still free: the CAS decides
             cur = (int64_t)atomicCAS((unsigned long long*)&t.keys[h], (unsigned long long)KT_EMPTY, (unsigned long long)v);
             if (cur == KT_EMPTY) {
-                if (new_count) atomicAdd(new_count, 1ull);
+                kt_count_new(new_count, limit, flags);
                 return (int64_t)h;
             }
         }
@@ -66,7 +75,7 @@ __global__ __launch_bounds__(256) void kt_load_k(KeyTab t, const int64_t* __rest
                                                  int* __restrict__ flags) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    const int64_t s = kt_slot(t, vals[i], nullptr);
+    const int64_t s = kt_slot(t, vals[i], nullptr, 0, nullptr);
     if (s < 0) {
         atomicOr(&flags[0], 1);
         return;
@@ -77,10 +86,11 @@ __global__ __launch_bounds__(256) void kt_load_k(KeyTab t, const int64_t* __rest
 // per row: the key id, or KT_NEW (first sighting in this batch: the row's index competes for the key's first row)
 __global__ __launch_bounds__(256) void kt_probe_k(KeyTab t, const void* __restrict__ col, int kind, int64_t n,
                                                   uint32_t* __restrict__ out, unsigned long long* __restrict__ new_count,
-                                                  int* __restrict__ flags) {
+                                                  unsigned long long limit, int* __restrict__ flags) {
     const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (r >= n) return;
-    const int64_t s = kt_slot(t, kt_value(col, kind, r), new_count);
+    if (*(volatile int*)&flags[1]) return;  // stopped: the table is being outgrown
+    const int64_t s = kt_slot(t, kt_value(col, kind, r), new_count, limit, flags);
     if (s < 0) {
         atomicOr(&flags[0], 1);
         out[r] = 0;
@@ -119,7 +129,7 @@ __global__ __launch_bounds__(256) void kt_fix_k(KeyTab t, const void* __restrict
                                                 uint32_t* __restrict__ out) {
     const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (r >= n || out[r] != KT_NEW) return;
-    const int64_t s = kt_slot(t, kt_value(col, kind, r), nullptr);  // present: inserted by the probe
+    const int64_t s = kt_slot(t, kt_value(col, kind, r), nullptr, 0, nullptr);  // present: inserted by the probe
     out[r] = s >= 0 ? t.ids[s] - 1u : 0u;
 }
 
@@ -132,8 +142,8 @@ void kt_load(const KeyTab& t, const int64_t* vals, uint32_t id0, int64_t n, int*
     if (n > 0) hipLaunchKernelGGL(kt_load_k, blocks(n), dim3(256), 0, st, t, vals, id0, n, flags);
 }
 void kt_probe(const KeyTab& t, const void* col, int kind, int64_t n, uint32_t* out, unsigned long long* new_count,
-              int* flags, hipStream_t st) {
-    if (n > 0) hipLaunchKernelGGL(kt_probe_k, blocks(n), dim3(256), 0, st, t, col, kind, n, out, new_count, flags);
+              unsigned long long limit, int* flags, hipStream_t st) {
+    if (n > 0) hipLaunchKernelGGL(kt_probe_k, blocks(n), dim3(256), 0, st, t, col, kind, n, out, new_count, limit, flags);
 }
 void kt_collect(const KeyTab& t, unsigned long long* pairs, int64_t* vals, unsigned long long* cnt, int64_t cap_out,
                 hipStream_t st) {
