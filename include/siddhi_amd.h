@@ -110,7 +110,9 @@ int sdg_push_events(sdg_engine* e, int stream, int64_t n, const int64_t* ts, con
  * FLOAT/DOUBLE the bit pattern in the low bits, BOOL 0/1, STRING an sdg_intern id); nulls[a] optional */
 int sdg_push_mixed(sdg_engine* e, int64_t n, const int32_t* streams, const int64_t* ts, int32_t n_attrs,
                    const int64_t* const* slots, const uint8_t* const* nulls);
-/* the same with device-resident columns (no copy; the caller keeps them alive until sdg_flush returns) */
+/* the same with device-resident columns (no copy; the caller keeps them alive until sdg_flush returns). Partition
+ * keys: string attributes as sdg_intern ids; int / long attributes as their values (mapped to key ids on the device,
+ * ValuePartitionExecutor.java:34-40 toString semantics); no null keys, no range partitions */
 int sdg_push_device(sdg_engine* e, int stream, int64_t n, const int64_t* d_ts, const void* const* d_cols,
                     const uint8_t* const* d_nulls);
 /* the clock moves to ts (playback: TimestampGeneratorImpl.setCurrentTimestamp when ts >= clock; live: the wall
