@@ -1483,8 +1483,9 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     // complete its deque's top (ordering comparisons on a numeric scan column only; chain_dq_summ_k)
     const bool numeric = a.sp.scan_t == VK_I32 || a.sp.scan_t == VK_I64 || a.sp.scan_t == VK_F32 || a.sp.scan_t == VK_F64;
     const bool ord_op = a.sp.scan_op == CMP_GT || a.sp.scan_op == CMP_GE || a.sp.scan_op == CMP_LT || a.sp.scan_op == CMP_LE;
-    if (a.deque_mode != DQ_OFF && !fused && nrows > 0 && !a.key && numeric && ord_op && a.sp.scan_mode != SCAN_TRUE &&
-        !getenv("SDG_DQ_NOSKIP")) {
+    static const bool summ_all = getenv("SDG_DQ_SUMM_ALL") != nullptr;  // A/B: summaries on keyed batches too
+    if (a.deque_mode != DQ_OFF && !fused && nrows > 0 && (!a.key || summ_all) && numeric && ord_op &&
+        a.sp.scan_mode != SCAN_TRUE && !getenv("SDG_DQ_NOSKIP")) {
         const int64_t nch = (nrows + DQ_CHUNK - 1) / DQ_CHUNK, ngr = nch * (DQ_CHUNK / DQ_GROUP);
         uint8_t* b = (uint8_t*)q.o_dqs.ensure((size_t)(nch + ngr) * 17);
         a.dq_hi = (int64_t*)b;
