@@ -1267,7 +1267,9 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                     i = j;
                 }
             };
+            hp.mark("sched_first_run");
             read_logs(false);
+            hp.mark("sched_read_logs");
             while ((int64_t)q.key_hash.size() < (int64_t)K) {  // HashMap hash of each key's toString
                 const size_t k = q.key_hash.size();
                 const std::string& ks = q.string_keys ? e->strings.strs[k] : q.keystr[k];
@@ -1286,6 +1288,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 horig.resize(nrows);
                 HIPCHECK(hipMemcpy(horig.data(), v_orig, nrows * 4, hipMemcpyDeviceToHost));
             }
+            hp.mark("sched_key_hash+segments");
             KeyRows kr;
             kr.seg_b = hseg_b.data();
             kr.seg_e = hseg_e.data();
@@ -1334,6 +1337,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             SchedSim::Result res;
             for (int tries = 0;; ++tries) {
                 q.sim.simulate(e->bc, logs, q.key_hash, kr, take, res, true);
+                hp.mark("sched_simulate_optimistic");
                 q.reordered = res.reordered;
                 if (q.reordered.empty()) break;
                 const int64_t nl = (int64_t)q.reordered.size();
@@ -1349,7 +1353,9 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 a.round = 1;
                 e->stats.match_launches += 1;
                 if (launch(false)) {
+                    hp.mark("sched_rerun_launch");
                     read_logs(true);
+                    hp.mark("sched_rerun_logs");
                     break;
                 }
                 // outputs or logs overflowed in the rerun (buffers grown): everything again from the batch start
@@ -1360,6 +1366,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             }
             q.runs.clear();
             q.sim.simulate(e->bc, logs, q.key_hash, kr, take, res);
+            hp.mark("sched_simulate_exact");
             for (auto& r : q.runs) {
                 if (r->overflow())
                     throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': a partition key exceeded max_partials "
