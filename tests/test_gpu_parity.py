@@ -118,6 +118,43 @@ def test_one_key_deque_shapes(qi, data, oracle_built):
     assert len(ref) > 10
 
 
+@pytest.mark.parametrize("qi", [0, 1, 4])
+def test_one_key_deque_nulls_and_nan(qi, oracle_built):
+    """null and NaN scan values never complete a partial nor start one (compare false): the chunk summaries
+    leave them out of their min / max"""
+    n = 8_000
+    cols = w.c1_columns(n)
+    i = np.arange(n)
+    price = cols["price"].copy()
+    price[i % 53 == 7] = np.nan
+    null = (i % 37 == 3).astype(np.uint8)
+    app = "@app:playback " + w.STOCK_STREAM + " @info(name = 'query1') from " + DQ_APPS[qi] + \
+        " select e1.id as e1id, e2.id as e2id insert into M;"
+    o = Oracle(app)
+    try:
+        for r in range(n):
+            o.send("StockStream", int(cols["ts"][r]), [int(cols["id"][r]), "IBM",
+                                                       None if null[r] else float(price[r]), int(cols["volume"][r])])
+        ref = [(x["ts"], tuple(v[1] for v in x["values"])) for x in o.outputs() if x["kind"] == "query"]
+    finally:
+        o.close()
+    rt = sa.SiddhiAppRuntime(app)
+    try:
+        h = rt.getInputHandler("StockStream")
+        sym = np.full(n, rt.intern("IBM"), np.uint32)
+        got = []
+        for s, e in ((0, n // 2), (n // 2, n)):
+            h.send_columns(cols["ts"][s:e], [cols["id"][s:e], sym[s:e], price[s:e], cols["volume"][s:e]],
+                           nulls=[None, None, null[s:e], None])
+            rt.flush(deliver=False)
+            types, ts, vals, nulls = rt.raw_outputs(0)
+            got += [(ts[k], (vals[0][k], vals[1][k])) for k in range(len(ts))]
+    finally:
+        rt.shutdown()
+    assert len(ref) > 10
+    assert got == ref
+
+
 @pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("batches", [1, 7])
 def test_c2_matches_oracle(batches, fused, oracle_built):
