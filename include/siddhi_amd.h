@@ -96,6 +96,9 @@ int sdg_query_output_schema(sdg_engine* e, int query, int32_t* n_attrs, const in
                             const char* const** names);
 uint32_t sdg_intern(sdg_engine* e, const char* s, size_t len);
 const char* sdg_string(sdg_engine* e, uint32_t id);
+/* sdg_intern for n strings at once (a binding's per-batch dictionary fill; C5's 10^7 partition keys per GPU):
+ * string i is bytes[offsets[i] .. offsets[i + 1]), offsets has n + 1 entries; its id goes to ids[i] */
+int sdg_intern_many(sdg_engine* e, int64_t n, const char* bytes, const int64_t* offsets, uint32_t* ids);
 
 /* columnar host batch for ONE stream: ts[n], cols[a] (typed as above), nulls[a] may be NULL */
 int sdg_push(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const void* const* cols,

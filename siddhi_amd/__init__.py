@@ -122,6 +122,7 @@ def load_library():
                                           ctypes.POINTER(ctypes.POINTER(ctypes.c_char_p))]
     L.sdg_intern.restype = U32
     L.sdg_intern.argtypes = [P, ctypes.c_char_p, ctypes.c_size_t]
+    L.sdg_intern_many.argtypes = [P, I64, P, P, P]
     L.sdg_string.restype = ctypes.c_char_p
     L.sdg_string.argtypes = [P, U32]
     L.sdg_push.argtypes = [P, I32, I64, P, P, P]
@@ -285,6 +286,18 @@ class SiddhiAppRuntime:
     def intern(self, s):
         b = s.encode()
         return self._L.sdg_intern(self._h, b, len(b))
+
+    def intern_many(self, data, offsets):
+        """bulk intern: string i = data[offsets[i]:offsets[i + 1]] (bytes / uint8 array, int64 offsets[n + 1]);
+        returns the ids (uint32 numpy array)"""
+        import numpy as np
+        buf = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else \
+            np.ascontiguousarray(data, dtype=np.uint8)
+        off = np.ascontiguousarray(offsets, dtype=np.int64)
+        n = len(off) - 1
+        ids = np.empty(max(n, 0), dtype=np.uint32)
+        _check(self._L.sdg_intern_many(self._h, n, buf.ctypes.data, off.ctypes.data, ids.ctypes.data))
+        return ids
 
     def string(self, i):
         r = self._L.sdg_string(self._h, i)

@@ -678,6 +678,22 @@ const uint32_t* device_key_ids(sdg_engine* e, QueryRt& q, const void* col, int k
             continue;
         }
         if (cnt == 0) return out;
+        // the probe inserted the new keys (ids 0) into the table: if anything below fails, the table is rebuilt from
+        // the dictionary at the next batch and the dictionary itself is rolled back to its K0 ids
+        struct Rollback {
+            QueryRt& q;
+            size_t K0;
+            bool armed = true;
+            ~Rollback() {
+                if (!armed) return;
+                q.kt_cap = 0;
+                q.kt_synced = 0;
+                for (size_t i = K0; i < q.keystr.size(); ++i) q.keydict.erase(q.keystr[i]);
+                q.keystr.resize(K0);
+                q.intkeys = IntKeyCache();
+                for (size_t i = 0; i < K0; ++i) q.intkeys.insert(std::stoll(q.keystr[i]), (uint32_t)i);  // int / long keys only
+            }
+        } rollback{q, K0};
         unsigned long long* d_pairs = (unsigned long long*)q.kt_pairs.ensure(cnt * 8);
         int64_t* d_vals = (int64_t*)q.kt_vals.ensure(cnt * 8);
         unsigned long long* d_n2 = (unsigned long long*)(d_c + 16);
@@ -705,6 +721,7 @@ const uint32_t* device_key_ids(sdg_engine* e, QueryRt& q, const void* col, int k
         kt_assign(t, d_slots, (uint32_t)K0, (int64_t)cnt, st);
         kt_fix(t, col, kind, n, out, st);
         q.kt_synced = q.keystr.size();
+        rollback.armed = false;
         return out;
     }
 }
@@ -1922,18 +1939,28 @@ int do_flush(sdg_engine* e) {
     e->stats.fused_ovf = 0;
     e->stats.sched_fires = e->stats.sched_shifted = e->stats.sched_host_keys = e->stats.sched_rerun_keys = 0;
     // a flush consumes its batch whether or not it succeeds: a failing query must not make the next flush
-    // replay the events onto the queries that already committed them
+    // replay the events onto the queries that already committed them. The batch's positions and its clock are
+    // consumed with it: queries that committed before a failing one hold carries, arenas and scheduler state
+    // stamped with positions [seq, seq + G) and the batch's clock, so the next flush starts after them
     struct Consume {
         sdg_engine* e;
+        int64_t G = 0;
+        bool clock_built = false;
         ~Consume() {
+            if (clock_built && G > 0) e->clock = e->bc.clk[G - 1];
+            e->seq += G;
             e->pending.clear();
             e->pending_n = 0;
         }
     } consume{e};
     int64_t G = 0;
     for (auto& c : e->pending) G += c.n;
+    consume.G = G;
     if (G >= (int64_t)0xFFFFFFF0) throw CompileError(SDG_ERR_CAPACITY, "a flush holds more than 2^32 - 16 events");
-    if (e->any_sched || e->any_purge) build_clock(e, G);
+    if (e->any_sched || e->any_purge) {
+        build_clock(e, G);
+        consume.clock_built = true;
+    }
     for (auto& q : e->qs) {
         drain(e, *q);  // earlier unpolled results go to the backlog first
         if (q->hq.plan.purge && q->purge_first == INT64_MIN) {  // the partition's first event: its clock reading
@@ -1957,8 +1984,6 @@ int do_flush(sdg_engine* e) {
         }
         flush_query(e, *q);
     }
-    if ((e->any_sched || e->any_purge) && G > 0) e->clock = e->bc.clk[G - 1];
-    e->seq += G;
     e->stats.ms_total = e->stats.ms_keygroup + e->stats.ms_match;
     return SDG_OK;
 }
@@ -2085,70 +2110,147 @@ void snapshot(sdg_engine* e, std::vector<uint8_t>& out) {
     }
 }
 
+// restore in two phases, like the reference (which deserialises the whole snapshot before touching a state): the
+// blob is parsed and validated completely first (device payloads stay as views into it), then applied. A truncated
+// or corrupt blob throws before any engine state changed.
 void restore(sdg_engine* e, const uint8_t* data, size_t len) {
     SnapR r{data, data + len};
     if (r.get<uint64_t>() != SNAP_MAGIC) throw CompileError(SDG_ERR_ARG, "not an engine snapshot");
     if (r.get<uint64_t>() != e->app_hash)
         throw CompileError(SDG_ERR_ARG, "the snapshot was taken from a different Siddhi app");  // CannotRestoreSiddhiAppStateException
-    hipStream_t st = e->stream;
+    struct View {
+        const uint8_t* p = nullptr;
+        size_t n = 0;
+    };
+    auto view = [&]() {
+        View v;
+        v.p = r.bytes(&v.n);
+        return v;
+    };
+    struct Stage {
+        int32_t chain = 0;
+        bool replay = false, nullable = false;
+        int64_t cn = 0;
+        View ckey, cts, cseq, cnulls;
+        std::vector<View> cvals;
+        std::vector<int64_t> ik;
+        std::vector<uint32_t> iv;
+        uint64_t in = 0;
+        std::vector<std::string> keystr;
+        std::vector<int32_t> key_hash;
+        nfa::Layout L{};
+        int64_t arena_keys = 0;
+        View arena, arena2, cur_bits, last_seen, agg;
+        int64_t purge_first = INT64_MIN, agg_keys = 0;
+        SchedSim sim;
+    };
     const int64_t seq = r.get<int64_t>();
     const int64_t clock = r.get<int64_t>();
     Interner strings;
     const uint64_t ns = r.get<uint64_t>();
     for (uint64_t i = 0; i < ns; ++i) strings.get(r.str());
     if (r.get<uint32_t>() != e->qs.size()) throw CompileError(SDG_ERR_ARG, "snapshot query count differs");
-    for (auto& qp : e->qs) {
-        QueryRt& q = *qp;
+    std::vector<Stage> stg(e->qs.size());
+    for (size_t qi = 0; qi < e->qs.size(); ++qi) {
+        const Plan& P = e->qs[qi]->hq.plan;
+        Stage& g = stg[qi];
+        g.chain = r.get<int32_t>();
+        g.replay = r.get<uint8_t>() != 0;
+        g.nullable = r.get<uint8_t>() != 0;
+        const int nc = std::max(P.n_cols, 1);
+        g.cn = r.get<int64_t>();
+        if (g.cn < 0) throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (carry count)");
+        if (g.cn > 0) {
+            g.ckey = view();
+            g.cts = view();
+            g.cseq = view();
+            for (int k = 0; k < nc; ++k) g.cvals.push_back(view());
+            g.cnulls = view();
+            bool ok = g.ckey.n == (size_t)g.cn * 4 && g.cts.n == (size_t)g.cn * 8 && g.cseq.n == (size_t)g.cn * 8 &&
+                      g.cnulls.n == (size_t)g.cn * 4;
+            for (const View& v : g.cvals) ok = ok && v.n == (size_t)g.cn * 8;
+            if (!ok) throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (carried partials)");
+        }
+        r.vec(g.ik);
+        r.vec(g.iv);
+        g.in = r.get<uint64_t>();
+        const uint64_t nks = r.get<uint64_t>();
+        if (nks > (uint64_t)(r.end - r.p) / 8) throw CompileError(SDG_ERR_ARG, "snapshot is truncated");
+        g.keystr.resize(nks);
+        for (auto& x : g.keystr) x = r.str();
+        r.vec(g.key_hash);
+        g.L = r.get<nfa::Layout>();
+        g.arena_keys = r.get<int64_t>();
+        if (g.arena_keys < 0) throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (arena keys)");
+        if (g.arena_keys > 0) {
+            g.arena = view();
+            g.arena2 = view();
+            g.cur_bits = view();
+            if (g.arena.n != (size_t)(g.arena_keys * g.L.bytes) || g.arena2.n != g.arena.n || g.cur_bits.n != (size_t)g.arena_keys)
+                throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (arenas)");
+        }
+        g.purge_first = r.get<int64_t>();
+        if (P.purge && g.arena_keys > 0) g.last_seen = view();
+        g.agg_keys = r.get<int64_t>();
+        if (g.agg_keys > 0) g.agg = view();
+        g.sim.setup(P.n_sched, P.partitioned, !P.playback);
+        r.p = g.sim.load(r.p, r.end);
+    }
+    if (r.p != r.end) throw CompileError(SDG_ERR_ARG, "snapshot has trailing bytes");
+    // ---- apply ------------------------------------------------------------------------------------------
+    hipStream_t st = e->stream;
+    auto up = [&](DevBuf& d, const View& v) {
+        void* x = d.ensure(v.n);
+        if (v.n) HIPCHECK(hipMemcpyAsync(x, v.p, v.n, hipMemcpyHostToDevice, st));
+    };
+    for (size_t qi = 0; qi < e->qs.size(); ++qi) {
+        QueryRt& q = *e->qs[qi];
         Plan& P = q.hq.plan;
-        P.chain = r.get<int32_t>();
-        q.replay_carries = r.get<uint8_t>() != 0;
-        q.carry_nullable = r.get<uint8_t>() != 0;
+        Stage& g = stg[qi];
+        P.chain = g.chain;
+        q.replay_carries = g.replay;
+        q.carry_nullable = g.nullable;
         const int nc = std::max(P.n_cols, 1);
         q.cur = 0;
         q.carry[1].n = 0;
         QueryRt::Carry& c = q.carry[0];
-        c.n = r.get<int64_t>();
+        c.n = g.cn;
         if (c.n > 0) {
             c.cap = c.n;
-            r.dev(c.key, st);
-            r.dev(c.ts, st);
-            r.dev(c.seq, st);
+            up(c.key, g.ckey);
+            up(c.ts, g.cts);
+            up(c.seq, g.cseq);
             c.vals.ensure((size_t)nc * c.n * 8);
-            for (int k = 0; k < nc; ++k) {
-                size_t n;
-                const uint8_t* b = r.bytes(&n);
-                HIPCHECK(hipMemcpy((int64_t*)c.vals.p + (size_t)k * c.cap, b, n, hipMemcpyHostToDevice));
-            }
-            r.dev(c.nulls, st);
+            for (int k = 0; k < nc; ++k)
+                HIPCHECK(hipMemcpyAsync((int64_t*)c.vals.p + (size_t)k * c.cap, g.cvals[k].p, g.cvals[k].n,
+                                        hipMemcpyHostToDevice, st));
+            up(c.nulls, g.cnulls);
         }
-        r.vec(q.intkeys.k);
-        r.vec(q.intkeys.v);
-        q.intkeys.n = (size_t)r.get<uint64_t>();
-        q.keystr.resize(r.get<uint64_t>());
+        q.intkeys.k = std::move(g.ik);
+        q.intkeys.v = std::move(g.iv);
+        q.intkeys.n = (size_t)g.in;
+        q.keystr = std::move(g.keystr);
         q.keydict.clear();
         q.kt_cap = 0;  // the device key table is rebuilt from the dictionary on the next device-resident batch
         q.kt_synced = 0;
-        for (size_t i = 0; i < q.keystr.size(); ++i) {
-            q.keystr[i] = r.str();
-            q.keydict[q.keystr[i]] = (uint32_t)i;
-        }
-        r.vec(q.key_hash);
-        q.L = r.get<nfa::Layout>();
-        q.arena_keys = r.get<int64_t>();
+        for (size_t i = 0; i < q.keystr.size(); ++i) q.keydict[q.keystr[i]] = (uint32_t)i;
+        q.key_hash = std::move(g.key_hash);
+        q.L = g.L;
+        q.arena_keys = g.arena_keys;
         if (q.arena_keys > 0) {
-            r.dev(q.arena, st);
-            r.dev(q.arena2, st);
-            r.dev(q.cur_bits, st);
+            up(q.arena, g.arena);
+            up(q.arena2, g.arena2);
+            up(q.cur_bits, g.cur_bits);
             q.ran_bits.ensure((size_t)q.arena_keys);
-            HIPCHECK(hipMemset(q.ran_bits.p, 0, (size_t)q.arena_keys));
+            HIPCHECK(hipMemsetAsync(q.ran_bits.p, 0, (size_t)q.arena_keys, st));
         }
-        q.purge_first = r.get<int64_t>();
-        if (P.purge && q.arena_keys > 0) r.dev(q.last_seen, st);
-        q.agg_keys = r.get<int64_t>();
-        if (q.agg_keys > 0) r.dev(q.agg_state, st);
-        r.p = q.sim.load(r.p, r.end);
+        q.purge_first = g.purge_first;
+        if (P.purge && q.arena_keys > 0) up(q.last_seen, g.last_seen);
+        q.agg_keys = g.agg_keys;
+        if (q.agg_keys > 0) up(q.agg_state, g.agg);
+        q.sim = std::move(g.sim);
+        HIPCHECK(hipStreamSynchronize(st));  // the views point into the caller's blob
     }
-    if (r.p != r.end) throw CompileError(SDG_ERR_ARG, "snapshot has trailing bytes");
     e->seq = seq;
     e->clock = clock;
     e->strings = std::move(strings);
@@ -2307,6 +2409,19 @@ int sdg_query_output_schema(sdg_engine* e, int q, int32_t* n, const int32_t** ty
 }
 
 uint32_t sdg_intern(sdg_engine* e, const char* s, size_t len) { return e->strings.get(std::string(s, len)); }
+int sdg_intern_many(sdg_engine* e, int64_t n, const char* bytes, const int64_t* offsets, uint32_t* ids) {
+    if (!e || n < 0 || (n > 0 && (!bytes || !offsets || !ids))) return fail(SDG_ERR_ARG, "bad intern arguments");
+    return guarded([&]() {
+        Interner& in = e->strings;
+        in.strs.reserve(in.strs.size() + (size_t)n);
+        in.ids.reserve(in.ids.size() + (size_t)n);
+        for (int64_t i = 0; i < n; ++i) {
+            if (offsets[i + 1] < offsets[i]) throw std::invalid_argument("intern offsets decrease");
+            ids[i] = in.get(std::string(bytes + offsets[i], (size_t)(offsets[i + 1] - offsets[i])));
+        }
+        return (int)SDG_OK;
+    });
+}
 const char* sdg_string(sdg_engine* e, uint32_t id) {
     return id < e->strings.strs.size() ? e->strings.strs[id].c_str() : nullptr;
 }

@@ -294,6 +294,7 @@ def extract(name, line, body, relpath, class_src):
     started = False
     expected_count = None
     remove_count = None
+    arrived = None  # True / False: the test asserts that some / no event arrived
     clock = LIVE_T0
     i = 0
     n = len(body)
@@ -463,6 +464,10 @@ def extract(name, line, body, relpath, class_src):
             joined = " ".join(t[1] for t in args).lower()
             m_in = "ineventcount" in joined
             m_rm = "removeeventcount" in joined
+            if re.search(r"\btrue\s*,\s*eventarrived\b", joined) or re.search(r"\beventarrived\s*,\s*true\b", joined):
+                arrived = True  # assertEquals("Event arrived", true, eventArrived): at least one event delivered
+            elif re.search(r"\bfalse\s*,\s*eventarrived\b", joined) or re.search(r"\beventarrived\s*,\s*false\b", joined):
+                arrived = False  # ... false, eventArrived: nothing delivered
             if (m_in or m_rm) and "getdata" not in joined:
                 pieces, depth, cur = [], 0, []
                 for t in args:
@@ -509,6 +514,7 @@ def extract(name, line, body, relpath, class_src):
         "expected": {
             "count": None if expected_count is None else {"callback": expected_count[0], "value": expected_count[1]},
             "remove_count": None if remove_count is None else {"callback": remove_count[0], "value": remove_count[1]},
+            "arrived": arrived,
         },
         "model": "playback timestamps (sleeps do not move the engine clock)" if playback else
                  "wall-clock test: Thread.sleep(d) -> modelled clock += d; timers fire as the clock passes them",

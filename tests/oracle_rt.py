@@ -314,6 +314,12 @@ def check_fixture(fx, outputs):
         got = len(per_cb[ci][1])
         if got != v:
             problems.append("remove-event count: expected %d got %d" % (v, got))
+    if exp.get("arrived") is not None:  # assertEquals(.., true / false, eventArrived) over every callback
+        n_any = sum(len(a) + len(r) for a, r in per_cb)
+        if exp["arrived"] and n_any == 0:
+            problems.append("expected at least one event, got none")
+        if not exp["arrived"] and n_any:
+            problems.append("expected no event, got %d" % n_any)
     for ci, cb in enumerate(cbs):
         rows = cb["rows"]
         if not rows:
