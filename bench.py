@@ -251,6 +251,191 @@ def ordered_gather_leg(rt, step_push, n, dev, dist, rank, world):
             "path": "sdg_export_device -> per-rank device sort -> RCCL send/recv to rank 0 -> merge"}
 
 
+def run_c5(args, rank, world, local, dist):
+    """C5 (BASELINE.json configs[4]): the C2 query over the 10^10-event / 10^8-key stream, key-hash sharded, every rank
+    generating its shard on its GPU (siddhi_amd/c5.py) in batches of 2^28 of its own events. A step = one rank flush
+    of one batch, inputs resident in HBM (all batches of the run are generated before the timed region). value =
+    events of every rank's timed flushes / max-over-ranks time. Outside the timed region: the ordered result gather
+    of one more batch to rank 0 (RCCL send/recv, G-way merge on the global position of the emitting event) and a
+    10^4-key oracle sample of this rank's shard (tests/c5_check.py)."""
+    import torch
+    import siddhi_amd as sa
+    from siddhi_amd import c5, shard
+    from siddhi_amd import workloads as w
+    dev = torch.device("cuda", local)
+    srank, sworld = rank, world
+    if args.c5_shard:  # one rank's shard of a larger run, measured on this one GPU
+        if world > 1:
+            raise SystemExit("--c5-shard is for a single process")
+        srank, sworld = (int(x) for x in args.c5_shard.split("/"))
+    rt = sa.SiddhiAppRuntime(w.C2_APP, device=local)
+    log("C5: interning this rank's keys (shard %d/%d)" % (srank, sworld))
+    sh = c5.C5Shard(rt, srank, sworld, dev, events=args.c5_events, batch=args.c5_batch)
+    nb = sh.n_batches()
+    nsteps = args.warmup + args.steps
+    if nsteps > nb:
+        raise SystemExit("C5: %d batches in the stream at this world size, %d requested" % (nb, nsteps))
+    log("C5: %d keys on this rank; generating %d batches of ~%d events" % (sh.n_keys, nsteps, args.c5_batch))
+    batches = [sh.generate(j) for j in range(nsteps)]
+    torch.cuda.synchronize()
+
+    def push(j):
+        cols, n = batches[j]
+        rt.push_device("StockStream", n, cols["ts"].data_ptr(), [cols["id"].data_ptr(), cols["sym"].data_ptr(),
+                                                                cols["price"].data_ptr(), cols["volume"].data_ptr()])
+        return n
+
+    def step(j):
+        n = push(j)
+        rt.flush(deliver=False)
+        rt.discard()
+        st = rt.stats()
+        if dist is not None:  # batch-boundary match-count all-gather (global output offsets)
+            cnt = torch.tensor([st.matches], dtype=torch.int64, device=dev)
+            allc = [torch.empty_like(cnt) for _ in range(world)]
+            dist.all_gather(allc, cnt)
+        return n, st
+
+    log("C5: warm-up (%d flushes)" % args.warmup)
+    for j in range(args.warmup):
+        step(j)
+    keys_k = ["ms_kg_hist", "ms_kg_prefix", "ms_kg_scatter", "ms_chain_carry", "ms_chain_match", "ms_chain_emit"]
+    acc = {k: 0.0 for k in keys_k}
+    events = matches = 0
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(args.warmup, nsteps):
+        n, st = step(j)
+        events += n
+        matches += st.matches
+        for k in keys_k:
+            acc[k] += getattr(st, k)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tot_events, tot_matches = events, matches
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        v = torch.tensor([events, matches], dtype=torch.int64, device=dev)
+        dist.all_reduce(v)
+        tot_events, tot_matches = int(v[0].item()), int(v[1].item())
+    K = args.steps
+    per_kernel = {k: acc[k] / K for k in keys_k}
+    dom = max(per_kernel, key=per_kernel.get)
+    step_bytes = (events * B_IN + matches * B_OUT) / K  # this rank's algorithmic bytes per flush
+    achieved = step_bytes / (per_kernel[dom] / 1000.0) / 1e9
+    names = {"ms_kg_scatter": "rx_scatter (all radix passes of the flush)", "ms_chain_match": "chain_deque_k",
+             "ms_chain_emit": "chain_match_k (emission)", "ms_chain_carry": "chain_carry_wave_k", "ms_kg_hist": "rx_hist",
+             "ms_kg_prefix": "rx_p1/p2/p3"}
+    out = {
+        "metric": "input events/sec matched (node) at 1/2/4/8 MI355X; % HBM roofline",
+        "value": tot_events / elapsed, "unit": "events/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
+        "ms_per_step": elapsed * 1000.0 / K, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (splitmix64 C5 generator on the GPU, siddhi_amd/c5.py), device-resident",
+        "config": {"workload": "C5: C2 query, %d events / 10^8 keys key-hash sharded over %d GPU(s)%s, batches of "
+                               "%d rank events" % (args.c5_events, sworld, "" if sworld == world else
+                                                   " (shard %d of %d measured on this GPU)" % (srank, sworld),
+                                                   args.c5_batch),
+                   "keys_this_rank": sh.n_keys, "events_per_rank_step": events / K, "matches_per_step": tot_matches / K,
+                   "parallelism": "key-hash shards x%d" % sworld, "path": "radix key sort + chain kernels"},
+        "roofline": {"bound": "hbm", "kernel": names.get(dom, dom), "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "algorithmic_bytes_per_launch": step_bytes,
+                     "step_frac": step_bytes / (elapsed / K) / 1e9 / HBM_PEAK_GBS, "kernel_ms": per_kernel},
+        "cpu_baseline": None,
+    }
+    del batches
+    torch.cuda.empty_cache()
+    if not args.no_gather and nsteps < nb:
+        log("C5: ordered result gather of batch %d (outside the timed region)" % nsteps)
+        cols, n = sh.generate(nsteps)
+        rt.push_device("StockStream", n, cols["ts"].data_ptr(), [cols["id"].data_ptr(), cols["sym"].data_ptr(),
+                                                                cols["price"].data_ptr(), cols["volume"].data_ptr()])
+        rt.flush(deliver=False)
+        del cols
+        m = int(rt.stats().matches)
+        t_ts = torch.empty(max(m, 1), dtype=torch.int64, device=dev)
+        t_seq, t_sub = torch.empty_like(t_ts), torch.empty_like(t_ts)
+        t_vals = torch.empty((2, max(m, 1)), dtype=torch.int64, device=dev)
+        rt.export_device(0, max(m, 1), t_ts.data_ptr(), t_seq.data_ptr(), t_sub.data_ptr(), t_vals.data_ptr())
+        recs = {"e2": t_vals[1, :m].contiguous(), "e1": t_vals[0, :m].contiguous(), "ts": t_ts[:m]}
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        if dist is None:
+            order = shard.lexsort([recs["e2"], recs["e1"]])
+            merged = {k: v[order] for k, v in recs.items()}
+        else:
+            merged = shard.ordered_gather(dist, rank, world, recs, ["e2", "e1"])
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - tg
+        if rank == 0:
+            e2, e1 = merged["e2"], merged["e1"]
+            ok = bool(((e2[1:] > e2[:-1]) | ((e2[1:] == e2[:-1]) & (e1[1:] > e1[:-1]))).all().item()) \
+                if e2.numel() > 1 else True
+            if not ok:
+                raise RuntimeError("C5 ordered gather: merged records are not in delivery order")
+            out["ordered_gather"] = {"records": int(e2.numel()), "ms": dt * 1000.0, "ordered": True,
+                                     "key": "(e2id = global position of the emitting event, e1id)",
+                                     "path": "sdg_export_device -> per-rank device sort -> RCCL send/recv to rank 0 "
+                                             "-> G-way merge (shard.merge_runs)"}
+        del t_ts, t_seq, t_sub, t_vals, recs, merged
+        torch.cuda.empty_cache()
+    if not args.no_parity:
+        log("C5: oracle sample of this rank's shard (%d keys)" % args.c5_sample)
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from c5_check import delivery_order, oracle_sample_rows, sample_records
+        rt.shutdown()
+        rt = sa.SiddhiAppRuntime(w.C2_APP, device=local)  # a fresh run of the same stream prefix
+        sh2 = c5.C5Shard(rt, srank, sworld, dev, events=args.c5_events, batch=args.c5_batch)
+        skeys, smap = sh2.sample(args.c5_sample)
+        rows, bad_all = [], {}
+        nf = min(2, nb)
+        for j in range(nf):
+            cols, n = sh2.generate(j)
+            rt.push_device("StockStream", n, cols["ts"].data_ptr(), [cols["id"].data_ptr(), cols["sym"].data_ptr(),
+                                                                    cols["price"].data_ptr(), cols["volume"].data_ptr()])
+            rt.flush(deliver=False)
+            del cols
+            m = int(rt.stats().matches)
+            t_ts = torch.empty(max(m, 1), dtype=torch.int64, device=dev)
+            t_seq, t_sub = torch.empty_like(t_ts), torch.empty_like(t_ts)
+            t_vals = torch.empty((2, max(m, 1)), dtype=torch.int64, device=dev)
+            rt.export_device(0, max(m, 1), t_ts.data_ptr(), t_seq.data_ptr(), t_sub.data_ptr(), t_vals.data_ptr())
+            bad = c5.check_matches(sh2, t_vals[0, :m], t_vals[1, :m], t_ts[:m])
+            for k, v in bad.items():
+                bad_all[k] = bad_all.get(k, 0) + v
+            rows.append(sample_records(sh2, smap, t_ts[:m], t_vals[0, :m], t_vals[1, :m]))
+            del t_ts, t_seq, t_sub, t_vals
+            torch.cuda.empty_cache()
+        _, g_end = sh2.global_range(nf - 1)
+        n_s, ref = oracle_sample_rows(sh2, skeys, smap, g_end)
+        got = delivery_order(np.concatenate(rows))
+        ok = got.shape == ref.shape and np.array_equal(got, ref) and not any(bad_all.values())
+        if not ok:
+            raise RuntimeError("C5: GPU match rows differ from the oracle on the %d-key sample (%d vs %d rows; %s)"
+                               % (len(skeys), len(got), len(ref), bad_all))
+        out["parity"] = {"sample_keys": len(skeys), "sample_events": int(n_s), "sample_matches": int(len(ref)),
+                         "flushes": nf, "bit_exact": True, "property_violations": bad_all}
+        if dist is not None:
+            okt = torch.tensor([1], dtype=torch.int64, device=dev)
+            dist.all_reduce(okt)
+            out["parity"]["ranks_checked"] = int(okt.item())
+    rt.shutdown()
+    log("done")
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -265,6 +450,13 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=1, help="end-to-end (host push -> poll) steps, 0 = skip")
     ap.add_argument("--no-gather", action="store_true", help="skip the ordered result gather leg")
+    ap.add_argument("--config", choices=["c2", "c5"], default="c2",
+                    help="c2 (default, the metric's 1-GPU config) or c5 (10^10 events / 10^8 keys, key-hash sharded)")
+    ap.add_argument("--c5-events", type=int, default=10 ** 10, help="C5: events of the whole stream")
+    ap.add_argument("--c5-batch", type=int, default=1 << 28, help="C5: rank events per flush")
+    ap.add_argument("--c5-sample", type=int, default=10_000, help="C5: partition keys in the oracle sample")
+    ap.add_argument("--c5-shard", default=None,
+                    help="C5 on one process: run shard R/W (rank R of a W-GPU run) instead of this process's rank")
     args = ap.parse_args()
 
     import torch
@@ -277,6 +469,8 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    if args.config == "c5":
+        return run_c5(args, rank, world, local, dist)
     import siddhi_amd as sa
     from siddhi_amd import workloads as w
 

@@ -41,6 +41,9 @@ for s in "$@"; do
         cpubase) run cpubase 900 python3 scripts/cpu_baselines.py --threads 16 ;;
         c4prof) run c4prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/c4prof" -o run --output-format csv -- python3 scripts/bench_configs.py --only c4 ;;
         c4test) run c4test 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -s --timeout 300 --timeout-method thread -p no:cacheprovider -k c4 ;;
+        r3tests) run r3tests 900 python3 -u -m pytest tests/test_gpu_robust.py tests/test_gpu_c5.py -m gpu -x -v --timeout 600 --timeout-method thread -p no:cacheprovider ;;
+        c5shard) run c5shard 900 python3 bench.py --config c5 --c5-shard 0/8 --steps 3 --warmup 1 ;;
+        c5prof) run c5prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/c5prof" -o run --output-format csv -- python3 bench.py --config c5 --c5-shard 0/8 --steps 1 --warmup 1 --no-parity --no-gather ;;
         *) echo "unknown step $s" ;;
     esac
 done

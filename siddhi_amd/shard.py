@@ -51,12 +51,39 @@ def lexsort(keys):
     return order
 
 
+def merge_runs(runs, key):
+    """G-way merge of sorted runs (dicts of torch tensors, records along the last dim) by their 1-D `key` column:
+    record i of run r lands at  i + sum_{r' < r} #{x in run r' : x <= v} + sum_{r' > r} #{x in run r' : x < v}
+    (binary searches into the other runs), so equal keys keep run order, then their order inside the run. Linear
+    in the records (times log of a run), no re-sort of the concatenation."""
+    import torch
+    runs = [r for r in runs if r[key].numel() > 0]
+    if not runs:
+        return None
+    if len(runs) == 1:
+        return runs[0]
+    dev = runs[0][key].device
+    total = sum(int(r[key].numel()) for r in runs)
+    out = {k: torch.empty(list(v.shape[:-1]) + [total], dtype=v.dtype, device=dev) for k, v in runs[0].items()}
+    for r, run in enumerate(runs):
+        v = run[key]
+        pos = torch.arange(v.numel(), device=dev, dtype=torch.int64)
+        for r2, other in enumerate(runs):
+            if r2 != r:
+                pos += torch.searchsorted(other[key], v, right=r2 < r)
+        for k, col in run.items():
+            out[k][..., pos] = col
+    return out
+
+
 def ordered_gather(dist, rank, world, cols, key_names):
     """Ordered result gather: `cols` maps names to this rank's record tensors (1-D [n], or 2-D
     [m, n] with records along the last dim) on the communication device. Every rank sorts its records by
     `key_names` on its device, the run lengths are all-gathered, and each rank's sorted run goes to rank 0
-    point-to-point (send/recv: RCCL over xGMI with the nccl backend, gloo on CPU), where the runs are merged by the
-    same key. Returns the merged dict on rank 0, None elsewhere."""
+    point-to-point (send/recv: RCCL over xGMI with the nccl backend, gloo on CPU), where the G runs are merged on the
+    first key (merge_runs: records of different ranks with equal first keys keep rank order, which is the
+    tie-break every caller's key implies -- either the first key is unique across ranks, e.g. the global position of
+    the emitting event, or the rank is the next key). Returns the merged dict on rank 0, None elsewhere."""
     import torch
     names = sorted(cols)
     ref = cols[key_names[0]]
@@ -81,6 +108,7 @@ def ordered_gather(dist, rank, world, cols, key_names):
             run[k] = torch.empty(shape, dtype=cols[k].dtype, device=ref.device)
             dist.recv(run[k], src=r)
         runs.append(run)
-    merged = {k: torch.cat([run[k] for run in runs], dim=-1) for k in names}
-    order = lexsort([merged[k] for k in key_names])  # the runs are sorted: a stable sort of their concatenation
-    return {k: merged[k][..., order] for k in names}
+    merged = merge_runs(runs, key_names[0])
+    if merged is None:
+        return {k: mine[k] for k in names}
+    return merged

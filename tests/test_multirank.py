@@ -90,3 +90,20 @@ def test_route_is_balanced_and_stable():
     counts = [(r == i).sum() for i in range(8)]
     assert min(counts) > 1100 and max(counts) < 1400
     assert (shard.route(keys, 8) == r).all()
+
+
+def test_merge_runs_is_a_stable_g_way_merge():
+    """shard.merge_runs == a stable sort of the concatenation by (key, run), for G sorted runs with ties inside and
+    across runs"""
+    g = torch.Generator().manual_seed(5)
+    runs = []
+    for r in range(5):
+        n = int(torch.randint(0, 400, (1,), generator=g))
+        k = torch.sort(torch.randint(0, 300, (n,), generator=g)).values
+        runs.append({"k": k, "run": torch.full((n,), r, dtype=torch.int64), "i": torch.arange(n),
+                     "v": torch.stack([k * 3, k * 5])})
+    m = shard.merge_runs(runs, "k")
+    cat = {c: torch.cat([r[c] for r in runs], dim=-1) for c in runs[0]}
+    order = shard.lexsort([cat["k"], cat["run"], cat["i"]])
+    for c in cat:
+        assert torch.equal(m[c], cat[c][..., order]), c
