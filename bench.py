@@ -301,7 +301,7 @@ def run_c5(args, rank, world, local, dist):
         step(j)
     keys_k = ["ms_kg_hist", "ms_kg_prefix", "ms_kg_scatter", "ms_chain_carry", "ms_chain_match", "ms_chain_emit"]
     acc = {k: 0.0 for k in keys_k}
-    events = matches = 0
+    events = matches = carries = 0
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -310,6 +310,7 @@ def run_c5(args, rank, world, local, dist):
         n, st = step(j)
         events += n
         matches += st.matches
+        carries += st.carry_in
         for k in keys_k:
             acc[k] += getattr(st, k)
     torch.cuda.synchronize()
@@ -343,6 +344,7 @@ def run_c5(args, rank, world, local, dist):
                                                    " (shard %d of %d measured on this GPU)" % (srank, sworld),
                                                    args.c5_batch),
                    "keys_this_rank": sh.n_keys, "events_per_rank_step": events / K, "matches_per_step": tot_matches / K,
+                   "carried_partials_per_rank_step": carries / K,
                    "parallelism": "key-hash shards x%d" % sworld, "path": "radix key sort + chain kernels"},
         "roofline": {"bound": "hbm", "kernel": names.get(dom, dom), "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,

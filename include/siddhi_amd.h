@@ -60,7 +60,8 @@ typedef struct sdg_engine sdg_engine;
 typedef struct sdg_opts {
     int32_t device;            /* HIP device ordinal (one engine per GPU) */
     int64_t batch_capacity;    /* max events buffered between flushes (0 = default 1<<24) */
-    int32_t max_partials;      /* per-key bounded partial-match slots for the generic NFA (0 = default) */
+    int32_t max_partials;      /* per-key partial-match slots the generic NFA starts with (0 = default 8; the arenas
+                                  double on overflow up to 4096) */
     int32_t flags;             /* SDG_COMPILE_ONLY: parse + lower only, no device (introspection on hosts
                                   without a GPU; push/flush then fail with SDG_ERR_DEVICE) */
 } sdg_opts;
@@ -182,6 +183,8 @@ typedef struct sdg_stats {
     double ms_sched_host;      /* host ms: scheduler simulation passes, log read-back, host replays */
     int64_t arena_growths;     /* generic NFA: times a key ran out of partial-match slots and the arenas doubled
                                   (the batch reran from its start; max_partials is the starting size, 4096 the cap) */
+    int64_t carry_in;          /* chain path: partials carried into the last flush from the one before */
+    int64_t carry_out;         /* chain path: partials the last flush carries into the next */
 } sdg_stats;
 int sdg_last_stats(sdg_engine* e, sdg_stats* out);
 

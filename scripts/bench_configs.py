@@ -118,7 +118,7 @@ def main():
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         print(json.dumps({"config": "C3 %s, %d keys x 100 events/step (host push)" % ("<2:5>" if tag == "c3" else "<1:5>", keys),
-                          "max_partials": args.max_partials or 64,
+                          "max_partials": args.max_partials or 8,
                           "events_per_s_end_to_end": n * args.c3_steps / dt, "ms_per_step": dt * 1000 / args.c3_steps,
                           "device_ms_per_step": dev_ms / args.c3_steps, "events_per_s_device": n * args.c3_steps / (dev_ms / 1000),
                           "matches_per_step": m / args.c3_steps, "events_per_flush": st.events}), flush=True)

@@ -44,6 +44,9 @@ for s in "$@"; do
         r3tests) run r3tests 900 python3 -u -m pytest tests/test_gpu_robust.py tests/test_gpu_c5.py -m gpu -x -v --timeout 600 --timeout-method thread -p no:cacheprovider ;;
         c5shard) run c5shard 900 python3 bench.py --config c5 --c5-shard 0/8 --steps 3 --warmup 1 ;;
         c5prof) run c5prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/c5prof" -o run --output-format csv -- python3 bench.py --config c5 --c5-shard 0/8 --steps 1 --warmup 1 --no-parity --no-gather ;;
+        cfgs) run cfgs 900 python3 scripts/bench_configs.py --only c3m,c3md,c2generic,c4 --c3-steps 2 ;;
+        cfgshbm) run cfgshbm 900 env SDG_NFA_HBM=1 python3 scripts/bench_configs.py --only c3md,c2generic --c3-steps 2 ;;
+        c5host) run c5host 900 env SDG_HOST_PROF=1 python3 bench.py --config c5 --c5-shard 0/8 --steps 3 --warmup 1 --no-parity --no-gather ;;
         *) echo "unknown step $s" ;;
     esac
 done

@@ -243,7 +243,7 @@ struct sdg_engine {
     hipEvent_t ev[12] = {};
     std::vector<PushChunk> pending;
     int64_t capacity = 1 << 24;
-    int32_t max_partials = 64;
+    int32_t max_partials = 8;  // starting slots per key (arenas double on overflow): small arenas stage in LDS
     int64_t pending_n = 0;
     int64_t seq = 0;             // batch positions flushed so far (sequence number of the next batch's position 0)
     int64_t clock = 0;           // currentTime(): playback = max event ts seen; live = the modelled wall clock
@@ -1433,7 +1433,9 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     QueryRt::Carry& cout = q.carry[q.cur ^ 1];
     // output / carry capacity with slack: a buffer that grows inside a timed flush costs a hipFree (device sync)
     // plus a multi-GB hipMalloc, so round up once instead of growing with every larger carry-in count
-    int64_t cap = nrows + nrows / 8 + cin.n + 4096;
+    // (carried partials: at least n/8 of headroom from the first batch on, so the batch after it -- the first with
+    // carries -- does not reallocate every output and carry buffer)
+    int64_t cap = nrows + nrows / 8 + std::max(cin.n, nrows / 8) + 4096;
     q.out_cap = cap;
     ChainArgs a;
     std::memset(&a, 0, sizeof a);
@@ -1537,6 +1539,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         if (err != hipSuccess) throw DeviceError(std::string(what) + ": " + hipGetErrorString(err));
     };
     dbg_sync("bucketize / staging");
+    ev_record(e->ev[3], st);  // after the buffer (re)allocations above: they stall the stream, not the kernels
     chain_carry(a, d_a, st);
     dbg_sync("chain_carry_k");
     ev_record(e->ev[8], st);
@@ -1627,8 +1630,10 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         ev_elapsed(&t, e->ev[5], e->ev[6]);
         e->stats.ms_kg_scatter += t;
     }
-    ev_elapsed(&t, e->ev[1], e->ev[8]);
+    ev_elapsed(&t, e->ev[3], e->ev[8]);
     e->stats.ms_chain_carry += t;
+    e->stats.carry_in += cin.n;
+    e->stats.carry_out += (int64_t)hc[1];
     ev_elapsed(&t, e->ev[8], e->ev[9]);
     e->stats.ms_chain_match += t;
     ev_elapsed(&t, e->ev[9], e->ev[2]);
@@ -1936,6 +1941,7 @@ int do_flush(sdg_engine* e) {
     e->stats.ms_chain_carry = e->stats.ms_chain_match = e->stats.ms_chain_emit = 0;
     e->stats.ms_nfa = e->stats.ms_nfa_kernel = e->stats.ms_sched_host = 0;
     e->stats.arena_growths = 0;
+    e->stats.carry_in = e->stats.carry_out = 0;
     e->stats.fused_ovf = 0;
     e->stats.sched_fires = e->stats.sched_shifted = e->stats.sched_host_keys = e->stats.sched_rerun_keys = 0;
     // a flush consumes its batch whether or not it succeeds: a failing query must not make the next flush

@@ -252,7 +252,12 @@ struct NfaArgs {
     const uint32_t* fire_off;
     const nfa::TimerFire* fires;
 };
-// a: host copy (launch geometry); d_a: device copy the kernel reads
+// a: host copy (launch geometry); d_a: device copy the kernel reads. Layouts of at most NFA_LDS_BUDGET /
+// NFA_LDS_MIN_LANES bytes per key run with the arenas staged in LDS (nfa_lds_k: one wave per block, lanes =
+// NFA_LDS_BUDGET / bytes keys per wave, four blocks per CU); larger ones in HBM (nfa_k)
+constexpr int64_t NFA_LDS_BUDGET = 36 * 1024;
+constexpr int NFA_LDS_MIN_LANES = 8;
+int nfa_lds_lanes(const nfa::Layout& L);
 void nfa_run(const NfaArgs& a, const NfaArgs* d_a, hipStream_t stream);
 // arena growth: the committed copy of every key (arena2 && cur[k] ? arena2 : arena) into `dst` in layout Ld
 void nfa_migrate(const Plan* plan, const uint8_t* arena, const uint8_t* arena2, const uint8_t* cur,

@@ -5,6 +5,7 @@
 // atomic per wave. Everything is integer/byte work bound by HBM, so no MFMA.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 
 #include "../engine/eval.h"
@@ -405,6 +406,117 @@ __global__ __launch_bounds__(256, TM ? 1 : SDG_NFA_MINB) void nfa_k(const NfaArg
     if (c.ovf()) atomicOr(&a.flags[2], 1);
 }
 
+// The same state machine with each key's arena staged in LDS (nfa_k walks it in HBM: one lane per key, every
+// access a separate cache line of a ~1-10 KB arena, 50-100x the algorithmic bytes, r2g_c3_pmc). A block is one
+// wave whose `lanes` first lanes each own a key: the wave copies the committed arenas of its keys into LDS
+// cooperatively (64 lanes x 16 B on one arena at a time: coalesced), every lane runs its key against its LDS copy
+// (the arena code addresses through CtxT::base, a generic pointer, so the same nfa.h code runs), and the wave
+// writes the arenas back, coalesced, into the working copy (double-buffered: the committed copy stays intact until
+// nfa_commit). Concurrency is bounded by LDS (keys in flight per CU = LDS / arena bytes); lanes per wave is sized
+// so that four such waves fit a CU, one per SIMD.
+template <bool TM>
+__global__ __launch_bounds__(64) void nfa_lds_k(const NfaArgs* __restrict__ pa, int lanes) {
+    const NfaArgs& a = *pa;
+    extern __shared__ __align__(16) uint8_t lds_arena[];
+    __shared__ int64_t stack_mem[STACK * 64];
+    const int lane = threadIdx.x;
+    const int64_t idx = (int64_t)blockIdx.x * lanes + lane;
+    const Plan* P = a.plan;
+    const int64_t kb = a.L.bytes;
+    bool active = lane < lanes;
+    int64_t k = 0;
+    if (active) {
+        if (a.list) {
+            active = idx < a.nlist;
+            if (active) k = a.list[idx];
+        } else {
+            active = idx < a.K;
+            k = idx;
+        }
+    }
+    int64_t b = 0, e = a.n;
+    const uint8_t* src = nullptr;
+    uint8_t* dst = nullptr;
+    if (active) {
+        if (a.seg_start) {
+            b = a.seg_start[k];
+            e = a.seg_end[k];
+        }
+        src = a.arena + k * kb;
+        dst = a.arena + k * kb;
+        if (a.arena2) {
+            if (a.cur[k]) src = a.arena2 + k * kb;
+            else dst = a.arena2 + k * kb;
+        }
+        if (!a.list && b >= e && P->partitioned) {
+            // no event of this key: it runs only for its queued timers (initPartition happens at a first event)
+            const nfa::KHead* h = (const nfa::KHead*)src;
+            if (!(h->flags & 2) || P->n_sched == 0) {
+                active = false;
+            } else {
+                bool queued = false;
+                const nfa::TQ* tq = (const nfa::TQ*)(src + a.L.off_tq);
+                for (int i = 0; i < a.L.n_sched; ++i) queued |= tq[i].n > 0;
+                active = queued;
+            }
+        }
+    }
+    const int64_t n16 = kb / 16;
+    // stage: the committed arenas of the active keys, one arena per wave instruction sweep
+    for (uint64_t m = __ballot(active); m; m &= m - 1) {
+        const int j = __ffsll((unsigned long long)m) - 1;
+        const uint4* s4 = (const uint4*)__shfl((long long)(uintptr_t)src, j);
+        uint4* d4 = (uint4*)(lds_arena + (int64_t)j * kb);
+        for (int64_t i = lane; i < n16; i += 64) d4[i] = s4[i];
+    }
+    __syncthreads();
+    bool ovf = false;
+    if (active) {
+        nfa::CtxT<TM> c;
+        c.P = P;
+        c.code = a.code;
+        c.consts = a.consts;
+        c.L = a.L;
+        c.base = lds_arena + (int64_t)lane * kb;
+        c.stk = stack_mem + lane;
+        c.stride = 64;
+        c.emit_ts = a.out_ts;
+        c.emit_vals = a.out_vals;
+        c.emit_nulls = a.out_nulls;
+        c.emit_seq = a.out_emit_seq;
+        c.emit_sub = a.out_sub;
+        c.emit_key = a.out_key;
+        c.emit_round = a.out_round;
+        c.round = a.round;
+        c.emit_count = a.out_count;
+        c.emit_cap = a.out_cap;
+        c.flags = &a.flags[0];
+        c.key = (uint32_t)k;
+        c.T = a.T;
+        c.fires = nullptr;
+        c.nfires = -1;
+        if (a.list) {
+            c.fires = a.fires + a.fire_off[idx];
+            c.nfires = (int32_t)(a.fire_off[idx + 1] - a.fire_off[idx]);
+        }
+        if (a.last_seen) c.purge = nfa::PurgeIn{a.purge_clk, a.purge_from, a.purge_idle, a.last_seen[k] ^ INT64_MIN};
+        nfa::KeyEvents ev{a.ts, a.qstream, a.orig, a.cols, a.nulls, b, e, a.seq_base, a.pos_off, a.vrank};
+        nfa::run_key(c, ev);
+        if (a.last_seen) a.last_seen[k] = c.purge.last ^ INT64_MIN;
+        ovf = c.ovf();
+        if (dst != src) a.ran[k] = 1;
+    }
+    if (ovf) atomicOr(&a.flags[2], 1);
+    __syncthreads();
+    // write back into the working copy
+    for (uint64_t m = __ballot(active); m; m &= m - 1) {
+        const int j = __ffsll((unsigned long long)m) - 1;
+        uint4* d4 = (uint4*)__shfl((long long)(uintptr_t)dst, j);
+        const uint4* s4 = (const uint4*)(lds_arena + (int64_t)j * kb);
+        for (int64_t i = lane; i < n16; i += 64) d4[i] = s4[i];
+    }
+}
+
 // arena growth: every key's committed state into the larger layout (nfa.h migrate_key)
 __global__ __launch_bounds__(256) void nfa_migrate_k(const Plan* __restrict__ plan, const uint8_t* __restrict__ arena,
                                                      const uint8_t* __restrict__ arena2, const uint8_t* __restrict__ cur,
@@ -589,11 +701,26 @@ void nfa_migrate(const Plan* plan, const uint8_t* arena, const uint8_t* arena2, 
                        Ls, dst, Ld, K);
 }
 
+int nfa_lds_lanes(const nfa::Layout& L) {
+    static const char* off = getenv("SDG_NFA_HBM");  // A/B: the arena-in-HBM kernel
+    if (off) return 0;
+    const int64_t lanes = NFA_LDS_BUDGET / L.bytes;
+    return lanes >= NFA_LDS_MIN_LANES ? (int)(lanes < 64 ? lanes : 64) : 0;
+}
+
 void nfa_run(const NfaArgs& a, const NfaArgs* d_a, hipStream_t stream) {
-    const int64_t lanes = a.list ? a.nlist : a.K;
-    if (lanes <= 0) return;
-    if (a.T.log) hipLaunchKernelGGL(nfa_k<true>, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, d_a);
-    else hipLaunchKernelGGL(nfa_k<false>, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, d_a);
+    const int64_t keys = a.list ? a.nlist : a.K;
+    if (keys <= 0) return;
+    const int lanes = nfa_lds_lanes(a.L);
+    if (lanes > 0) {
+        const unsigned grid = (unsigned)((keys + lanes - 1) / lanes);
+        const size_t lds = (size_t)lanes * (size_t)a.L.bytes;
+        if (a.T.log) hipLaunchKernelGGL(nfa_lds_k<true>, dim3(grid), dim3(64), lds, stream, d_a, lanes);
+        else hipLaunchKernelGGL(nfa_lds_k<false>, dim3(grid), dim3(64), lds, stream, d_a, lanes);
+        return;
+    }
+    if (a.T.log) hipLaunchKernelGGL(nfa_k<true>, dim3((unsigned)((keys + 255) / 256)), dim3(256), 0, stream, d_a);
+    else hipLaunchKernelGGL(nfa_k<false>, dim3((unsigned)((keys + 255) / 256)), dim3(256), 0, stream, d_a);
 }
 
 void nfa_commit(uint8_t* cur, uint8_t* ran, int64_t K, hipStream_t stream) {
