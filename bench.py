@@ -112,10 +112,11 @@ def cpu_baseline(cols, syms, sample):
     return n / dt, matches, dt
 
 
-def parity_check(cols, syms, sample, dev_cols, device):
+def parity_check(cols, syms, sample, dev_cols, device, flushes=3):
     """Outside the timed region: the first `sample` events of this rank's bench stream through a fresh runtime on
-    the GPU (device-resident, the bench's own path) and through the oracle; the match rows (ts, e1id, e2id) must be
-    identical and in the same delivery order, or the bench fails."""
+    the GPU (device-resident, the bench's own path, in `flushes` consecutive batches like the timed steps, so
+    partials are carried across batch boundaries at the bench's ~10 events per key-window) and through the oracle;
+    the match rows (ts, e1id, e2id) must be identical and in the same delivery order, or the bench fails."""
     import siddhi_amd as sa
     from siddhi_amd import workloads as w
     sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -125,11 +126,19 @@ def parity_check(cols, syms, sample, dev_cols, device):
     sym_ids = np.array([rt.intern(s) for s in syms], dtype=np.uint32)
     d_id, d_sym, d_price, d_vol, d_ts = dev_cols
     assert int(sym_ids[cols["key"][0]]) == int(d_sym[0].item())  # same dictionary ids as the bench runtime
-    rt.push_device("StockStream", n, d_ts.data_ptr(), [d_id.data_ptr(), d_sym.data_ptr(), d_price.data_ptr(),
-                                                       d_vol.data_ptr()])
-    rt.flush(deliver=False)
-    gts, gvals, gnulls, _ = rt.poll_arrays(0)
+    parts, carried = [], 0
+    bounds = np.linspace(0, n, flushes + 1).astype(np.int64)
+    for f in range(flushes):
+        lo, hi = int(bounds[f]), int(bounds[f + 1])
+        rt.push_device("StockStream", hi - lo, d_ts[lo:].data_ptr(), [d_id[lo:].data_ptr(), d_sym[lo:].data_ptr(),
+                                                                      d_price[lo:].data_ptr(), d_vol[lo:].data_ptr()])
+        rt.flush(deliver=False)
+        carried += rt.stats().carry_in
+        parts.append(rt.poll_arrays(0))
     rt.shutdown()
+    gts = np.concatenate([p[0] for p in parts])
+    gvals = np.concatenate([p[1] for p in parts], axis=1)
+    gnulls = np.concatenate([p[2] for p in parts], axis=1)
     o = Oracle(w.C2_APP)
     L = lib()
     ids = np.array([L.orc_intern(o.h, s.encode()) for s in syms], dtype=np.int64)
@@ -151,7 +160,8 @@ def parity_check(cols, syms, sample, dev_cols, device):
     if not ok:
         raise RuntimeError("GPU match rows differ from the oracle on the first %d bench events (%d vs %d rows)"
                            % (n, len(gts), len(ots)))
-    return {"events": n, "matches": int(len(ots)), "bit_exact": True}
+    return {"events": n, "matches": int(len(ots)), "bit_exact": True, "flushes": flushes,
+            "partials_carried_across_flushes": int(carried)}
 
 
 def cpu_baseline_sharded(cols, syms, sample, threads):

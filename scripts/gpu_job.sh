@@ -47,6 +47,8 @@ for s in "$@"; do
         cfgs) run cfgs 900 python3 scripts/bench_configs.py --only c3m,c3md,c2generic,c4 --c3-steps 2 ;;
         cfgshbm) run cfgshbm 900 env SDG_NFA_HBM=1 python3 scripts/bench_configs.py --only c3md,c2generic --c3-steps 2 ;;
         c5host) run c5host 900 env SDG_HOST_PROF=1 python3 bench.py --config c5 --c5-shard 0/8 --steps 3 --warmup 1 --no-parity --no-gather ;;
+        kt) run kt 900 python3 -u -m pytest tests/test_gpu_keytab.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "keytab or keys or regime or c3 or c4" ;;
+        cfgs3) run cfgs3 900 python3 scripts/bench_configs.py --only c3m,c3md,c2generic --c3-steps 2 ;;
         *) echo "unknown step $s" ;;
     esac
 done

@@ -79,6 +79,44 @@ struct HostPin {
     }
 };
 
+enum KeyClass { KC_NONE = 0, KC_INT = 1, KC_F32 = 2, KC_F64 = 3, KC_BOOL = 4 };
+int key_class_of(uint8_t kind) {
+    switch (kind) {
+        case VK_I32: case VK_I64: return KC_INT;
+        case VK_F32: return KC_F32;
+        case VK_F64: return KC_F64;
+        case VK_BOOL: return KC_BOOL;
+        default: return KC_NONE;
+    }
+}
+// the device key table's 64-bit value of a key (keytab.hip kt_value) <-> the key's toString (the dictionary text)
+int64_t key_value_of_string(int kc, const std::string& s) {
+    switch (kc) {
+        case KC_F64: {
+            const double d = std::strtod(s.c_str(), nullptr);  // Java's toString: "NaN", "Infinity", "1.0E10" parse
+            int64_t b;
+            std::memcpy(&b, &d, 8);
+            return std::isnan(d) ? 0x7FF8000000000000ll : b;
+        }
+        case KC_F32: {
+            const float f = std::strtof(s.c_str(), nullptr);
+            uint32_t b;
+            std::memcpy(&b, &f, 4);
+            return std::isnan(f) ? 0x7FC00000ll : (int64_t)b;
+        }
+        case KC_BOOL: return s == "true" ? 1 : 0;
+        default: return std::stoll(s);
+    }
+}
+std::string key_string_of_value(int kc, int64_t v) {
+    switch (kc) {
+        case KC_F64: return java_real_string(bits_f64(v), false);
+        case KC_F32: return java_real_string(bits_f32(v), true);
+        case KC_BOOL: return v ? "true" : "false";
+        default: return std::to_string(v);
+    }
+}
+
 int width_of(uint8_t kind) {
     switch (kind) {
         case VK_I64: case VK_F64: return 8;
@@ -156,7 +194,9 @@ struct QueryRt {
     DevBuf d_plan, d_code, d_consts, d_args, o_mq, o_ovf, o_ovfc, o_dqs;
     HostPin h_args, h_ret;  // chain path: ChainArgs pair; counters (16 B) | flags (16 B) | overflow count (8 B)
     bool string_keys = true;                        // all partition keys are string attributes (ids used as keys)
-    bool int_keys = false;                          // all partition keys are int / long attributes (device key table)
+    // device key table (device-resident batches): the class every partition key attribute of the query shares --
+    // KC_INT (int / long), KC_F32, KC_F64, KC_BOOL -- or KC_NONE (string keys, mixed classes, range partitions)
+    int key_class = 0;
     // device key table (keytab.hip) for device-resident batches of int / long keys: a mirror of keydict's ids
     DevBuf kt_keys, kt_ids, kt_first, kt_cnt, kt_pairs, kt_vals, kt_slots;
     uint64_t kt_cap = 0;
@@ -622,7 +662,7 @@ void kt_sync(sdg_engine* e, QueryRt& q) {
     const size_t K = q.keystr.size();
     if (q.kt_synced >= K) return;
     std::vector<int64_t> vals(K - q.kt_synced);
-    for (size_t i = q.kt_synced; i < K; ++i) vals[i - q.kt_synced] = std::stoll(q.keystr[i]);  // int / long keys only
+    for (size_t i = q.kt_synced; i < K; ++i) vals[i - q.kt_synced] = key_value_of_string(q.key_class, q.keystr[i]);
     int64_t* d_vals = (int64_t*)q.kt_vals.ensure(vals.size() * 8);
     int* d_flags = (int*)((uint8_t*)q.kt_cnt.ensure(32) + 8);
     HIPCHECK(hipMemcpy(d_vals, vals.data(), vals.size() * 8, hipMemcpyHostToDevice));
@@ -691,7 +731,8 @@ const uint32_t* device_key_ids(sdg_engine* e, QueryRt& q, const void* col, int k
                 for (size_t i = K0; i < q.keystr.size(); ++i) q.keydict.erase(q.keystr[i]);
                 q.keystr.resize(K0);
                 q.intkeys = IntKeyCache();
-                for (size_t i = 0; i < K0; ++i) q.intkeys.insert(std::stoll(q.keystr[i]), (uint32_t)i);  // int / long keys only
+                if (q.key_class == KC_INT)
+                    for (size_t i = 0; i < K0; ++i) q.intkeys.insert(std::stoll(q.keystr[i]), (uint32_t)i);
             }
         } rollback{q, K0};
         unsigned long long* d_pairs = (unsigned long long*)q.kt_pairs.ensure(cnt * 8);
@@ -711,10 +752,10 @@ const uint32_t* device_key_ids(sdg_engine* e, QueryRt& q, const void* col, int k
             const uint32_t i = order[j];
             const uint32_t id = (uint32_t)(K0 + j);
             slots[j] = (uint32_t)(pairs[i] & 0xFFFFFFFFull);
-            std::string ks = std::to_string(vals[i]);
+            std::string ks = key_string_of_value(q.key_class, vals[i]);
             if (!q.keydict.emplace(ks, id).second) throw DeviceError("device key table out of step with the dictionary");
             q.keystr.push_back(std::move(ks));
-            q.intkeys.insert(vals[i], id);
+            if (q.key_class == KC_INT) q.intkeys.insert(vals[i], id);
         }
         uint32_t* d_slots = (uint32_t*)q.kt_slots.ensure(cnt * 4);
         HIPCHECK(hipMemcpy(d_slots, slots.data(), cnt * 4, hipMemcpyHostToDevice));
@@ -775,8 +816,9 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         }
         if (partitioned) {
             if (ranged) throw CompileError(SDG_ERR_UNSUPPORTED, "device-resident batches of a range partition");
-            if (!q.string_keys && !q.int_keys)
-                throw CompileError(SDG_ERR_UNSUPPORTED, "device-resident batches need string or int / long partition keys");
+            if (!q.string_keys && q.key_class == KC_NONE)
+                throw CompileError(SDG_ERR_UNSUPPORTED, "device-resident batches of a partition whose key attributes mix "
+                                                        "types");
             int ai = h.key_attr[qpos];
             if (c.d_nulls[ai]) throw CompileError(SDG_ERR_UNSUPPORTED, "null partition keys in device-resident batches");
             if (q.string_keys) d_key = (const uint32_t*)c.d_cols[ai];
@@ -2328,9 +2370,9 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             e->any_purge |= P.purge != 0;
             for (size_t i = 0; i < q->hq.key_kind.size(); ++i)
                 if (q->hq.key_attr[i] >= 0 && q->hq.key_kind[i] != VK_STR) q->string_keys = false;
-            q->int_keys = P.partitioned && !q->hq.key_kind.empty();
+            q->key_class = P.partitioned && !q->hq.key_kind.empty() ? key_class_of(q->hq.key_kind[0]) : KC_NONE;
             for (size_t i = 0; i < q->hq.key_kind.size(); ++i)
-                q->int_keys &= q->hq.key_attr[i] >= 0 && (q->hq.key_kind[i] == VK_I32 || q->hq.key_kind[i] == VK_I64);
+                if (q->hq.key_attr[i] < 0 || key_class_of(q->hq.key_kind[i]) != q->key_class) q->key_class = KC_NONE;
             if (!e->compile_only) upload_plan(e.get(), *q);
             e->qs.push_back(std::move(q));
         }

@@ -398,9 +398,27 @@ struct CtxT {
     SDG_HD bool is_absent(int p) const {  // instanceof AbsentPreStateProcessor
         return TM && (P->st[p].kind == PK_ABSENT || (P->st[p].kind == PK_LOGICAL && P->st[p].absent));
     }
+    // one slot of a shared output counter. On the GPU the lanes of the wave that reach this point together (the
+    // exec mask: every lane emitting at this call site now) share ONE atomic -- a per-record atomic on one counter
+    // serialises in L2 at ~10^8/s, which was most of nfa_k's time on match-heavy queries (C3: 10^7 matches per
+    // flush). On the host (tests/native, KeyRun replays) a plain increment.
+    SDG_HD static unsigned long long reserve(unsigned long long* counter) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const uint64_t m = __ballot(1);
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        const int lane = __lane_id();
+        unsigned long long base = 0;
+        if (lane == leader) base = atomicAdd(counter, (unsigned long long)__popcll(m));
+        base = __shfl(base, leader);
+        const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+        return base + (unsigned long long)__popcll(m & below);
+#else
+        return __atomic_fetch_add(counter, 1ull, __ATOMIC_RELAXED);
+#endif
+    }
     SDG_HD void log_rec(uint8_t type, int sch, uint8_t origin, int64_t t) {
         if (!TM || !T.log) return;
-        const unsigned long long i = __atomic_fetch_add(T.log_count, 1ull, __ATOMIC_RELAXED);
+        const unsigned long long i = reserve(T.log_count);
         const uint32_t kseq = head().kseq++;
         if ((int64_t)i >= T.log_cap) {  // counted: the host grows the log and reruns
             __atomic_fetch_or(flags + 5, 1, __ATOMIC_RELAXED);
@@ -505,7 +523,7 @@ struct CtxT {
     SDG_HD void emit(int16_t s) {  // QuerySelector.processNoGroupBy for one StateEvent (insert current events)
         // (timer emissions: cur_seq = the position of the fire, cur_sub negative -- before that event's own)
         if (se(s).type != T_CURRENT) return;
-        unsigned long long slot = __atomic_fetch_add(emit_count, 1ull, __ATOMIC_RELAXED);
+        unsigned long long slot = reserve(emit_count);
         if ((int64_t)slot >= emit_cap) {
             __atomic_fetch_or(flags, 1, __ATOMIC_RELAXED);
             return;

@@ -1,4 +1,4 @@
-// Device-resident partition key table for integral (int / long) partition attributes: an open-addressed HBM hash
+// Device-resident partition key table for int / long / float / double / bool partition attributes: an open-addressed HBM hash
 // table from the key value to the dense key id the rest of the engine indexes its per-key state with (arenas,
 // carries, segments). ValuePartitionExecutor keys a partition by the attribute's toString (reference:
 // core/partition/executor/ValuePartitionExecutor.java, PartitionStreamReceiver.java:262-272); Java's toString is
@@ -27,8 +27,24 @@ __device__ __forceinline__ uint64_t kt_mix(uint64_t z) {
     return z ^ (z >> 31);
 }
 
+// the 64-bit value standing for a key's toString. A query's table holds one class of key attribute (integral,
+// float, double or bool: engine.cpp key_class), so the encodings never meet: int / long sign-extended (equal values
+// print alike); double / float bit patterns -- Double/Float.toString is injective on them (-0.0 prints "-0.0", 0.0
+// "0.0") except that every NaN prints "NaN", so NaNs map to the canonical NaN; bool 0 / 1
 __device__ __forceinline__ int64_t kt_value(const void* col, int kind, int64_t r) {
-    return kind == VK_I32 ? (int64_t)((const int32_t*)col)[r] : ((const int64_t*)col)[r];
+    switch (kind) {
+        case VK_I32: return (int64_t)((const int32_t*)col)[r];
+        case VK_F64: {
+            const int64_t b = ((const int64_t*)col)[r];
+            return (b & 0x7FFFFFFFFFFFFFFFll) > 0x7FF0000000000000ll ? 0x7FF8000000000000ll : b;
+        }
+        case VK_F32: {
+            const int32_t b = ((const int32_t*)col)[r];
+            return (b & 0x7FFFFFFF) > 0x7F800000 ? 0x7FC00000ll : (int64_t)(uint32_t)b;
+        }
+        case VK_BOOL: return ((const uint8_t*)col)[r] ? 1 : 0;
+        default: return ((const int64_t*)col)[r];
+    }
 }
 
 // a new key: counted; once the table would be over half full, flags[1] stops the pass (the host grows the table)

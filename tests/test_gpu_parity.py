@@ -405,9 +405,11 @@ def oracle_batch_rows(app, stream, ts, slot_cols, nv, str_col=None):
         o.close()
 
 
-def test_c2_bench_regime_vs_oracle(oracle_built):
+@pytest.mark.parametrize("flushes", [1, 4])
+def test_c2_bench_regime_vs_oracle(flushes, oracle_built):
     """2M events over 10k keys at the bench's rate (100 events/ms: ~10 events per key-window), device-resident,
-    fused path; the whole match list must equal the oracle's, in delivery order"""
+    fused path, in 1 or 4 consecutive flushes (the bench's steps: partials carried across every batch boundary at
+    ~10 events per key-window); the whole match list must equal the oracle's, in delivery order"""
     import torch
     n, keys = 2_000_000, 10_000
     cols = w.c2_columns(n, keys=keys, per_ms=100)
@@ -418,11 +420,24 @@ def test_c2_bench_regime_vs_oracle(oracle_built):
         dev = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in
                [("ts", cols["ts"]), ("id", cols["id"]), ("sym", sym_ids[cols["key"]].astype(np.int32)),
                 ("price", cols["price"]), ("vol", cols["volume"])]}
-        rt.push_device("StockStream", n, dev["ts"].data_ptr(),
-                       [dev["id"].data_ptr(), dev["sym"].data_ptr(), dev["price"].data_ptr(), dev["vol"].data_ptr()])
-        rt.flush(deliver=False)
-        assert rt.stats().fused == 1
-        gts, gvals, gnulls, gseq = rt.poll_arrays(0)
+        parts, carried = [], 0
+        bounds = np.linspace(0, n, flushes + 1).astype(np.int64)
+        for f in range(flushes):
+            lo, hi = int(bounds[f]), int(bounds[f + 1])
+            rt.push_device("StockStream", hi - lo, dev["ts"][lo:].data_ptr(),
+                           [dev["id"][lo:].data_ptr(), dev["sym"][lo:].data_ptr(), dev["price"][lo:].data_ptr(),
+                            dev["vol"][lo:].data_ptr()])
+            rt.flush(deliver=False)
+            st = rt.stats()
+            assert st.fused == 1
+            carried += st.carry_in
+            parts.append(rt.poll_arrays(0))
+        if flushes > 1:
+            assert carried > 1000  # partials really crossed the batch boundaries
+        gts = np.concatenate([p[0] for p in parts])
+        gvals = np.concatenate([p[1] for p in parts], axis=1)
+        gnulls = np.concatenate([p[2] for p in parts], axis=1)
+        gseq = np.concatenate([p[3] for p in parts])
     finally:
         rt.shutdown()
     ots, ovals, _ = oracle_batch_rows(w.C2_APP, "StockStream", cols["ts"],
@@ -464,11 +479,10 @@ def test_radix_path_million_keys_vs_oracle(oracle_built):
     assert np.array_equal(gts, ots) and np.array_equal(gvals.T, ovals)
 
 
-@pytest.mark.parametrize("query", ["<1:5>", "<2:5>"])
-def test_c3_long_keys_vs_oracle(query, oracle_built):
-    """C3 generator (long partition keys, 10^4 keys x 100 events) through the host push, generic keyed NFA; the
-    <1:5> form matches, the literal <2:5> form never does"""
-    keys = 10_000
+@pytest.mark.parametrize("query,keys", [("<1:5>", 10_000), ("<2:5>", 10_000), ("<1:5>", 100_000)])
+def test_c3_long_keys_vs_oracle(query, keys, oracle_built):
+    """C3 generator (long partition keys, 10^4 / 10^5 keys x 100 events) through the host push, generic keyed NFA;
+    the <1:5> form matches, the literal <2:5> form never does"""
     c = w.c3_columns(keys)
     app = w.C3_APP.replace("<2:5>", query)
     rt = sa.SiddhiAppRuntime(app)
@@ -580,7 +594,7 @@ def product_c4(c, end, batches=3):
     return ts, vals, nulls, stats
 
 
-@pytest.mark.parametrize("keys", [10_000, 30_000])
+@pytest.mark.parametrize("keys", [10_000, 30_000, 100_000])
 def test_c4_vs_oracle(keys, oracle_built):
     """C4 at >= 10^4 keys, timers falling due mid-run and at the final advance_time: every match,
     in the reference's delivery order (TreeMultimap collapse included)"""
