@@ -49,6 +49,8 @@ for s in "$@"; do
         c5host) run c5host 900 env SDG_HOST_PROF=1 python3 bench.py --config c5 --c5-shard 0/8 --steps 3 --warmup 1 --no-parity --no-gather ;;
         kt) run kt 900 python3 -u -m pytest tests/test_gpu_keytab.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "keytab or keys or regime or c3 or c4" ;;
         cfgs3) run cfgs3 900 python3 scripts/bench_configs.py --only c3m,c3md,c2generic --c3-steps 2 ;;
+        purge) run purge 900 python3 -u -m pytest tests/test_gpu_select.py tests/test_gpu_parity.py tests/test_gpu_snapshot.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "purge or Purge or absent or Absent or select or snapshot" ;;
+        c3mdprof) run c3mdprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/c3mdprof" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 1 --warmup 1 ;;
         *) echo "unknown step $s" ;;
     esac
 done

@@ -188,8 +188,9 @@ class QC {
         p.purge = 0;
         if (q_.partition_index >= 0 && app_.partitions[q_.partition_index].purge) {
             const sql::Partition& pt = app_.partitions[q_.partition_index];
-            if (p.n_sched > 0 || p.n_agg > 0)
-                throw CompileError(SDG_ERR_UNSUPPORTED, "@purge with absent states or aggregators is not on the device path");
+            if (p.n_sched > 0 && p.n_agg > 0)  // (each alone is on the device)
+                throw CompileError(SDG_ERR_UNSUPPORTED, "@purge with absent states and aggregators in one query is not "
+                                                        "on the device path");
             for (const auto& w : pt.with)  // the partition's keys are refreshed by any of its streams' events
                 if (std::find(h_.streams.begin(), h_.streams.end(), app_.stream_index(w.stream_id)) == h_.streams.end())
                     throw CompileError(SDG_ERR_UNSUPPORTED, "@purge: every query of the partition must read all its streams");

@@ -224,6 +224,10 @@ struct QueryRt {
     // @purge: per-key clock reading at the key's last event (stored XOR INT64_MIN: zero bytes = never seen), its
     // copy at the batch start (a rerun starts from it), the partition's first initPartition reading
     DevBuf last_seen, last_seen_bak;
+    // @purge with aggregators: per record "purged since the key's previous record" (aggregator states restart), per
+    // key "purged after its last record" (applied after the post pass)
+    DevBuf o_flags, g_flags, ps_reset, agg_reset_flags;
+    bool purge_agg = false;
     int64_t purge_first = INT64_MIN;
     SchedSim::RankMap last_rank;
     std::vector<uint32_t> reordered;  // keys rerun with the scheduler's fire order (sorted)
@@ -1192,14 +1196,17 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             a.T.log_cap = q.log_cap;
         }
         a.L = q.L;
-        if (P.purge) {  // a rerun of the batch (arena growth, output regrowth) starts from the batch-start readings
+        if (P.purge) {  // every run (first, reruns) reads the batch-start readings and writes the run's
             a.last_seen = q.last_seen.as<int64_t>();
             a.purge_clk = e->d_clk.as<int64_t>();
             a.purge_from = q.purge_first == INT64_MIN ? INT64_MAX : q.purge_first + P.purge_interval_ms;
             a.purge_idle = P.purge_idle_ms;
             HIPCHECK(hipMemcpyAsync(q.last_seen_bak.ensure((size_t)q.arena_keys * 8), q.last_seen.p, (size_t)q.arena_keys * 8,
                                     hipMemcpyDeviceToDevice, st));
+            a.last_seen_in = q.last_seen_bak.as<int64_t>();
         }
+        q.purge_agg = P.purge && P.n_agg > 0;
+        if (q.purge_agg) a.agg_reset = (uint8_t*)q.agg_reset_flags.ensure((size_t)q.arena_keys);
         if (q.replay_carries) replay_carries(e, q, a, multi_stream);
         int64_t cap = std::max<int64_t>(q.out_cap, 2 * nrows + 4096);
         unsigned long long* counters = (unsigned long long*)q.counters.ensure(16);
@@ -1218,13 +1225,13 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             a.out_emit_seq = (int64_t*)q.o_emit.ensure(cap * 8);
             a.out_sub = (int64_t*)q.o_first.ensure(cap * 8);
             a.out_round = timers ? (uint8_t*)q.o_round.ensure(cap) : nullptr;
+            a.out_flags = q.purge_agg ? (uint8_t*)q.o_flags.ensure(cap) : nullptr;
         };
         int hf[8];
         unsigned long long hc[2];
         // one launch; returns false when a growable buffer (outputs, scheduler log) overflowed
         auto launch = [&](bool first) -> bool {
-            if (first && P.purge)
-                HIPCHECK(hipMemcpyAsync(q.last_seen.p, q.last_seen_bak.p, (size_t)q.arena_keys * 8, hipMemcpyDeviceToDevice, st));
+            if (first && q.purge_agg) HIPCHECK(hipMemsetAsync(a.agg_reset, 0, (size_t)q.arena_keys, st));
             if (first) {
                 HIPCHECK(hipMemsetAsync(counters, 0, 16, st));
                 if (!(partitioned && nrows > 0)) HIPCHECK(hipMemsetAsync(flags, 0, 32, st));
@@ -1390,7 +1397,14 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                         if (m) HIPCHECK(hipMemcpy(r->nulls[c].data(), v_nulls[c] + b, m, hipMemcpyDeviceToHost));
                     }
                 }
-                r->start(&P, h.code.data(), h.consts.data(), q.L, T, e->seq);
+                if (P.purge) {  // the key's batch-start reading of its last activity
+                    int64_t ls = 0;
+                    HIPCHECK(hipMemcpy(&ls, q.last_seen_bak.as<int64_t>() + k, 8, hipMemcpyDeviceToHost));
+                    const nfa::PurgeIn pin{e->bc.clk.data(), a.purge_from, a.purge_idle, ls ^ INT64_MIN};
+                    r->start(&P, h.code.data(), h.consts.data(), q.L, T, e->seq, &pin);
+                } else {
+                    r->start(&P, h.code.data(), h.consts.data(), q.L, T, e->seq);
+                }
                 return r;
             };
             SchedSim::Result res;
@@ -1434,6 +1448,10 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 HIPCHECK(hipMemcpy(&cur, q.cur_bits.as<uint8_t>() + r->key, 1, hipMemcpyDeviceToHost));
                 uint8_t* work = (cur ? q.arena.as<uint8_t>() : q.arena2.as<uint8_t>()) + (int64_t)r->key * q.L.bytes;
                 HIPCHECK(hipMemcpy(work, r->arena.data(), q.L.bytes, hipMemcpyHostToDevice));
+                if (P.purge) {
+                    const int64_t ls = r->purge_last() ^ INT64_MIN;
+                    HIPCHECK(hipMemcpy(q.last_seen.as<int64_t>() + r->key, &ls, 8, hipMemcpyHostToDevice));
+                }
             }
             q.sim.commit();
             q.last_rank = std::move(res.rank);
@@ -1721,6 +1739,18 @@ void drain(sdg_engine* e, QueryRt& q) {
     if (q.polled) return;
     q.polled = true;
     const int64_t n = q.out_n;
+    // @purge with aggregators: keys purged after their last record restart their aggregator states -- after this
+    // flush's records went through the post pass
+    struct TailReset {
+        sdg_engine* e;
+        QueryRt& q;
+        ~TailReset() {
+            if (!q.purge_agg || q.agg_keys <= 0 || !q.agg_reset_flags.p) return;
+            agg_reset((int64_t*)q.agg_state.p, q.hq.plan.n_agg, q.agg_reset_flags.as<uint8_t>(),
+                      std::min<int64_t>(q.agg_keys, q.arena_keys), e->stream);
+            (void)hipStreamSynchronize(e->stream);
+        }
+    } tail_reset{e, q};
     if (n <= 0) return;
     const int na = q.hq.plan.n_out;  // every column of the records (hidden selector columns included)
     const bool post = q.hq.plan.has_post;
@@ -1739,6 +1769,7 @@ void drain(sdg_engine* e, QueryRt& q) {
     int64_t vstride = q.out_cap;
     const void* src_nulls = q.o_nulls.p;
     const void* src_key = q.o_key.p;
+    const void* src_flags = q.o_flags.p;
     const bool dev_order = !q.last_timers && n > 1;
     if (dev_order) {
         const size_t wb = order_workspace(n);
@@ -1762,6 +1793,11 @@ void drain(sdg_engine* e, QueryRt& q) {
             gather_u32((const uint32_t*)q.o_key.p, perm, n, gk, st);
             src_key = gk;
         }
+        if (q.purge_agg) {
+            uint8_t* gf = (uint8_t*)q.g_flags.ensure((size_t)n);
+            gather_u8((const uint8_t*)q.o_flags.p, perm, n, gf, st);
+            src_flags = gf;
+        }
         src_ts = gts;
         src_emit = gem;
         src_first = nullptr;
@@ -1769,7 +1805,11 @@ void drain(sdg_engine* e, QueryRt& q) {
         vstride = n;
     }
     std::vector<uint32_t> okey;
-    std::vector<uint8_t> oround;
+    std::vector<uint8_t> oround, oflags;
+    if (q.purge_agg) {  // (no timers: purge with aggregators excludes absent states, so no host replay records)
+        oflags.resize(n);
+        HIPCHECK(hipMemcpyAsync(oflags.data(), src_flags, n, hipMemcpyDeviceToHost, st));
+    }
     if (q.last_timers || post) {  // keys: the aggregators' state, and for timer matches: drop the records of keys
         okey.resize(n);            // replayed on the host, order the fires
         HIPCHECK(hipMemcpyAsync(okey.data(), src_key, n * 4, hipMemcpyDeviceToHost, st));
@@ -1850,9 +1890,11 @@ void drain(sdg_engine* e, QueryRt& q) {
         fv.resize((size_t)na * nk);
         fn.resize(nk);
         uint32_t kmax = 0;
+        std::vector<uint8_t> fr(q.purge_agg ? nk : 0);
         for (int64_t i = 0; i < nk; ++i) {
             const int64_t s = ord[i];
             const bool dev = s < n;
+            if (q.purge_agg) fr[i] = dev ? oflags[s] : 0;
             fk[i] = dev ? okey[s] : hkey[s - n];
             kmax = std::max(kmax, fk[i]);
             fn[i] = dev ? nulls[s] : hnulls[s - n];
@@ -1892,6 +1934,11 @@ void drain(sdg_engine* e, QueryRt& q) {
         pa.nulls = dn;
         pa.pass = dp;
         pa.agg_state = (int64_t*)q.agg_state.p;
+        if (q.purge_agg) {
+            uint8_t* dr = (uint8_t*)q.ps_reset.ensure((size_t)nk);
+            HIPCHECK(hipMemcpyAsync(dr, fr.data(), (size_t)nk, hipMemcpyHostToDevice, st));
+            pa.reset = dr;
+        }
         select_post(pa, q.hq.plan.partitioned ? dk : nullptr, kbits, q.ps_ws.ensure(select_post_workspace(nk)), st);
         fpass.resize(nk);
         HIPCHECK(hipMemcpyAsync(fv.data(), dv, (size_t)(P.n_user_out + P.n_list_cols) * nk * 8, hipMemcpyDeviceToHost, st));

@@ -29,8 +29,9 @@ struct KeyRun {
     size_t lread = 0;
 
     void start(const Plan* P, const Instr* code, const int64_t* consts, const nfa::Layout& L, const nfa::TimerIn& T,
-               int64_t seq_base) {
+               int64_t seq_base, const nfa::PurgeIn* purge = nullptr) {
         P_ = P;
+        if (purge) c_.purge = *purge;
         n_out_ = P->n_out;
         ncols_ = P->n_cols;
         c_.P = P;
@@ -78,6 +79,7 @@ struct KeyRun {
     }
     bool overflow() { return c_.ovf() || flags_[0] || flags_[5]; }
     int64_t next_row_pos() const { return p_ < (int64_t)ts.size() ? (int64_t)pos[p_] : -1; }
+    int64_t purge_last() const { return c_.purge.last; }  // the key's last activity after the replay (@purge)
 
    private:
     const Plan* P_ = nullptr;

@@ -73,7 +73,8 @@ struct TQ {
 
 // scheduler log (device -> host scheduler simulation): every fire a key run performs and every notify time it
 // pushes, in the key's order (kseq)
-enum : uint8_t { LOG_PUSH = 0, LOG_FIRE = 1, LOG_POP = 2, LOG_FIRE_END = 3 };
+// LOG_PURGE: @purge destroyed the key's states before the event at g (its SchedulerStates leave every scheduler)
+enum : uint8_t { LOG_PUSH = 0, LOG_FIRE = 1, LOG_POP = 2, LOG_FIRE_END = 3, LOG_PURGE = 4 };
 constexpr uint8_t ORIGIN_EVENT = 0xFF;
 struct SchedLog {
     uint32_t key;
@@ -210,6 +211,9 @@ struct CtxT {
     int64_t emit_cap;
     int* flags;
     uint32_t key;
+    uint8_t* emit_flags = nullptr;  // [emit_cap] per record: 1 = the key was purged since its previous record (the
+                                    // selector's aggregator states restart before it); nullptr: not recorded
+    bool purge_pending = false;     // purged, no record emitted since
     int64_t seq_base;   // sequence number of batch position 0
     int64_t cur_seq;
     int64_t cur_sub;
@@ -529,6 +533,8 @@ struct CtxT {
             return;
         }
         emit_ts[slot] = se(s).ts;
+        if (emit_flags) emit_flags[slot] = purge_pending ? 1 : 0;
+        purge_pending = false;
         emit_seq[slot] = cur_seq;
         emit_sub[slot] = cur_sub++;
         emit_key[slot] = key;
@@ -1302,9 +1308,14 @@ SDG_HD bool key_row(CtxT<TM>& c, const KeyEvents& ev, int64_t p, bool& need_init
     if (c.purge.clk) {
         const int64_t now = c.purge.clk[g];
         if (!need_init && c.purge.last != INT64_MIN && now >= c.purge.from && c.purge.last + c.purge.idle < now) {
+            const uint32_t kseq = c.head().kseq;  // the run's log order continues across the reset
             c.arena_init();  // the key's states destroyed (cleanGroupByStates); its partition key is new again
             c.head().flags = 2;
+            c.head().kseq = kseq;
             need_init = true;
+            c.purge_pending = true;
+            // the key's SchedulerStates are destroyed with them (the scheduler simulation mirrors it)
+            if (TM && P->n_sched) c.log_rec(LOG_PURGE, 0, ORIGIN_EVENT, now);
         }
         c.purge.last = now;  // partitionKeys.put(key, currentTime)
     }

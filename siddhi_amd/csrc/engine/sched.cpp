@@ -213,6 +213,28 @@ void SchedSim::remove_if_empty(int sch, uint32_t key) {  // returnState / return
     k.stamp = k.cseq = 0;
 }
 
+void SchedSim::purge(uint32_t key) {  // @purge: the key's SchedulerState leaves every scheduler (map.remove)
+    for (SchedState& S : work_.sc) {
+        if (key >= S.ks.size()) continue;
+        KS& k = S.ks[key];
+        if (k.n) {
+            due_del(k);
+            if (k.spill >= 0) {
+                work_.spill[k.spill].clear();
+                work_.spill_free.push_back(k.spill);
+                k.spill = -1;
+            }
+            k.n = 0;
+        }
+        if (k.in_map && partitioned_) {
+            S.bin[(uint32_t)k.hash & (S.cap - 1)]--;
+            --S.size;
+            k.in_map = false;
+            k.stamp = k.cseq = 0;
+        }
+    }
+}
+
 namespace {
 // SDG_SCHED_PROF=1: per-section host time of simulate() on stderr (diagnostics)
 struct SecProf {
@@ -279,7 +301,10 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
         return c;
     };
     auto posof = [&](size_t i) -> int64_t { return logs[i].g == 0xFFFFFFFFu ? -1 : (int64_t)logs[i].g; };
-    auto is_evpush = [&](size_t i) { return logs[i].type == nfa::LOG_PUSH && logs[i].origin == nfa::ORIGIN_EVENT; };
+    // records made while processing an event (its pushes, a purge before it): applied at their positions
+    auto is_evpush = [&](size_t i) {
+        return (logs[i].type == nfa::LOG_PUSH && logs[i].origin == nfa::ORIGIN_EVENT) || logs[i].type == nfa::LOG_PURGE;
+    };
     std::vector<size_t> evp;  // pushes made while processing events, applied at their positions
     for (size_t i = 0; i < logs.size();) {
         size_t j = i;
@@ -344,6 +369,7 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
             const SchedLog& L = r->log[r->lread];
             if (L.type == nfa::LOG_PUSH) notify(L.sched, key, L.t);
             else if (L.type == nfa::LOG_POP) pop(L.sched, key);
+            else if (L.type == nfa::LOG_PURGE) purge(key);
         }
     };
     auto add_fire = [&](KC& c, const nfa::TimerFire& f, uint32_t rk) {
@@ -530,8 +556,11 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
         prof.lap(4);
         // 4. the device keys' pushes made by the event at g
         for (; ep < evp.size() && posof(evp[ep]) == g; ++ep) {
-            const uint8_t m = kc[logs[evp[ep]].key].mode;
-            if (m == DEV || (optimistic && m == PENDING)) notify(logs[evp[ep]].sched, logs[evp[ep]].key, logs[evp[ep]].t);
+            const SchedLog& L = logs[evp[ep]];
+            const uint8_t m = kc[L.key].mode;
+            if (m != DEV && !(optimistic && m == PENDING)) continue;
+            if (L.type == nfa::LOG_PURGE) purge(L.key);
+            else notify(L.sched, L.key, L.t);
         }
         ++g;
         prof.lap(5);

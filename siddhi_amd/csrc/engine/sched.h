@@ -234,6 +234,7 @@ class SchedSim {
     void notify(int sch, uint32_t key, int64_t t);  // Scheduler.notifyAt
     void pop(int sch, uint32_t key);
     void remove_if_empty(int sch, uint32_t key);
+    void purge(uint32_t key);
     bool queued(int sch, uint32_t key) const {
         const SchedState& S = work_.sc[sch];
         return key < S.ks.size() && S.ks[key].n > 0;

@@ -242,8 +242,12 @@ struct NfaArgs {
     int* flags;                       // [0] output overflow, [2] arena overflow, [5] scheduler log overflow
     // timers (queries with absent states)
     nfa::TimerIn T;
-    // @purge: per-key last activity (persistent, INT64_MIN = never), the clock, the purge window
+    // @purge: per-key last activity (persistent, INT64_MIN = never), the clock, the purge window. A run reads the
+    // batch-start readings (last_seen_in) and writes the run's (last_seen), so any key can rerun from the batch start
     int64_t* last_seen;               // nullptr: the query's partition does not purge
+    const int64_t* last_seen_in;
+    uint8_t* out_flags;               // [out_cap] per record: aggregator reset before it (nullptr: not recorded)
+    uint8_t* agg_reset;               // [K] set for a key purged after its last record of the run (nullptr: none)
     const int64_t* purge_clk;
     int64_t purge_from, purge_idle;
     // rerun mode: run only list[0..nlist) with the explicit fire lists fires[fire_off[i] .. fire_off[i + 1])
@@ -272,6 +276,7 @@ void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t e
                    size_t work_bytes, uint32_t** perm_out, hipStream_t stream);
 void gather_i64(const int64_t* src, const uint32_t* perm, int64_t n, int64_t* dst, hipStream_t stream);
 void gather_u32(const uint32_t* src, const uint32_t* perm, int64_t n, uint32_t* dst, hipStream_t stream);
+void gather_u8(const uint8_t* src, const uint32_t* perm, int64_t n, uint8_t* dst, hipStream_t stream);
 
 // the selector's post pass (order.hip): aggregators per key in delivery order, select items over them, having
 struct SelPostArgs {
@@ -286,10 +291,13 @@ struct SelPostArgs {
     int64_t* agg_state;               // [K][n_agg][2], persistent per partition key
     const uint32_t* perm;             // set by select_post
     const uint32_t* key_sorted;
+    const uint8_t* reset;             // [n] 1: the record's key was purged since its previous record (nullptr: none)
 };
 size_t select_post_workspace(int64_t n);
 // key: [n] partition key ids < 2^kbits (nullptr / kbits 0: unpartitioned, one run)
 void select_post(SelPostArgs a, const uint32_t* key, int kbits, void* work, hipStream_t stream);
+// keys flagged in flags[K] (purged after their last record): aggregator states zeroed, flags cleared
+void agg_reset(int64_t* agg_state, int n_agg, uint8_t* flags, int64_t K, hipStream_t stream);
 
 // device partition key table for integral partition attributes (keytab.hip): value -> dense key id
 struct KeyTab {

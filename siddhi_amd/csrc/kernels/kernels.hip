@@ -399,10 +399,12 @@ __global__ __launch_bounds__(256, TM ? 1 : SDG_NFA_MINB) void nfa_k(const NfaArg
         c.nfires = (int32_t)(a.fire_off[idx + 1] - a.fire_off[idx]);
     }
     // last_seen is stored XOR INT64_MIN, so the zero-filled array reads as "never seen"
-    if (a.last_seen) c.purge = nfa::PurgeIn{a.purge_clk, a.purge_from, a.purge_idle, a.last_seen[k] ^ INT64_MIN};
+    if (a.last_seen) c.purge = nfa::PurgeIn{a.purge_clk, a.purge_from, a.purge_idle, a.last_seen_in[k] ^ INT64_MIN};
+    c.emit_flags = a.out_flags;
     nfa::KeyEvents ev{a.ts, a.qstream, a.orig, a.cols, a.nulls, b, e, a.seq_base, a.pos_off, a.vrank};
     nfa::run_key(c, ev);
     if (a.last_seen) a.last_seen[k] = c.purge.last ^ INT64_MIN;
+    if (a.agg_reset && c.purge_pending) a.agg_reset[k] = 1;
     if (c.ovf()) atomicOr(&a.flags[2], 1);
 }
 
@@ -499,10 +501,12 @@ __global__ __launch_bounds__(64) void nfa_lds_k(const NfaArgs* __restrict__ pa, 
             c.fires = a.fires + a.fire_off[idx];
             c.nfires = (int32_t)(a.fire_off[idx + 1] - a.fire_off[idx]);
         }
-        if (a.last_seen) c.purge = nfa::PurgeIn{a.purge_clk, a.purge_from, a.purge_idle, a.last_seen[k] ^ INT64_MIN};
+        if (a.last_seen) c.purge = nfa::PurgeIn{a.purge_clk, a.purge_from, a.purge_idle, a.last_seen_in[k] ^ INT64_MIN};
+        c.emit_flags = a.out_flags;
         nfa::KeyEvents ev{a.ts, a.qstream, a.orig, a.cols, a.nulls, b, e, a.seq_base, a.pos_off, a.vrank};
         nfa::run_key(c, ev);
         if (a.last_seen) a.last_seen[k] = c.purge.last ^ INT64_MIN;
+        if (a.agg_reset && c.purge_pending) a.agg_reset[k] = 1;
         ovf = c.ovf();
         if (dst != src) a.ran[k] = 1;
     }

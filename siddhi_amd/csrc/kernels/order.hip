@@ -82,6 +82,9 @@ void gather_i64(const int64_t* src, const uint32_t* perm, int64_t n, int64_t* ds
 void gather_u32(const uint32_t* src, const uint32_t* perm, int64_t n, uint32_t* dst, hipStream_t stream) {
     if (n > 0) hipLaunchKernelGGL(gather_k<uint32_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, src, perm, n, dst);
 }
+void gather_u8(const uint8_t* src, const uint32_t* perm, int64_t n, uint8_t* dst, hipStream_t stream) {
+    if (n > 0) hipLaunchKernelGGL(gather_k<uint8_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, src, perm, n, dst);
+}
 
 // ---- the selector's post pass (QuerySelector.processNoGroupBy :161-205 for aggregators and having) ------------
 // Records arrive in delivery order. Attribute aggregators keep their state per partition key and see that key's
@@ -186,6 +189,8 @@ __global__ __launch_bounds__(256) void sel_post_k(SelPostArgs a) {
     int64_t* stk = stk_mem + threadIdx.x;
     for (int64_t q = p; q < a.n && (!a.key_sorted || a.key_sorted[q] == k); ++q) {
         const int64_t i = a.perm ? (int64_t)a.perm[q] : q;
+        if (a.reset && a.reset[i])  // @purge destroyed the key's aggregator states before this record
+            for (int g = 0; g < 2 * na; ++g) st[g] = 0;
         const uint32_t nm0 = a.nulls[i];
         PostAcc acc{P, a.vals, a.vstride, i, nm0, st};
         for (int j = 0; j < P->n_user_out; ++j) {  // select items over aggregators, in order, then having
@@ -199,6 +204,14 @@ __global__ __launch_bounds__(256) void sel_post_k(SelPostArgs a) {
         a.nulls[i] = acc.nm;
         a.pass[i] = P->having.len == 0 ? 1 : (uint8_t)pass(a.code, P->having, a.consts, acc, stk, 256);
     }
+}
+
+// keys purged after their last record of the flush: their aggregator states restart (zero = fresh)
+__global__ __launch_bounds__(256) void agg_reset_k(int64_t* __restrict__ st, int na, uint8_t* __restrict__ flag, int64_t K) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= K || !flag[k]) return;
+    for (int g = 0; g < 2 * na; ++g) st[k * 2 * na + g] = 0;
+    flag[k] = 0;
 }
 
 __global__ __launch_bounds__(256) void iota_k(uint32_t* __restrict__ x, int64_t n) {
@@ -236,6 +249,11 @@ void select_post(SelPostArgs a, const uint32_t* key, int kbits, void* work, hipS
         a.key_sorted = ks;
     }
     hipLaunchKernelGGL(sel_post_k, dim3(a.key_sorted ? grid : 1u), dim3(256), 0, stream, a);
+}
+
+void agg_reset(int64_t* agg_state, int n_agg, uint8_t* flags, int64_t K, hipStream_t stream) {
+    if (K > 0) hipLaunchKernelGGL(agg_reset_k, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, agg_state,
+                                  n_agg > 0 ? n_agg : 1, flags, K);
 }
 
 }  // namespace sdg

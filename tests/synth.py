@@ -209,6 +209,15 @@ PURGE_APPS = {
                                   "select e1.id as a, e2.id as b insert into O;", idle="2 sec"),
     "purge_sequence": purge_part("@info(name='q') from every e1=S[price>30], e2=T[price>e1.price]+, "
                                  "e3=S[price>e2[0].price] select e1.id as a, e2[0].id as b, e3.id as c insert into O;"),
+    # absent states: the purge destroys the key's pending absence candidates and its SchedulerState (timer queue)
+    "purge_absent": purge_part("@info(name='q') from every e1=S[price>70] -> not T[price>e1.price] for 3 sec "
+                               "select e1.id as a insert into O;"),
+    "purge_absent_logical": purge_part("@info(name='q') from every e1=S[price>60] -> "
+                                       "(not T[price>e1.price] for 2 sec and e3=S[price<20]) "
+                                       "select e1.id as a, e3.id as c insert into O;"),
+    # aggregators: the purge restarts the key's aggregator states (cleanGroupByStates of the selector's holders)
+    "purge_agg": purge_part("@info(name='q') from every e1=S[price>60] -> e2=T[price>e1.price] "
+                            "select e1.id as a, count() as n, sum(e2.price) as s, max(e1.volume) as m insert into O;"),
 }
 
 
