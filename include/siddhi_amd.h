@@ -185,6 +185,8 @@ typedef struct sdg_stats {
                                   (the batch reran from its start; max_partials is the starting size, 4096 the cap) */
     int64_t carry_in;          /* chain path: partials carried into the last flush from the one before */
     int64_t carry_out;         /* chain path: partials the last flush carries into the next */
+    int64_t arena_slots;       /* generic NFA: per-key arenas allocated after the last flush (queries summed); keys
+                                  whose state the reference destroys down to their start seeds give theirs back */
 } sdg_stats;
 int sdg_last_stats(sdg_engine* e, sdg_stats* out);
 

@@ -250,7 +250,13 @@ struct QueryRt {
     DevBuf rp_ts, rp_qs, rp_seg, rp_segend, rp_cols[MAX_COLS], rp_nulls[MAX_COLS];
     // generic NFA: per-key partial-match arenas (persist across batches)
     DevBuf arena;
-    int64_t arena_keys = 0;
+    int64_t arena_keys = 0;                         // arenas allocated (per key; reclaiming queries: per slot)
+    // reclaiming queries (nfa.h to_idle): keys whose state the reference destroys down to the start processors' seeds
+    // give their arena slot back and keep an idle record; arenas are sized by live keys, not by keys ever seen
+    bool reclaim = false;
+    int64_t map_keys = 0;                           // keys covered by slot_of / idle_rec
+    DevBuf slot_of, idle_rec, slot_key, init_from, releasable, idle_out, free_slots, pool_ctr;
+    HostPin pool_ret;
     nfa::Layout L{};
     // outputs
     DevBuf o_ts, o_key, o_vals, o_nulls, o_emit, o_first, counters, flags;
@@ -1141,7 +1147,73 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         // copies + the per-key committed-copy bit, so a key can be rerun from its batch-start state (scheduler
         // reruns, arena growth)
         const int64_t kb = q.L.bytes;
-        if (q.arena_keys < a.K) {
+        const int ib = nfa::idle_bytes(P.n_states);
+        auto slot_pool = [&]() {
+            SlotPool sp;
+            sp.slot_of = q.slot_of.as<int32_t>();
+            sp.idle_rec = q.idle_rec.as<uint8_t>();
+            sp.slot_key = q.slot_key.as<int32_t>();
+            sp.init_from = q.init_from.as<uint8_t>();
+            sp.releasable = q.releasable.as<uint8_t>();
+            sp.idle_out = q.idle_out.as<uint8_t>();
+            sp.free_slots = q.free_slots.as<int32_t>();
+            sp.counters = (unsigned int*)q.pool_ctr.ensure(16);
+            sp.idle_bytes = ib;
+            return sp;
+        };
+        auto regrow = [&](DevBuf& buf, int64_t old_n, int64_t new_n, int64_t per, int fill) {
+            DevBuf nb;
+            nb.ensure((size_t)std::max<int64_t>(new_n * per, 8));
+            HIPCHECK(hipMemsetAsync(nb.p, fill, (size_t)(new_n * per), st));
+            if (old_n) HIPCHECK(hipMemcpyAsync(nb.p, buf.p, (size_t)(old_n * per), hipMemcpyDeviceToDevice, st));
+            HIPCHECK(hipStreamSynchronize(st));
+            std::swap(nb.p, buf.p);
+            std::swap(nb.cap, buf.cap);
+        };
+        if (q.reclaim) {
+            // the key map covers every key; slots go to the keys with rows in this batch that have none
+            if (q.map_keys < a.K) {
+                const int64_t nk = std::max<int64_t>(a.K, q.map_keys + q.map_keys / 2);
+                regrow(q.slot_of, q.map_keys, nk, 4, 0xFF);  // -1: never seen
+                regrow(q.idle_rec, q.map_keys, nk, ib, 0);
+                q.map_keys = nk;
+            }
+            SlotPool sp = slot_pool();
+            if (q.arena_keys == 0) HIPCHECK(hipMemsetAsync(sp.counters, 0, 16, st));
+            HIPCHECK(hipMemsetAsync(sp.counters + 1, 0, 4, st));
+            nfa_slots_need(sp, partitioned ? v_seg : nullptr, partitioned ? v_segend : nullptr, a.K, st);
+            unsigned int* hc2 = (unsigned int*)q.pool_ret.ensure(16);
+            HIPCHECK(hipMemcpyAsync(hc2, sp.counters, 8, hipMemcpyDeviceToHost, st));
+            HIPCHECK(hipStreamSynchronize(st));
+            const int64_t top = hc2[0], need = hc2[1];
+            if (need > top) {  // grow the pool: the new slots onto the free stack
+                const int64_t old_n = q.arena_keys;
+                const int64_t nn = std::max<int64_t>(2 * old_n, old_n + (need - top) + (need - top) / 4 + 1024);
+                regrow(q.arena, old_n, nn, kb, 0);
+                regrow(q.arena2, old_n, nn, kb, 0);
+                regrow(q.cur_bits, old_n, nn, 1, 0);
+                regrow(q.ran_bits, old_n, nn, 1, 0);
+                regrow(q.init_from, old_n, nn, 1, 0);
+                regrow(q.releasable, old_n, nn, 1, 0);
+                regrow(q.slot_key, old_n, nn, 4, 0);
+                regrow(q.free_slots, old_n, nn, 4, 0);
+                q.idle_out.ensure((size_t)nn * ib);
+                std::vector<int32_t> ids(nn - old_n);
+                for (int64_t i = 0; i < nn - old_n; ++i) ids[i] = (int32_t)(old_n + i);
+                HIPCHECK(hipMemcpy(q.free_slots.as<int32_t>() + top, ids.data(), ids.size() * 4, hipMemcpyHostToDevice));
+                const unsigned int ntop = (unsigned int)(top + (nn - old_n));
+                HIPCHECK(hipMemcpy(sp.counters, &ntop, 4, hipMemcpyHostToDevice));
+                q.arena_keys = nn;
+                sp = slot_pool();
+            }
+            nfa_slots_assign(sp, partitioned ? v_seg : nullptr, partitioned ? v_segend : nullptr, a.K, st);
+            a.slot_of = sp.slot_of;
+            a.init_from = sp.init_from;
+            a.idle_rec = sp.idle_rec;
+            a.idle_out = sp.idle_out;
+            a.releasable = sp.releasable;
+            a.idle_bytes = ib;
+        } else if (q.arena_keys < a.K) {
             int64_t nk = std::max<int64_t>(a.K, q.arena_keys + q.arena_keys / 2);
             auto grow = [&](DevBuf& buf, int64_t per) {
                 DevBuf nb;
@@ -1463,7 +1535,9 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             e->stats.ms_sched_host += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_sched).count() -
                                       (e->stats.ms_nfa_kernel - k_before);
         }
-        nfa_commit(q.cur_bits.as<uint8_t>(), q.ran_bits.as<uint8_t>(), q.arena_keys, st);
+        if (q.reclaim) nfa_commit_slots(slot_pool(), q.cur_bits.as<uint8_t>(), q.ran_bits.as<uint8_t>(), q.arena_keys, st);
+        else nfa_commit(q.cur_bits.as<uint8_t>(), q.ran_bits.as<uint8_t>(), q.arena_keys, st);
+        e->stats.arena_slots += q.arena_keys;
         ev_record(e->ev[2], st);
         HIPCHECK(hipStreamSynchronize(st));
         float ms_kg = 0, ms_m = 0, t;
@@ -2031,6 +2105,7 @@ int do_flush(sdg_engine* e) {
     e->stats.ms_nfa = e->stats.ms_nfa_kernel = e->stats.ms_sched_host = 0;
     e->stats.arena_growths = 0;
     e->stats.carry_in = e->stats.carry_out = 0;
+    e->stats.arena_slots = 0;
     e->stats.fused_ovf = 0;
     e->stats.sched_fires = e->stats.sched_shifted = e->stats.sched_host_keys = e->stats.sched_rerun_keys = 0;
     // a flush consumes its batch whether or not it succeeds: a failing query must not make the next flush
@@ -2196,6 +2271,21 @@ void snapshot(sdg_engine* e, std::vector<uint8_t>& out) {
             w.dev(q.arena2.p, (size_t)(q.arena_keys * q.L.bytes), st);
             w.dev(q.cur_bits.p, (size_t)q.arena_keys, st);
         }
+        // reclaiming queries: the key -> slot map, idle records, the slots' keys and the free stack
+        w.put<uint8_t>(q.reclaim);
+        if (q.reclaim) {
+            const size_t ib = (size_t)nfa::idle_bytes(P.n_states);
+            w.put<int64_t>(q.map_keys);
+            if (q.map_keys > 0) {
+                w.dev(q.slot_of.p, (size_t)q.map_keys * 4, st);
+                w.dev(q.idle_rec.p, (size_t)q.map_keys * ib, st);
+            }
+            if (q.arena_keys > 0) {
+                w.dev(q.slot_key.p, (size_t)q.arena_keys * 4, st);
+                w.dev(q.free_slots.p, (size_t)q.arena_keys * 4, st);
+                w.dev(q.pool_ctr.p, 4, st);
+            }
+        }
         w.put<int64_t>(q.purge_first);
         if (P.purge && q.arena_keys > 0) w.dev(q.last_seen.p, (size_t)q.arena_keys * 8, st);
         // selector aggregators per key
@@ -2236,6 +2326,9 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
         nfa::Layout L{};
         int64_t arena_keys = 0;
         View arena, arena2, cur_bits, last_seen, agg;
+        bool reclaim = false;
+        int64_t map_keys = 0;
+        View slot_of, idle_rec, slot_key, free_slots, pool_ctr;
         int64_t purge_first = INT64_MIN, agg_keys = 0;
         SchedSim sim;
     };
@@ -2283,6 +2376,26 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
             g.cur_bits = view();
             if (g.arena.n != (size_t)(g.arena_keys * g.L.bytes) || g.arena2.n != g.arena.n || g.cur_bits.n != (size_t)g.arena_keys)
                 throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (arenas)");
+        }
+        g.reclaim = r.get<uint8_t>() != 0;
+        if (g.reclaim != e->qs[qi]->reclaim) throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (arena mode)");
+        if (g.reclaim) {
+            const size_t ib = (size_t)nfa::idle_bytes(P.n_states);
+            g.map_keys = r.get<int64_t>();
+            if (g.map_keys < 0) throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (key map)");
+            if (g.map_keys > 0) {
+                g.slot_of = view();
+                g.idle_rec = view();
+                if (g.slot_of.n != (size_t)g.map_keys * 4 || g.idle_rec.n != (size_t)g.map_keys * ib)
+                    throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (key map)");
+            }
+            if (g.arena_keys > 0) {
+                g.slot_key = view();
+                g.free_slots = view();
+                g.pool_ctr = view();
+                if (g.slot_key.n != (size_t)g.arena_keys * 4 || g.free_slots.n != g.slot_key.n || g.pool_ctr.n != 4)
+                    throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (arena slots)");
+            }
         }
         g.purge_first = r.get<int64_t>();
         if (P.purge && g.arena_keys > 0) g.last_seen = view();
@@ -2338,6 +2451,23 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
             up(q.cur_bits, g.cur_bits);
             q.ran_bits.ensure((size_t)q.arena_keys);
             HIPCHECK(hipMemsetAsync(q.ran_bits.p, 0, (size_t)q.arena_keys, st));
+        }
+        if (q.reclaim) {
+            q.map_keys = g.map_keys;
+            if (q.map_keys > 0) {
+                up(q.slot_of, g.slot_of);
+                up(q.idle_rec, g.idle_rec);
+            }
+            if (q.arena_keys > 0) {
+                up(q.slot_key, g.slot_key);
+                up(q.free_slots, g.free_slots);
+                q.pool_ctr.ensure(16);
+                HIPCHECK(hipMemsetAsync(q.pool_ctr.p, 0, 16, st));
+                HIPCHECK(hipMemcpyAsync(q.pool_ctr.p, g.pool_ctr.p, 4, hipMemcpyHostToDevice, st));
+                HIPCHECK(hipMemsetAsync(q.init_from.ensure((size_t)q.arena_keys), 0, (size_t)q.arena_keys, st));
+                HIPCHECK(hipMemsetAsync(q.releasable.ensure((size_t)q.arena_keys), 0, (size_t)q.arena_keys, st));
+                q.idle_out.ensure((size_t)q.arena_keys * nfa::idle_bytes(P.n_states));
+            }
         }
         q.purge_first = g.purge_first;
         if (P.purge && q.arena_keys > 0) up(q.last_seen, g.last_seen);
@@ -2420,6 +2550,8 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             q->key_class = P.partitioned && !q->hq.key_kind.empty() ? key_class_of(q->hq.key_kind[0]) : KC_NONE;
             for (size_t i = 0; i < q->hq.key_kind.size(); ++i)
                 if (q->hq.key_attr[i] < 0 || key_class_of(q->hq.key_kind[i]) != q->key_class) q->key_class = KC_NONE;
+            // arenas sized by live keys (nfa.h to_idle): partitioned generic-NFA queries without timers or @purge
+            q->reclaim = P.partitioned && !P.chain && P.n_sched == 0 && !P.purge && !getenv("SDG_NO_RECLAIM");
             if (!e->compile_only) upload_plan(e.get(), *q);
             e->qs.push_back(std::move(q));
         }

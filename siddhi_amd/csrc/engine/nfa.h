@@ -1206,6 +1206,79 @@ struct CtxT {
     }
 };
 
+// ---- idle keys: the reference's state destruction (StreamPreState.canDestroy :443-448 via
+// PartitionStateHolder.returnState :51-70) ------------------------------------------------------------------------
+// The reference destroys a key's processor state once it is empty and not initialised: every non-start processor
+// whose lists drained. Only the start processors' states (initialised, holding their seed StateEvents) stay. A key
+// in that condition -- non-start processors empty, start processors holding nothing but fresh seeds (no event in any
+// slot, timestamp -1, each referenced once) -- needs no partial-match arena: it is kept as an idle record (the start
+// processors' flags and seed counts), and its arena slot goes back to the pool. At the key's next event the arena
+// is rebuilt from the record (non-start processors fresh, as the reference re-creates them; seeds are
+// interchangeable). Queries with absent states (timer queues) or @purge keep their arenas.
+constexpr int IDLE_PER_STATE = 12;  // 8 PState flag bytes, int16 pending / newAndEvery seed counts
+SDG_HD int idle_bytes(int n_states) { return (4 + IDLE_PER_STATE * n_states + 15) & ~15; }
+
+template <bool TM>
+SDG_HD bool to_idle(CtxT<TM>& c, uint8_t* rec) {
+    if (c.ovf()) return false;
+    KHead& h = c.head();
+    if (!(h.flags & 2)) return false;
+    c.gc();
+    if (h.nd_used || h.rc_used) return false;
+    int entries = 0;
+    for (int p = 0; p < c.L.n_states; ++p) {
+        const PState& st = c.ps(p);
+        if (st.last_sched || st.last_arrival) return false;
+        if (!c.P->st[p].is_start && (st.pn || st.nw)) return false;
+        for (int l = 0; l < 2; ++l) {
+            const int16_t* lst = l ? c.newe(p) : c.pend(p);
+            const int n = l ? st.nw : st.pn;
+            for (int j = 0; j < n; ++j) {
+                const SE& e = c.se(lst[j]);
+                if (e.type != T_CURRENT || e.ts != -1) return false;
+                const int16_t* sl = c.slots(lst[j]);
+                for (int k = 0; k < c.L.n_states; ++k)
+                    if (sl[k] != NIL) return false;
+            }
+            entries += n;
+        }
+    }
+    if (entries != h.se_used) return false;  // no seed shared between lists (logical partners)
+    *(int32_t*)rec = h.flags;
+    for (int p = 0; p < c.L.n_states; ++p) {
+        uint8_t* r = rec + 4 + IDLE_PER_STATE * p;
+        const PState& st = c.ps(p);
+        const uint8_t* f = &st.changed;  // the 8 flag bytes: changed .. pad
+        for (int b = 0; b < 8; ++b) r[b] = f[b];
+        *(int16_t*)(r + 8) = st.pn;
+        *(int16_t*)(r + 10) = st.nw;
+    }
+    return true;
+}
+
+template <bool TM>
+SDG_HD void from_idle(CtxT<TM>& c, const uint8_t* rec) {
+    c.arena_init();
+    c.head().flags = *(const int32_t*)rec;
+    for (int p = 0; p < c.L.n_states; ++p) {
+        const uint8_t* r = rec + 4 + IDLE_PER_STATE * p;
+        const int16_t pn = *(const int16_t*)(r + 8), nw = *(const int16_t*)(r + 10);
+        if (!c.P->st[p].is_start) continue;  // destroyed: fresh (arena_init)
+        PState& st = c.ps(p);
+        uint8_t* f = &st.changed;
+        for (int b = 0; b < 8; ++b) f[b] = r[b];
+        for (int l = 0; l < 2; ++l) {
+            const int n = l ? nw : pn;
+            for (int j = 0; j < n; ++j) {
+                const int16_t s = c.se_alloc();
+                if (s == NIL) return;
+                if (l) c.push(c.newe(p), st.nw, s);
+                else c.push(c.pend(p), st.pn, s);
+            }
+        }
+    }
+}
+
 // one key's committed arena into a larger layout (more partial-match slots, same states / columns / schedulers):
 // header, processor states, the lists (re-strided), timer queues (unrolled to start at 0) and every pool object at
 // its index; the free lists are then rebuilt by a mark-sweep in the new layout (the lists are the only roots

@@ -248,6 +248,14 @@ struct NfaArgs {
     const int64_t* last_seen_in;
     uint8_t* out_flags;               // [out_cap] per record: aggregator reset before it (nullptr: not recorded)
     uint8_t* agg_reset;               // [K] set for a key purged after its last record of the run (nullptr: none)
+    // idle keys (nfa.h to_idle / from_idle; nullptr unless the query reclaims arenas): arenas, cur / ran bits are
+    // indexed by slot, slot_of maps keys to slots
+    const int32_t* slot_of;           // [K] arena slot of key k; -1 never seen, -2 idle (its record in idle_rec)
+    const uint8_t* init_from;         // [slots] 1: the slot's key starts fresh in this batch, 2: from its idle record
+    const uint8_t* idle_rec;          // [K][idle_bytes]
+    uint8_t* idle_out;                // [slots][idle_bytes] the record of a key that ended the run idle
+    uint8_t* releasable;              // [slots] 1: the slot's key ended idle (the slot returns to the pool at commit)
+    int32_t idle_bytes;
     const int64_t* purge_clk;
     int64_t purge_from, purge_idle;
     // rerun mode: run only list[0..nlist) with the explicit fire lists fires[fire_off[i] .. fire_off[i + 1])
@@ -268,6 +276,24 @@ void nfa_migrate(const Plan* plan, const uint8_t* arena, const uint8_t* arena2, 
                  const nfa::Layout& Ls, uint8_t* dst, const nfa::Layout& Ld, int64_t K, hipStream_t stream);
 // double-buffered arenas: flip `cur` of every key a run touched (`ran`), clearing `ran`
 void nfa_commit(uint8_t* cur, uint8_t* ran, int64_t K, hipStream_t stream);
+// idle keys: the pool of arena slots
+struct SlotPool {
+    int32_t* slot_of;                 // [K]
+    uint8_t* idle_rec;                // [K][idle_bytes]
+    int32_t* slot_key;                // [slots] key of each assigned slot
+    uint8_t* init_from;               // [slots]
+    uint8_t* releasable;              // [slots]
+    uint8_t* idle_out;                // [slots][idle_bytes]
+    int32_t* free_slots;              // [slots] stack of free slot ids
+    unsigned int* counters;           // [0] free stack top, [1] keys needing a slot (nfa_slots_need)
+    int32_t idle_bytes;
+};
+// keys with rows in this batch but no slot (seg: the key segments; nullptr + K 1: one key) -> counters[1]
+void nfa_slots_need(const SlotPool& sp, const uint32_t* seg_start, const uint32_t* seg_end, int64_t K, hipStream_t st);
+// give each such key a slot from the free stack (the host made sure there are enough)
+void nfa_slots_assign(const SlotPool& sp, const uint32_t* seg_start, const uint32_t* seg_end, int64_t K, hipStream_t st);
+// nfa_commit for slot-indexed arenas, then every slot whose key ended idle: record saved, slot back to the pool
+void nfa_commit_slots(const SlotPool& sp, uint8_t* cur, uint8_t* ran, int64_t slots, hipStream_t st);
 
 // delivery order of n match records (order.hip): perm = the record indices sorted by (emit - emit_base as u32,
 // sub - sub_bias as a 48-bit key); work = order_workspace(n) bytes

@@ -350,11 +350,18 @@ __global__ __launch_bounds__(256, TM ? 1 : SDG_NFA_MINB) void nfa_k(const NfaArg
     }
     const Plan* P = a.plan;
     const int64_t kb = a.L.bytes;
-    uint8_t* src = a.arena + k * kb;
+    int64_t s = k;  // arena slot
+    uint8_t from = 0;
+    if (a.slot_of) {
+        s = a.slot_of[k];
+        if (s < 0) return;  // no rows (reclaiming queries have no timers)
+        from = a.init_from[s];
+    }
+    uint8_t* src = a.arena + s * kb;
     uint8_t* dst = src;
     if (a.arena2) {
-        if (a.cur[k]) src = a.arena2 + k * kb;
-        else dst = a.arena2 + k * kb;
+        if (a.cur[s]) src = a.arena2 + s * kb;
+        else dst = a.arena2 + s * kb;
     }
     if (!a.list && b >= e && P->partitioned) {
         // no event of this key: it runs only for its queued timers (initPartition happens at a first event)
@@ -365,11 +372,15 @@ __global__ __launch_bounds__(256, TM ? 1 : SDG_NFA_MINB) void nfa_k(const NfaArg
         for (int i = 0; i < a.L.n_sched; ++i) queued |= tq[i].n > 0;
         if (!queued) return;
     }
-    if (dst != src) {  // work on the other copy: the committed state stays intact until nfa_commit
+    if (from) {  // no committed arena: fresh (zeros), or rebuilt from the idle record below
+        uint4* d4 = (uint4*)dst;
+        for (int64_t i = 0; i < kb / 16; ++i) d4[i] = make_uint4(0, 0, 0, 0);
+        if (dst != src) a.ran[s] = 1;
+    } else if (dst != src) {  // work on the other copy: the committed state stays intact until nfa_commit
         const uint4* s4 = (const uint4*)src;
         uint4* d4 = (uint4*)dst;
         for (int64_t i = 0; i < kb / 16; ++i) d4[i] = s4[i];
-        a.ran[k] = 1;
+        a.ran[s] = 1;
     }
     nfa::CtxT<TM> c;
     c.P = P;
@@ -401,10 +412,12 @@ __global__ __launch_bounds__(256, TM ? 1 : SDG_NFA_MINB) void nfa_k(const NfaArg
     // last_seen is stored XOR INT64_MIN, so the zero-filled array reads as "never seen"
     if (a.last_seen) c.purge = nfa::PurgeIn{a.purge_clk, a.purge_from, a.purge_idle, a.last_seen_in[k] ^ INT64_MIN};
     c.emit_flags = a.out_flags;
+    if (from == 2) nfa::from_idle(c, a.idle_rec + k * a.idle_bytes);
     nfa::KeyEvents ev{a.ts, a.qstream, a.orig, a.cols, a.nulls, b, e, a.seq_base, a.pos_off, a.vrank};
     nfa::run_key(c, ev);
     if (a.last_seen) a.last_seen[k] = c.purge.last ^ INT64_MIN;
     if (a.agg_reset && c.purge_pending) a.agg_reset[k] = 1;
+    if (a.releasable) a.releasable[s] = nfa::to_idle(c, a.idle_out + s * a.idle_bytes) ? 1 : 0;
     if (c.ovf()) atomicOr(&a.flags[2], 1);
 }
 
@@ -439,16 +452,25 @@ __global__ __launch_bounds__(64) void nfa_lds_k(const NfaArgs* __restrict__ pa, 
     int64_t b = 0, e = a.n;
     const uint8_t* src = nullptr;
     uint8_t* dst = nullptr;
+    int64_t s = k;     // arena slot
+    uint8_t from = 0;  // 1: a fresh key, 2: rebuilt from its idle record (no committed arena to stage)
     if (active) {
         if (a.seg_start) {
             b = a.seg_start[k];
             e = a.seg_end[k];
         }
-        src = a.arena + k * kb;
-        dst = a.arena + k * kb;
+        if (a.slot_of) {
+            s = a.slot_of[k];
+            if (s < 0) active = false;  // no rows (slots go to keys with rows; reclaiming queries have no timers)
+            else from = a.init_from[s];
+        }
+    }
+    if (active) {
+        src = a.arena + s * kb;
+        dst = a.arena + s * kb;
         if (a.arena2) {
-            if (a.cur[k]) src = a.arena2 + k * kb;
-            else dst = a.arena2 + k * kb;
+            if (a.cur[s]) src = a.arena2 + s * kb;
+            else dst = a.arena2 + s * kb;
         }
         if (!a.list && b >= e && P->partitioned) {
             // no event of this key: it runs only for its queued timers (initPartition happens at a first event)
@@ -464,12 +486,15 @@ __global__ __launch_bounds__(64) void nfa_lds_k(const NfaArgs* __restrict__ pa, 
         }
     }
     const int64_t n16 = kb / 16;
-    // stage: the committed arenas of the active keys, one arena per wave instruction sweep
+    // stage: the committed arenas of the active keys, one arena per wave instruction sweep (zeros for a key that
+    // has none: fresh, or rebuilt from its idle record below)
     for (uint64_t m = __ballot(active); m; m &= m - 1) {
         const int j = __ffsll((unsigned long long)m) - 1;
         const uint4* s4 = (const uint4*)__shfl((long long)(uintptr_t)src, j);
+        const int fj = __shfl((int)from, j);
         uint4* d4 = (uint4*)(lds_arena + (int64_t)j * kb);
-        for (int64_t i = lane; i < n16; i += 64) d4[i] = s4[i];
+        if (fj) for (int64_t i = lane; i < n16; i += 64) d4[i] = make_uint4(0, 0, 0, 0);
+        else for (int64_t i = lane; i < n16; i += 64) d4[i] = s4[i];
     }
     __syncthreads();
     bool ovf = false;
@@ -503,12 +528,14 @@ __global__ __launch_bounds__(64) void nfa_lds_k(const NfaArgs* __restrict__ pa, 
         }
         if (a.last_seen) c.purge = nfa::PurgeIn{a.purge_clk, a.purge_from, a.purge_idle, a.last_seen_in[k] ^ INT64_MIN};
         c.emit_flags = a.out_flags;
+        if (from == 2) nfa::from_idle(c, a.idle_rec + k * a.idle_bytes);
         nfa::KeyEvents ev{a.ts, a.qstream, a.orig, a.cols, a.nulls, b, e, a.seq_base, a.pos_off, a.vrank};
         nfa::run_key(c, ev);
         if (a.last_seen) a.last_seen[k] = c.purge.last ^ INT64_MIN;
         if (a.agg_reset && c.purge_pending) a.agg_reset[k] = 1;
+        if (a.releasable) a.releasable[s] = nfa::to_idle(c, a.idle_out + s * a.idle_bytes) ? 1 : 0;
         ovf = c.ovf();
-        if (dst != src) a.ran[k] = 1;
+        if (dst != src) a.ran[s] = 1;
     }
     if (ovf) atomicOr(&a.flags[2], 1);
     __syncthreads();
@@ -533,6 +560,45 @@ __global__ __launch_bounds__(256) void nfa_migrate_k(const Plan* __restrict__ pl
     c.L = Ld;
     c.base = dst + k * Ld.bytes;
     nfa::migrate_key(c, src, Ls);
+}
+
+__device__ __forceinline__ bool has_rows(const uint32_t* seg_start, const uint32_t* seg_end, int64_t k) {
+    return !seg_start || seg_end[k] > seg_start[k];
+}
+__global__ __launch_bounds__(256) void nfa_slots_need_k(SlotPool sp, const uint32_t* __restrict__ seg_start,
+                                                        const uint32_t* __restrict__ seg_end, int64_t K) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool need = k < K && sp.slot_of[k] < 0 && has_rows(seg_start, seg_end, k);
+    const uint64_t m = __ballot(need);
+    if (m && lane_id() == __ffsll((unsigned long long)m) - 1) atomicAdd(&sp.counters[1], (unsigned)__popcll(m));
+}
+__global__ __launch_bounds__(256) void nfa_slots_assign_k(SlotPool sp, const uint32_t* __restrict__ seg_start,
+                                                          const uint32_t* __restrict__ seg_end, int64_t K) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= K) return;
+    const int32_t cur = sp.slot_of[k];
+    if (cur >= 0 || !has_rows(seg_start, seg_end, k)) return;
+    const unsigned top = atomicSub(&sp.counters[0], 1u);  // (the host grew the pool to cover every such key)
+    const int32_t s = sp.free_slots[top - 1];
+    sp.slot_of[k] = s;
+    sp.slot_key[s] = (int32_t)k;
+    sp.init_from[s] = cur == -2 ? 2 : 1;
+}
+__global__ __launch_bounds__(256) void nfa_commit_slots_k(SlotPool sp, uint8_t* __restrict__ cur, uint8_t* __restrict__ ran,
+                                                          int64_t S) {
+    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= S || !ran[s]) return;
+    cur[s] ^= 1;
+    ran[s] = 0;
+    sp.init_from[s] = 0;
+    if (!sp.releasable[s]) return;
+    sp.releasable[s] = 0;
+    const int64_t k = sp.slot_key[s];
+    const int ib = sp.idle_bytes;
+    for (int i = 0; i < ib; i += 4) *(int32_t*)(sp.idle_rec + k * ib + i) = *(const int32_t*)(sp.idle_out + s * ib + i);
+    sp.slot_of[k] = -2;
+    const unsigned top = atomicAdd(&sp.counters[0], 1u);
+    sp.free_slots[top] = (int32_t)s;
 }
 
 __global__ __launch_bounds__(256) void nfa_commit_k(uint8_t* __restrict__ cur, uint8_t* __restrict__ ran, int64_t K) {
@@ -725,6 +791,16 @@ void nfa_run(const NfaArgs& a, const NfaArgs* d_a, hipStream_t stream) {
     }
     if (a.T.log) hipLaunchKernelGGL(nfa_k<true>, dim3((unsigned)((keys + 255) / 256)), dim3(256), 0, stream, d_a);
     else hipLaunchKernelGGL(nfa_k<false>, dim3((unsigned)((keys + 255) / 256)), dim3(256), 0, stream, d_a);
+}
+
+void nfa_slots_need(const SlotPool& sp, const uint32_t* seg_start, const uint32_t* seg_end, int64_t K, hipStream_t st) {
+    if (K > 0) hipLaunchKernelGGL(nfa_slots_need_k, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, st, sp, seg_start, seg_end, K);
+}
+void nfa_slots_assign(const SlotPool& sp, const uint32_t* seg_start, const uint32_t* seg_end, int64_t K, hipStream_t st) {
+    if (K > 0) hipLaunchKernelGGL(nfa_slots_assign_k, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, st, sp, seg_start, seg_end, K);
+}
+void nfa_commit_slots(const SlotPool& sp, uint8_t* cur, uint8_t* ran, int64_t slots, hipStream_t st) {
+    if (slots > 0) hipLaunchKernelGGL(nfa_commit_slots_k, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, sp, cur, ran, slots);
 }
 
 void nfa_commit(uint8_t* cur, uint8_t* ran, int64_t K, hipStream_t stream) {

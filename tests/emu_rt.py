@@ -35,6 +35,8 @@ def lib():
         L.emu_sched_stat.restype = I64
         L.emu_sched_stat.argtypes = [I32]
         L.emu_start.argtypes = [P, I64]
+        L.emu_set_reclaim.argtypes = [I32]
+        L.emu_idles.restype = I64
         L.emu_num_queries.argtypes = [P]
         for f in ("emu_query_name", "emu_query_target"):
             getattr(L, f).restype = ctypes.c_char_p

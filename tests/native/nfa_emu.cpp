@@ -107,6 +107,8 @@ BatchClock batch_clock(Emu* e) {
 
 size_t reordered_ = 0, taken_ = 0;
 double us_[3] = {0, 0, 0};
+int g_reclaim = 0;      // emu_set_reclaim: every idle key goes through its idle record after each run (nfa.h to_idle)
+int64_t idles_ = 0;     // keys rebuilt from an idle record (all flushes)
 int64_t growths_ = 0;  // arena doublings (all flushes)  // cumulative: optimistic pass, reruns, exact pass (microseconds)  // last flush's scheduler statistics (tests)
 
 int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
@@ -248,6 +250,20 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
             ko.push_back(std::move(o));
         }
         klog[k].assign(logs.begin(), logs.begin() + (int64_t)lcount);
+        // as the engine's reclaiming queries: a key that ends idle keeps only its idle record; its arena is rebuilt
+        // from it (here at once, on the device at the key's next batch -- the same state)
+        if (g_reclaim && P.partitioned && P.n_sched == 0 && !P.purge) {
+            std::vector<uint8_t> rec((size_t)nfa::idle_bytes(P.n_states));
+            if (nfa::to_idle(c, rec.data())) {
+                std::fill(q.arenas[k].begin(), q.arenas[k].end(), 0);
+                nfa::CtxT<true> c2;
+                c2.P = &P;
+                c2.L = q.L;
+                c2.base = q.arenas[k].data();
+                nfa::from_idle(c2, rec.data());
+                ++idles_;
+            }
+        }
         return 0;
     };
     // as the engine: a key out of partial-match slots doubles every key's arena (nfa.h migrate_key from the
@@ -469,6 +485,9 @@ int emu_start(void* h, int64_t ts) {
     if (!e->app.playback) e->clock = ts;
     return 0;
 }
+
+void emu_set_reclaim(int on) { g_reclaim = on; }
+int64_t emu_idles() { return idles_; }
 
 int emu_flush(void* h) {
     Emu* e = (Emu*)h;

@@ -14,8 +14,18 @@ def query_rows(outs, kind="query"):
     return [(o["name"], o["ts"], tuple(o["values"])) for o in outs if o["kind"] == kind and not o["expired"]]
 
 
+@pytest.fixture(params=[0, 1], ids=["arenas", "idle_records"])
+def reclaim(request, emu_built):
+    """1: every key that ends a run idle goes through its idle record (nfa.h to_idle / from_idle), as the engine's
+    reclaiming queries do when a key's state shrinks to what the reference keeps (canDestroy)"""
+    import emu_rt
+    emu_rt.lib().emu_set_reclaim(request.param)
+    yield request.param
+    emu_rt.lib().emu_set_reclaim(0)
+
+
 @pytest.mark.parametrize("path", PATHS, ids=golden_util.fixture_ids())
-def test_golden_fixture_on_host_nfa(path, oracle_built, emu_built):
+def test_golden_fixture_on_host_nfa(path, reclaim, oracle_built, emu_built):
     fx = golden_util.load(path)
     try:
         got = run_emu_fixture(fx)

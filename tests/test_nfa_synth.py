@@ -18,16 +18,20 @@ def oracle_rows(app, tr):
 
 
 @pytest.mark.parametrize("name", sorted(synth.APPS))
-@pytest.mark.parametrize("batches", [1, 4])
+@pytest.mark.parametrize("batches", [1, 4, 40])
 def test_synthetic_trace(name, batches, oracle_built, emu_built):
+    """40 batches with idle records: keys go idle between batches and are rebuilt from their records"""
+    import emu_rt
     app = synth.APPS[name]
     tr = synth.trace(1500, keys=4, seed=zlib.crc32(name.encode()) % 1000, null_rate=0.05 if name == "arith_nulls" else 0.0)
     ref = oracle_rows(app, tr)
+    emu_rt.lib().emu_set_reclaim(1 if batches == 40 else 0)
     e = EmuAdapter(app, max_partials=256)
     try:
         got = synth.run(e, tr, batches)
     finally:
         e.close()
+        emu_rt.lib().emu_set_reclaim(0)
     if name != "c3_sequence":  # the literal C3 (<2:5> in a sequence) never matches under the reference semantics
         assert len(ref) > 0, "trace produces no matches; test is vacuous"
     assert got == ref
