@@ -137,6 +137,18 @@ struct PushChunk {
     const int64_t* d_ts = nullptr;
     std::vector<const void*> d_cols;
     std::vector<const uint8_t*> d_nulls;
+    // a host push staged in HBM at push time (device == true): its rows are [stage_off, stage_off + n) of the
+    // engine's staging columns of its stream; d_ts / d_cols / d_nulls are resolved when the flush starts
+    int64_t stage_off = -1;
+};
+
+// the device staging of one stream's host pushes (sdg_push / sdg_push_events): columns appended in push order, so
+// a query of that stream sees every staged push of a batch as one contiguous device range (zero-copy flush path)
+struct Stage {
+    DevBuf ts;
+    std::vector<DevBuf> cols, nulls;
+    std::vector<char> has_nulls;
+    int64_t n = 0, cap = 0;
 };
 
 // integral partition values -> dictionary id (open addressing). Java's toString is injective on int/long and
@@ -310,6 +322,8 @@ struct sdg_engine {
     bool no_fused = false;
     uint64_t app_hash = 0;       // FNV-1a of the app text: a snapshot restores only into the app it came from
     std::vector<uint8_t> snap;   // the last sdg_snapshot's bytes (valid until the next snapshot / destroy)
+    std::vector<Stage> stage;    // per stream: host pushes staged in HBM (see stageable)
+    std::vector<char> stage_ok;  // per stream: every query of the stream takes device-resident batches
 };
 
 namespace {
@@ -813,10 +827,27 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     const bool ranged = std::find(h.key_attr.begin(), h.key_attr.end(), -2) != h.key_attr.end();
     const uint8_t* d_vrank = nullptr;
     bool zero_copy = parts.size() == 1 && parts[0]->device && !multi_stream && parts[0]->stream >= 0;
+    // several staged host pushes of the query's one stream: consecutive rows of the stream's staging
+    bool staged_run = !zero_copy && !multi_stream && !parts.empty();
+    for (size_t i = 0; i < parts.size() && staged_run; ++i)
+        staged_run = parts[i]->device && parts[i]->stage_off >= 0 && parts[i]->stream == parts[0]->stream &&
+                     (i == 0 || parts[i]->stage_off == parts[i - 1]->stage_off + parts[i - 1]->n);
+    if (staged_run) zero_copy = true;
     if (zero_copy) {
         const PushChunk& c = *parts[0];
         int qpos = h.stream_pos(c.stream);
         pos_off = part_pos[0];
+        bool contiguous = true;  // batch positions of the rows: one run, or a map (other streams' rows between)
+        for (size_t i = 1; i < parts.size(); ++i) contiguous &= part_pos[i] == part_pos[i - 1] + parts[i - 1]->n;
+        if (!contiguous) {
+            std::vector<uint32_t> vpos((size_t)n);
+            size_t o = 0;
+            for (size_t i = 0; i < parts.size(); ++i)
+                for (int64_t r = 0; r < parts[i]->n; ++r) vpos[o++] = (uint32_t)(part_pos[i] + r);
+            d_vpos = (const uint32_t*)q.d_vpos.ensure((size_t)std::max<int64_t>(n, 1) * 4);
+            HIPCHECK(hipMemcpy((void*)d_vpos, vpos.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+            pos_off = 0;
+        }
         d_ts = c.d_ts;
         for (int k = 0; k < nc; ++k) {
             int ai = h.col_attr[qpos][k];
@@ -2121,8 +2152,13 @@ int do_flush(sdg_engine* e) {
             e->seq += G;
             e->pending.clear();
             e->pending_n = 0;
+            for (Stage& S : e->stage) {
+                S.n = 0;
+                std::fill(S.has_nulls.begin(), S.has_nulls.end(), 0);
+            }
         }
     } consume{e};
+    resolve_staged(e);
     int64_t G = 0;
     for (auto& c : e->pending) G += c.n;
     consume.G = G;
@@ -2560,6 +2596,18 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             for (auto& a : s.attrs) t.push_back((int32_t)a.type);
             e->stream_types.push_back(t);
         }
+        // streams whose host pushes go to HBM at push time: every query reading them takes device-resident batches
+        // (one stream; no range partition; string keys or one class of value keys)
+        e->stage.resize(e->stream_types.size());
+        e->stage_ok.assign(e->stream_types.size(), 1);
+        for (auto& q : e->qs) {
+            const HostQuery& h = q->hq;
+            const bool ranged = std::find(h.key_attr.begin(), h.key_attr.end(), -2) != h.key_attr.end();
+            const bool ok = h.streams.size() == 1 && !ranged &&
+                            (!h.plan.partitioned || q->string_keys || q->key_class != KC_NONE);
+            if (!ok)
+                for (int s2 : h.streams) e->stage_ok[s2] = 0;
+        }
         for (auto& q : e->qs) {
             e->out_types.push_back(q->hq.out_types);
             std::vector<const char*> nm;
@@ -2654,6 +2702,86 @@ const char* sdg_string(sdg_engine* e, uint32_t id) {
 }
 
 namespace {
+// a host push straight into HBM (the stream's staging columns): the flush then takes the zero-copy device path
+// instead of re-assembling rows on the host (InputHandler.send -> pinned columnar batches, BASELINE north_star).
+// Only when every query of the stream takes device-resident batches and the push has no null partition key.
+bool stage_push(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const void* const* cols,
+                const uint8_t* const* nulls, PushChunk& c) {
+    if (e->compile_only || getenv("SDG_NO_STAGE") || stream >= (int)e->stage_ok.size() || !e->stage_ok[stream]) return false;
+    const auto& types = e->stream_types[stream];
+    for (auto& qp : e->qs) {  // null partition keys are dropped by the host path (PartitionStreamReceiver :262-272)
+        const HostQuery& h = qp->hq;
+        const int qpos = h.stream_pos(stream);
+        if (qpos < 0 || !h.plan.partitioned) continue;
+        const int ai = h.key_attr[qpos];
+        if (ai >= 0 && nulls && nulls[ai])
+            for (int64_t r = 0; r < n; ++r)
+                if (nulls[ai][r]) return false;
+    }
+    for (size_t a = 0; a < types.size(); ++a)
+        if (!cols[a]) throw std::invalid_argument("missing column");
+    Stage& S = e->stage[stream];
+    if (S.cols.size() != types.size()) {
+        S.cols = std::vector<DevBuf>(types.size());
+        S.nulls = std::vector<DevBuf>(types.size());
+        S.has_nulls.assign(types.size(), 0);
+    }
+    if (S.n + n > S.cap) {  // grow, keeping the rows staged so far
+        const int64_t nc = std::max<int64_t>(S.n + n, 2 * S.cap);
+        auto keep = [&](DevBuf& b, int w) {
+            DevBuf nb;
+            nb.ensure((size_t)nc * w);
+            if (S.n) HIPCHECK(hipMemcpy(nb.p, b.p, (size_t)S.n * w, hipMemcpyDeviceToDevice));
+            std::swap(nb.p, b.p);
+            std::swap(nb.cap, b.cap);
+        };
+        keep(S.ts, 8);
+        for (size_t a = 0; a < types.size(); ++a) {
+            keep(S.cols[a], width_of((uint8_t)types[a]));
+            if (S.has_nulls[a]) keep(S.nulls[a], 1);
+        }
+        S.cap = nc;
+    }
+    hipStream_t st = e->stream;
+    HIPCHECK(hipMemcpyAsync(S.ts.as<int64_t>() + S.n, ts, (size_t)n * 8, hipMemcpyHostToDevice, st));
+    for (size_t a = 0; a < types.size(); ++a) {
+        const int w = width_of((uint8_t)types[a]);
+        HIPCHECK(hipMemcpyAsync((uint8_t*)S.cols[a].p + (size_t)S.n * w, cols[a], (size_t)n * w, hipMemcpyHostToDevice, st));
+        bool any = false;
+        if (nulls && nulls[a])
+            for (int64_t r = 0; r < n && !any; ++r) any = nulls[a][r] != 0;
+        if (any && !S.has_nulls[a]) {  // the first nulls of this attribute: earlier rows are not null
+            S.nulls[a].ensure((size_t)S.cap);
+            HIPCHECK(hipMemsetAsync(S.nulls[a].p, 0, (size_t)S.n, st));
+            S.has_nulls[a] = 1;
+        }
+        if (any) HIPCHECK(hipMemcpyAsync((uint8_t*)S.nulls[a].p + S.n, nulls[a], (size_t)n, hipMemcpyHostToDevice, st));
+        else if (S.has_nulls[a]) HIPCHECK(hipMemsetAsync((uint8_t*)S.nulls[a].p + S.n, 0, (size_t)n, st));
+    }
+    HIPCHECK(hipStreamSynchronize(st));  // the caller's buffers are free when the push returns
+    c.device = true;
+    c.stage_off = S.n;
+    S.n += n;
+    return true;
+}
+
+// staged chunks: their device pointers into the staging (stable from here to the end of the flush)
+void resolve_staged(sdg_engine* e) {
+    for (PushChunk& c : e->pending) {
+        if (c.stage_off < 0) continue;
+        Stage& S = e->stage[c.stream];
+        c.d_ts = S.ts.as<int64_t>() + c.stage_off;
+        const size_t na = S.cols.size();
+        c.d_cols.assign(na, nullptr);
+        c.d_nulls.assign(na, nullptr);
+        for (size_t a = 0; a < na; ++a) {
+            const int w = width_of((uint8_t)e->stream_types[c.stream][a]);
+            c.d_cols[a] = (const uint8_t*)S.cols[a].p + (size_t)c.stage_off * w;
+            if (S.has_nulls[a]) c.d_nulls[a] = (const uint8_t*)S.nulls[a].p + c.stage_off;
+        }
+    }
+}
+
 int push_host(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const void* const* cols,
               const uint8_t* const* nulls, bool event_array) {
     if (!e || stream < 0 || stream >= (int)e->stream_types.size() || n < 0 || (n > 0 && !ts))
@@ -2672,6 +2800,12 @@ int push_host(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const voi
         c.n = n;
         c.device = false;
         c.no_adv = event_array;
+        if (n > 0 && stage_push(e, stream, n, ts, cols, nulls, c)) {
+            e->pending_n += n;
+            e->pending.push_back(std::move(c));
+            if (e->pending_n >= e->capacity) return do_flush(e);
+            return (int)SDG_OK;
+        }
         c.ts.assign(ts, ts + n);
         const auto& types = e->stream_types[stream];
         c.cols.resize(types.size());

@@ -774,7 +774,9 @@ void nfa_migrate(const Plan* plan, const uint8_t* arena, const uint8_t* arena2, 
 int nfa_lds_lanes(const nfa::Layout& L) {
     static const char* off = getenv("SDG_NFA_HBM");  // A/B: the arena-in-HBM kernel
     if (off) return 0;
-    const int64_t lanes = NFA_LDS_BUDGET / L.bytes;
+    static const char* bud = getenv("SDG_NFA_LDS");  // A/B: LDS bytes per block (wave)
+    const int64_t budget = bud ? atoll(bud) : NFA_LDS_BUDGET;
+    const int64_t lanes = budget / L.bytes;
     return lanes >= NFA_LDS_MIN_LANES ? (int)(lanes < 64 ? lanes : 64) : 0;
 }
 
