@@ -43,6 +43,12 @@ struct DevBuf {
     DevBuf() = default;
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p(o.p), cap(o.cap) { o.p = nullptr; o.cap = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        std::swap(p, o.p);
+        std::swap(cap, o.cap);
+        return *this;
+    }
     ~DevBuf() { if (p) (void)hipFree(p); }
     void* ensure(size_t bytes) {
         if (bytes == 0) bytes = 8;
@@ -322,8 +328,10 @@ struct sdg_engine {
     bool no_fused = false;
     uint64_t app_hash = 0;       // FNV-1a of the app text: a snapshot restores only into the app it came from
     std::vector<uint8_t> snap;   // the last sdg_snapshot's bytes (valid until the next snapshot / destroy)
-    std::vector<Stage> stage;    // per stream: host pushes staged in HBM (see stageable)
+    std::vector<Stage> stage;    // per stream: host pushes staged in HBM (see stage_push)
     std::vector<char> stage_ok;  // per stream: every query of the stream takes device-resident batches
+    std::vector<char> host_pending;  // per stream: the pending batch holds host rows of it (no staging until flush)
+    bool no_stage = false;       // mixed pushes seen: host assembly for every stream from then on
 };
 
 namespace {
@@ -2124,6 +2132,8 @@ void build_clock(sdg_engine* e, int64_t G) {
     HIPCHECK(hipMemcpyAsync(dn, bc.nadv.data(), (G + 1) * 4, hipMemcpyHostToDevice, e->stream));
 }
 
+void resolve_staged(sdg_engine* e);
+
 int do_flush(sdg_engine* e) {
     if (e->compile_only) throw DeviceError("engine was compiled with SDG_COMPILE_ONLY");
     HIPCHECK(hipSetDevice(e->device));
@@ -2156,6 +2166,7 @@ int do_flush(sdg_engine* e) {
                 S.n = 0;
                 std::fill(S.has_nulls.begin(), S.has_nulls.end(), 0);
             }
+            std::fill(e->host_pending.begin(), e->host_pending.end(), 0);
         }
     } consume{e};
     resolve_staged(e);
@@ -2600,6 +2611,7 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
         // (one stream; no range partition; string keys or one class of value keys)
         e->stage.resize(e->stream_types.size());
         e->stage_ok.assign(e->stream_types.size(), 1);
+        e->host_pending.assign(e->stream_types.size(), 0);
         for (auto& q : e->qs) {
             const HostQuery& h = q->hq;
             const bool ranged = std::find(h.key_attr.begin(), h.key_attr.end(), -2) != h.key_attr.end();
@@ -2705,9 +2717,39 @@ namespace {
 // a host push straight into HBM (the stream's staging columns): the flush then takes the zero-copy device path
 // instead of re-assembling rows on the host (InputHandler.send -> pinned columnar batches, BASELINE north_star).
 // Only when every query of the stream takes device-resident batches and the push has no null partition key.
+// staged chunks back to host columns: a query's batch view is assembled on the host when a stream's rows mix staged
+// and host pushes (a push with a null partition key, a mixed push)
+void unstage(sdg_engine* e, int stream) {
+    for (PushChunk& c : e->pending) {
+        if (c.stage_off < 0 || (stream >= 0 && c.stream != stream)) continue;
+        Stage& S = e->stage[c.stream];
+        const auto& types = e->stream_types[c.stream];
+        c.ts.resize(c.n);
+        HIPCHECK(hipMemcpy(c.ts.data(), S.ts.as<int64_t>() + c.stage_off, (size_t)c.n * 8, hipMemcpyDeviceToHost));
+        c.cols.assign(types.size(), {});
+        c.nulls.assign(types.size(), {});
+        for (size_t a = 0; a < types.size(); ++a) {
+            const int w = width_of((uint8_t)types[a]);
+            c.cols[a].resize((size_t)c.n * w);
+            HIPCHECK(hipMemcpy(c.cols[a].data(), (const uint8_t*)S.cols[a].p + (size_t)c.stage_off * w, (size_t)c.n * w,
+                               hipMemcpyDeviceToHost));
+            if (S.has_nulls[a]) {
+                c.nulls[a].resize((size_t)c.n);
+                HIPCHECK(hipMemcpy(c.nulls[a].data(), (const uint8_t*)S.nulls[a].p + c.stage_off, (size_t)c.n,
+                                   hipMemcpyDeviceToHost));
+            }
+        }
+        c.device = false;
+        c.stage_off = -1;
+        e->host_pending[c.stream] = 1;
+    }
+}
+
 bool stage_push(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const void* const* cols,
                 const uint8_t* const* nulls, PushChunk& c) {
-    if (e->compile_only || getenv("SDG_NO_STAGE") || stream >= (int)e->stage_ok.size() || !e->stage_ok[stream]) return false;
+    if (e->compile_only || e->no_stage || getenv("SDG_NO_STAGE") || stream >= (int)e->stage_ok.size() ||
+        !e->stage_ok[stream] || e->host_pending[stream])
+        return false;
     const auto& types = e->stream_types[stream];
     for (auto& qp : e->qs) {  // null partition keys are dropped by the host path (PartitionStreamReceiver :262-272)
         const HostQuery& h = qp->hq;
@@ -2716,7 +2758,11 @@ bool stage_push(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const v
         const int ai = h.key_attr[qpos];
         if (ai >= 0 && nulls && nulls[ai])
             for (int64_t r = 0; r < n; ++r)
-                if (nulls[ai][r]) return false;
+                if (nulls[ai][r]) {
+                    unstage(e, stream);  // this push goes to the host: so do the stream's earlier ones
+                    e->host_pending[stream] = 1;
+                    return false;
+                }
     }
     for (size_t a = 0; a < types.size(); ++a)
         if (!cols[a]) throw std::invalid_argument("missing column");
@@ -2838,6 +2884,10 @@ int sdg_push_mixed(sdg_engine* e, int64_t n, const int32_t* streams, const int64
                    const int64_t* const* slots, const uint8_t* const* nulls) {
     if (!e || n < 0 || (n > 0 && (!ts || !streams || !slots)) || n_attrs < 0) return fail(SDG_ERR_ARG, "bad push arguments");
     return guarded([&]() {
+        if (!e->no_stage) {  // rows of several streams per push: host assembly from here on
+            unstage(e, -1);
+            e->no_stage = true;
+        }
         PushChunk c;
         c.stream = -2;
         c.n = n;
