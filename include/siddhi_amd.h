@@ -91,6 +91,11 @@ int sdg_stream_schema(sdg_engine* e, int stream, int32_t* n_attrs, const int32_t
 int sdg_num_queries(sdg_engine* e);
 /* device path chosen for a query: 0 = chain kernel (independent partials), 1 = generic keyed NFA */
 int sdg_query_path(sdg_engine* e, int query);
+/* what a multi-GPU deployment needs to know about a query (siddhi_amd/shard.py ShardedAppRuntime): */
+#define SDG_Q_PARTITIONED 1    /* partition with (...): keys are independent, the query shards by key hash */
+#define SDG_Q_TIMERS 2         /* absent states: the reference's Scheduler collapses due timers across ALL keys
+                                  (Scheduler.java:75-98), so key shards on different GPUs would change the result */
+int sdg_query_flags(sdg_engine* e, int query);
 const char* sdg_query_name(sdg_engine* e, int query);
 const char* sdg_query_target(sdg_engine* e, int query);
 int sdg_query_output_schema(sdg_engine* e, int query, int32_t* n_attrs, const int32_t** types,

@@ -114,6 +114,7 @@ def load_library():
     L.sdg_stream_schema.argtypes = [P, I32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.POINTER(ctypes.c_int32))]
     L.sdg_num_queries.argtypes = [P]
     L.sdg_query_path.argtypes = [P, I32]
+    L.sdg_query_flags.argtypes = [P, I32]
     L.sdg_query_name.restype = ctypes.c_char_p
     L.sdg_query_name.argtypes = [P, I32]
     L.sdg_query_target.restype = ctypes.c_char_p
@@ -224,6 +225,7 @@ class SiddhiAppRuntime:
                      (1 if compile_only else 0) | (2 if force_generic else 0) | (0 if fused else 4))
         _check(L.sdg_compile(app_text.encode(), ctypes.byref(opts), ctypes.byref(h)))
         self._h = h
+        self._compile_only = compile_only
         self.playback = "@app:playback" in app_text.replace(" ", "").lower()
         import re as _re
         m = _re.search(r"@app:name\(\s*['\"]([^'\"]*)['\"]", app_text)
@@ -266,7 +268,8 @@ class SiddhiAppRuntime:
     def shutdown(self):
         if self._h:
             try:
-                self.flush()
+                if not self._compile_only:
+                    self.flush()
             finally:
                 self._L.sdg_destroy(self._h)
                 self._h = None
@@ -280,6 +283,10 @@ class SiddhiAppRuntime:
             pass
 
     # --- engine ----------------------------------------------------------------------------------------
+    def query_flags(self):
+        """per query: SDG_Q_PARTITIONED (1) | SDG_Q_TIMERS (2)"""
+        return [self._L.sdg_query_flags(self._h, q) for q in range(len(self._queries))]
+
     def query_paths(self):
         """device path per query: 0 chain kernel, 1 generic keyed NFA"""
         return [self._L.sdg_query_path(self._h, q) for q in range(len(self._queries))]

@@ -146,6 +146,10 @@ struct PushChunk {
     // a host push staged in HBM at push time (device == true): its rows are [stage_off, stage_off + n) of the
     // engine's staging columns of its stream; d_ts / d_cols / d_nulls are resolved when the flush starts
     int64_t stage_off = -1;
+    // a mixed chunk's raw rows in HBM (uploaded at the first flush that builds a query view from them on the device)
+    bool m_up = false;
+    DevBuf m_streams, m_ts, m_slots, m_nulls;
+    std::vector<char> m_has_null;
 };
 
 // the device staging of one stream's host pushes (sdg_push / sdg_push_events): columns appended in push order, so
@@ -253,6 +257,7 @@ struct QueryRt {
     std::vector<std::unique_ptr<KeyRun>> runs;
     // batch staging
     DevBuf st_ts, st_qs, st_key, st_vrank, st_cols[MAX_COLS], st_nulls[MAX_COLS];
+    DevBuf mv_work, mv_tot, mv_args, kt_vals_in;  // device-side views of mixed pushes
     // sorted view
     DevBuf so_ts, so_qs, so_key, so_orig, so_vrank, so_cols[MAX_COLS], so_nulls[MAX_COLS], seg, kg_counts, kg_gsum;
     DevBuf bk_plan;                                 // fused path: bstart[257] + bseg[257]
@@ -544,6 +549,124 @@ void chain_staging(const HostQuery& h, ChainArgs& a, bool carry_nullable) {
     const FastPred& f0 = P.fast[0];
     a.f0_on_x = f0.kind == FP_CONST && f0.sa == 0 && (f0.ia == 0 || f0.ia == -1) && f0.ca == sp.scan_col &&
                 f0.ka == sp.scan_col_kind;
+}
+
+// the batch view of a query whose rows all come from mixed pushes, built on the device (ingest.hip): each chunk's
+// raw rows go to HBM once per flush, then a stable compaction writes the query's view rows (its streams, null keys
+// dropped), physical columns, stream positions, batch positions and key values. Returns the view's row count.
+int64_t mixed_view(sdg_engine* e, QueryRt& q, const std::vector<const PushChunk*>& parts,
+                   const std::vector<int64_t>& part_pos, int64_t n, const int64_t** d_ts, const uint8_t** d_qs,
+                   const void** d_cols, const uint8_t** d_nulls, const uint32_t** d_vpos) {
+    const HostQuery& h = q.hq;
+    const Plan& P = h.plan;
+    hipStream_t st = e->stream;
+    const int nc = P.n_cols;
+    const bool multi = h.streams.size() > 1;
+    MixedViewArgs proto;
+    std::memset(&proto, 0, sizeof proto);
+    for (int s2 = 0; s2 < MV_MAX_STREAMS; ++s2) proto.qpos[s2] = -1;
+    for (size_t i = 0; i < h.streams.size(); ++i) proto.qpos[h.streams[i]] = (int8_t)i;
+    proto.partitioned = P.partitioned;
+    for (size_t i = 0; i < h.streams.size(); ++i) {
+        proto.key_attr[i] = P.partitioned ? h.key_attr[i] : -1;
+        proto.key_kind[i] = P.partitioned ? h.key_kind[i] : 0;
+        for (int k = 0; k < nc; ++k) proto.col_attr[i][k] = (int8_t)h.col_attr[i][k];
+    }
+    proto.n_cols = nc;
+    for (int k = 0; k < nc; ++k) proto.col_width[k] = (uint8_t)width_of(P.col_kind[k]);
+    // raw rows to HBM (once per chunk and flush) and the per-chunk view row counts
+    std::vector<MixedViewArgs> args(parts.size(), proto);
+    bool col_null[MAX_COLS] = {};
+    size_t wsz = 0;
+    for (const PushChunk* pc : parts) wsz = std::max(wsz, mixed_view_workspace(pc->n));
+    uint8_t* work = (uint8_t*)q.mv_work.ensure(parts.size() * ((wsz + 255) & ~(size_t)255) + 256);
+    int64_t* d_tot = (int64_t*)q.mv_tot.ensure(parts.size() * 8 + 8);
+    MixedViewArgs* d_args = (MixedViewArgs*)q.mv_args.ensure(parts.size() * sizeof(MixedViewArgs));
+    for (size_t pi = 0; pi < parts.size(); ++pi) {
+        PushChunk& c = const_cast<PushChunk&>(*parts[pi]);
+        const int na = (int)c.cols.size();
+        if (!c.m_up) {
+            c.m_streams.ensure((size_t)c.n * 4);
+            c.m_ts.ensure((size_t)c.n * 8);
+            c.m_slots.ensure((size_t)std::max(na, 1) * c.n * 8);
+            HIPCHECK(hipMemcpyAsync(c.m_streams.p, c.rstream.data(), (size_t)c.n * 4, hipMemcpyHostToDevice, st));
+            HIPCHECK(hipMemcpyAsync(c.m_ts.p, c.ts.data(), (size_t)c.n * 8, hipMemcpyHostToDevice, st));
+            for (int a = 0; a < na; ++a)
+                HIPCHECK(hipMemcpyAsync((int64_t*)c.m_slots.p + (size_t)a * c.n, c.cols[a].data(), (size_t)c.n * 8,
+                                        hipMemcpyHostToDevice, st));
+            c.m_has_null.assign(na, 0);
+            int nn = 0;
+            for (int a = 0; a < na; ++a)
+                if (!c.nulls[a].empty())
+                    for (int64_t r = 0; r < c.n && !c.m_has_null[a]; ++r) c.m_has_null[a] = c.nulls[a][r] != 0;
+            for (int a = 0; a < na; ++a) nn += c.m_has_null[a];
+            if (nn) {
+                c.m_nulls.ensure((size_t)na * c.n);
+                for (int a = 0; a < na; ++a)
+                    if (c.m_has_null[a])
+                        HIPCHECK(hipMemcpyAsync((uint8_t*)c.m_nulls.p + (size_t)a * c.n, c.nulls[a].data(), (size_t)c.n,
+                                                hipMemcpyHostToDevice, st));
+            }
+            c.m_up = true;
+        }
+        MixedViewArgs& a = args[pi];
+        a.n = c.n;
+        a.pos0 = part_pos[pi];
+        a.streams = c.m_streams.as<int32_t>();
+        a.ts = c.m_ts.as<int64_t>();
+        for (int x = 0; x < na; ++x) {
+            a.slots[x] = c.m_slots.as<int64_t>() + (size_t)x * c.n;
+            a.slot_nulls[x] = c.m_has_null[x] ? (const uint8_t*)c.m_nulls.p + (size_t)x * c.n : nullptr;
+        }
+        for (size_t i = 0; i < h.streams.size(); ++i)
+            for (int k = 0; k < nc; ++k) {
+                const int ai = h.col_attr[i][k];
+                if (ai >= 0 && ai < na && c.m_has_null[ai]) col_null[k] = true;
+            }
+    }
+    HIPCHECK(hipMemcpyAsync(d_args, args.data(), parts.size() * sizeof(MixedViewArgs), hipMemcpyHostToDevice, st));
+    for (size_t pi = 0; pi < parts.size(); ++pi)
+        mixed_view_count(args[pi], d_args + pi, work + pi * ((wsz + 255) & ~(size_t)255), d_tot + pi, st);
+    std::vector<int64_t> tot(parts.size());
+    HIPCHECK(hipMemcpyAsync(tot.data(), d_tot, parts.size() * 8, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    int64_t rows = 0;
+    for (int64_t t : tot) rows += t;
+    const size_t cnt = (size_t)std::max<int64_t>(rows, 1);
+    int64_t* ots = (int64_t*)q.st_ts.ensure(cnt * 8);
+    uint32_t* opos = (uint32_t*)q.d_vpos.ensure(cnt * 4);
+    uint8_t* oqs = multi ? (uint8_t*)q.st_qs.ensure(cnt) : nullptr;
+    int64_t* okey = P.partitioned ? (int64_t*)q.kt_vals_in.ensure(cnt * 8) : nullptr;
+    for (int k = 0; k < nc; ++k) {
+        d_cols[k] = q.st_cols[k].ensure(cnt * width_of(P.col_kind[k]));
+        d_nulls[k] = col_null[k] ? (const uint8_t*)q.st_nulls[k].ensure(cnt) : nullptr;
+    }
+    int64_t o = 0;
+    for (size_t pi = 0; pi < parts.size(); ++pi) {
+        MixedViewArgs& a = args[pi];
+        a.out_ts = ots + o;
+        a.out_pos = opos + o;
+        a.out_qs = oqs ? oqs + o : nullptr;
+        a.out_key = okey ? okey + o : nullptr;
+        for (int k = 0; k < nc; ++k) {
+            a.out_cols[k] = (uint8_t*)d_cols[k] + (size_t)o * width_of(P.col_kind[k]);
+            a.out_nulls[k] = d_nulls[k] ? (uint8_t*)d_nulls[k] + o : nullptr;
+        }
+        o += tot[pi];
+    }
+    HIPCHECK(hipMemcpyAsync(d_args, args.data(), parts.size() * sizeof(MixedViewArgs), hipMemcpyHostToDevice, st));
+    for (size_t pi = 0; pi < parts.size(); ++pi)
+        mixed_view_write(args[pi], d_args + pi, work + pi * ((wsz + 255) & ~(size_t)255), st);
+    if (P.partitioned && q.string_keys && rows > 0) {  // string ids are the key ids
+        uint32_t* k32 = (uint32_t*)q.st_key.ensure(cnt * 4);
+        narrow_u32(okey, rows, k32, st);
+    }
+    HIPCHECK(hipStreamSynchronize(st));  // (args / totals are host vectors)
+    *d_ts = ots;
+    *d_qs = oqs;
+    *d_vpos = opos;
+    (void)n;
+    return rows;
 }
 
 // A chain query moving to the generic NFA: its carried partials (e1 events still pending at the end of the last
@@ -874,6 +997,19 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             else d_key = device_key_ids(e, q, c.d_cols[ai], h.key_kind[qpos], n);
         }
         nrows = n;
+    }
+    // mixed pushes only (C4's interleaved streams): the view is built on the device from the raw slot rows
+    bool dev_mixed = !zero_copy && !parts.empty() && !ranged && !getenv("SDG_NO_DEVMIX") &&
+                     (!partitioned || q.string_keys || q.key_class != KC_NONE) &&
+                     e->stream_types.size() <= (size_t)MV_MAX_STREAMS;
+    for (const PushChunk* c : parts) dev_mixed &= c->stream == -2 && !c->device && c->cols.size() <= (size_t)MV_MAX_ATTRS;
+    if (dev_mixed) {
+        nrows = mixed_view(e, q, parts, part_pos, n, &d_ts, &d_qs, d_cols, d_nulls, &d_vpos);
+        if (partitioned) {
+            if (q.string_keys) d_key = q.st_key.as<uint32_t>();
+            else d_key = device_key_ids(e, q, q.kt_vals_in.as<int64_t>(), VK_I64, nrows);
+        }
+    } else if (zero_copy) {
     } else {
         // assemble on the host (host chunks) / device-to-device (device chunks)
         std::vector<int64_t> ts;
@@ -1941,6 +2077,36 @@ void drain(sdg_engine* e, QueryRt& q) {
         HIPCHECK(hipMemcpyAsync(vals + (size_t)j * n, src_vals + (size_t)j * vstride, n * 8, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
     if (!q.nulls_valid) std::memset(nulls, 0, (size_t)n * 4);
+    // records already in delivery order on the device, nothing to drop, rank or aggregate: the columns join the
+    // backlog as they are (a memcpy per column instead of a per-record walk)
+    if (dev_order && !post && q.runs.empty()) {
+        const int nu = q.hq.plan.n_user_out + q.hq.plan.n_list_cols;
+        const size_t b = q.acc_ts.size();
+        q.acc_ts.resize(b + n);
+        q.acc_seq.resize(b + n);
+        std::memcpy(q.acc_ts.data() + b, ts, (size_t)n * 8);
+        std::memcpy(q.acc_seq.data() + b, emit, (size_t)n * 8);
+        q.acc_vals.resize(nu);
+        q.acc_nulls.resize(nu);
+        for (int j = 0; j < nu; ++j) {
+            q.acc_vals[j].resize(b + n);
+            std::memcpy(q.acc_vals[j].data() + b, vals + (size_t)j * n, (size_t)n * 8);
+            q.acc_nulls[j].resize(b + n);
+            uint8_t* dn = q.acc_nulls[j].data() + b;
+            if (q.nulls_valid)
+                for (int64_t i = 0; i < n; ++i) dn[i] = (nulls[i] >> j) & 1u;
+            else
+                std::memset(dn, 0, (size_t)n);
+        }
+        for (int j = 0; j < q.hq.plan.n_user_out; ++j)  // OP_SLOTLEN counted to cap + 1: a longer chain
+            if (q.hq.plan.out_multi[j])
+                for (int64_t i = 0; i < n; ++i)
+                    if (q.acc_vals[j][b + i] > q.hq.plan.out_list_cap[j])
+                        throw CompileError(SDG_ERR_CAPACITY, "query '" + q.hq.name + "': a multi-value selection holds "
+                                                             "more than " + std::to_string(q.hq.plan.out_list_cap[j]) +
+                                                             " events");
+        return;
+    }
     // the host replays' records join the device's (same layout, after them)
     int64_t nh = 0;
     for (auto& r : q.runs) nh += (int64_t)r->count;
@@ -2681,6 +2847,11 @@ int sdg_stream_schema(sdg_engine* e, int s, int32_t* n, const int32_t** types) {
 }
 
 int sdg_num_queries(sdg_engine* e) { return e ? (int)e->qs.size() : 0; }
+int sdg_query_flags(sdg_engine* e, int q) {
+    if (!e || q < 0 || q >= (int)e->qs.size()) return -1;
+    const Plan& P = e->qs[q]->hq.plan;
+    return (P.partitioned ? SDG_Q_PARTITIONED : 0) | (P.n_sched > 0 ? SDG_Q_TIMERS : 0);
+}
 int sdg_query_path(sdg_engine* e, int q) {
     if (!e || q < 0 || q >= (int)e->qs.size()) return -1;
     return e->qs[q]->hq.plan.chain ? 0 : 1;

@@ -325,6 +325,37 @@ void select_post(SelPostArgs a, const uint32_t* key, int kbits, void* work, hipS
 // keys flagged in flags[K] (purged after their last record): aggregator states zeroed, flags cleared
 void agg_reset(int64_t* agg_state, int n_agg, uint8_t* flags, int64_t K, hipStream_t stream);
 
+// ---- device-side batch view of mixed pushes (ingest.hip) ------------------------------------------------------
+constexpr int MV_MAX_STREAMS = 64;
+constexpr int MV_MAX_ATTRS = 64;
+struct MixedViewArgs {
+    int64_t n;                                // rows of the mixed chunk
+    int64_t pos0;                             // batch position of its row 0
+    const int32_t* streams;                   // [n] app stream of each row
+    const int64_t* ts;                        // [n]
+    const int64_t* slots[MV_MAX_ATTRS];       // [attr][n] 64-bit slots (sdg_push_mixed)
+    const uint8_t* slot_nulls[MV_MAX_ATTRS];  // [attr][n] or nullptr
+    int8_t qpos[MV_MAX_STREAMS];              // app stream -> the query's stream position (-1: not read)
+    int32_t partitioned;
+    int32_t key_attr[MAX_STATES];             // [query stream] partition key attribute
+    uint8_t key_kind[MAX_STATES];
+    int32_t n_cols;
+    int8_t col_attr[MAX_STATES][MAX_COLS];    // [query stream][physical column] attribute or -1
+    uint8_t col_width[MAX_COLS];
+    // outputs: the query's view rows of this chunk (arrival order)
+    int64_t* out_ts;
+    uint32_t* out_pos;                        // batch position
+    uint8_t* out_qs;                          // query stream position (nullptr: single stream)
+    int64_t* out_key;                         // key value (key table encoding; string ids) if partitioned
+    void* out_cols[MAX_COLS];
+    uint8_t* out_nulls[MAX_COLS];             // nullptr: no null possible in the column
+};
+size_t mixed_view_workspace(int64_t n);
+// the chunk's view row count into *d_total (device); then the rows (work must be kept between the two calls)
+void mixed_view_count(const MixedViewArgs& a, const MixedViewArgs* d_a, void* work, int64_t* d_total, hipStream_t st);
+void mixed_view_write(const MixedViewArgs& a, const MixedViewArgs* d_a, void* work, hipStream_t st);
+void narrow_u32(const int64_t* src, int64_t n, uint32_t* dst, hipStream_t st);
+
 // device partition key table for integral partition attributes (keytab.hip): value -> dense key id
 struct KeyTab {
     int64_t* keys;    // [cap + 1]

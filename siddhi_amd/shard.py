@@ -112,3 +112,46 @@ def ordered_gather(dist, rank, world, cols, key_names):
     if merged is None:
         return {k: mine[k] for k in names}
     return merged
+
+
+Q_PARTITIONED, Q_TIMERS = 1, 2
+
+
+class ShardedAppRuntime:
+    """One rank's share of a Siddhi app on an N-GPU node: partitioned queries are key-hash sharded
+    (rank r processes the events whose partition key hashes to r, `owner`), unpartitioned queries run as replicas
+    on rank 0. N > 1 is refused with OperationNotSupportedException for queries with absent states: the reference's
+    Scheduler collapses the due timers of ALL partition keys into one TreeMultimap per clock advance
+    (Scheduler.java:75-98, only the first state per due time fires), so which fires it delays depends on keys that
+    would live on other GPUs -- sharding them would silently change the matches (7,857 vs 9,790).
+    Such an app runs on one GPU (world 1), where the engine reproduces the collapse exactly."""
+
+    def __init__(self, app_text, rank, world, device=0, key_attr=None, **kw):
+        import siddhi_amd as sa
+        self.rank, self.world = rank, world
+        self.rt = sa.SiddhiAppRuntime(app_text, device=device, **kw)
+        flags = self.rt.query_flags()
+        if world > 1 and any(f & Q_TIMERS for f in flags):
+            names = [q[0] for q, f in zip(self.rt._queries, flags) if f & Q_TIMERS]
+            self.rt.shutdown()
+            raise sa.OperationNotSupportedException(
+                "queries %s have absent states: the reference's scheduler orders timers across all partition keys "
+                "(Scheduler.java:75-98), so they cannot be key-sharded over %d GPUs; run the app on one GPU" % (names, world))
+        self.sharded = all(f & Q_PARTITIONED for f in flags)
+        self.replica = not self.sharded  # an unpartitioned query: every event, on rank 0 only
+        self.key_attr = key_attr or {}    # stream id -> index of its partition attribute
+
+    def mine(self, stream_id, row):
+        """whether this rank processes the event"""
+        if self.world == 1:
+            return True
+        if self.replica:
+            return self.rank == 0
+        return owner(row[self.key_attr[stream_id]], self.world) == self.rank
+
+    def send(self, stream_id, ts, row):
+        if self.mine(stream_id, row):
+            self.rt.getInputHandler(stream_id).send(ts, row)
+
+    def shutdown(self):
+        self.rt.shutdown()

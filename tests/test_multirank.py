@@ -107,3 +107,24 @@ def test_merge_runs_is_a_stable_g_way_merge():
     order = shard.lexsort([cat["k"], cat["run"], cat["i"]])
     for c in cat:
         assert torch.equal(m[c], cat[c][..., order]), c
+
+
+def test_sharded_runtime_refuses_absent_states_at_n_gt_1():
+    """N > 1 semantics for absent queries: refused, because the reference's scheduler collapse is
+    global across keys; the same app on one GPU is accepted"""
+    import siddhi_amd as sa
+    from siddhi_amd import workloads as w
+    flags = sa.SiddhiAppRuntime(w.C4_APP, compile_only=True).query_flags()
+    assert flags == [shard.Q_PARTITIONED | shard.Q_TIMERS]
+    assert sa.SiddhiAppRuntime(w.C2_APP, compile_only=True).query_flags() == [shard.Q_PARTITIONED]
+    assert sa.SiddhiAppRuntime(w.C1_APP, compile_only=True).query_flags() == [0]
+    with pytest.raises(sa.OperationNotSupportedException):
+        shard.ShardedAppRuntime(w.C4_APP, 0, 2, compile_only=True)
+    rt = shard.ShardedAppRuntime(w.C4_APP, 0, 1, compile_only=True)
+    assert rt.sharded
+    s2 = shard.ShardedAppRuntime(w.C2_APP, 1, 4, compile_only=True, key_attr={"StockStream": 1})
+    keys = ["S%05d" % k for k in range(2000)]
+    mine = [k for k in keys if s2.mine("StockStream", [0, k, 1.0, 1])]
+    assert mine == [k for k in keys if shard.owner(k, 4) == 1]
+    r1 = shard.ShardedAppRuntime(w.C1_APP, 1, 2, compile_only=True)
+    assert r1.replica and not r1.mine("StockStream", [0, "IBM", 1.0, 1])
