@@ -53,6 +53,8 @@ for s in "$@"; do
         c3mdprof) run c3mdprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/c3mdprof" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 1 --warmup 1 ;;
         churn) run churn 600 python3 -u -m pytest tests/test_gpu_churn.py -m gpu -x -v -s --timeout 500 --timeout-method thread -p no:cacheprovider ;;
         ldssweep) for b in 36864 18432 12288 9216 6144 3072; do run lds$b 300 env SDG_NFA_LDS=$b python3 scripts/bench_configs.py --only c3md,c2generic --c3-steps 1 --warmup 1; done; grep -h "^{" $OUT/lds*.log ;;
+        mixed) run mixed 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_select.py tests/test_gpu_snapshot.py tests/test_gpu_robust.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "c4 or absent or Absent or snapshot or select or failed or corrupt or mixed" ;;
+        c4b) run c4b 600 python3 scripts/bench_configs.py --only c4 && run c4bhost 600 env SDG_NO_DEVMIX=1 python3 scripts/bench_configs.py --only c4 ;;
         *) echo "unknown step $s" ;;
     esac
 done
