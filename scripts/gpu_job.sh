@@ -55,6 +55,7 @@ for s in "$@"; do
         ldssweep) for b in 36864 18432 12288 9216 6144 3072; do run lds$b 300 env SDG_NFA_LDS=$b python3 scripts/bench_configs.py --only c3md,c2generic --c3-steps 1 --warmup 1; done; grep -h "^{" $OUT/lds*.log ;;
         mixed) run mixed 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_select.py tests/test_gpu_snapshot.py tests/test_gpu_robust.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "c4 or absent or Absent or snapshot or select or failed or corrupt or mixed" ;;
         c4b) run c4b 600 python3 scripts/bench_configs.py --only c4 && run c4bhost 600 env SDG_NO_DEVMIX=1 python3 scripts/bench_configs.py --only c4 ;;
+        c5lane) run c5a 600 python3 bench.py --config c5 --c5-shard 0/8 --steps 3 --warmup 1 --no-parity --no-gather && run c5b 600 env SDG_CARRY_LANE=1 python3 bench.py --config c5 --c5-shard 0/8 --steps 3 --warmup 1 --no-parity --no-gather; grep -h "^{" $OUT/c5a.log $OUT/c5b.log | python3 -c "import json,sys; [print(json.loads(l)['ms_per_step'], json.loads(l)['roofline']['kernel_ms']) for l in sys.stdin]" ;;
         *) echo "unknown step $s" ;;
     esac
 done
