@@ -58,6 +58,8 @@ for s in "$@"; do
         c5lane) run c5a 600 python3 bench.py --config c5 --c5-shard 0/8 --steps 3 --warmup 1 --no-parity --no-gather && run c5b 600 env SDG_CARRY_LANE=1 python3 bench.py --config c5 --c5-shard 0/8 --steps 3 --warmup 1 --no-parity --no-gather; grep -h "^{" $OUT/c5a.log $OUT/c5b.log | python3 -c "import json,sys; [print(json.loads(l)['ms_per_step'], json.loads(l)['roofline']['kernel_ms']) for l in sys.stdin]" ;;
         pmc2) i=0; for c in "FETCH_SIZE" "WRITE_SIZE"; do i=$((i+1)); run pmc$i 180 rocprofv3 --pmc $c --kernel-trace -d "$OUT/pmc$i" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-parity --no-gather --e2e-steps 0; done ;;
         c3pmc2) i=0; for c in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_INSTS_FLAT SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS"; do i=$((i+1)); run c3pmc$i 180 rocprofv3 --pmc $c --kernel-trace -d "$OUT/c3pmc$i" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 1 --warmup 0; done ;;
+        ldsconf) run ldsconf 180 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace -d "$OUT/ldsconf" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 1 --warmup 0 ;;
+        c5) run c5 600 python3 bench.py --config c5 --c5-shard 0/8 --steps 3 --warmup 1 --no-gather ;;
         *) echo "unknown step $s" ;;
     esac
 done

@@ -536,9 +536,10 @@ class SiddhiAppRuntime:
                 for cb in self._callbacks.get(target, []):
                     cb.receive([ev])
 
-    def poll_arrays(self, q):
-        """numpy view of one poll: (ts[n], values[n_attrs][n] int64 payloads, nulls[n_attrs][n], event_seq[n]);
-        copies, so they stay valid after the next poll"""
+    def poll_arrays(self, q, copy=True):
+        """numpy arrays of one poll: (ts[n], values[n_attrs][n] int64 payloads, nulls[n_attrs][n], event_seq[n]);
+        copy=True: copies, valid after the next poll; copy=False: views of the engine's poll buffers (sdg_poll's
+        contract: valid until the next sdg_poll of this query), values / nulls as lists of per-attribute arrays"""
         import numpy as np
         out = _Out()
         _check(self._L.sdg_poll(self._h, q, ctypes.byref(out)))
@@ -546,6 +547,11 @@ class SiddhiAppRuntime:
         if n == 0:
             z = np.zeros(0, np.int64)
             return z, np.zeros((na, 0), np.int64), np.zeros((na, 0), np.uint8), z
+        if not copy:
+            return (np.ctypeslib.as_array(out.ts, (n,)),
+                    [np.ctypeslib.as_array(out.values[j], (n,)) for j in range(na)],
+                    [np.ctypeslib.as_array(out.nulls[j], (n,)) for j in range(na)],
+                    np.ctypeslib.as_array(out.event_seq, (n,)))
         ts = np.ctypeslib.as_array(out.ts, (n,)).copy()
         seq = np.ctypeslib.as_array(out.event_seq, (n,)).copy()
         vals = np.stack([np.ctypeslib.as_array(out.values[j], (n,)).copy() for j in range(na)]) if na else \

@@ -20,6 +20,7 @@
 #include "../siddhiql/parser.h"
 #include "compile.h"
 #include "keyrun.h"
+#include "hostpar.h"
 #include "sched.h"
 
 namespace sdg {
@@ -289,15 +290,16 @@ struct QueryRt {
     bool carry_nullable = false;                    // the carried partials came from a batch with null columns
     // delivered rows not yet polled, in delivery order (drain(): an auto-flush inside sdg_push, or several
     // sdg_flush calls before one sdg_poll, keep appending here -- never overwritten)
-    std::vector<int64_t> acc_ts, acc_seq;
-    std::vector<std::vector<int64_t>> acc_vals;
-    std::vector<std::vector<uint8_t>> acc_nulls;
+    // (acc_* and h_* swap at each poll, so their columns keep their capacity from poll to poll)
+    HostVec<int64_t> acc_ts, acc_seq;
+    std::vector<HostVec<int64_t>> acc_vals;
+    std::vector<HostVec<uint8_t>> acc_nulls;
     HostPin h_rb;                                   // pinned read-back staging
     // host copies for sdg_poll
-    std::vector<int64_t> h_ts, h_seq;
-    std::vector<uint8_t> h_expired;
-    std::vector<std::vector<int64_t>> h_vals;
-    std::vector<std::vector<uint8_t>> h_nulls;
+    HostVec<int64_t> h_ts, h_seq;
+    HostVec<uint8_t> h_expired;
+    std::vector<HostVec<int64_t>> h_vals;
+    std::vector<HostVec<uint8_t>> h_nulls;
     std::vector<const int64_t*> h_vptr;
     std::vector<const uint8_t*> h_nptr;
 };
@@ -337,6 +339,8 @@ struct sdg_engine {
     std::vector<char> stage_ok;  // per stream: every query of the stream takes device-resident batches
     std::vector<char> host_pending;  // per stream: the pending batch holds host rows of it (no staging until flush)
     bool no_stage = false;       // mixed pushes seen: host assembly for every stream from then on
+    HostPin bounce[2];           // pinned chunks of the pageable host -> HBM copies (h2d)
+    hipEvent_t bounce_ev[2] = {};
 };
 
 namespace {
@@ -2076,7 +2080,6 @@ void drain(sdg_engine* e, QueryRt& q) {
     for (int j = 0; j < na; ++j)
         HIPCHECK(hipMemcpyAsync(vals + (size_t)j * n, src_vals + (size_t)j * vstride, n * 8, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
-    if (!q.nulls_valid) std::memset(nulls, 0, (size_t)n * 4);
     // records already in delivery order on the device, nothing to drop, rank or aggregate: the columns join the
     // backlog as they are (a memcpy per column instead of a per-record walk)
     if (dev_order && !post && q.runs.empty()) {
@@ -2084,19 +2087,21 @@ void drain(sdg_engine* e, QueryRt& q) {
         const size_t b = q.acc_ts.size();
         q.acc_ts.resize(b + n);
         q.acc_seq.resize(b + n);
-        std::memcpy(q.acc_ts.data() + b, ts, (size_t)n * 8);
-        std::memcpy(q.acc_seq.data() + b, emit, (size_t)n * 8);
+        par_memcpy(q.acc_ts.data() + b, ts, (size_t)n * 8);
+        par_memcpy(q.acc_seq.data() + b, emit, (size_t)n * 8);
         q.acc_vals.resize(nu);
         q.acc_nulls.resize(nu);
         for (int j = 0; j < nu; ++j) {
             q.acc_vals[j].resize(b + n);
-            std::memcpy(q.acc_vals[j].data() + b, vals + (size_t)j * n, (size_t)n * 8);
+            par_memcpy(q.acc_vals[j].data() + b, vals + (size_t)j * n, (size_t)n * 8);
             q.acc_nulls[j].resize(b + n);
             uint8_t* dn = q.acc_nulls[j].data() + b;
             if (q.nulls_valid)
-                for (int64_t i = 0; i < n; ++i) dn[i] = (nulls[i] >> j) & 1u;
+                par_range(n, 1 << 20, [&](int64_t lo, int64_t hi) {
+                    for (int64_t i = lo; i < hi; ++i) dn[i] = (nulls[i] >> j) & 1u;
+                });
             else
-                std::memset(dn, 0, (size_t)n);
+                par_range(n, 16 << 20, [&](int64_t lo, int64_t hi) { std::memset(dn + lo, 0, (size_t)(hi - lo)); });
         }
         for (int j = 0; j < q.hq.plan.n_user_out; ++j)  // OP_SLOTLEN counted to cap + 1: a longer chain
             if (q.hq.plan.out_multi[j])
@@ -2107,6 +2112,7 @@ void drain(sdg_engine* e, QueryRt& q) {
                                                              " events");
         return;
     }
+    if (!q.nulls_valid) std::memset(nulls, 0, (size_t)n * 4);
     // the host replays' records join the device's (same layout, after them)
     int64_t nh = 0;
     for (auto& r : q.runs) nh += (int64_t)r->count;
@@ -2808,6 +2814,8 @@ void sdg_destroy(sdg_engine* e) {
     e->qs.clear();
     for (auto& ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
+    for (auto& ev : e->bounce_ev)
+        if (ev) (void)hipEventDestroy(ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
@@ -2916,6 +2924,31 @@ void unstage(sdg_engine* e, int stream) {
     }
 }
 
+// a pageable host buffer into HBM on the engine's stream: large ones through two pinned chunks, the threads' copy
+// of chunk i+1 overlapping the DMA of chunk i (the runtime's pageable path copies on one thread). The source is
+// free when the stream has caught up.
+void h2d(sdg_engine* e, void* dst, const void* src, size_t bytes) {
+    constexpr size_t CH = (size_t)32 << 20;
+    static const bool direct = getenv("SDG_PAGEABLE") != nullptr;
+    if (bytes < ((size_t)4 << 20) || direct) {
+        HIPCHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->stream));
+        return;
+    }
+    for (int k = 0; k < 2; ++k) {
+        e->bounce[k].ensure(CH);
+        if (!e->bounce_ev[k]) HIPCHECK(hipEventCreateWithFlags(&e->bounce_ev[k], hipEventDisableTiming));
+    }
+    size_t i = 0;
+    for (size_t off = 0; off < bytes; off += CH, ++i) {
+        const int k = (int)(i & 1);
+        const size_t len = std::min(CH, bytes - off);
+        HIPCHECK(hipEventSynchronize(e->bounce_ev[k]));  // the chunk's previous DMA has read it
+        par_memcpy(e->bounce[k].p, (const uint8_t*)src + off, len);
+        HIPCHECK(hipMemcpyAsync((uint8_t*)dst + off, e->bounce[k].p, len, hipMemcpyHostToDevice, e->stream));
+        HIPCHECK(hipEventRecord(e->bounce_ev[k], e->stream));
+    }
+}
+
 bool stage_push(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const void* const* cols,
                 const uint8_t* const* nulls, PushChunk& c) {
     if (e->compile_only || e->no_stage || getenv("SDG_NO_STAGE") || stream >= (int)e->stage_ok.size() ||
@@ -2960,10 +2993,10 @@ bool stage_push(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const v
         S.cap = nc;
     }
     hipStream_t st = e->stream;
-    HIPCHECK(hipMemcpyAsync(S.ts.as<int64_t>() + S.n, ts, (size_t)n * 8, hipMemcpyHostToDevice, st));
+    h2d(e, S.ts.as<int64_t>() + S.n, ts, (size_t)n * 8);
     for (size_t a = 0; a < types.size(); ++a) {
         const int w = width_of((uint8_t)types[a]);
-        HIPCHECK(hipMemcpyAsync((uint8_t*)S.cols[a].p + (size_t)S.n * w, cols[a], (size_t)n * w, hipMemcpyHostToDevice, st));
+        h2d(e, (uint8_t*)S.cols[a].p + (size_t)S.n * w, cols[a], (size_t)n * w);
         bool any = false;
         if (nulls && nulls[a])
             for (int64_t r = 0; r < n && !any; ++r) any = nulls[a][r] != 0;
@@ -2972,7 +3005,7 @@ bool stage_push(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const v
             HIPCHECK(hipMemsetAsync(S.nulls[a].p, 0, (size_t)S.n, st));
             S.has_nulls[a] = 1;
         }
-        if (any) HIPCHECK(hipMemcpyAsync((uint8_t*)S.nulls[a].p + S.n, nulls[a], (size_t)n, hipMemcpyHostToDevice, st));
+        if (any) h2d(e, (uint8_t*)S.nulls[a].p + S.n, nulls[a], (size_t)n);
         else if (S.has_nulls[a]) HIPCHECK(hipMemsetAsync((uint8_t*)S.nulls[a].p + S.n, 0, (size_t)n, st));
     }
     HIPCHECK(hipStreamSynchronize(st));  // the caller's buffers are free when the push returns
@@ -3154,8 +3187,8 @@ int sdg_poll(sdg_engine* e, int qi, sdg_out* out) {
         q.h_nulls.swap(q.acc_nulls);
         q.acc_ts.clear();
         q.acc_seq.clear();
-        q.acc_vals.clear();
-        q.acc_nulls.clear();
+        for (auto& v : q.acc_vals) v.clear();
+        for (auto& v : q.acc_nulls) v.clear();
         q.h_vals.resize(na);
         q.h_nulls.resize(na);
         q.h_expired.assign(n, 0);

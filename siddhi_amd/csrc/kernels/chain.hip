@@ -1367,7 +1367,12 @@ void chain_deque(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
 
 void chain_carry(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
     if (a.cin_n <= 0) return;
-    if (!a.generic && a.sp.scan_mode != SCAN_GENERIC && !getenv("SDG_CARRY_LANE"))
+    // a wave per carried partial pays when its key's rows are many (one key, C1; 10^4 keys, C2: ~10^4 rows each);
+    // with short segments (C5: ~21 rows per key) one lane per partial is 3.7x faster (profiles/r3i_c5_carry_ab.log)
+    static const int force = getenv("SDG_CARRY_LANE") ? 1 : getenv("SDG_CARRY_WAVE") ? 2 : 0;
+    const bool short_segments = a.key && a.K > 0 && a.n <= (int64_t)a.K * 256;
+    const bool lane = force ? force == 1 : short_segments;
+    if (!a.generic && a.sp.scan_mode != SCAN_GENERIC && !lane)
         hipLaunchKernelGGL(chain_carry_wave_k, dim3((unsigned)((a.cin_n + 4 * CW_PER_WAVE - 1) / (4 * CW_PER_WAVE))),
                            dim3(256), 0, stream, d_a);
     else

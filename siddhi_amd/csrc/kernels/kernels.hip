@@ -429,6 +429,12 @@ __global__ __launch_bounds__(256, TM ? 1 : SDG_NFA_MINB) void nfa_k(const NfaArg
 // writes the arenas back, coalesced, into the working copy (double-buffered: the committed copy stays intact until
 // nfa_commit). Concurrency is bounded by LDS (keys in flight per CU = LDS / arena bytes); lanes per wave is sized
 // so that four such waves fit a CU, one per SIMD.
+// Lane stride of the LDS arenas: every lane walks the same arena offsets, so a stride that is a multiple of 256 B
+// (or of 64 B: 4 banks apart) puts the lanes of one wave-instruction on a few of the 64 banks -- r3i's C3 pass
+// counted 1.09e10 SQ_LDS_BANK_CONFLICT cycles against 2.09e9 LDS instructions. A stride of 2 (mod 4) dwords gives
+// the 32 lanes of a ds_read_b64 group 32 distinct bank pairs (the arena code reads 8-byte fields).
+__host__ __device__ __forceinline__ int64_t nfa_lds_stride(int64_t kb) { return ((kb >> 3) & 1) ? kb : kb + 8; }
+
 template <bool TM>
 __global__ __launch_bounds__(64) void nfa_lds_k(const NfaArgs* __restrict__ pa, int lanes) {
     const NfaArgs& a = *pa;
@@ -485,16 +491,17 @@ __global__ __launch_bounds__(64) void nfa_lds_k(const NfaArgs* __restrict__ pa, 
             }
         }
     }
-    const int64_t n16 = kb / 16;
+    const int64_t n8 = kb / 8;
+    const int64_t ks = nfa_lds_stride(kb);
     // stage: the committed arenas of the active keys, one arena per wave instruction sweep (zeros for a key that
     // has none: fresh, or rebuilt from its idle record below)
     for (uint64_t m = __ballot(active); m; m &= m - 1) {
         const int j = __ffsll((unsigned long long)m) - 1;
-        const uint4* s4 = (const uint4*)__shfl((long long)(uintptr_t)src, j);
+        const uint2* s8 = (const uint2*)__shfl((long long)(uintptr_t)src, j);
         const int fj = __shfl((int)from, j);
-        uint4* d4 = (uint4*)(lds_arena + (int64_t)j * kb);
-        if (fj) for (int64_t i = lane; i < n16; i += 64) d4[i] = make_uint4(0, 0, 0, 0);
-        else for (int64_t i = lane; i < n16; i += 64) d4[i] = s4[i];
+        uint2* d8 = (uint2*)(lds_arena + (int64_t)j * ks);
+        if (fj) for (int64_t i = lane; i < n8; i += 64) d8[i] = make_uint2(0, 0);
+        else for (int64_t i = lane; i < n8; i += 64) d8[i] = s8[i];
     }
     __syncthreads();
     bool ovf = false;
@@ -504,7 +511,7 @@ __global__ __launch_bounds__(64) void nfa_lds_k(const NfaArgs* __restrict__ pa, 
         c.code = a.code;
         c.consts = a.consts;
         c.L = a.L;
-        c.base = lds_arena + (int64_t)lane * kb;
+        c.base = lds_arena + (int64_t)lane * ks;
         c.stk = stack_mem + lane;
         c.stride = 64;
         c.emit_ts = a.out_ts;
@@ -542,9 +549,9 @@ __global__ __launch_bounds__(64) void nfa_lds_k(const NfaArgs* __restrict__ pa, 
     // write back into the working copy
     for (uint64_t m = __ballot(active); m; m &= m - 1) {
         const int j = __ffsll((unsigned long long)m) - 1;
-        uint4* d4 = (uint4*)__shfl((long long)(uintptr_t)dst, j);
-        const uint4* s4 = (const uint4*)(lds_arena + (int64_t)j * kb);
-        for (int64_t i = lane; i < n16; i += 64) d4[i] = s4[i];
+        uint2* d8 = (uint2*)__shfl((long long)(uintptr_t)dst, j);
+        const uint2* s8 = (const uint2*)(lds_arena + (int64_t)j * ks);
+        for (int64_t i = lane; i < n8; i += 64) d8[i] = s8[i];
     }
 }
 
@@ -776,7 +783,7 @@ int nfa_lds_lanes(const nfa::Layout& L) {
     if (off) return 0;
     static const char* bud = getenv("SDG_NFA_LDS");  // A/B: LDS bytes per block (wave)
     const int64_t budget = bud ? atoll(bud) : NFA_LDS_BUDGET;
-    const int64_t lanes = budget / L.bytes;
+    const int64_t lanes = budget / nfa_lds_stride(L.bytes);
     return lanes >= NFA_LDS_MIN_LANES ? (int)(lanes < 64 ? lanes : 64) : 0;
 }
 
@@ -786,7 +793,7 @@ void nfa_run(const NfaArgs& a, const NfaArgs* d_a, hipStream_t stream) {
     const int lanes = nfa_lds_lanes(a.L);
     if (lanes > 0) {
         const unsigned grid = (unsigned)((keys + lanes - 1) / lanes);
-        const size_t lds = (size_t)lanes * (size_t)a.L.bytes;
+        const size_t lds = (size_t)lanes * (size_t)nfa_lds_stride(a.L.bytes);
         if (a.T.log) hipLaunchKernelGGL(nfa_lds_k<true>, dim3(grid), dim3(64), lds, stream, d_a, lanes);
         else hipLaunchKernelGGL(nfa_lds_k<false>, dim3(grid), dim3(64), lds, stream, d_a, lanes);
         return;
