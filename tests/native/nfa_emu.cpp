@@ -194,10 +194,14 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
     bool arena_ovf = false;
     auto run_one = [&](uint32_t k, const nfa::TimerFire* fires, int nfires) -> int {
         const int64_t cap = 2 * (seg_e[k] - seg_b[k]) + 4096 + 64 * (int64_t)std::max(nfires, 0);
-        std::vector<int64_t> o_ts(cap), o_vals((size_t)std::max(P.n_out, 1) * cap), o_seq(cap), o_sub(cap);
-        std::vector<uint32_t> o_nulls(cap), o_key(cap);
+        // scratch reused across runs (grow-only: a per-key allocation of the log alone was 2 MB)
+        static std::vector<int64_t> o_ts, o_vals, o_seq, o_sub;
+        static std::vector<uint32_t> o_nulls, o_key;
+        static std::vector<nfa::SchedLog> logs(1 << 16);
+        auto grow = [](auto& v, size_t n) { if (v.size() < n) v.resize(n); };
+        grow(o_ts, cap); grow(o_vals, (size_t)std::max(P.n_out, 1) * cap); grow(o_seq, cap); grow(o_sub, cap);
+        grow(o_nulls, cap); grow(o_key, cap);
         unsigned long long count = 0, lcount = 0;
-        std::vector<nfa::SchedLog> logs(1 << 16);
         int flags[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         nfa::CtxT<true> c;
         c.P = &P;
@@ -341,6 +345,20 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
             r->start(&P, h.code.data(), h.consts.data(), q.L, T, e->seq);
             return r;
         };
+        if (const char* dump = getenv("SDG_SIM_DUMP")) {  // the optimistic pass's inputs (scripts/simbench.cpp)
+            FILE* f = std::fopen(dump, "wb");
+            auto wv = [&](const auto& v) {
+                const uint64_t m = v.size();
+                std::fwrite(&m, 8, 1, f);
+                if (m) std::fwrite(v.data(), sizeof(v[0]), m, f);
+            };
+            const int64_t hdr[6] = {bc.G, bc.clock0, (int64_t)P.n_sched, (int64_t)P.partitioned,
+                                    (int64_t)!e->app.playback, n};
+            std::fwrite(hdr, 8, 6, f);
+            wv(bc.clk); wv(bc.adv); wv(bc.nadv); wv(all); wv(q.key_hash); wv(seg_b); wv(seg_e);
+            wv(std::vector<uint32_t>(gpos.begin(), gpos.begin() + n));
+            std::fclose(f);
+        }
         // optimistic pass: keys the scheduler reorders are rerun with its fire order (the device does this in one
         // launch), then the exact pass decides, replaying on the host only what still differs
         auto t0 = std::chrono::steady_clock::now();
