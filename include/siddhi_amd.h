@@ -68,6 +68,7 @@ typedef struct sdg_opts {
 #define SDG_COMPILE_ONLY 1
 #define SDG_FORCE_GENERIC 2    /* run every query on the generic keyed-NFA kernel (testing: both kernels on one query) */
 #define SDG_NO_FUSED 4         /* chain path: always key-sort with the full radix (testing: both chain kernels on one query) */
+#define SDG_NO_SEQ3 8          /* sequences of the seq3 shape on the generic keyed NFA instead (testing: both kernels) */
 
 typedef struct sdg_out {
     int64_t n;                 /* output events */
@@ -89,7 +90,8 @@ const char* sdg_last_error(void);
 int sdg_stream_index(sdg_engine* e, const char* stream_id);
 int sdg_stream_schema(sdg_engine* e, int stream, int32_t* n_attrs, const int32_t** types);
 int sdg_num_queries(sdg_engine* e);
-/* device path chosen for a query: 0 = chain kernel (independent partials), 1 = generic keyed NFA */
+/* device path chosen for a query: 0 = chain kernel (independent partials), 1 = generic keyed NFA, 2 = register
+ * sequence kernel (SEQUENCE `every e1=S[..], e2=S[..]<m:n>, e3=S[..]`, seq3.hip) */
 int sdg_query_path(sdg_engine* e, int query);
 /* what a multi-GPU deployment needs to know about a query (siddhi_amd/shard.py ShardedAppRuntime): */
 #define SDG_Q_PARTITIONED 1    /* partition with (...): keys are independent, the query shards by key hash */
@@ -169,7 +171,7 @@ typedef struct sdg_stats {
     double ms_total;           /* device ms: whole flush */
     int64_t keygroup_launches;
     int64_t match_launches;
-    int32_t path;              /* 0 chain (independent partials), 1 generic keyed NFA */
+    int32_t path;              /* 0 chain (independent partials), 1 generic keyed NFA, 2 register sequence kernel */
     int32_t overflow;          /* capacity overflows detected (0 on a valid run) */
     /* device ms per kernel (HIP events on the engine's stream), summed over the flush's queries */
     double ms_kg_hist, ms_kg_prefix, ms_kg_scatter, ms_chain_carry, ms_chain_match;

@@ -60,6 +60,9 @@ for s in "$@"; do
         c3pmc2) i=0; for c in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_INSTS_FLAT SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS"; do i=$((i+1)); run c3pmc$i 180 rocprofv3 --pmc $c --kernel-trace -d "$OUT/c3pmc$i" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 1 --warmup 0; done ;;
         ldsconf) run ldsconf 180 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace -d "$OUT/ldsconf" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 1 --warmup 0 ;;
         c5) run c5 600 python3 bench.py --config c5 --c5-shard 0/8 --steps 3 --warmup 1 --no-gather ;;
+        seq3) run seq3 900 python3 -u -m pytest tests/test_gpu_seq3.py tests/test_gpu_snapshot.py tests/test_gpu_robust.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider && run seq3p 900 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "c3 or many_keys" ;;
+        seq3cfg) run seq3cfg 600 python3 scripts/bench_configs.py --only c3md,c3m --c3-steps 3 && run seq3gen 600 env SDG_NO_SEQ3=1 python3 scripts/bench_configs.py --only c3md --c3-steps 2 ;;
+        seq3prof) run seq3prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/seq3prof" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 2 --warmup 1 ;;
         *) echo "unknown step $s" ;;
     esac
 done

@@ -217,12 +217,13 @@ class InputHandler:
 
 class SiddhiAppRuntime:
     def __init__(self, app_text, device=0, batch_capacity=0, compile_only=False, force_generic=False, fused=True,
-                 max_partials=0):
+                 max_partials=0, seq3=True):
         L = load_library()
         self._L = L
         h = ctypes.c_void_p()
         opts = _Opts(device, batch_capacity, max_partials,
-                     (1 if compile_only else 0) | (2 if force_generic else 0) | (0 if fused else 4))
+                     (1 if compile_only else 0) | (2 if force_generic else 0) | (0 if fused else 4) |
+                     (0 if seq3 else 8))
         _check(L.sdg_compile(app_text.encode(), ctypes.byref(opts), ctypes.byref(h)))
         self._h = h
         self._compile_only = compile_only
@@ -288,7 +289,7 @@ class SiddhiAppRuntime:
         return [self._L.sdg_query_flags(self._h, q) for q in range(len(self._queries))]
 
     def query_paths(self):
-        """device path per query: 0 chain kernel, 1 generic keyed NFA"""
+        """device path per query: 0 chain kernel, 1 generic keyed NFA, 2 register sequence kernel (seq3)"""
         return [self._L.sdg_query_path(self._h, q) for q in range(len(self._queries))]
 
     def intern(self, s):

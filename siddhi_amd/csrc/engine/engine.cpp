@@ -282,6 +282,11 @@ struct QueryRt {
     DevBuf slot_of, idle_rec, slot_key, init_from, releasable, idle_out, free_slots, pool_ctr;
     HostPin pool_ret;
     nfa::Layout L{};
+    // the register sequence kernel (seq3.hip) instead of the generic NFA: its per-key state, SoA with stride s3_kcap
+    bool seq3 = false;
+    Seq3Spec s3{};
+    DevBuf s3_hdr, s3_pn, s3_qn, s3_vals;
+    int64_t s3_kcap = 0;
     // outputs
     DevBuf o_ts, o_key, o_vals, o_nulls, o_emit, o_first, counters, flags;
     int64_t out_n = 0, out_cap = 0;
@@ -333,6 +338,7 @@ struct sdg_engine {
     bool compile_only = false;
     bool force_generic = false;
     bool no_fused = false;
+    bool no_seq3 = false;        // SDG_NO_SEQ3 / SDG_FORCE_GENERIC: seq3-shaped sequences on the generic NFA
     uint64_t app_hash = 0;       // FNV-1a of the app text: a snapshot restores only into the app it came from
     std::vector<uint8_t> snap;   // the last sdg_snapshot's bytes (valid until the next snapshot / destroy)
     std::vector<Stage> stage;    // per stream: host pushes staged in HBM (see stage_push)
@@ -457,6 +463,86 @@ int64_t range_stack[STACK];
 bool range_holds(const HostQuery& h, const HostQuery::RangeKey& rk, int qpos, const PushChunk& c, int64_t r, bool mixed) {
     RowAcc acc{&h, qpos, &c, r, mixed};
     return pass(h.code.data(), rk.cond, h.consts.data(), acc, range_stack, 1);
+}
+
+// The register sequence kernel (seq3.hip) covers SEQUENCE `every e1=S[f1], e2=S[f2]<m:n>, e3=S[f3]` over one stream
+// (StateInputStreamParser.java:76-408 wiring: e1 the every-start re-armed by its own post processor, e2 a count
+// state with min >= 1 forwarding to e3, e3 the last), without within, timers, @purge, aggregators or range
+// partitions, with FastPred filters and plain-attribute selects whose state events are e1, e2[0], e2[last] or e3.
+// Fills the spec (operands resolved per processor context) or returns false (the generic NFA runs the query).
+bool seq3_spec_(const HostQuery& h, Seq3Spec& s, int& why);
+bool seq3_spec(const HostQuery& h, Seq3Spec& s) {
+    int why = 0;
+    const bool ok = seq3_spec_(h, s, why);
+    if (!ok && getenv("SDG_SEQ3_WHY")) fprintf(stderr, "seq3: query '%s' not eligible (check %d)\n", h.name.c_str(), why);
+    return ok;
+}
+bool seq3_spec_(const HostQuery& h, Seq3Spec& s, int& why) {
+    const Plan& P = h.plan;
+    if (P.chain || !P.seq || P.n_states != 3 || P.has_within || P.n_sched || P.purge || P.has_post) return why = 1, false;
+    if (h.streams.size() != 1 || P.n_cols < 1 || P.n_cols > S3_MAX_COLS || P.n_out > S3_MAX_OUT) return why = 2, false;
+    for (int x : h.key_attr)
+        if (x == -2) return why = 3, false;  // range partitions
+    const StateRow &r0 = P.st[0], &r1 = P.st[1], &r2 = P.st[2];
+    if (r0.kind != PK_STREAM || !r0.is_start || r0.next != 1 || r0.next_every != 0 || (r0.within_every != -1 && r0.within_every != 0) ||
+        r0.callback != -1)
+        return why = 4, false;
+    if (r1.kind != PK_COUNT || r1.is_start || r1.next != 2 || r1.next_every != -1 || r1.callback != -1 ||
+        r1.min_count < 1 || r1.min_count > (1 << 23) || (r1.max_count != INT32_MAX && r1.max_count > (1 << 23)) ||
+        r1.max_count < r1.min_count)
+        return why = 5, false;
+    if (r2.kind != PK_STREAM || r2.is_start || r2.next != -1 || r2.next_every != -1 || r2.callback != -1) return why = 6, false;
+    if (r0.stream != r1.stream || r1.stream != r2.stream) return why = 7, false;
+    const RecvRow& rv = P.recv[0];
+    if (rv.n != 3 || !rv.multi || rv.procs[rv.order[0]] != 2 || rv.procs[rv.order[1]] != 1 || rv.procs[rv.order[2]] != 0)
+        return why = 8, false;
+    for (int j = 0; j < P.n_out; ++j)
+        if (P.out_multi[j] || P.out_post[j]) return why = 9, false;
+    std::memset(&s, 0, sizeof s);
+    s.nc = P.n_cols;
+    s.n_out = P.n_out;
+    s.min_count = r1.min_count;
+    s.max_count = r1.max_count;
+    for (int c = 0; c < P.n_cols; ++c) s.col_kind[c] = P.col_kind[c];
+    // (slot, chain index) of a state event -> the register event of processor context `ctx`
+    // (0: the e1 filter, the event is e1; 1: the e2 filter, Q with the event as e2[last]; 2: the e3 filter / select)
+    auto src = [](int ctx, int slot, int chain, int8_t* out) -> bool {
+        if (chain != 0 && chain != -1) return false;
+        if (ctx == 0) *out = slot == 0 ? S3_Y : S3_NULL;
+        else if (ctx == 1) *out = slot == 0 ? S3_E1 : slot == 1 ? (chain == 0 ? S3_E2F : S3_Y) : S3_NULL;
+        else *out = slot == 0 ? S3_E1 : slot == 1 ? (chain == 0 ? S3_E2F : S3_E2L) : slot == 2 ? S3_Y : S3_NULL;
+        return slot >= 0 && slot < 3;
+    };
+    for (int p = 0; p < 3; ++p) {
+        const FastPred& f = P.fast[p];
+        S3Pred& d = s.f[p];
+        if (f.kind == FP_TRUE || (f.kind == FP_NONE && P.st[p].filter.len == 0)) {
+            d.kind = FP_TRUE;
+            continue;
+        }
+        if (f.kind != FP_CONST && f.kind != FP_SLOT) return why = 11, false;
+        d.kind = f.kind;
+        d.op = f.op;
+        d.t = f.t;
+        d.konst = f.konst;
+        if (!src(p, f.sa, f.ia, &d.a.src) || f.ca < 0 || f.ca >= P.n_cols) return why = 12, false;
+        d.a.col = (uint8_t)f.ca;
+        d.a.kind = f.ka;
+        if (f.kind == FP_SLOT) {
+            if (!src(p, f.sb, f.ib, &d.b.src) || f.cb < 0 || f.cb >= P.n_cols) return why = 13, false;
+            d.b.col = (uint8_t)f.cb;
+            d.b.kind = f.kb;
+        }
+    }
+    for (int j = 0; j < P.n_out; ++j) {
+        const Prog pr = P.out_prog[j];
+        if (pr.len != 1 || h.code[pr.start].op != OP_LOAD) return why = 14, false;
+        const Instr in = h.code[pr.start];
+        if (!src(2, in.a, in.c, &s.out[j].src) || in.b < 0 || in.b >= P.n_cols) return why = 15, false;
+        s.out[j].col = (uint8_t)in.b;
+        s.out[j].kind = in.k;
+    }
+    return true;
 }
 
 // chain_match_k's LDS tile: the columns the state-1 filter reads from its own event (the scanned rows), and
@@ -1304,6 +1390,110 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     }
     hp.mark("keygroup_enqueue");
     ev_record(e->ev[1], st);
+    if (!P.chain && q.seq3) {
+        // ---- register sequence kernel (seq3.hip): per-key state grows to K keys (zeros: no partial) -------------
+        const int64_t KK = partitioned ? (int64_t)K : 1;
+        const int s3nc = q.s3.nc;
+        if (q.s3_kcap < KK) {
+            const int64_t nk = std::max<int64_t>(KK, q.s3_kcap + q.s3_kcap / 2);
+            auto grow = [&](DevBuf& buf, int64_t per, int groups) {  // SoA: each of `groups` fields re-strided
+                DevBuf nb;
+                nb.ensure((size_t)(nk * per * groups));
+                HIPCHECK(hipMemsetAsync(nb.p, 0, (size_t)(nk * per * groups), st));
+                for (int g = 0; g < groups && q.s3_kcap > 0; ++g)
+                    HIPCHECK(hipMemcpyAsync((uint8_t*)nb.p + g * nk * per, (const uint8_t*)buf.p + g * q.s3_kcap * per,
+                                            (size_t)(q.s3_kcap * per), hipMemcpyDeviceToDevice, st));
+                HIPCHECK(hipStreamSynchronize(st));
+                std::swap(nb.p, buf.p);
+                std::swap(nb.cap, buf.cap);
+            };
+            grow(q.s3_hdr, 4, 1);
+            grow(q.s3_pn, 4, 1);
+            grow(q.s3_qn, 4, 1);
+            grow(q.s3_vals, 8, 6 * s3nc);
+            q.s3_kcap = nk;
+        }
+        Seq3Args a;
+        std::memset(&a, 0, sizeof a);
+        a.sp = q.s3;
+        a.n = nrows;
+        a.ts = v_ts;
+        a.seg_start = partitioned ? v_seg : nullptr;
+        a.seg_end = partitioned ? v_segend : nullptr;
+        a.K = (int32_t)KK;
+        // emission position = seq_base + (orig ? orig[r] : r): orig holds view rows unless d_vpos mapped them
+        a.orig = v_orig;
+        a.pos_off = 0;
+        a.seq_base = e->seq + (d_vpos ? 0 : pos_off);
+        for (int k = 0; k < nc; ++k) { a.cols[k] = v_cols[k]; a.nulls[k] = v_nulls[k]; }
+        a.st_hdr = q.s3_hdr.as<uint32_t>();
+        a.st_pn = q.s3_pn.as<uint32_t>();
+        a.st_qn = q.s3_qn.as<uint32_t>();
+        a.st_vals = q.s3_vals.as<int64_t>();
+        a.kcap = q.s3_kcap;
+        // at most one match per event: nrows records never overflow (no rerun, so the state updates in place)
+        const int64_t cap = std::max<int64_t>(q.out_cap, nrows + 64);
+        q.out_cap = cap;
+        a.out_cap = cap;
+        unsigned long long* counters = (unsigned long long*)q.counters.ensure(16);
+        HIPCHECK(hipMemsetAsync(counters, 0, 16, st));
+        if (!(partitioned && nrows > 0)) HIPCHECK(hipMemsetAsync(flags, 0, 32, st));
+        a.out_count = counters;
+        a.flags = flags;
+        a.out_ts = (int64_t*)q.o_ts.ensure(cap * 8);
+        a.out_key = (uint32_t*)q.o_key.ensure(cap * 4);
+        a.out_vals = (int64_t*)q.o_vals.ensure((size_t)std::max(P.n_out, 1) * cap * 8);
+        a.out_nulls = (uint32_t*)q.o_nulls.ensure(cap * 4);
+        a.out_emit_seq = (int64_t*)q.o_emit.ensure(cap * 8);
+        a.out_sub = (int64_t*)q.o_first.ensure(cap * 8);
+        Seq3Args* h_a = (Seq3Args*)q.h_args.ensure(std::max(sizeof(NfaArgs), 2 * sizeof(ChainArgs)));
+        Seq3Args* d_a = (Seq3Args*)q.d_args.ensure(std::max(sizeof(NfaArgs), 2 * sizeof(ChainArgs)));
+        static_assert(sizeof(Seq3Args) <= 2 * sizeof(ChainArgs), "seq3 arguments fit the argument staging");
+        *h_a = a;
+        HIPCHECK(hipMemcpyAsync(d_a, h_a, sizeof(Seq3Args), hipMemcpyHostToDevice, st));
+        ev_record(e->ev[8], st);
+        seq3_run(a, d_a, st);
+        ev_record(e->ev[2], st);
+        unsigned long long hc = 0;
+        int hf[8];
+        HIPCHECK(hipMemcpyAsync(&hc, counters, 8, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(hf, flags, 32, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        if (hf[4]) throw CompileError(SDG_ERR_ARG, "device-resident partition key ids out of range (not from sdg_intern)");
+        if (hf[0] || (int64_t)hc > cap) throw DeviceError("seq3: more matches than events (internal error)");
+        e->stats.match_launches += 1;
+        q.last_timers = false;
+        q.last_rank.clear();
+        q.taken.clear();
+        q.reordered.clear();
+        q.runs.clear();
+        q.last_seq_base = e->seq;
+        q.emit_base = e->seq;
+        q.sub_is_seq = false;
+        float ms_kg = 0, ms_m = 0, t;
+        ev_elapsed(&ms_kg, e->ev[0], e->ev[1]);
+        ev_elapsed(&ms_m, e->ev[1], e->ev[2]);
+        e->stats.ms_keygroup += ms_kg;
+        e->stats.ms_match += ms_m;
+        if (partitioned && nrows > 0) {
+            ev_elapsed(&t, e->ev[4], e->ev[5]);
+            e->stats.ms_kg_hist += t;
+            ev_elapsed(&t, e->ev[6], e->ev[7]);
+            e->stats.ms_kg_prefix += t;
+            ev_elapsed(&t, e->ev[5], e->ev[6]);
+            e->stats.ms_kg_scatter += t;
+        }
+        ev_elapsed(&t, e->ev[8], e->ev[2]);
+        e->stats.ms_nfa += t;
+        e->stats.ms_nfa_kernel += t;
+        e->stats.events += nrows;
+        q.out_n = (int64_t)hc;
+        q.polled = false;
+        q.nulls_valid = true;
+        e->stats.matches += q.out_n;
+        e->stats.path = 2;
+        return true;
+    }
     if (!P.chain) {
         NfaArgs a;
         std::memset(&a, 0, sizeof a);
@@ -1737,6 +1927,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         e->stats.events += nrows;
         q.out_n = (int64_t)hc[0];
         q.polled = false;
+        q.nulls_valid = true;  // (a chain query that moved here may have left it false)
         e->stats.matches += q.out_n;
         e->stats.path = 1;
         return true;
@@ -2510,6 +2701,14 @@ void snapshot(sdg_engine* e, std::vector<uint8_t>& out) {
         // selector aggregators per key
         w.put<int64_t>(q.agg_keys);
         if (q.agg_keys > 0) w.dev(q.agg_state.p, (size_t)q.agg_keys * (size_t)std::max(P.n_agg, 1) * 16, st);
+        // register sequence kernel: the per-key partials (SoA, stride s3_kcap)
+        w.put<int64_t>(q.s3_kcap);
+        if (q.s3_kcap > 0) {
+            w.dev(q.s3_hdr.p, (size_t)q.s3_kcap * 4, st);
+            w.dev(q.s3_pn.p, (size_t)q.s3_kcap * 4, st);
+            w.dev(q.s3_qn.p, (size_t)q.s3_kcap * 4, st);
+            w.dev(q.s3_vals.p, (size_t)q.s3_kcap * 8 * 6 * q.s3.nc, st);
+        }
         q.sim.save(out);
     }
 }
@@ -2549,6 +2748,8 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
         int64_t map_keys = 0;
         View slot_of, idle_rec, slot_key, free_slots, pool_ctr;
         int64_t purge_first = INT64_MIN, agg_keys = 0;
+        int64_t s3_kcap = 0;
+        View s3_hdr, s3_pn, s3_qn, s3_vals;
         SchedSim sim;
     };
     const int64_t seq = r.get<int64_t>();
@@ -2620,6 +2821,18 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
         if (P.purge && g.arena_keys > 0) g.last_seen = view();
         g.agg_keys = r.get<int64_t>();
         if (g.agg_keys > 0) g.agg = view();
+        g.s3_kcap = r.get<int64_t>();
+        if (g.s3_kcap < 0 || (g.s3_kcap > 0 && !e->qs[qi]->seq3)) throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (sequence state)");
+        if (g.s3_kcap > 0) {
+            g.s3_hdr = view();
+            g.s3_pn = view();
+            g.s3_qn = view();
+            g.s3_vals = view();
+            const size_t kc = (size_t)g.s3_kcap;
+            if (g.s3_hdr.n != kc * 4 || g.s3_pn.n != kc * 4 || g.s3_qn.n != kc * 4 ||
+                g.s3_vals.n != kc * 8 * 6 * (size_t)e->qs[qi]->s3.nc)
+                throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (sequence state)");
+        }
         g.sim.setup(P.n_sched, P.partitioned, !P.playback);
         r.p = g.sim.load(r.p, r.end);
     }
@@ -2692,6 +2905,13 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
         if (P.purge && q.arena_keys > 0) up(q.last_seen, g.last_seen);
         q.agg_keys = g.agg_keys;
         if (q.agg_keys > 0) up(q.agg_state, g.agg);
+        q.s3_kcap = g.s3_kcap;
+        if (q.s3_kcap > 0) {
+            up(q.s3_hdr, g.s3_hdr);
+            up(q.s3_pn, g.s3_pn);
+            up(q.s3_qn, g.s3_qn);
+            up(q.s3_vals, g.s3_vals);
+        }
         q.sim = std::move(g.sim);
         HIPCHECK(hipStreamSynchronize(st));  // the views point into the caller's blob
     }
@@ -2737,6 +2957,7 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             e->compile_only = (opts->flags & SDG_COMPILE_ONLY) != 0;
             e->force_generic = (opts->flags & SDG_FORCE_GENERIC) != 0;
             e->no_fused = (opts->flags & SDG_NO_FUSED) != 0;
+            e->no_seq3 = (opts->flags & (SDG_NO_SEQ3 | SDG_FORCE_GENERIC)) != 0;
         }
         if (opts && opts->max_partials > 0) {
             if (opts->max_partials > 4096) throw CompileError(SDG_ERR_ARG, "max_partials must be <= 4096");
@@ -2770,7 +2991,8 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             for (size_t i = 0; i < q->hq.key_kind.size(); ++i)
                 if (q->hq.key_attr[i] < 0 || key_class_of(q->hq.key_kind[i]) != q->key_class) q->key_class = KC_NONE;
             // arenas sized by live keys (nfa.h to_idle): partitioned generic-NFA queries without timers or @purge
-            q->reclaim = P.partitioned && !P.chain && P.n_sched == 0 && !P.purge && !getenv("SDG_NO_RECLAIM");
+            q->seq3 = !e->no_seq3 && !getenv("SDG_NO_SEQ3") && seq3_spec(q->hq, q->s3);
+            q->reclaim = P.partitioned && !P.chain && !q->seq3 && P.n_sched == 0 && !P.purge && !getenv("SDG_NO_RECLAIM");
             if (!e->compile_only) upload_plan(e.get(), *q);
             e->qs.push_back(std::move(q));
         }
@@ -2862,7 +3084,7 @@ int sdg_query_flags(sdg_engine* e, int q) {
 }
 int sdg_query_path(sdg_engine* e, int q) {
     if (!e || q < 0 || q >= (int)e->qs.size()) return -1;
-    return e->qs[q]->hq.plan.chain ? 0 : 1;
+    return e->qs[q]->hq.plan.chain ? 0 : e->qs[q]->seq3 ? 2 : 1;
 }
 const char* sdg_query_name(sdg_engine* e, int q) { return e->qs[q]->hq.name.c_str(); }
 const char* sdg_query_target(sdg_engine* e, int q) { return e->qs[q]->hq.target.c_str(); }

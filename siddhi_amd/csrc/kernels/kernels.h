@@ -264,6 +264,71 @@ struct NfaArgs {
     const uint32_t* fire_off;
     const nfa::TimerFire* fires;
 };
+// ---- register sequence kernel (seq3.hip): SEQUENCE `every e1=S[f1], e2=S[f2]<m:n>, e3=S[f3]` ------------------
+// Per partition key the reference holds at most one partial waiting at e2 (Q) and one at e3 (P; the same object as Q
+// while the count state both forwards and keeps it): SEQUENCE addState keeps one state event per newAndEvery list
+// (StreamPreStateProcessor.java:214-227, CountPreStateProcessor.java:97-125) and every pending list is cleared before
+// each event (resetState :288-305). So a key's whole state is two partials of three events each (e1, e2[0],
+// e2[last]) -- registers instead of an arena. tests/seq3_model.py states the model; tests/test_seq3_model.py pins it
+// against the oracle.
+constexpr int S3_MAX_COLS = 4;   // physical columns stored per event
+constexpr int S3_MAX_OUT = 8;
+constexpr int S3_STAGE = 256;    // output records staged in LDS per wave (one global reservation per flush of them)
+enum S3Src : int8_t { S3_NULL = -1, S3_E1 = 0, S3_E2F = 1, S3_E2L = 2, S3_Y = 3 };
+struct S3Operand {
+    int8_t src;      // S3Src: which event of the partial (Y = the event being processed)
+    uint8_t col;     // physical column
+    uint8_t kind;    // its kind
+    uint8_t pad;
+};
+struct S3Pred {      // FastPred with its operands resolved for one processor's context
+    uint8_t kind;    // FP_TRUE / FP_CONST / FP_SLOT
+    uint8_t op, t, pad;
+    S3Operand a, b;
+    int64_t konst;
+};
+struct Seq3Spec {
+    int32_t nc;                      // physical columns (<= S3_MAX_COLS), stored for every event of a partial
+    int32_t n_out;
+    int32_t min_count, max_count;    // max INT32_MAX: unbounded
+    uint8_t col_kind[S3_MAX_COLS];
+    S3Pred f[3];                     // e1 filter (Y = the e1 candidate), e2 filter (E1, E2F, Y = e2[last]),
+                                     // e3 filter (E1, E2F, E2L of P, Y = e3)
+    S3Operand out[S3_MAX_OUT];       // select items, resolved like the e3 filter
+};
+struct Seq3Args {
+    Seq3Spec sp;
+    int64_t n;
+    const int64_t* ts;                // sorted view
+    const uint32_t* seg_start;        // [K] (nullptr: unpartitioned, one key over [0, n))
+    const uint32_t* seg_end;
+    int32_t K;
+    const uint32_t* orig;             // sorted -> batch position (nullptr: pos_off + row)
+    int64_t pos_off;
+    int64_t seq_base;
+    const void* cols[S3_MAX_COLS];
+    const uint8_t* nulls[S3_MAX_COLS];
+    // per-key state, SoA with stride kcap (persistent; zeros = no partial): hdr bit 0 P, bit 1 Q, bit 2 P is Q,
+    // bits 8..31 Q's e2 count (saturating); pn / qn null bits of P / Q (e1 bits 0.., e2[0] 8.., e2[last] 16..);
+    // vals[(g * nc + c) * kcap + k], g = P.e1, P.e2[0], P.e2[last], Q.e1, Q.e2[0], Q.e2[last]
+    uint32_t* st_hdr;
+    uint32_t* st_pn;
+    uint32_t* st_qn;
+    int64_t* st_vals;
+    int64_t kcap;
+    // outputs (at most one record per event: out_cap >= n never overflows)
+    int64_t out_cap;
+    unsigned long long* out_count;
+    int64_t* out_ts;
+    uint32_t* out_key;
+    int64_t* out_vals;                // [n_out][out_cap]
+    uint32_t* out_nulls;
+    int64_t* out_emit_seq;
+    int64_t* out_sub;
+    int* flags;                       // [0] output overflow
+};
+void seq3_run(const Seq3Args& a, const Seq3Args* d_a, hipStream_t stream);
+
 // a: host copy (launch geometry); d_a: device copy the kernel reads. Layouts of at most NFA_LDS_BUDGET /
 // NFA_LDS_MIN_LANES bytes per key run with the arenas staged in LDS (nfa_lds_k: one wave per block, lanes =
 // NFA_LDS_BUDGET / bytes keys per wave, four blocks per CU); larger ones in HBM (nfa_k)

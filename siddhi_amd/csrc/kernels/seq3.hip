@@ -1,0 +1,269 @@
+// gfx950 register kernel for the SEQUENCE shape `every e1=S[f1], e2=S[f2]<m:n>, e3=S[f3]` on one stream (C3).
+//
+// Why a key's state fits in registers (kernels.h Seq3Spec; reference paths under modules/siddhi-core/src/main/java/
+// io/siddhi/core/query/input/stream/state/): before each event SequenceMultiProcessStreamReceiver resets every state
+// (pending lists cleared, StreamPreStateProcessor.java:288-305) and moves newAndEvery to pending (:308-323); SEQUENCE
+// addState keeps at most one state event per newAndEvery list (:214-227, CountPreStateProcessor.java:97-125). So per
+// key there is one partial waiting at e2 (Q) and one at e3 (P) at most. Per event, in the receiver's reverse state
+// order (PatternMultiProcessStreamReceiver.java:33-39):
+//   e3: P matches -> emitted; its e3 slot stays set, so e2 drops the same object (CountPreStateProcessor.java:58-62)
+//   e2: Q takes the event (addEvent before the filter, :64-66); passing, CountPostStateProcessor.java:49-58 forwards it
+//       to e3 and keeps it at e2 (n != max) -- both only when n >= min -- else it is gone with the next reset
+//   e1: the every-seed (one per key, StreamPostStateProcessor.java:64-83 re-arms it) starts a new partial, which e2
+//       accepts only if Q did not stay there (its newAndEvery list is still empty)
+// tests/seq3_model.py is this model in Python; tests/test_seq3_model.py checks it against the oracle.
+//
+// One lane per partition key walks the key's events of the key-sorted view (4 rows loaded per step); the rest of
+// the state machine is register arithmetic. Matches (at most one per event) are ranked with a wave ballot, staged
+// in LDS and written out as coalesced runs with one global reservation per S3_STAGE - 64 records (a reservation per
+// wave-step would serialise ~10^6 atomics on one L2 address).
+#include <hip/hip_runtime.h>
+
+#include "../engine/eval.h"
+#include "kernels.h"
+#include "wave.h"
+
+namespace sdg {
+
+namespace {
+
+constexpr int S3_G = 4;  // rows loaded per step
+
+template <int NC>
+struct S3Ev {
+    int64_t v[NC];
+};
+
+template <int NC>
+__device__ __forceinline__ int64_t s3_pick(const S3Ev<NC>& e, int c) {
+    int64_t r = e.v[0];
+#pragma unroll
+    for (int i = 1; i < NC; ++i)
+        if (c == i) r = e.v[i];
+    return r;
+}
+
+// operand of a filter / select item in one partial's context (nm: the partial's null bits, yn: the event's);
+// false = null
+template <int NC>
+__device__ __forceinline__ bool s3_get(const S3Operand& o, const S3Ev<NC>& e1, const S3Ev<NC>& ef, const S3Ev<NC>& el,
+                                       const S3Ev<NC>& y, uint32_t nm, uint32_t yn, int64_t* v) {
+    switch (o.src) {
+        case S3_E1: *v = s3_pick(e1, o.col); return !((nm >> o.col) & 1u);
+        case S3_E2F: *v = s3_pick(ef, o.col); return !((nm >> (8 + o.col)) & 1u);
+        case S3_E2L: *v = s3_pick(el, o.col); return !((nm >> (16 + o.col)) & 1u);
+        case S3_Y: *v = s3_pick(y, o.col); return !((yn >> o.col) & 1u);
+        default: *v = 0; return false;
+    }
+}
+
+// fast_pass (eval.h) over resolved operands: null -> false, Java binary numeric promotion to f.t
+template <int NC>
+__device__ __forceinline__ bool s3_pass(const S3Pred& f, const S3Ev<NC>& e1, const S3Ev<NC>& ef, const S3Ev<NC>& el,
+                                        const S3Ev<NC>& y, uint32_t nm, uint32_t yn) {
+    if (f.kind == FP_TRUE) return true;
+    int64_t x, z;
+    if (!s3_get(f.a, e1, ef, el, y, nm, yn, &x)) return false;
+    x = cvt(x, f.a.kind, f.t);
+    if (f.kind == FP_CONST) {
+        z = f.konst;
+    } else {
+        if (!s3_get(f.b, e1, ef, el, y, nm, yn, &z)) return false;
+        z = cvt(z, f.b.kind, f.t);
+    }
+    return cmp(f.op, f.t, x, z);
+}
+
+template <int NC>
+__global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
+    const Seq3Args& a = *pa;
+    const Seq3Spec& sp = a.sp;
+    extern __shared__ __align__(16) uint8_t s3_lds[];
+    int64_t* l_ts = (int64_t*)s3_lds;
+    int64_t* l_seq = l_ts + S3_STAGE;
+    int64_t* l_vals = l_seq + S3_STAGE;  // [n_out][S3_STAGE]
+    uint32_t* l_key = (uint32_t*)(l_vals + (int64_t)sp.n_out * S3_STAGE);
+    uint32_t* l_nul = l_key + S3_STAGE;
+    const int lane = threadIdx.x;
+    const int64_t k = (int64_t)blockIdx.x * 64 + lane;
+    int64_t b = 0, e = 0;
+    if (k < a.K) {
+        if (a.seg_start) {
+            b = a.seg_start[k];
+            e = a.seg_end[k];
+        } else {
+            e = a.n;
+        }
+    }
+    const bool has = b < e;
+    if (!__any(has)) return;  // one wave per block: a uniform exit
+    const int64_t kc = a.kcap;
+    uint32_t hdr = 0, pn = 0, qn = 0;
+    S3Ev<NC> P1{}, PF{}, PL{}, Q1{}, QF{}, QL{};
+    if (has) {
+        hdr = a.st_hdr[k];
+        if (hdr & 2u) {
+            qn = a.st_qn[k];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                Q1.v[c] = a.st_vals[(int64_t)(3 * NC + c) * kc + k];
+                QF.v[c] = a.st_vals[(int64_t)(4 * NC + c) * kc + k];
+                QL.v[c] = a.st_vals[(int64_t)(5 * NC + c) * kc + k];
+            }
+        }
+        if (hdr & 4u) {  // P is Q: stored once
+            P1 = Q1; PF = QF; PL = QL;
+            pn = qn;
+        } else if (hdr & 1u) {
+            pn = a.st_pn[k];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                P1.v[c] = a.st_vals[(int64_t)(0 * NC + c) * kc + k];
+                PF.v[c] = a.st_vals[(int64_t)(1 * NC + c) * kc + k];
+                PL.v[c] = a.st_vals[(int64_t)(2 * NC + c) * kc + k];
+            }
+        }
+    }
+    const uint32_t mn = (uint32_t)sp.min_count, mx = (uint32_t)sp.max_count;
+    const uint64_t lt = lanemask_lt();
+    int staged = 0;
+    auto flush = [&]() {
+        __syncthreads();  // the staged records of every lane (one-wave block)
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(a.out_count, (unsigned long long)staged);
+        base = __shfl(base, 0);
+        for (int i = lane; i < staged; i += 64) {
+            const int64_t o = (int64_t)base + i;
+            if (o >= a.out_cap) {
+                atomicOr(&a.flags[0], 1);
+                continue;
+            }
+            a.out_ts[o] = l_ts[i];
+            a.out_emit_seq[o] = l_seq[i];
+            a.out_sub[o] = 0;
+            a.out_key[o] = l_key[i];
+            a.out_nulls[o] = l_nul[i];
+            for (int j = 0; j < sp.n_out; ++j) a.out_vals[(int64_t)j * a.out_cap + o] = l_vals[j * S3_STAGE + i];
+        }
+        __syncthreads();
+        staged = 0;
+    };
+    for (int64_t i = 0; __any(b + i < e); i += S3_G) {
+        S3Ev<NC> yv[S3_G];
+        uint32_t yn[S3_G];
+        int64_t yts[S3_G];
+#pragma unroll
+        for (int g = 0; g < S3_G; ++g) {  // the step's loads first: they overlap
+            const int64_t r = b + i + g;
+            yn[g] = 0;
+            yts[g] = 0;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) yv[g].v[c] = 0;
+            if (r < e) {
+                yts[g] = a.ts[r];
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    yv[g].v[c] = load_col(a.cols[c], sp.col_kind[c], r);
+                    if (a.nulls[c] && a.nulls[c][r]) yn[g] |= 1u << c;
+                }
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < S3_G; ++g) {
+            const int64_t r = b + i + g;
+            const bool act = r < e;
+            const S3Ev<NC>& y = yv[g];
+            // e3 (first in the receiver's order)
+            const bool em = act && (hdr & 1u) && s3_pass(sp.f[2], P1, PF, PL, y, pn, yn[g]);
+            const uint64_t m = __ballot(em);
+            if (m) {
+                if (em) {
+                    const int at = staged + __popcll(m & lt);
+                    l_ts[at] = yts[g];
+                    l_seq[at] = a.seq_base + (a.orig ? (int64_t)a.orig[r] : a.pos_off + r);
+                    l_key[at] = (uint32_t)k;
+                    uint32_t nm = 0;
+                    for (int j = 0; j < sp.n_out; ++j) {
+                        int64_t v;
+                        const bool ok = s3_get(sp.out[j], P1, PF, PL, y, pn, yn[g], &v);
+                        l_vals[j * S3_STAGE + at] = ok ? v : 0;
+                        if (!ok) nm |= 1u << j;
+                    }
+                    l_nul[at] = nm;
+                }
+                staged += __popcll(m);
+            }
+            if (act) {
+                // e2: Q takes the event unless e3 just consumed the same object
+                uint32_t cnt = hdr >> 8, nh = 0;
+                if ((hdr & 2u) && !(em && (hdr & 4u))) {
+                    const uint32_t n1 = cnt < 0xFFFFFFu ? cnt + 1 : cnt;
+                    if (cnt == 0) {  // e2[0] is this event
+                        QF = y;
+                        qn = (qn & ~0xFF00u) | (yn[g] << 8);
+                    }
+                    if (s3_pass(sp.f[1], Q1, QF, y, y, qn, yn[g]) && n1 >= mn) {
+                        P1 = Q1;
+                        PF = QF;
+                        PL = y;
+                        pn = (qn & 0xFFFFu) | (yn[g] << 16);
+                        nh = 1u;
+                        if (n1 != mx) {  // kept at e2 too: one object
+                            QL = y;
+                            qn = pn;
+                            cnt = n1;
+                            nh |= 2u | 4u;
+                        }
+                    }
+                }
+                // e1: the every-seed starts a partial when e2's list is still empty
+                if (!(nh & 2u) && s3_pass(sp.f[0], y, y, y, y, 0u, yn[g])) {
+                    Q1 = y;
+                    qn = yn[g];
+                    cnt = 0;
+                    nh |= 2u;
+                }
+                hdr = nh | (cnt << 8);
+            }
+            if (staged > S3_STAGE - 64) flush();
+        }
+    }
+    if (staged) flush();
+    if (has) {
+        a.st_hdr[k] = hdr;
+        if (hdr & 2u) {
+            a.st_qn[k] = qn;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                a.st_vals[(int64_t)(3 * NC + c) * kc + k] = Q1.v[c];
+                a.st_vals[(int64_t)(4 * NC + c) * kc + k] = QF.v[c];
+                a.st_vals[(int64_t)(5 * NC + c) * kc + k] = QL.v[c];
+            }
+        }
+        if ((hdr & 1u) && !(hdr & 4u)) {
+            a.st_pn[k] = pn;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                a.st_vals[(int64_t)(0 * NC + c) * kc + k] = P1.v[c];
+                a.st_vals[(int64_t)(1 * NC + c) * kc + k] = PF.v[c];
+                a.st_vals[(int64_t)(2 * NC + c) * kc + k] = PL.v[c];
+            }
+        }
+    }
+}
+
+}  // namespace
+
+void seq3_run(const Seq3Args& a, const Seq3Args* d_a, hipStream_t stream) {
+    if (a.K <= 0 || a.n <= 0) return;
+    const unsigned grid = (unsigned)((a.K + 63) / 64);
+    const size_t lds = (size_t)S3_STAGE * (16 + 8 * (size_t)a.sp.n_out + 8);
+    switch (a.sp.nc) {
+        case 1: hipLaunchKernelGGL(seq3_k<1>, dim3(grid), dim3(64), lds, stream, d_a); break;
+        case 2: hipLaunchKernelGGL(seq3_k<2>, dim3(grid), dim3(64), lds, stream, d_a); break;
+        case 3: hipLaunchKernelGGL(seq3_k<3>, dim3(grid), dim3(64), lds, stream, d_a); break;
+        default: hipLaunchKernelGGL(seq3_k<4>, dim3(grid), dim3(64), lds, stream, d_a); break;
+    }
+}
+
+}  // namespace sdg

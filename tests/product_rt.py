@@ -8,8 +8,9 @@ TAG = {sa.INT: "i", sa.LONG: "l", sa.FLOAT: "f", sa.DOUBLE: "d", sa.BOOL: "b", s
 
 
 class ProductAdapter:
-    def __init__(self, app, force_generic=False, fused=True, max_partials=0):
-        self.rt = sa.SiddhiAppRuntime(app, force_generic=force_generic, fused=fused, max_partials=max_partials)
+    def __init__(self, app, force_generic=False, fused=True, max_partials=0, seq3=True):
+        self.rt = sa.SiddhiAppRuntime(app, force_generic=force_generic, fused=fused, max_partials=max_partials,
+                                      seq3=seq3)
         self.handlers = {}
         self.records = []
 

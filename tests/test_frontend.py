@@ -2,6 +2,7 @@
 import pytest
 
 import siddhi_amd as sa
+import synth
 from siddhi_amd import workloads as w
 
 
@@ -41,9 +42,15 @@ def test_errors_map_to_reference_exceptions(app, exc):
         compile_only(app)
 
 
-def test_sequence_lowers_to_generic_nfa():
-    rt = compile_only(w.C3_APP)
+def test_sequence_lowers_to_seq3_or_generic_nfa():
+    """the C3 shape runs on the register sequence kernel (path 2); SDG_NO_SEQ3 / other sequences: generic NFA"""
+    assert compile_only(w.C3_APP).query_paths() == [2]
+    rt = sa.SiddhiAppRuntime(w.C3_APP, compile_only=True, seq3=False)
     assert rt.query_paths() == [1]
+    for a in ("c3_sequence", "c3_sequence_min1"):
+        assert compile_only(synth.APPS[a]).query_paths() == [2]
+    for a in ("sequence_plus", "sequence_star_within", "count_pattern"):  # two streams / within / pattern: generic
+        assert compile_only(synth.APPS[a]).query_paths() == [1]
 
 
 def test_absent_states_lower_to_schedulers():

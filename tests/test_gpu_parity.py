@@ -278,8 +278,10 @@ def test_generic_nfa_synthetic_on_gpu(name, batches, oracle_built):
     assert got == ref
 
 
-def test_generic_nfa_many_keys_on_gpu(oracle_built):
-    """C3 (<1:5> form) over 3000 keys: thousands of lanes, arenas grown across batches as keys appear"""
+@pytest.mark.parametrize("seq3", [False, True])
+def test_generic_nfa_many_keys_on_gpu(seq3, oracle_built):
+    """C3 (<1:5> form) over 3000 keys: thousands of lanes, arenas grown across batches as keys appear (generic NFA),
+    and the same on the register sequence kernel"""
     app = synth.APPS["c3_sequence_min1"]
     tr = synth.trace(40_000, keys=3000, seed=11, two_streams=False)
     o = Oracle(app)
@@ -287,8 +289,9 @@ def test_generic_nfa_many_keys_on_gpu(oracle_built):
         ref = synth.run(o, tr)
     finally:
         o.close()
-    p = ProductAdapter(app)
+    p = ProductAdapter(app, seq3=seq3)
     try:
+        assert p.rt.query_paths() == [2 if seq3 else 1]
         got = synth.run(p, tr, 3)
     finally:
         p.close()
@@ -479,15 +482,17 @@ def test_radix_path_million_keys_vs_oracle(oracle_built):
     assert np.array_equal(gts, ots) and np.array_equal(gvals.T, ovals)
 
 
-@pytest.mark.parametrize("query,keys", [("<1:5>", 10_000), ("<2:5>", 10_000), ("<1:5>", 100_000)])
-def test_c3_long_keys_vs_oracle(query, keys, oracle_built):
-    """C3 generator (long partition keys, 10^4 / 10^5 keys x 100 events) through the host push, generic keyed NFA;
-    the <1:5> form matches, the literal <2:5> form never does"""
+@pytest.mark.parametrize("query,keys,seq3", [("<1:5>", 10_000, False), ("<2:5>", 10_000, False),
+                                             ("<1:5>", 100_000, False), ("<1:5>", 10_000, True),
+                                             ("<2:5>", 10_000, True), ("<1:5>", 100_000, True)])
+def test_c3_long_keys_vs_oracle(query, keys, seq3, oracle_built):
+    """C3 generator (long partition keys, 10^4 / 10^5 keys x 100 events) through the host push, on the generic keyed
+    NFA and on the register sequence kernel; the <1:5> form matches, the literal <2:5> form never does"""
     c = w.c3_columns(keys)
     app = w.C3_APP.replace("<2:5>", query)
-    rt = sa.SiddhiAppRuntime(app)
+    rt = sa.SiddhiAppRuntime(app, seq3=seq3)
     try:
-        assert rt.query_paths() == [1]
+        assert rt.query_paths() == [2 if seq3 else 1]
         rt.getInputHandler("S").send_columns(c["ts"], [c["id"], c["key"], c["price"], c["volume"]])
         rt.flush(deliver=False)
         gts, gvals, gnulls, _ = rt.poll_arrays(0)
