@@ -63,6 +63,7 @@ for s in "$@"; do
         seq3) run seq3 900 python3 -u -m pytest tests/test_gpu_seq3.py tests/test_gpu_snapshot.py tests/test_gpu_robust.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider && run seq3p 900 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "c3 or many_keys" ;;
         seq3cfg) run seq3cfg 600 python3 scripts/bench_configs.py --only c3md,c3m --c3-steps 3 && run seq3gen 600 env SDG_NO_SEQ3=1 python3 scripts/bench_configs.py --only c3md --c3-steps 2 ;;
         seq3prof) run seq3prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/seq3prof" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 2 --warmup 1 ;;
+        s3ab) run s3g16 600 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && run s3g8 600 env SDG_S3_G=8 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && run s3pmc 180 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/s3pmc" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 1 --warmup 0 && run s3pmcw 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/s3pmcw" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 1 --warmup 0 ;;
         *) echo "unknown step $s" ;;
     esac
 done

@@ -1340,7 +1340,7 @@ struct KeyEvents {
     const void* const* cols;
     const uint8_t* const* nulls;
     int64_t b, e, seq_base;
-    int64_t pos_off;          // batch position of row 0 when orig is nullptr
+    int64_t pos_off;          // batch position of view row 0 (row p: pos_off + (orig ? orig[p] : p))
     const uint8_t* vrank = nullptr;  // range partitions: the range a row came from -- one event sent to several keys
                                      // is processed key after key in range order (PartitionStreamReceiver.receive)
 };
@@ -1370,7 +1370,7 @@ SDG_HD bool key_begin(CtxT<TM>& c, const KeyEvents& ev) {  // returns need_init 
     }
     return fresh;
 }
-SDG_HD int64_t key_pos(const KeyEvents& ev, int64_t p) { return ev.orig ? (int64_t)ev.orig[p] : ev.pos_off + p; }
+SDG_HD int64_t key_pos(const KeyEvents& ev, int64_t p) { return ev.pos_off + (ev.orig ? (int64_t)ev.orig[p] : p); }
 // row p (fires due before it have run); returns false when the key overflowed
 template <bool TM>
 SDG_HD bool key_row(CtxT<TM>& c, const KeyEvents& ev, int64_t p, bool& need_init) {

@@ -61,7 +61,7 @@ std::string java_real_string(double x, bool is_float);
 int32_t java_spread_hash(const std::string& s);
 
 // a batch's rows by key (the sorted view): key k's rows are [seg_b[k], seg_e[k]), row p at batch position
-// orig ? orig[p] : pos_off + p (ascending within a key)
+// pos_off + (orig ? orig[p] : p) (ascending within a key)
 struct KeyRows {
     const uint32_t* seg_b = nullptr;
     const uint32_t* seg_e = nullptr;
@@ -69,7 +69,7 @@ struct KeyRows {
     const uint32_t* orig = nullptr;
     int64_t pos_off = 0;
     int64_t n = 0;
-    int64_t pos(int64_t p) const { return orig ? (int64_t)orig[p] : pos_off + p; }
+    int64_t pos(int64_t p) const { return pos_off + (orig ? (int64_t)orig[p] : p); }
 };
 
 class SchedSim {

@@ -13,11 +13,13 @@
 //       accepts only if Q did not stay there (its newAndEvery list is still empty)
 // tests/seq3_model.py is this model in Python; tests/test_seq3_model.py checks it against the oracle.
 //
-// One lane per partition key walks the key's events of the key-sorted view (4 rows loaded per step); the rest of
+// One lane per partition key walks the key's events of the key-sorted view (16 rows loaded per step); the rest of
 // the state machine is register arithmetic. Matches (at most one per event) are ranked with a wave ballot, staged
 // in LDS and written out as coalesced runs with one global reservation per S3_STAGE - 64 records (a reservation per
 // wave-step would serialise ~10^6 atomics on one L2 address).
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 
 #include "../engine/eval.h"
 #include "kernels.h"
@@ -27,7 +29,10 @@ namespace sdg {
 
 namespace {
 
-constexpr int S3_G = 4;  // rows loaded per step
+// rows loaded per step, all loads issued before the step's state machine runs. Each lane walks its own key's
+// segment, so one load instruction touches 64 cache lines; a step of 16 8-byte rows consumes whole 128-byte lines
+// while they are in flight (4 rows per step measured 6.6 ms per 10^8 events on C3: with ~11 waves per CU the lines
+// were evicted between steps and refetched, ~16x the algorithmic read traffic)
 
 template <int NC>
 struct S3Ev {
@@ -74,7 +79,7 @@ __device__ __forceinline__ bool s3_pass(const S3Pred& f, const S3Ev<NC>& e1, con
     return cmp(f.op, f.t, x, z);
 }
 
-template <int NC>
+template <int NC, int S3_G>
 __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
     const Seq3Args& a = *pa;
     const Seq3Spec& sp = a.sp;
@@ -148,6 +153,63 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
         __syncthreads();
         staged = 0;
     };
+    // one event through e3, e2, e1 (the state machine; y = the event, r its sorted row)
+    auto row_step = [&](const S3Ev<NC>& y, uint32_t ynn, int64_t yt, int64_t r) {
+        const bool act = r < e;
+        // e3 (first in the receiver's order)
+        const bool em = act && (hdr & 1u) && s3_pass(sp.f[2], P1, PF, PL, y, pn, ynn);
+        const uint64_t m = __ballot(em);
+        if (m) {
+            if (em) {
+                const int at = staged + __popcll(m & lt);
+                l_ts[at] = yt;
+                l_seq[at] = a.seq_base + (a.orig ? (int64_t)a.orig[r] : a.pos_off + r);
+                l_key[at] = (uint32_t)k;
+                uint32_t nm = 0;
+                for (int j = 0; j < sp.n_out; ++j) {
+                    int64_t v;
+                    const bool ok = s3_get(sp.out[j], P1, PF, PL, y, pn, ynn, &v);
+                    l_vals[j * S3_STAGE + at] = ok ? v : 0;
+                    if (!ok) nm |= 1u << j;
+                }
+                l_nul[at] = nm;
+            }
+            staged += __popcll(m);
+        }
+        if (act) {
+            // e2: Q takes the event unless e3 just consumed the same object
+            uint32_t cnt = hdr >> 8, nh = 0;
+            if ((hdr & 2u) && !(em && (hdr & 4u))) {
+                const uint32_t n1 = cnt < 0xFFFFFFu ? cnt + 1 : cnt;
+                if (cnt == 0) {  // e2[0] is this event
+                    QF = y;
+                    qn = (qn & ~0xFF00u) | (ynn << 8);
+                }
+                if (s3_pass(sp.f[1], Q1, QF, y, y, qn, ynn) && n1 >= mn) {
+                    P1 = Q1;
+                    PF = QF;
+                    PL = y;
+                    pn = (qn & 0xFFFFu) | (ynn << 16);
+                    nh = 1u;
+                    if (n1 != mx) {  // kept at e2 too: one object
+                        QL = y;
+                        qn = pn;
+                        cnt = n1;
+                        nh |= 2u | 4u;
+                    }
+                }
+            }
+            // e1: the every-seed starts a partial when e2's list is still empty
+            if (!(nh & 2u) && s3_pass(sp.f[0], y, y, y, y, 0u, ynn)) {
+                Q1 = y;
+                qn = ynn;
+                cnt = 0;
+                nh |= 2u;
+            }
+            hdr = nh | (cnt << 8);
+        }
+        if (staged > S3_STAGE - 64) flush();
+    };
     for (int64_t i = 0; __any(b + i < e); i += S3_G) {
         S3Ev<NC> yv[S3_G];
         uint32_t yn[S3_G];
@@ -168,64 +230,20 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
                 }
             }
         }
+        // four rows per round through one copy of the state machine, then the registers rotate by four (static
+        // indices throughout: a dynamically indexed register array would live in scratch)
+#pragma unroll 1
+        for (int q4 = 0; q4 < S3_G; q4 += 4) {
 #pragma unroll
-        for (int g = 0; g < S3_G; ++g) {
-            const int64_t r = b + i + g;
-            const bool act = r < e;
-            const S3Ev<NC>& y = yv[g];
-            // e3 (first in the receiver's order)
-            const bool em = act && (hdr & 1u) && s3_pass(sp.f[2], P1, PF, PL, y, pn, yn[g]);
-            const uint64_t m = __ballot(em);
-            if (m) {
-                if (em) {
-                    const int at = staged + __popcll(m & lt);
-                    l_ts[at] = yts[g];
-                    l_seq[at] = a.seq_base + (a.orig ? (int64_t)a.orig[r] : a.pos_off + r);
-                    l_key[at] = (uint32_t)k;
-                    uint32_t nm = 0;
-                    for (int j = 0; j < sp.n_out; ++j) {
-                        int64_t v;
-                        const bool ok = s3_get(sp.out[j], P1, PF, PL, y, pn, yn[g], &v);
-                        l_vals[j * S3_STAGE + at] = ok ? v : 0;
-                        if (!ok) nm |= 1u << j;
-                    }
-                    l_nul[at] = nm;
+            for (int g = 0; g < 4; ++g) row_step(yv[g], yn[g], yts[g], b + i + q4 + g);
+            if (q4 + 4 < S3_G) {
+#pragma unroll
+                for (int g = 0; g + 4 < S3_G; ++g) {
+                    yv[g] = yv[g + 4];
+                    yn[g] = yn[g + 4];
+                    yts[g] = yts[g + 4];
                 }
-                staged += __popcll(m);
             }
-            if (act) {
-                // e2: Q takes the event unless e3 just consumed the same object
-                uint32_t cnt = hdr >> 8, nh = 0;
-                if ((hdr & 2u) && !(em && (hdr & 4u))) {
-                    const uint32_t n1 = cnt < 0xFFFFFFu ? cnt + 1 : cnt;
-                    if (cnt == 0) {  // e2[0] is this event
-                        QF = y;
-                        qn = (qn & ~0xFF00u) | (yn[g] << 8);
-                    }
-                    if (s3_pass(sp.f[1], Q1, QF, y, y, qn, yn[g]) && n1 >= mn) {
-                        P1 = Q1;
-                        PF = QF;
-                        PL = y;
-                        pn = (qn & 0xFFFFu) | (yn[g] << 16);
-                        nh = 1u;
-                        if (n1 != mx) {  // kept at e2 too: one object
-                            QL = y;
-                            qn = pn;
-                            cnt = n1;
-                            nh |= 2u | 4u;
-                        }
-                    }
-                }
-                // e1: the every-seed starts a partial when e2's list is still empty
-                if (!(nh & 2u) && s3_pass(sp.f[0], y, y, y, y, 0u, yn[g])) {
-                    Q1 = y;
-                    qn = yn[g];
-                    cnt = 0;
-                    nh |= 2u;
-                }
-                hdr = nh | (cnt << 8);
-            }
-            if (staged > S3_STAGE - 64) flush();
         }
     }
     if (staged) flush();
@@ -258,11 +276,19 @@ void seq3_run(const Seq3Args& a, const Seq3Args* d_a, hipStream_t stream) {
     if (a.K <= 0 || a.n <= 0) return;
     const unsigned grid = (unsigned)((a.K + 63) / 64);
     const size_t lds = (size_t)S3_STAGE * (16 + 8 * (size_t)a.sp.n_out + 8);
+    static const char* gs = getenv("SDG_S3_G");  // A/B: rows loaded per step (8 or 16)
+    const bool g16 = !(gs && atoi(gs) == 8);
     switch (a.sp.nc) {
-        case 1: hipLaunchKernelGGL(seq3_k<1>, dim3(grid), dim3(64), lds, stream, d_a); break;
-        case 2: hipLaunchKernelGGL(seq3_k<2>, dim3(grid), dim3(64), lds, stream, d_a); break;
-        case 3: hipLaunchKernelGGL(seq3_k<3>, dim3(grid), dim3(64), lds, stream, d_a); break;
-        default: hipLaunchKernelGGL(seq3_k<4>, dim3(grid), dim3(64), lds, stream, d_a); break;
+        case 1:
+            if (g16) hipLaunchKernelGGL((seq3_k<1, 16>), dim3(grid), dim3(64), lds, stream, d_a);
+            else hipLaunchKernelGGL((seq3_k<1, 8>), dim3(grid), dim3(64), lds, stream, d_a);
+            break;
+        case 2:
+            if (g16) hipLaunchKernelGGL((seq3_k<2, 16>), dim3(grid), dim3(64), lds, stream, d_a);
+            else hipLaunchKernelGGL((seq3_k<2, 8>), dim3(grid), dim3(64), lds, stream, d_a);
+            break;
+        case 3: hipLaunchKernelGGL((seq3_k<3, 8>), dim3(grid), dim3(64), lds, stream, d_a); break;
+        default: hipLaunchKernelGGL((seq3_k<4, 8>), dim3(grid), dim3(64), lds, stream, d_a); break;
     }
 }
 

@@ -13,7 +13,7 @@ from test_seq3_model import F2, F3, app as seq_app
 pytestmark = pytest.mark.gpu
 
 
-def run_both(app, tr, batches, seq3=True):
+def run_both(app, tr, batches, seq3=True, path=None):
     o = Oracle(app)
     try:
         ref = synth.run(o, tr)
@@ -21,7 +21,7 @@ def run_both(app, tr, batches, seq3=True):
         o.close()
     p = ProductAdapter(app, seq3=seq3)
     try:
-        assert p.rt.query_paths() == [2 if seq3 else 1]
+        assert p.rt.query_paths() == [path if path is not None else 2 if seq3 else 1]
         got = synth.run(p, tr, batches)
     finally:
         p.close()
@@ -49,6 +49,14 @@ def test_seq3_shapes_vs_oracle(lo, hi, f2kind, f3kind, oracle_built):
     assert got == ref
     if lo == 1:
         assert len(ref) > 50
+
+
+def test_seq3_ineligible_filter_runs_generic(oracle_built):
+    """an arithmetic e2 filter is not a FastPred: the same shape stays on the generic keyed NFA"""
+    app = seq_app(1, 5, F3["last"], "price>=e2[0].price - 5")
+    tr = price_trace(4000, keys=9, seed=2, dom=[15, 21, 22, 23, 25, 30])
+    ref, got = run_both(app, tr, 3, path=1)
+    assert len(ref) > 20 and got == ref
 
 
 @pytest.mark.parametrize("batches", [1, 3, 17])
@@ -107,3 +115,33 @@ def test_seq3_device_resident_long_keys(oracle_built):
     ots, ovals, _ = oracle_batch_rows(app, "S", c["ts"], [c["id"], c["key"], c["price"].view(np.int64), c["volume"]], 4)
     assert len(ots) > 10_000
     assert np.array_equal(gts, ots) and np.array_equal(gvals.T, ovals)
+
+
+@pytest.mark.parametrize("seq3", [True, False])
+def test_event_seq_counts_other_streams(seq3):
+    """event_seq of a partitioned sequence's matches is the global position of the emitting event: stream A's 100
+    events pushed before B's in the same flush come first (view rows of B map to positions 100..)"""
+    app = ("@app:playback define stream A (id long, key string, price double, volume int); "
+           "define stream B (id long, key string, price double, volume int); "
+           "partition with (key of A, key of B) begin "
+           "@info(name='qa') from every e1=A[price>20] -> e2=A[price>e1.price] within 1 sec "
+           "select e1.id as a, e2.id as b insert into OA; "
+           "@info(name='qb') from every e1=B[price>20], e2=B[price>e1.price]<1:5>, e3=B[price<e2[last].price] "
+           "select e1.id as a, e3.id as d insert into OB; end;")
+    rt = sa.SiddhiAppRuntime(app, seq3=seq3)
+    try:
+        assert rt.query_paths() == [0, 2 if seq3 else 1]
+        n = 100
+        rng = np.random.default_rng(1)
+        k = [rt.intern("k%d" % (i % 3)) for i in range(n)]
+        for sid in ("A", "B"):
+            ts = 1000 + np.arange(n, dtype=np.int64)
+            rt.getInputHandler(sid).send_columns(ts, [np.arange(n, dtype=np.int64), np.array(k, np.uint32),
+                                                      rng.choice([15.0, 22.0, 25.0, 28.0], n), np.zeros(n, np.int32)])
+        rt.flush(deliver=False)
+        _, vals, _, seq = rt.poll_arrays(1)
+    finally:
+        rt.shutdown()
+    assert len(seq) > 5
+    # the emitting event is e3 (attribute d = its id = its index within B): position = 100 + d
+    assert np.array_equal(seq, n + vals[1])

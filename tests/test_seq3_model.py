@@ -22,7 +22,7 @@ def model(tr, lo, hi, f2kind, f3kind):
     for i, (ts, row) in enumerate(tr):
         keys.setdefault(row[1], []).append((i, row))
     f1 = lambda y: y[2] > 20
-    f2 = {"e1": lambda y, e1, l: y[2] > e1[2], "first": lambda y, e1, l: y[2] >= l[0][2] - 5}[f2kind]
+    f2 = {"e1": lambda y, e1, l: y[2] > e1[2], "first": lambda y, e1, l: y[2] >= l[0][2]}[f2kind]
     f3 = {"last": lambda y, e1, l: y[2] < l[-1][2], "e1": lambda y, e1, l: y[2] < e1[2]}[f3kind]
     out = []
     for k, evs in keys.items():
@@ -47,7 +47,7 @@ def trace(n, keys, seed, dom):
     return [(int(ts[i]), [i, "k%d" % rng.integers(0, keys), float(rng.choice(dom)), 0]) for i in range(n)]
 
 
-F2 = {"e1": "price>e1.price", "first": "price>=e2[0].price - 5"}
+F2 = {"e1": "price>e1.price", "first": "price>=e2[0].price"}
 F3 = {"last": "price<e2[last].price", "e1": "price<e1.price"}
 
 
