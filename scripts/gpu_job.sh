@@ -64,6 +64,7 @@ for s in "$@"; do
         seq3cfg) run seq3cfg 600 python3 scripts/bench_configs.py --only c3md,c3m --c3-steps 3 && run seq3gen 600 env SDG_NO_SEQ3=1 python3 scripts/bench_configs.py --only c3md --c3-steps 2 ;;
         seq3prof) run seq3prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/seq3prof" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 2 --warmup 1 ;;
         s3ab) run s3g16 600 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && run s3g8 600 env SDG_S3_G=8 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && run s3pmc 180 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/s3pmc" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 1 --warmup 0 && run s3pmcw 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/s3pmcw" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 1 --warmup 0 ;;
+        mr) run mr 600 python3 -u -m pytest tests/test_gpu_multirank.py -m gpu -x -v --timeout 500 --timeout-method thread -p no:cacheprovider ;;
         *) echo "unknown step $s" ;;
     esac
 done

@@ -285,7 +285,7 @@ struct QueryRt {
     // the register sequence kernel (seq3.hip) instead of the generic NFA: its per-key state, SoA with stride s3_kcap
     bool seq3 = false;
     Seq3Spec s3{};
-    DevBuf s3_hdr, s3_pn, s3_qn, s3_vals;
+    DevBuf s3_hdr, s3_pn, s3_qn, s3_vals, s3_ts;
     int64_t s3_kcap = 0;
     // outputs
     DevBuf o_ts, o_key, o_vals, o_nulls, o_emit, o_first, counters, flags;
@@ -479,7 +479,7 @@ bool seq3_spec(const HostQuery& h, Seq3Spec& s) {
 }
 bool seq3_spec_(const HostQuery& h, Seq3Spec& s, int& why) {
     const Plan& P = h.plan;
-    if (P.chain || !P.seq || P.n_states != 3 || P.has_within || P.n_sched || P.purge || P.has_post) return why = 1, false;
+    if (P.chain || !P.seq || P.n_states != 3 || P.n_sched || P.purge || P.has_post) return why = 1, false;
     if (h.streams.size() != 1 || P.n_cols < 1 || P.n_cols > S3_MAX_COLS || P.n_out > S3_MAX_OUT) return why = 2, false;
     for (int x : h.key_attr)
         if (x == -2) return why = 3, false;  // range partitions
@@ -503,6 +503,8 @@ bool seq3_spec_(const HostQuery& h, Seq3Spec& s, int& why) {
     s.n_out = P.n_out;
     s.min_count = r1.min_count;
     s.max_count = r1.max_count;
+    s.has_within = P.has_within;
+    s.within_ms = P.within_ms;
     for (int c = 0; c < P.n_cols; ++c) s.col_kind[c] = P.col_kind[c];
     // (slot, chain index) of a state event -> the register event of processor context `ctx`
     // (0: the e1 filter, the event is e1; 1: the e2 filter, Q with the event as e2[last]; 2: the e3 filter / select)
@@ -1337,7 +1339,14 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         a.key_flag = zero_copy ? flags + 4 : nullptr;  // caller-supplied device ids: range-check against K
         a.orig_in = d_vpos;                            // orig_sorted: view rows (+ pos_off), or positions
         int c = 0;
-        a.src[c] = d_ts; a.dst[c] = q.so_ts.ensure(nrows * 8); a.width[c] = 8; v_ts = (const int64_t*)a.dst[c]; ++c;
+        // the register sequence kernel reads ts only for its output rows: gathered through orig (view rows) from the
+        // arrival-order column instead of moved by every radix pass (a quarter of C3's sort traffic)
+        const bool ts_by_orig = q.seq3 && !fused && !d_vpos && !P.has_within;
+        if (ts_by_orig) {
+            v_ts = nullptr;
+        } else {
+            a.src[c] = d_ts; a.dst[c] = q.so_ts.ensure(nrows * 8); a.width[c] = 8; v_ts = (const int64_t*)a.dst[c]; ++c;
+        }
         if (d_qs) { a.src[c] = d_qs; a.dst[c] = q.so_qs.ensure(nrows); a.width[c] = 1; v_qs = (const uint8_t*)a.dst[c]; ++c; }
         if (d_vrank) { a.src[c] = d_vrank; a.dst[c] = q.so_vrank.ensure(nrows); a.width[c] = 1; v_vrank = (const uint8_t*)a.dst[c]; ++c; }
         for (int k = 0; k < nc; ++k) {
@@ -1411,6 +1420,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             grow(q.s3_pn, 4, 1);
             grow(q.s3_qn, 4, 1);
             grow(q.s3_vals, 8, 6 * s3nc);
+            grow(q.s3_ts, 8, 2);
             q.s3_kcap = nk;
         }
         Seq3Args a;
@@ -1418,6 +1428,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         a.sp = q.s3;
         a.n = nrows;
         a.ts = v_ts;
+        a.ts_view = d_ts;  // v_ts == nullptr: output ts = ts_view[orig[r]]
         a.seg_start = partitioned ? v_seg : nullptr;
         a.seg_end = partitioned ? v_segend : nullptr;
         a.K = (int32_t)KK;
@@ -1430,6 +1441,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         a.st_pn = q.s3_pn.as<uint32_t>();
         a.st_qn = q.s3_qn.as<uint32_t>();
         a.st_vals = q.s3_vals.as<int64_t>();
+        a.st_ts = q.s3_ts.as<int64_t>();
         a.kcap = q.s3_kcap;
         // at most one match per event: nrows records never overflow (no rerun, so the state updates in place)
         const int64_t cap = std::max<int64_t>(q.out_cap, nrows + 64);
@@ -2708,6 +2720,7 @@ void snapshot(sdg_engine* e, std::vector<uint8_t>& out) {
             w.dev(q.s3_pn.p, (size_t)q.s3_kcap * 4, st);
             w.dev(q.s3_qn.p, (size_t)q.s3_kcap * 4, st);
             w.dev(q.s3_vals.p, (size_t)q.s3_kcap * 8 * 6 * q.s3.nc, st);
+            w.dev(q.s3_ts.p, (size_t)q.s3_kcap * 16, st);
         }
         q.sim.save(out);
     }
@@ -2749,7 +2762,7 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
         View slot_of, idle_rec, slot_key, free_slots, pool_ctr;
         int64_t purge_first = INT64_MIN, agg_keys = 0;
         int64_t s3_kcap = 0;
-        View s3_hdr, s3_pn, s3_qn, s3_vals;
+        View s3_hdr, s3_pn, s3_qn, s3_vals, s3_ts;
         SchedSim sim;
     };
     const int64_t seq = r.get<int64_t>();
@@ -2828,9 +2841,10 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
             g.s3_pn = view();
             g.s3_qn = view();
             g.s3_vals = view();
+            g.s3_ts = view();
             const size_t kc = (size_t)g.s3_kcap;
             if (g.s3_hdr.n != kc * 4 || g.s3_pn.n != kc * 4 || g.s3_qn.n != kc * 4 ||
-                g.s3_vals.n != kc * 8 * 6 * (size_t)e->qs[qi]->s3.nc)
+                g.s3_vals.n != kc * 8 * 6 * (size_t)e->qs[qi]->s3.nc || g.s3_ts.n != kc * 16)
                 throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (sequence state)");
         }
         g.sim.setup(P.n_sched, P.partitioned, !P.playback);
@@ -2911,6 +2925,7 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
             up(q.s3_pn, g.s3_pn);
             up(q.s3_qn, g.s3_qn);
             up(q.s3_vals, g.s3_vals);
+            up(q.s3_ts, g.s3_ts);
         }
         q.sim = std::move(g.sim);
         HIPCHECK(hipStreamSynchronize(st));  // the views point into the caller's blob

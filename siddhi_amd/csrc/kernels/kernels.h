@@ -291,6 +291,8 @@ struct Seq3Spec {
     int32_t nc;                      // physical columns (<= S3_MAX_COLS), stored for every event of a partial
     int32_t n_out;
     int32_t min_count, max_count;    // max INT32_MAX: unbounded
+    int32_t has_within;              // `within T`: a partial whose e1 is more than T away is dropped before the event
+    int64_t within_ms;
     uint8_t col_kind[S3_MAX_COLS];
     S3Pred f[3];                     // e1 filter (Y = the e1 candidate), e2 filter (E1, E2F, Y = e2[last]),
                                      // e3 filter (E1, E2F, E2L of P, Y = e3)
@@ -299,7 +301,8 @@ struct Seq3Spec {
 struct Seq3Args {
     Seq3Spec sp;
     int64_t n;
-    const int64_t* ts;                // sorted view
+    const int64_t* ts;                // sorted view (nullptr: not sorted; the output ts is ts_view[orig[r]])
+    const int64_t* ts_view;           // arrival-order ts of the query's view rows
     const uint32_t* seg_start;        // [K] (nullptr: unpartitioned, one key over [0, n))
     const uint32_t* seg_end;
     int32_t K;
@@ -315,6 +318,7 @@ struct Seq3Args {
     uint32_t* st_pn;
     uint32_t* st_qn;
     int64_t* st_vals;
+    int64_t* st_ts;                   // [2][kcap] e1 timestamps of P and Q (has_within)
     int64_t kcap;
     // outputs (at most one record per event: out_cap >= n never overflows)
     int64_t out_cap;

@@ -37,29 +37,36 @@ namespace {
 template <int NC>
 struct S3Ev {
     int64_t v[NC];
+    // element-wise (a struct copy of 24+ bytes becomes a memcpy that pins the arrays to scratch)
+    __device__ __forceinline__ void set(const S3Ev& o) {
+#pragma unroll
+        for (int i = 0; i < NC; ++i) v[i] = o.v[i];
+    }
 };
 
+// e.v[c] for a (wave-uniform) column index, as masked ORs: a select chain over 3+ entries is turned into an
+// indexed load by the optimizer, which moves every such register array to scratch
 template <int NC>
 __device__ __forceinline__ int64_t s3_pick(const S3Ev<NC>& e, int c) {
-    int64_t r = e.v[0];
+    int64_t r = 0;
 #pragma unroll
-    for (int i = 1; i < NC; ++i)
-        if (c == i) r = e.v[i];
+    for (int i = 0; i < NC; ++i) r |= e.v[i] & -(int64_t)(c == i);
     return r;
 }
 
 // operand of a filter / select item in one partial's context (nm: the partial's null bits, yn: the event's);
-// false = null
+// false = null. Every candidate is picked and the result masked: a switch over the four events is merged by the
+// optimizer into a load through a selected pointer, which moves the events to scratch
 template <int NC>
 __device__ __forceinline__ bool s3_get(const S3Operand& o, const S3Ev<NC>& e1, const S3Ev<NC>& ef, const S3Ev<NC>& el,
                                        const S3Ev<NC>& y, uint32_t nm, uint32_t yn, int64_t* v) {
-    switch (o.src) {
-        case S3_E1: *v = s3_pick(e1, o.col); return !((nm >> o.col) & 1u);
-        case S3_E2F: *v = s3_pick(ef, o.col); return !((nm >> (8 + o.col)) & 1u);
-        case S3_E2L: *v = s3_pick(el, o.col); return !((nm >> (16 + o.col)) & 1u);
-        case S3_Y: *v = s3_pick(y, o.col); return !((yn >> o.col) & 1u);
-        default: *v = 0; return false;
-    }
+    const int c = o.col;
+    const int64_t m1 = -(int64_t)(o.src == S3_E1), mf = -(int64_t)(o.src == S3_E2F), ml = -(int64_t)(o.src == S3_E2L),
+                  my = -(int64_t)(o.src == S3_Y);
+    *v = (s3_pick(e1, c) & m1) | (s3_pick(ef, c) & mf) | (s3_pick(el, c) & ml) | (s3_pick(y, c) & my);
+    const uint32_t nb = o.src == S3_E1 ? (nm >> c) : o.src == S3_E2F ? (nm >> (8 + c)) : o.src == S3_E2L ? (nm >> (16 + c))
+                      : o.src == S3_Y ? (yn >> c) : 1u;
+    return !(nb & 1u);
 }
 
 // fast_pass (eval.h) over resolved operands: null -> false, Java binary numeric promotion to f.t
@@ -105,6 +112,9 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
     const int64_t kc = a.kcap;
     uint32_t hdr = 0, pn = 0, qn = 0;
     S3Ev<NC> P1{}, PF{}, PL{}, Q1{}, QF{}, QL{};
+    int64_t pts = 0, qts = 0;  // e1 timestamps (within)
+    const bool wth = sp.has_within != 0;
+    const int64_t within = sp.within_ms;
     if (has) {
         hdr = a.st_hdr[k];
         if (hdr & 2u) {
@@ -116,8 +126,12 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
                 QL.v[c] = a.st_vals[(int64_t)(5 * NC + c) * kc + k];
             }
         }
+        if (wth) {
+            if (hdr & 1u) pts = a.st_ts[k];
+            if (hdr & 2u) qts = a.st_ts[kc + k];
+        }
         if (hdr & 4u) {  // P is Q: stored once
-            P1 = Q1; PF = QF; PL = QL;
+            P1.set(Q1); PF.set(QF); PL.set(QL);
             pn = qn;
         } else if (hdr & 1u) {
             pn = a.st_pn[k];
@@ -132,7 +146,7 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
     const uint32_t mn = (uint32_t)sp.min_count, mx = (uint32_t)sp.max_count;
     const uint64_t lt = lanemask_lt();
     int staged = 0;
-    auto flush = [&]() {
+    auto flush = [&]() __attribute__((always_inline)) {
         __syncthreads();  // the staged records of every lane (one-wave block)
         unsigned long long base = 0;
         if (lane == 0) base = atomicAdd(a.out_count, (unsigned long long)staged);
@@ -154,16 +168,23 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
         staged = 0;
     };
     // one event through e3, e2, e1 (the state machine; y = the event, r its sorted row)
-    auto row_step = [&](const S3Ev<NC>& y, uint32_t ynn, int64_t yt, int64_t r) {
+    auto row_step = [&](const S3Ev<NC>& y, uint32_t ynn, int64_t yt, int64_t r) __attribute__((always_inline)) {
         const bool act = r < e;
+        if (wth && act) {  // stabilizeStates: expireEvents drops a partial whose e1 is more than T away (isExpired)
+            int64_t d = pts - yt;
+            if ((hdr & 1u) && (d < 0 ? -d : d) > within) hdr &= ~5u;
+            d = qts - yt;
+            if ((hdr & 2u) && (d < 0 ? -d : d) > within) hdr &= ~6u;
+        }
         // e3 (first in the receiver's order)
         const bool em = act && (hdr & 1u) && s3_pass(sp.f[2], P1, PF, PL, y, pn, ynn);
         const uint64_t m = __ballot(em);
         if (m) {
             if (em) {
                 const int at = staged + __popcll(m & lt);
-                l_ts[at] = yt;
-                l_seq[at] = a.seq_base + (a.orig ? (int64_t)a.orig[r] : a.pos_off + r);
+                const int64_t o = a.orig ? (int64_t)a.orig[r] : a.pos_off + r;
+                l_ts[at] = a.ts ? yt : a.ts_view[o];
+                l_seq[at] = a.seq_base + o;
                 l_key[at] = (uint32_t)k;
                 uint32_t nm = 0;
                 for (int j = 0; j < sp.n_out; ++j) {
@@ -182,17 +203,18 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
             if ((hdr & 2u) && !(em && (hdr & 4u))) {
                 const uint32_t n1 = cnt < 0xFFFFFFu ? cnt + 1 : cnt;
                 if (cnt == 0) {  // e2[0] is this event
-                    QF = y;
+                    QF.set(y);
                     qn = (qn & ~0xFF00u) | (ynn << 8);
                 }
                 if (s3_pass(sp.f[1], Q1, QF, y, y, qn, ynn) && n1 >= mn) {
-                    P1 = Q1;
-                    PF = QF;
-                    PL = y;
+                    pts = qts;
+                    P1.set(Q1);
+                    PF.set(QF);
+                    PL.set(y);
                     pn = (qn & 0xFFFFu) | (ynn << 16);
                     nh = 1u;
                     if (n1 != mx) {  // kept at e2 too: one object
-                        QL = y;
+                        QL.set(y);
                         qn = pn;
                         cnt = n1;
                         nh |= 2u | 4u;
@@ -201,7 +223,8 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
             }
             // e1: the every-seed starts a partial when e2's list is still empty
             if (!(nh & 2u) && s3_pass(sp.f[0], y, y, y, y, 0u, ynn)) {
-                Q1 = y;
+                Q1.set(y);
+                qts = yt;
                 qn = ynn;
                 cnt = 0;
                 nh |= 2u;
@@ -222,7 +245,7 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
 #pragma unroll
             for (int c = 0; c < NC; ++c) yv[g].v[c] = 0;
             if (r < e) {
-                yts[g] = a.ts[r];
+                if (a.ts) yts[g] = a.ts[r];
 #pragma unroll
                 for (int c = 0; c < NC; ++c) {
                     yv[g].v[c] = load_col(a.cols[c], sp.col_kind[c], r);
@@ -239,7 +262,7 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
             if (q4 + 4 < S3_G) {
 #pragma unroll
                 for (int g = 0; g + 4 < S3_G; ++g) {
-                    yv[g] = yv[g + 4];
+                    yv[g].set(yv[g + 4]);
                     yn[g] = yn[g + 4];
                     yts[g] = yts[g + 4];
                 }
@@ -249,6 +272,10 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
     if (staged) flush();
     if (has) {
         a.st_hdr[k] = hdr;
+        if (wth) {
+            if (hdr & 1u) a.st_ts[k] = pts;
+            if (hdr & 2u) a.st_ts[kc + k] = qts;
+        }
         if (hdr & 2u) {
             a.st_qn[k] = qn;
 #pragma unroll

@@ -16,14 +16,21 @@ the semantics the seq3 kernel (siddhi_amd/csrc/kernels/seq3.hip) implements. Der
 Test infrastructure only (tests/test_seq3_model.py pins it against the oracle on random traces)."""
 
 
-def run_key(events, f1, f2, f3, m, n):
+def run_key(events, f1, f2, f3, m, n, within=None, ts=None):
     """events: list of (pos, row) of ONE key in order; f1(y), f2(y, e1, e2_list_with_y), f3(y, e1, e2_list).
-    Returns [(pos, (e1, e2_list, y))] matches in order."""
+    within: `within T` (ts(row) gives an event's timestamp): before each event, stabilizeStates expires a partial
+    whose e1 is more than T away (StreamPreStateProcessor.isExpired :118-129; the every-start's extra seed from
+    withinEveryPreStateProcessor changes no output: e2 keeps one partial). Returns [(pos, (e1, e2_list, y))]."""
     out = []
     P = None      # partial at e3: (e1, e2 list)
     Q = None      # partial at e2: (e1, e2 list)
     same = False  # P is Q (one object)
     for pos, y in events:
+        if within is not None:
+            if P is not None and abs(ts(P[0]) - ts(y)) > within:
+                P, same = None, False
+            if Q is not None and abs(ts(Q[0]) - ts(y)) > within:
+                Q, same = None, False
         consumed = False
         if P is not None:
             if f3(y, P[0], P[1]):

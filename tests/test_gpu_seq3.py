@@ -51,6 +51,18 @@ def test_seq3_shapes_vs_oracle(lo, hi, f2kind, f3kind, oracle_built):
         assert len(ref) > 50
 
 
+@pytest.mark.parametrize("within", [0, 3, 8])
+@pytest.mark.parametrize("lo,hi", [(1, 5), (1, -1)])
+def test_seq3_within_vs_oracle(lo, hi, within, oracle_built):
+    """`within T`: partials whose e1 is more than T away are expired before the event (also across flushes)"""
+    app = seq_app(lo, hi, within=within)
+    tr = price_trace(6000, keys=13, seed=within * 7 + lo, dom=[15, 21, 22, 23, 25, 30])
+    ref, got = run_both(app, tr, 5)
+    assert got == ref
+    if within >= 3:
+        assert len(ref) > 50
+
+
 def test_seq3_ineligible_filter_runs_generic(oracle_built):
     """an arithmetic e2 filter is not a FastPred: the same shape stays on the generic keyed NFA"""
     app = seq_app(1, 5, F3["last"], "price>=e2[0].price - 5")

@@ -11,14 +11,16 @@ from seq3_model import run_key
 DEFS = "@app:playback define stream S (id long, key string, price double, volume int); "
 
 
-def app(lo, hi, f3="price<e2[last].price", f2="price>e1.price"):
+def app(lo, hi, f3="price<e2[last].price", f2="price>e1.price", within=None):
     q = "<%d:%d>" % (lo, hi) if hi >= 0 else ("+" if lo == 1 else "<%d:>" % lo)
-    return (DEFS + "partition with (key of S) begin @info(name='q') from every e1=S[price>20], e2=S[%s]%s, e3=S[%s] "
-            "select e1.id as a, e2[0].id as b, e2[last].id as c, e3.id as d insert into O; end;" % (f2, q, f3))
+    w = " within %d milliseconds" % within if within is not None else ""
+    return (DEFS + "partition with (key of S) begin @info(name='q') from every e1=S[price>20], e2=S[%s]%s, e3=S[%s]%s "
+            "select e1.id as a, e2[0].id as b, e2[last].id as c, e3.id as d insert into O; end;" % (f2, q, f3, w))
 
 
-def model(tr, lo, hi, f2kind, f3kind):
+def model(tr, lo, hi, f2kind, f3kind, within=None):
     keys = {}
+    tsof = {row[0]: ts for ts, row in tr}
     for i, (ts, row) in enumerate(tr):
         keys.setdefault(row[1], []).append((i, row))
     f1 = lambda y: y[2] > 20
@@ -26,7 +28,7 @@ def model(tr, lo, hi, f2kind, f3kind):
     f3 = {"last": lambda y, e1, l: y[2] < l[-1][2], "e1": lambda y, e1, l: y[2] < e1[2]}[f3kind]
     out = []
     for k, evs in keys.items():
-        for pos, (e1, l2, y) in run_key(evs, f1, f2, f3, lo, hi):
+        for pos, (e1, l2, y) in run_key(evs, f1, f2, f3, lo, hi, within, lambda r: tsof[r[0]]):
             out.append((pos, (e1[0], l2[0][0], l2[-1][0], y[0])))
     out.sort()
     return [(tr[p][0], v) for p, v in out]
@@ -63,6 +65,20 @@ def test_model_vs_oracle(lo, hi, f2kind, f3kind):
         assert model(tr, lo, hi, f2kind, f3kind) == want, (lo, hi, seed)
         total += len(want)
     if lo == 1:
+        assert total > 0
+
+
+@pytest.mark.parametrize("within", [0, 2, 5, 9])
+@pytest.mark.parametrize("lo,hi", [(1, 5), (1, -1), (2, 3)])
+def test_model_within_vs_oracle(lo, hi, within):
+    text = app(lo, hi, within=within)
+    total = 0
+    for seed in range(5):
+        tr = trace(800, keys=3 + seed, seed=seed * 11 + within, dom=[15, 21, 22, 23, 25, 30])
+        want = oracle(tr, text)
+        assert model(tr, lo, hi, "e1", "last", within) == want, (lo, hi, within, seed)
+        total += len(want)
+    if lo == 1 and within >= 2:
         assert total > 0
 
 
