@@ -261,6 +261,7 @@ struct QueryRt {
     DevBuf mv_work, mv_tot, mv_args, kt_vals_in;  // device-side views of mixed pushes
     // sorted view
     DevBuf so_ts, so_qs, so_key, so_orig, so_vrank, so_cols[MAX_COLS], so_nulls[MAX_COLS], seg, kg_counts, kg_gsum;
+    DevBuf so_lkey;                                 // fused path: u8 local keys of the bucket view
     DevBuf bk_plan;                                 // fused path: bstart[257] + bseg[257]
     // carries (double buffered)
     struct Carry {
@@ -1326,6 +1327,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     hp.mark("view");
     ev_record(e->ev[0], st);
     const uint32_t* v_segend = nullptr;
+    const uint32_t* v_ts32 = nullptr;  // fused path's slim bucket view (ts offsets, local keys)
+    const uint8_t* v_lkey = nullptr;
     int* flags = (int*)q.flags.ensure(32);  // [0] output overflow [1] decreasing ts [2] bounds [3] mono [4] key range
     int bbits = 0;
     uint32_t* b_start = nullptr;
@@ -1333,6 +1336,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     if (partitioned && nrows > 0) {
         KeyGroupArgs a;
         std::memset(&a, 0, sizeof a);
+        a.ts32_col = -1;
         a.n = nrows;
         a.K = (int32_t)K;
         a.keys = d_key;
@@ -1372,7 +1376,20 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             b_start = (uint32_t*)q.bk_plan.ensure(2 * 257 * 4);
             b_seg = b_start + 257;
             HIPCHECK(hipMemsetAsync(flags, 0, 32, st));
+            // the slim bucket view: ts as u32 offsets from the batch's first ts, keys as u8 local keys (the matcher
+            // regroups by them; the bucket is the range a row lies in)
+            static const bool wide = getenv("SDG_FU_WIDE") != nullptr;  // A/B: int64 ts + u32 keys
+            if (!wide) {
+                a.ts32_col = 0;
+                a.ts_base = d_ts;
+                a.lkey_out = (uint8_t*)q.so_lkey.ensure(nrows);
+            }
             bucketize(a, bbits, 0 /* ts is payload column 0 */, flags + 3, b_start, b_seg, FU_OWN, st, g_no_events ? nullptr : &e->ev[4]);
+            if (!wide) {
+                v_ts32 = (const uint32_t*)a.dst[0];
+                v_lkey = a.lkey_out;
+                v_ts = nullptr;
+            }
             if (getenv("SDG_DEBUG")) {  // validate the bucket plan on the host before the matcher reads it
                 std::vector<uint32_t> hp(2 * 257);
                 HIPCHECK(hipMemcpyAsync(hp.data(), b_start, 2 * 257 * 4, hipMemcpyDeviceToHost, st));
@@ -1386,7 +1403,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             HIPCHECK(hipMemsetAsync(flags, 0, 32, st));
             keygroup(a, st, g_no_events ? nullptr : &e->ev[4]);
         }
-        v_key = a.keys_sorted;
+        v_key = v_lkey ? nullptr : a.keys_sorted;
         v_seg = a.seg_start;
         v_segend = a.seg_end;
         v_orig = a.orig_sorted;
@@ -1960,6 +1977,9 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     a.consts = q.d_consts.as<int64_t>();
     a.n = nrows;
     a.ts = v_ts;
+    a.ts32 = v_ts32;
+    a.ts_base = v_ts32 ? d_ts : nullptr;
+    a.lkey = v_lkey;
     a.qstream = multi_stream ? v_qs : nullptr;
     a.key = partitioned ? v_key : nullptr;
     a.seg_start = partitioned ? v_seg : nullptr;

@@ -33,8 +33,16 @@ struct View {
 
 __device__ __forceinline__ bool in_view(const View& v, int64_t r) { return r >= v.lo && r < v.hi; }
 
+// the fused path's slim bucket view (bucketize): ts as u32 offsets from the batch's first ts, keys as u8 local keys
+__device__ __forceinline__ int64_t vts(const ChainArgs& a, int64_t r) {
+    return a.ts32 ? *a.ts_base + (int64_t)a.ts32[r] : a.ts[r];
+}
+// row r of a bucket view belongs to key kf (the caller scans kf's bucket, so the local key decides)
+__device__ __forceinline__ bool bkey_is(const ChainArgs& a, int64_t r, uint32_t kf) {
+    return a.lkey ? a.lkey[r] == (uint8_t)(kf >> a.bbits) : a.key[r] == kf;
+}
 __device__ __forceinline__ int64_t ts_row(const ChainArgs& a, const View& v, int64_t r) {
-    return in_view(v, r) ? cm_lds[v.ots + (r - v.lo)] : a.ts[r];
+    return in_view(v, r) ? cm_lds[v.ots + (r - v.lo)] : vts(a, r);
 }
 __device__ __forceinline__ int qs_row(const ChainArgs& a, const View& v, int64_t r) {
     if (!a.qstream) return 0;
@@ -157,7 +165,7 @@ __device__ int64_t scan_typed(const ChainArgs& a, const View& v, int64_t from, i
     for (; q < end; ++q) {
         if (filt) {  // bucket view rows are time-ordered: past the window at any row, no later row can match
             if (has_within && ts_row(a, v, q) - ts0 > within) return -1;
-            if (a.key[q] != kf) continue;
+            if (!bkey_is(a, q, kf)) continue;
             if (ts_row(a, v, q) < ts0) atomicOr(&a.flags[1], 1);  // the key's time went back across batches
         }
         // StreamPreStateProcessor.isExpired: |start.ts - now| > within, checked before the event is processed
@@ -206,7 +214,7 @@ __device__ __forceinline__ int64_t chain_scan(const ChainArgs& a, ChainAcc& acc,
     for (int64_t q = from; q < end; ++q) {
         if (a.bstart) {  // bucket view: time-ordered rows (see scan_typed)
             if (sp.has_within && ts_row(a, acc.V, q) - ts0 > sp.within_ms) return -1;
-            if (a.key[q] != kf) continue;
+            if (!bkey_is(a, q, kf)) continue;
             if (ts_row(a, acc.V, q) < ts0) atomicOr(&a.flags[1], 1);
         }
         if (sp.has_within) {
@@ -700,10 +708,10 @@ __device__ int64_t wave_scan_typed(const ChainArgs& a, int64_t from, int64_t end
             const int64_t q = q0 + u * 64 + lane;
             bool stop = false, hit = false;
             if (q < end) {
-                const int64_t d = a.ts[q] - ts0;
+                const int64_t d = vts(a, q) - ts0;
                 if (filt && has_within && d > within) {
                     stop = true;  // time-ordered bucket: no later row of the key is alive
-                } else if (!filt || a.key[q] == kf) {
+                } else if (!filt || bkey_is(a, q, kf)) {
                     if (filt && d < 0) atomicOr(&a.flags[1], 1);  // the key's time went back across batches
                     if (has_within && (d < 0 ? -d : d) > within) stop = true;  // isExpired at this event of the key
                     else if (qs_row(a, View{}, q) == a.s1) {
@@ -796,7 +804,7 @@ __global__ __launch_bounds__(256) void chain_carry_wave_k(const ChainArgs* __res
             b = key < (uint32_t)a.K ? (int64_t)a.seg_start[key] : 0;
             e = key < (uint32_t)a.K ? (int64_t)a.seg_end[key] : 0;
         }
-        if (!a.bstart && b < e && a.ts[b] < a.cin_ts[c] && lane == 0) atomicOr(&a.flags[1], 1);  // time went back
+        if (!a.bstart && b < e && vts(a, b) < a.cin_ts[c] && lane == 0) atomicOr(&a.flags[1], 1);  // time went back
         ChainAcc acc{&a, View{}, -1, c, -1};
         int64_t k = sp.scan_konst;
         uint8_t op = sp.scan_op;
@@ -920,8 +928,8 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
 #pragma unroll
         for (int x = 0; x < NW; ++x) wc[x][d] = 0;
     if (!FU_OK(lo >= 0 && nr >= 1 && lo + nr <= a.n && b < a.nb, 1)) return;
-    const int64_t tbase = a.ts[lo];
-    const int64_t tlast = a.ts[lo + nr - 1];
+    const int64_t tbase = vts(a, lo);
+    const int64_t tlast = vts(a, lo + nr - 1);
     uint32_t rkey[FU_PT];
     int64_t rts[FU_PT], rx[FU_PT];
     const void* xcol = a.cols[col];
@@ -929,8 +937,13 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
     for (int r = 0; r < FU_PT; ++r) {
         const int row = w * WROWS + r * 64 + lane;
         const int64_t g = lo + min(row, nr - 1);  // clamped: rows past nr are loaded but not staged
-        rkey[r] = a.key[g];
-        rts[r] = a.ts[g];
+        if (a.lkey) {  // slim view: u8 local key, u32 ts offset
+            rkey[r] = (uint32_t)a.lkey[g] << a.bbits;
+            rts[r] = tbase + ((int64_t)a.ts32[g] - (int64_t)a.ts32[lo]);
+        } else {
+            rkey[r] = a.key[g];
+            rts[r] = a.ts[g];
+        }
         rx[r] = kind == VK_F64 || kind == VK_I64 ? ((const int64_t*)xcol)[g] : load_col(xcol, kind, g);
     }
     FU_TRACE(2);
@@ -1274,7 +1287,8 @@ __global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __r
         if (out == MQ_CARRY) {
             const int64_t cs = (int64_t)bbase[1] + wcnt[1][k][w] + __popcll(bc & lt);
             if (cs >= a.carry_cap) atomicOr(&a.flags[0], 1);
-            else if (FU_OK(p < a.n, 7)) emit_carry(a, View{}, cs, p, a.key[p], a.seq_base + (int64_t)a.orig[p]);
+            else if (FU_OK(p < a.n, 7))
+                emit_carry(a, View{}, cs, p, ((uint32_t)s_lk[sw(pos)] << a.bbits) | (uint32_t)b, a.seq_base + (int64_t)a.orig[p]);
         } else {
             const int64_t os = (int64_t)bbase[2] + wcnt[2][k][w] + __popcll(bo & lt);
             if (FU_OK(os < a.n, 8)) a.ovf_rows[os] = (uint32_t)p;  // os < the batch's rows (capacity n)
@@ -1297,9 +1311,15 @@ __global__ __launch_bounds__(256) void chain_fovf_k(const ChainArgs* __restrict_
         if (i < total) {
             p = a.ovf_rows[i];
             acc.r0 = p;
-            key = a.key[p];
-            const int64_t end = a.bstart[(key & ((1u << a.bbits) - 1u)) + 1];
-            const int64_t q = chain_scan<false>(a, acc, p + 1, end, a.ts[p], nullptr, 0, key);
+            int bl = 0, bh = a.nb;  // the bucket of row p: the last one starting at or before it
+            while (bh - bl > 1) {
+                const int mid = (bl + bh) >> 1;
+                if ((int64_t)a.bstart[mid] <= p) bl = mid;
+                else bh = mid;
+            }
+            key = a.lkey ? (((uint32_t)a.lkey[p] << a.bbits) | (uint32_t)bl) : a.key[p];
+            const int64_t end = a.bstart[bl + 1];
+            const int64_t q = chain_scan<false>(a, acc, p + 1, end, vts(a, p), nullptr, 0, key);
             if (q >= 0) { has = true; qhit = q; }
             else if (q == -2) carry = true;
         }

@@ -41,6 +41,12 @@ struct KeyGroupArgs {
     int* key_flag;                    // non-null: set to 1 when some key >= K (the first histogram pass checks)
     const uint32_t* orig_in;          // [n] batch position of each input row (nullptr: the row index itself);
                                       // orig_sorted then holds positions
+    // bucketize only (the fused path's slim bucket view): payload column ts32_col (int64 ts) is written as u32
+    // offsets from *ts_base (the batch's first ts; an offset past 2^32 sets the mono flag), and the keys as u8 local
+    // keys key >> bits into lkey_out instead of keys_sorted (ts32_col < 0 / lkey_out nullptr: off)
+    int32_t ts32_col = -1;
+    const int64_t* ts_base = nullptr;
+    uint8_t* lkey_out = nullptr;
 };
 // bytes of workspace for n events; fills the workspace pointers of `a` from `base`
 size_t keygroup_workspace(int64_t n, int32_t K, int32_t ncols, const uint8_t* widths);
@@ -160,6 +166,11 @@ struct ChainArgs {
     // fused bucket path (chain_fused_k): the view is bucket-ordered (bucketize), not key-sorted. bstart != nullptr
     // switches chain_carry_k / chain_fovf_k to scanning a key's bucket with a key filter.
     const uint32_t* bstart;           // [nb + 1] bucket row ranges
+    // the slim bucket view (bucketize with ts32 / lkey): ts = *ts_base + ts32[r], key = lkey[r] << bbits | bucket;
+    // ts / key are nullptr then
+    const uint32_t* ts32;
+    const int64_t* ts_base;
+    const uint8_t* lkey;
     const uint32_t* bseg;             // [nb + 1] block plan (exclusive prefix of segments per bucket)
     int32_t nb, bbits, lbits;         // buckets = 2^bbits; local key = key >> bbits < 2^lbits <= 256
     volatile int64_t* dbg;            // SDG_DEBUG: host-mapped progress trace [block * 4 + wave] (nullptr: off)

@@ -154,6 +154,10 @@ struct RxPass {
     int bits;
     int mono_col;             // >= 0: payload column holding ts; flag a decrease in arrival order (bucketize)
     int* mono_flag;
+    int ts32_col;             // >= 0: that payload column (int64 ts) is written as u32 offsets from *ts_base
+    const int64_t* ts_base;
+    uint8_t* lkey_out;        // non-null: u8 keys >> lkey_shift here instead of keys_out
+    int lkey_shift;
 };
 
 // stable tile scatter. Tile element e = w * 1024 + r * 64 + lane belongs to wave w (16 rounds r), so a wave
@@ -282,8 +286,10 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {  // 4 wa
         }
         __syncthreads();
         if (c + 1 < a.ncols) load_word(c + 1, nxt);
-        const int wd = c < 0 ? 8 : a.width[c];
+        const bool to32 = c >= 0 && c == a.ts32_col;
+        const int wd = c < 0 ? 8 : to32 ? 4 : a.width[c];
         void* dst = c < 0 ? nullptr : a.dst[c];
+        const int64_t tb = to32 ? *a.ts_base : 0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int j = r * RX_THREADS + t;
@@ -292,8 +298,13 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {  // 4 wa
                 const uint32_t o = gbase[dj] + (uint32_t)j - tstart[dj];
                 const uint64_t v = stage[j];
                 if (c < 0) {
-                    a.keys_out[o] = (uint32_t)v;
+                    if (a.lkey_out) a.lkey_out[o] = (uint8_t)((uint32_t)v >> a.lkey_shift);
+                    else a.keys_out[o] = (uint32_t)v;
                     a.orig_out[o] = (uint32_t)(v >> 32);
+                } else if (to32) {
+                    const int64_t d = (int64_t)v - tb;
+                    if ((uint64_t)d > 0xFFFFFFFFull) *a.mono_flag = 1;  // span past u32 (or time went back)
+                    ((uint32_t*)dst)[o] = (uint32_t)d;
                 } else if (wd == 8) {
                     ((uint64_t*)dst)[o] = v;
                 } else if (wd == 4) {
@@ -690,6 +701,7 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
         rp.nb = nb;
         rp.bits = b;
         rp.mono_col = -1;
+        rp.ts32_col = -1;
         hipLaunchKernelGGL(rx_scatter, dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, rp);
     }
     if (marks) (void)hipEventRecord(marks[2], stream);
@@ -765,6 +777,10 @@ void bucketize(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, uint
     rp.bits = bits;
     rp.mono_col = ts_col;
     rp.mono_flag = mono_flag;
+    rp.ts32_col = a.ts32_col;
+    rp.ts_base = a.ts_base;
+    rp.lkey_out = a.lkey_out;
+    rp.lkey_shift = bits;
     hipLaunchKernelGGL(rx_scatter, dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, rp);
     if (marks) (void)hipEventRecord(marks[2], stream);
     hipLaunchKernelGGL(bk_plan, dim3(1), dim3(256), 0, stream, a.tot, a.n, nb, seg_rows, bstart, bseg);
