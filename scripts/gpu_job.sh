@@ -65,6 +65,9 @@ for s in "$@"; do
         seq3prof) run seq3prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/seq3prof" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 2 --warmup 1 ;;
         s3ab) run s3g16 600 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && run s3g8 600 env SDG_S3_G=8 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && run s3pmc 180 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/s3pmc" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 1 --warmup 0 && run s3pmcw 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/s3pmcw" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 1 --warmup 0 ;;
         mr) run mr 600 python3 -u -m pytest tests/test_gpu_multirank.py -m gpu -x -v --timeout 500 --timeout-method thread -p no:cacheprovider ;;
+        s3ab2) run s3f16 600 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && run s3f8 600 env SDG_S3_G=8 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && run s3gen 600 env SDG_S3_GENERIC=1 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && run s3prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/s3prof" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 2 --warmup 1 ;;
+        s3pmc2) run s3sw 600 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && run s3sw8 600 env SDG_S3_G=8 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && i=0 && for c in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_INSTS_FLAT SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS" "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE"; do i=$((i+1)); run s3c$i 180 rocprofv3 --pmc $c --kernel-trace -d "$OUT/s3c$i" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 1 --warmup 1 || break; done ;;
+        cfgall) run cfgall 900 python3 scripts/bench_configs.py --only c1,c3m,c3md,c4 --c3-steps 3 ;;
         *) echo "unknown step $s" ;;
     esac
 done

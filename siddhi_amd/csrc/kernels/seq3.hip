@@ -13,7 +13,7 @@
 //       accepts only if Q did not stay there (its newAndEvery list is still empty)
 // tests/seq3_model.py is this model in Python; tests/test_seq3_model.py checks it against the oracle.
 //
-// One lane per partition key walks the key's events of the key-sorted view (16 rows loaded per step); the rest of
+// One lane per partition key walks the key's events of the key-sorted view (8 rows loaded per step); the rest of
 // the state machine is register arithmetic. Matches (at most one per event) are ranked with a wave ballot, staged
 // in LDS and written out as coalesced runs with one global reservation per S3_STAGE - 64 records (a reservation per
 // wave-step would serialise ~10^6 atomics on one L2 address).
@@ -29,10 +29,12 @@ namespace sdg {
 
 namespace {
 
-// rows loaded per step, all loads issued before the step's state machine runs. Each lane walks its own key's
-// segment, so one load instruction touches 64 cache lines; a step of 16 8-byte rows consumes whole 128-byte lines
-// while they are in flight (4 rows per step measured 6.6 ms per 10^8 events on C3: with ~11 waves per CU the lines
-// were evicted between steps and refetched, ~16x the algorithmic read traffic)
+// Rows are loaded S3_G per step (all loads issued before the step's state machine runs), the registers rotating by
+// four through one copy of the 4-row body. Measured on C3 (10^8 events, 10^6 keys; profiles/r3q_*, r3r): the kernel
+// is issue-bound, not memory-bound -- FETCH_SIZE 2-3x the algorithmic bytes, ~600 instructions per row (26k VALU +
+// 33k SALU per wave for ~100 rows: uniform operand dispatch, divergent state updates). 4-row steps with the kind
+// dispatch inlined at every compare made a 48-63 KB kernel (6.6 ms); the F64 variant (8-byte columns, double
+// compares) and an out-of-line generic compare brought it to ~25 KB (6.0 ms at 16 rows per step, less at 8).
 
 template <int NC>
 struct S3Ev {
@@ -55,38 +57,50 @@ __device__ __forceinline__ int64_t s3_pick(const S3Ev<NC>& e, int c) {
 }
 
 // operand of a filter / select item in one partial's context (nm: the partial's null bits, yn: the event's);
-// false = null. Every candidate is picked and the result masked: a switch over the four events is merged by the
-// optimizer into a load through a selected pointer, which moves the events to scratch
+// false = null. `src` is wave-uniform, so this is a scalar branch; the empty asm in each arm keeps the optimizer
+// from merging the arms into one load through a selected pointer (which moves the four events to scratch)
 template <int NC>
 __device__ __forceinline__ bool s3_get(const S3Operand& o, const S3Ev<NC>& e1, const S3Ev<NC>& ef, const S3Ev<NC>& el,
                                        const S3Ev<NC>& y, uint32_t nm, uint32_t yn, int64_t* v) {
     const int c = o.col;
-    const int64_t m1 = -(int64_t)(o.src == S3_E1), mf = -(int64_t)(o.src == S3_E2F), ml = -(int64_t)(o.src == S3_E2L),
-                  my = -(int64_t)(o.src == S3_Y);
-    *v = (s3_pick(e1, c) & m1) | (s3_pick(ef, c) & mf) | (s3_pick(el, c) & ml) | (s3_pick(y, c) & my);
-    const uint32_t nb = o.src == S3_E1 ? (nm >> c) : o.src == S3_E2F ? (nm >> (8 + c)) : o.src == S3_E2L ? (nm >> (16 + c))
-                      : o.src == S3_Y ? (yn >> c) : 1u;
+    int64_t x = 0;
+    uint32_t nb = 1u;
+    switch (o.src) {
+        case S3_E1: x = s3_pick(e1, c); asm volatile("" : "+v"(x)); nb = nm >> c; break;
+        case S3_E2F: x = s3_pick(ef, c); asm volatile("" : "+v"(x)); nb = nm >> (8 + c); break;
+        case S3_E2L: x = s3_pick(el, c); asm volatile("" : "+v"(x)); nb = nm >> (16 + c); break;
+        case S3_Y: x = s3_pick(y, c); asm volatile("" : "+v"(x)); nb = yn >> c; break;
+        default: break;
+    }
+    *v = x;
     return !(nb & 1u);
 }
 
-// fast_pass (eval.h) over resolved operands: null -> false, Java binary numeric promotion to f.t
-template <int NC>
+// the generic comparison (any kinds, Java binary numeric promotion): one out-of-line copy -- inlined at every call
+// site, its kind / operator switches made the kernel ~60 KB, and instruction fetch, not memory, bound it
+__device__ __noinline__ bool s3_cmp_generic(uint32_t opt, uint32_t kinds, int64_t x, int64_t z) {
+    const uint8_t op = (uint8_t)opt, t = (uint8_t)(opt >> 8), ka = (uint8_t)kinds, kb = (uint8_t)(kinds >> 8);
+    x = cvt(x, ka, t);
+    if (!(kinds >> 16)) z = cvt(z, kb, t);  // FP_CONST: already of kind t
+    return cmp(op, t, x, z);
+}
+
+// fast_pass (eval.h) over resolved operands: null -> false, Java binary numeric promotion to f.t. F64: every
+// predicate compares doubles (operands and constants already double: no conversion)
+template <bool F64, int NC>
 __device__ __forceinline__ bool s3_pass(const S3Pred& f, const S3Ev<NC>& e1, const S3Ev<NC>& ef, const S3Ev<NC>& el,
                                         const S3Ev<NC>& y, uint32_t nm, uint32_t yn) {
     if (f.kind == FP_TRUE) return true;
     int64_t x, z;
     if (!s3_get(f.a, e1, ef, el, y, nm, yn, &x)) return false;
-    x = cvt(x, f.a.kind, f.t);
-    if (f.kind == FP_CONST) {
-        z = f.konst;
-    } else {
-        if (!s3_get(f.b, e1, ef, el, y, nm, yn, &z)) return false;
-        z = cvt(z, f.b.kind, f.t);
-    }
-    return cmp(f.op, f.t, x, z);
+    if (f.kind == FP_CONST) z = f.konst;
+    else if (!s3_get(f.b, e1, ef, el, y, nm, yn, &z)) return false;
+    if (F64) return cmpT<double>(f.op, bits_f64(x), bits_f64(z));
+    return s3_cmp_generic((uint32_t)f.op | ((uint32_t)f.t << 8), (uint32_t)f.a.kind | ((uint32_t)f.b.kind << 8) |
+                                                                     (f.kind == FP_CONST ? 1u << 16 : 0u), x, z);
 }
 
-template <int NC, int S3_G>
+template <int NC, int S3_G, bool F64>
 __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
     const Seq3Args& a = *pa;
     const Seq3Spec& sp = a.sp;
@@ -177,7 +191,7 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
             if ((hdr & 2u) && (d < 0 ? -d : d) > within) hdr &= ~6u;
         }
         // e3 (first in the receiver's order)
-        const bool em = act && (hdr & 1u) && s3_pass(sp.f[2], P1, PF, PL, y, pn, ynn);
+        const bool em = act && (hdr & 1u) && s3_pass<F64>(sp.f[2], P1, PF, PL, y, pn, ynn);
         const uint64_t m = __ballot(em);
         if (m) {
             if (em) {
@@ -206,7 +220,7 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
                     QF.set(y);
                     qn = (qn & ~0xFF00u) | (ynn << 8);
                 }
-                if (s3_pass(sp.f[1], Q1, QF, y, y, qn, ynn) && n1 >= mn) {
+                if (s3_pass<F64>(sp.f[1], Q1, QF, y, y, qn, ynn) && n1 >= mn) {
                     pts = qts;
                     P1.set(Q1);
                     PF.set(QF);
@@ -222,7 +236,7 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
                 }
             }
             // e1: the every-seed starts a partial when e2's list is still empty
-            if (!(nh & 2u) && s3_pass(sp.f[0], y, y, y, y, 0u, ynn)) {
+            if (!(nh & 2u) && s3_pass<F64>(sp.f[0], y, y, y, y, 0u, ynn)) {
                 Q1.set(y);
                 qts = yt;
                 qn = ynn;
@@ -248,7 +262,7 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
                 if (a.ts) yts[g] = a.ts[r];
 #pragma unroll
                 for (int c = 0; c < NC; ++c) {
-                    yv[g].v[c] = load_col(a.cols[c], sp.col_kind[c], r);
+                    yv[g].v[c] = F64 ? ((const int64_t*)a.cols[c])[r] : load_col(a.cols[c], sp.col_kind[c], r);
                     if (a.nulls[c] && a.nulls[c][r]) yn[g] |= 1u << c;
                 }
             }
@@ -303,20 +317,35 @@ void seq3_run(const Seq3Args& a, const Seq3Args* d_a, hipStream_t stream) {
     if (a.K <= 0 || a.n <= 0) return;
     const unsigned grid = (unsigned)((a.K + 63) / 64);
     const size_t lds = (size_t)S3_STAGE * (16 + 8 * (size_t)a.sp.n_out + 8);
-    static const char* gs = getenv("SDG_S3_G");  // A/B: rows loaded per step (8 or 16)
-    const bool g16 = !(gs && atoi(gs) == 8);
+    // rows loaded per step: 8 (C3 12.9 ms per 10^8 events vs 13.6 with 16: fewer VGPRs, more waves; r3q)
+    static const char* gs = getenv("SDG_S3_G");  // A/B
+    const bool g16 = gs && atoi(gs) == 16;
+    // F64: 8-byte columns and double comparisons only (C3): no kind dispatch in the row loop
+    bool f64 = !getenv("SDG_S3_GENERIC");
+    for (int c = 0; c < a.sp.nc; ++c) f64 &= a.sp.col_kind[c] == VK_I64 || a.sp.col_kind[c] == VK_F64;
+    for (int p = 0; p < 3; ++p) {
+        const S3Pred& f = a.sp.f[p];
+        if (f.kind == FP_TRUE) continue;
+        f64 &= f.t == VK_F64 && f.a.kind == VK_F64 && (f.kind == FP_CONST || f.b.kind == VK_F64);
+    }
+#define S3_LAUNCH(NC_, G_)                                                                              \
+    do {                                                                                                \
+        if (f64) hipLaunchKernelGGL((seq3_k<NC_, G_, true>), dim3(grid), dim3(64), lds, stream, d_a);   \
+        else hipLaunchKernelGGL((seq3_k<NC_, G_, false>), dim3(grid), dim3(64), lds, stream, d_a);      \
+    } while (0)
     switch (a.sp.nc) {
         case 1:
-            if (g16) hipLaunchKernelGGL((seq3_k<1, 16>), dim3(grid), dim3(64), lds, stream, d_a);
-            else hipLaunchKernelGGL((seq3_k<1, 8>), dim3(grid), dim3(64), lds, stream, d_a);
+            if (g16) S3_LAUNCH(1, 16);
+            else S3_LAUNCH(1, 8);
             break;
         case 2:
-            if (g16) hipLaunchKernelGGL((seq3_k<2, 16>), dim3(grid), dim3(64), lds, stream, d_a);
-            else hipLaunchKernelGGL((seq3_k<2, 8>), dim3(grid), dim3(64), lds, stream, d_a);
+            if (g16) S3_LAUNCH(2, 16);
+            else S3_LAUNCH(2, 8);
             break;
-        case 3: hipLaunchKernelGGL((seq3_k<3, 8>), dim3(grid), dim3(64), lds, stream, d_a); break;
-        default: hipLaunchKernelGGL((seq3_k<4, 8>), dim3(grid), dim3(64), lds, stream, d_a); break;
+        case 3: S3_LAUNCH(3, 8); break;
+        default: S3_LAUNCH(4, 8); break;
     }
+#undef S3_LAUNCH
 }
 
 }  // namespace sdg
