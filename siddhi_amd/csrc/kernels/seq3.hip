@@ -44,6 +44,10 @@ struct S3Ev {
 #pragma unroll
         for (int i = 0; i < NC; ++i) v[i] = o.v[i];
     }
+    __device__ __forceinline__ void set_if(bool c, const S3Ev& o) {  // a select, not a branch
+#pragma unroll
+        for (int i = 0; i < NC; ++i) v[i] = c ? o.v[i] : v[i];
+    }
 };
 
 // e.v[c] for a (wave-uniform) column index, as masked ORs: a select chain over 3+ entries is turned into an
@@ -100,7 +104,7 @@ __device__ __forceinline__ bool s3_pass(const S3Pred& f, const S3Ev<NC>& e1, con
                                                                      (f.kind == FP_CONST ? 1u << 16 : 0u), x, z);
 }
 
-template <int NC, int S3_G, bool F64>
+template <int NC, int S3_G, bool F64, bool SEL>
 __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
     const Seq3Args& a = *pa;
     const Seq3Spec& sp = a.sp;
@@ -182,7 +186,66 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
         staged = 0;
     };
     // one event through e3, e2, e1 (the state machine; y = the event, r its sorted row)
+    // The state updates are selects, not branches: with divergent lanes every branch of a per-row if/else ran anyway,
+    // and the exec-mask bookkeeping around them cost more than the selects
     auto row_step = [&](const S3Ev<NC>& y, uint32_t ynn, int64_t yt, int64_t r) __attribute__((always_inline)) {
+        const bool act = r < e;
+        bool hasP = act && (hdr & 1u), hasQ = act && (hdr & 2u);
+        const bool same = (hdr & 4u) != 0;
+        if (wth) {  // stabilizeStates: expireEvents drops a partial whose e1 is more than T away (isExpired)
+            int64_t d = pts - yt;
+            hasP = hasP && (d < 0 ? -d : d) <= within;
+            d = qts - yt;
+            hasQ = hasQ && (d < 0 ? -d : d) <= within;
+        }
+        // e3 (first in the receiver's order)
+        const bool em = hasP && s3_pass<F64>(sp.f[2], P1, PF, PL, y, pn, ynn);
+        const uint64_t m = __ballot(em);
+        if (m) {
+            if (em) {
+                const int at = staged + __popcll(m & lt);
+                const int64_t o = a.orig ? (int64_t)a.orig[r] : a.pos_off + r;
+                l_ts[at] = a.ts ? yt : a.ts_view[o];
+                l_seq[at] = a.seq_base + o;
+                l_key[at] = (uint32_t)k;
+                uint32_t nm = 0;
+                for (int j = 0; j < sp.n_out; ++j) {
+                    int64_t v;
+                    const bool ok = s3_get(sp.out[j], P1, PF, PL, y, pn, ynn, &v);
+                    l_vals[j * S3_STAGE + at] = ok ? v : 0;
+                    if (!ok) nm |= 1u << j;
+                }
+                l_nul[at] = nm;
+            }
+            staged += __popcll(m);
+        }
+        // e2: Q takes the event unless e3 just consumed the same object; e2[0] is this event when Q has none yet
+        const uint32_t cnt = hdr >> 8;
+        const uint32_t n1 = cnt < 0xFFFFFFu ? cnt + 1 : cnt;
+        const bool qfirst = cnt == 0;
+        QF.set_if(qfirst, y);
+        const uint32_t qn2 = qfirst ? ((qn & ~0xFF00u) | (ynn << 8)) : qn;
+        const bool adv = hasQ && !(em && same) && n1 >= mn && s3_pass<F64>(sp.f[1], Q1, QF, y, y, qn2, ynn);
+        const bool keep = adv && n1 != mx;  // kept at e2 too: one object
+        const uint32_t pn2 = (qn2 & 0xFFFFu) | (ynn << 16);
+        P1.set_if(adv, Q1);
+        PF.set_if(adv, QF);
+        PL.set_if(adv, y);
+        pn = adv ? pn2 : pn;
+        pts = adv ? qts : pts;
+        QL.set_if(keep, y);
+        // e1: the every-seed starts a partial when e2's list is still empty
+        const bool fresh = act && !keep && s3_pass<F64>(sp.f[0], y, y, y, y, 0u, ynn);
+        Q1.set_if(fresh, y);
+        qts = fresh ? yt : qts;
+        qn = fresh ? ynn : keep ? pn2 : qn;
+        const uint32_t ncnt = fresh ? 0u : keep ? n1 : cnt;
+        const uint32_t nh = (adv ? 1u : 0u) | (keep || fresh ? 2u : 0u) | (keep ? 4u : 0u);
+        hdr = act ? (nh | (ncnt << 8)) : hdr;
+        if (staged > S3_STAGE - 64) flush();
+    };
+    // the branchy form of the same step (A/B: SDG_S3_BRANCH=1)
+    auto row_step_br = [&](const S3Ev<NC>& y, uint32_t ynn, int64_t yt, int64_t r) __attribute__((always_inline)) {
         const bool act = r < e;
         if (wth && act) {  // stabilizeStates: expireEvents drops a partial whose e1 is more than T away (isExpired)
             int64_t d = pts - yt;
@@ -272,7 +335,10 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
 #pragma unroll 1
         for (int q4 = 0; q4 < S3_G; q4 += 4) {
 #pragma unroll
-            for (int g = 0; g < 4; ++g) row_step(yv[g], yn[g], yts[g], b + i + q4 + g);
+            for (int g = 0; g < 4; ++g) {
+                if (SEL) row_step(yv[g], yn[g], yts[g], b + i + q4 + g);
+                else row_step_br(yv[g], yn[g], yts[g], b + i + q4 + g);
+            }
             if (q4 + 4 < S3_G) {
 #pragma unroll
                 for (int g = 0; g + 4 < S3_G; ++g) {
@@ -322,6 +388,7 @@ void seq3_run(const Seq3Args& a, const Seq3Args* d_a, hipStream_t stream) {
     const bool g16 = gs && atoi(gs) == 16;
     // F64: 8-byte columns and double comparisons only (C3): no kind dispatch in the row loop
     bool f64 = !getenv("SDG_S3_GENERIC");
+    static const bool sel = !getenv("SDG_S3_BRANCH");  // A/B: the branchy state update (F64 variant only)
     for (int c = 0; c < a.sp.nc; ++c) f64 &= a.sp.col_kind[c] == VK_I64 || a.sp.col_kind[c] == VK_F64;
     for (int p = 0; p < 3; ++p) {
         const S3Pred& f = a.sp.f[p];
@@ -330,8 +397,9 @@ void seq3_run(const Seq3Args& a, const Seq3Args* d_a, hipStream_t stream) {
     }
 #define S3_LAUNCH(NC_, G_)                                                                              \
     do {                                                                                                \
-        if (f64) hipLaunchKernelGGL((seq3_k<NC_, G_, true>), dim3(grid), dim3(64), lds, stream, d_a);   \
-        else hipLaunchKernelGGL((seq3_k<NC_, G_, false>), dim3(grid), dim3(64), lds, stream, d_a);      \
+        if (f64 && sel) hipLaunchKernelGGL((seq3_k<NC_, G_, true, true>), dim3(grid), dim3(64), lds, stream, d_a);  \
+        else if (f64) hipLaunchKernelGGL((seq3_k<NC_, G_, true, false>), dim3(grid), dim3(64), lds, stream, d_a);   \
+        else hipLaunchKernelGGL((seq3_k<NC_, G_, false, true>), dim3(grid), dim3(64), lds, stream, d_a);           \
     } while (0)
     switch (a.sp.nc) {
         case 1:
