@@ -464,6 +464,42 @@ def run_c5(args, rank, world, local, dist):
         dist.destroy_process_group()
 
 
+class _HostStagedDist:
+    """torch.distributed over gloo with CUDA tensors staged through host memory: a rehearsal of the N > 1 path
+    (SDG_BENCH_BACKEND=gloo, every rank on one GPU with SDG_BENCH_SHARE_GPU=1) on a one-GPU box. The measured
+    multi-GPU runs use the nccl backend (RCCL over xGMI) directly."""
+
+    def __init__(self, d):
+        self.d = d
+        self.ReduceOp = d.ReduceOp
+
+    def barrier(self):
+        self.d.barrier()
+
+    def all_gather(self, out, t):
+        host = [x.cpu() for x in out]
+        self.d.all_gather(host, t.cpu())
+        for x, y in zip(out, host):
+            x.copy_(y)
+
+    def all_reduce(self, t, op=None):
+        c = t.cpu()
+        self.d.all_reduce(c, op=op if op is not None else self.d.ReduceOp.SUM)
+        t.copy_(c)
+
+    def send(self, t, dst):
+        self.d.send(t.contiguous().cpu(), dst=dst)
+
+    def recv(self, t, src):
+        import torch
+        c = torch.empty(t.shape, dtype=t.dtype)
+        self.d.recv(c, src=src)
+        t.copy_(c)
+
+    def destroy_process_group(self):
+        self.d.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -491,11 +527,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("SDG_BENCH_SHARE_GPU"):  # rehearsal: every rank on GPU 0 (see _HostStagedDist)
+        local = 0
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        import torch.distributed as tdist
+        if os.environ.get("SDG_BENCH_BACKEND", "nccl") == "gloo":
+            tdist.init_process_group("gloo")
+            dist = _HostStagedDist(tdist)
+        else:
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist = tdist
 
     if args.config == "c5":
         return run_c5(args, rank, world, local, dist)

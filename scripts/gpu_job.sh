@@ -69,6 +69,7 @@ for s in "$@"; do
         s3pmc2) run s3sw 600 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && run s3sw8 600 env SDG_S3_G=8 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && i=0 && for c in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_INSTS_FLAT SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS" "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE"; do i=$((i+1)); run s3c$i 180 rocprofv3 --pmc $c --kernel-trace -d "$OUT/s3c$i" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 1 --warmup 1 || break; done ;;
         cfgall) run cfgall 900 python3 scripts/bench_configs.py --only c1,c3m,c3md,c4 --c3-steps 3 ;;
         s3sel) run s3t 600 python3 -u -m pytest tests/test_gpu_seq3.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider && run s3tb 600 env SDG_S3_BRANCH=1 python3 -u -m pytest tests/test_gpu_seq3.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "shapes or within" && run s3sel 600 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && run s3br 600 env SDG_S3_BRANCH=1 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && run s3sel16 600 env SDG_S3_G=16 python3 scripts/bench_configs.py --only c3md --c3-steps 3 ;;
+        mrbench) run mrbench 600 env SDG_BENCH_BACKEND=gloo SDG_BENCH_SHARE_GPU=1 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --events 30000000 --no-cpu ;;
         *) echo "unknown step $s" ;;
     esac
 done
