@@ -881,9 +881,11 @@ static_assert((FU_DQ & (FU_DQ - 1)) == 0, "sw() swizzles at the deque chunk size
 __device__ __forceinline__ int sw(int p) { return p ^ ((p / FU_DQ) & (FU_DQ - 1)); }
 static_assert(FU_ROWS < 65536, "chain_fused_k: u16 rows / run offsets");
 
-// SAME: the scanned column's kind is the comparison kind (no conversion in the scan loop)
-template <int K, bool SAME>
-__global__ __launch_bounds__(FU_THREADS) void chain_fused_k(const ChainArgs* __restrict__ pa) {
+// SAME: the scanned column's kind is the comparison kind (no conversion in the scan loop). W: minimum waves per SIMD
+// the allocator must allow -- 8 = four 512-thread blocks per CU (LDS 4 x 40 KB fits); at 6 it used 104 SGPRs, which
+// admits 6 waves per SIMD = 3 blocks (MI355X_MICROARCH residency rule). 8 costs SGPR / VGPR spills.
+template <int K, bool SAME, int W>
+__global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* __restrict__ pa) {
     using C = KT<K>;
     using T = typename C::T;
     constexpr int NW = FU_THREADS / 64;
@@ -1399,6 +1401,9 @@ void chain_carry(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
         hipLaunchKernelGGL(chain_carry_k, dim3((unsigned)((a.cin_n + 255) / 256)), dim3(256), 0, stream, d_a);
 }
 
+#ifndef SDG_FU_W8_DEFAULT
+#define SDG_FU_W8_DEFAULT 0
+#endif
 int64_t chain_fused_grid(int64_t n, int nb) {
     const int64_t g = (n + FU_OWN - 1) / FU_OWN + nb;
     return (g + 7) / 8 * 8;
@@ -1408,10 +1413,14 @@ void chain_fused(const ChainArgs& a, const ChainArgs* d_a, int64_t grid, hipStre
     if (a.n <= 0) return;
     const dim3 g((unsigned)grid), b(FU_THREADS);
     const bool same = a.sp.scan_col_kind == a.sp.scan_t;
+    static const char* wv = getenv("SDG_FU_WPS");  // A/B: 8 (four blocks per CU) or 6
+    const bool w8 = wv ? atoi(wv) == 8 : SDG_FU_W8_DEFAULT;
 #define FU_LAUNCH(KK)                                                                                    \
     do {                                                                                                 \
-        if (same) hipLaunchKernelGGL((chain_fused_k<KK, true>), g, b, 0, stream, d_a);                   \
-        else hipLaunchKernelGGL((chain_fused_k<KK, false>), g, b, 0, stream, d_a);                       \
+        if (same && w8) hipLaunchKernelGGL((chain_fused_k<KK, true, 8>), g, b, 0, stream, d_a);          \
+        else if (same) hipLaunchKernelGGL((chain_fused_k<KK, true, 6>), g, b, 0, stream, d_a);          \
+        else if (w8) hipLaunchKernelGGL((chain_fused_k<KK, false, 8>), g, b, 0, stream, d_a);           \
+        else hipLaunchKernelGGL((chain_fused_k<KK, false, 6>), g, b, 0, stream, d_a);                   \
     } while (0)
     switch (a.sp.scan_t) {
         case VK_I32: FU_LAUNCH(VK_I32); break;
