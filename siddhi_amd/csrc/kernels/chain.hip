@@ -290,8 +290,9 @@ __device__ __forceinline__ void emit_carry(const ChainArgs& a, const View& v, in
 constexpr uint32_t CM_NONE = 0xFFFFFFFFu, CM_CARRY = 0xFFFFFFFEu;
 static_assert(MQ_NONE == CM_NONE && MQ_CARRY == CM_CARRY, "emit-only mode reads mq as chain_match_k results");
 
+// GEN = false is compiled for 8 waves per SIMD (its 102 SGPRs admitted 6); the interpreter variant keeps its registers
 template <bool GEN>
-__global__ __launch_bounds__(CM_THREADS) void chain_match_k(const ChainArgs* __restrict__ pa) {
+__global__ __launch_bounds__(CM_THREADS, GEN ? 1 : 8) void chain_match_k(const ChainArgs* __restrict__ pa) {
     const ChainArgs& a = *pa;
     const ChainSpec& sp = a.sp;
     const int tid = threadIdx.x;
@@ -304,7 +305,9 @@ __global__ __launch_bounds__(CM_THREADS) void chain_match_k(const ChainArgs* __r
     v.oc0 = v.ots + CM_ROWS;
     v.oc1 = v.oc0 + CM_ROWS;
     v.oqs = (v.ots + (1 + a.n_stage) * CM_ROWS) * 8;
-    const int ores = (v.oqs + (a.qstream ? CM_ROWS : 0) + 3) / 4;  // u32 index of the per-event results
+    // u32 index of the per-event results (emit-only: right after the stack -- nothing is staged, and the launch
+    // allocates only the stack and the results, chain_lds_bytes)
+    const int ores = a.mq_in ? v.ots * 2 : (v.oqs + (a.qstream ? CM_ROWS : 0) + 3) / 4;
     int64_t* stk = cm_lds + tid;                                   // used only when a.lds_stack
     uint32_t* res = (uint32_t*)cm_lds + ores;
     __shared__ uint32_t wcnt[2][CM_EPT][CM_THREADS / 64];          // matches / carries per (round, wave)
@@ -634,7 +637,7 @@ __global__ __launch_bounds__(256) void chain_ovf_k(const ChainArgs* __restrict__
     }
 }
 
-__global__ __launch_bounds__(256) void chain_carry_k(const ChainArgs* __restrict__ pa) {
+__global__ __launch_bounds__(256, 8) void chain_carry_k(const ChainArgs* __restrict__ pa) {
     const ChainArgs& a = *pa;
     __shared__ int64_t stack_mem[STACK * 256];
     int64_t* stk = stack_mem + threadIdx.x;
@@ -785,7 +788,7 @@ __global__ __launch_bounds__(256) void chain_ovf_wave_k(const ChainArgs* __restr
 // Block = 4 waves x CW_PER_WAVE partials; lane i of a wave keeps the result of its i-th partial, and the block
 // reserves its match / carry output with one atomic per counter (one atomic per partial serialised in L2:
 // ~10^8/s, 0.2 ms for 2 x 10^4 carries).
-__global__ __launch_bounds__(256) void chain_carry_wave_k(const ChainArgs* __restrict__ pa) {
+__global__ __launch_bounds__(256, 8) void chain_carry_wave_k(const ChainArgs* __restrict__ pa) {
     const ChainArgs& a = *pa;
     const ChainSpec& sp = a.sp;
     const int lane = lane_id(), w = threadIdx.x >> 6;
@@ -1342,6 +1345,7 @@ __global__ __launch_bounds__(256) void chain_fovf_k(const ChainArgs* __restrict_
 }  // namespace
 
 size_t chain_lds_bytes(const ChainArgs& a) {
+    if (a.mq_in) return (a.lds_stack ? (size_t)STACK * CM_THREADS * 8 : 0) + (size_t)CM_EPT * CM_THREADS * 4;
     size_t b = (a.lds_stack ? (size_t)STACK * CM_THREADS * 8 : 0) + (size_t)(1 + a.n_stage) * CM_ROWS * 8;
     b += a.qstream ? CM_ROWS : 0;
     b = (b + 3) & ~size_t(3);
