@@ -156,7 +156,7 @@ void SchedSim::resize(SchedState& S) {  // HashMap.resize(): 16 / 12, then doubl
     }
     S.bin.assign(S.cap, 0);
     S.due.clear();
-    for (size_t key = 0; key < S.ks.size(); ++key) {
+    for (size_t key = 0; key < S.kend; ++key) {  // (ks is sized for every key of the batch; only these can be in)
         KS& k = S.ks[key];
         if (!k.in_map) continue;
         S.bin[(uint32_t)k.hash & (S.cap - 1)]++;
@@ -175,6 +175,7 @@ void SchedSim::notify(int sch, uint32_t key, int64_t t) {
         if (!k->in_map) {
             k->hash = (*hash_)[key];
             k->in_map = true;
+            S.kend = std::max(S.kend, (size_t)key + 1);
             k->stamp = ++S.stamp;
             k->cseq = ++work_.cseq;
             uint32_t& bc = S.bin[(uint32_t)k->hash & (S.cap - 1)];
@@ -184,6 +185,7 @@ void SchedSim::notify(int sch, uint32_t key, int64_t t) {
         }
     } else if (!k->in_map) {  // SingleStateHolder: created on first use, never removed
         k->in_map = true;
+        S.kend = std::max(S.kend, (size_t)key + 1);
         k->cseq = ++work_.cseq;
     }
     const bool was_empty = k->n == 0;
@@ -660,6 +662,8 @@ const uint8_t* SchedSim::load(const uint8_t* p, const uint8_t* end) {
     st.sc.resize(ns);
     for (SchedState& S : st.sc) {
         get_vec(p, end, S.ks);
+        for (size_t i = 0; i < S.ks.size(); ++i)
+            if (S.ks[i].in_map) S.kend = i + 1;
         const uint64_t nd = get<uint64_t>(p, end);
         for (uint64_t i = 0; i < nd; ++i) {
             const int64_t t = get<int64_t>(p, end);

@@ -204,6 +204,7 @@ class SchedSim {
         std::vector<KS> ks;                                 // [dense key id]
         std::map<int64_t, std::vector<DueE>> due;           // head time -> min-heap of states (lazy deletion)
         uint64_t cap = 0, threshold = 0, size = 0, stamp = 0;
+        size_t kend = 0;                                    // keys [0, kend) have ever entered the map (resize scans them)
         std::vector<uint32_t> bin;                          // keys per bucket (treeifyBin on a small table resizes)
     };
     struct State {
