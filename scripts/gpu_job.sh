@@ -37,7 +37,7 @@ for s in "$@"; do
         c3pmc) i=0; for c in "FETCH_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_INSTS_FLAT SQ_INST_CYCLES_VMEM_RD SQ_WAIT_INST_LDS" "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum"; do i=$((i+1)); run c3pmc$i 180 rocprofv3 --pmc $c --kernel-trace -d "$OUT/c3pmc$i" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3m --c3-steps 1 --warmup 0; done ;;
         c3ns) for ns in 8 16 32 64; do run c3ns$ns 300 python3 scripts/bench_configs.py --only c3m --c3-steps 1 --warmup 1 --max-partials $ns; done ;;
         abdq) run abnew 300 python3 bench.py --steps 5 --warmup 2 --no-cpu && run abold 300 env SDG_FU_OLDDQ=1 python3 bench.py --steps 5 --warmup 2 --no-cpu ;;
-        phases) for sk in 4 8 16 2 0; do run ph$sk 200 env SDG_FU_SKIP=$sk python3 bench.py --steps 3 --warmup 1 --no-cpu --no-parity --e2e-steps 0; done; for sk in 2 0; do run phold$sk 200 env SDG_FU_OLDDQ=1 SDG_FU_SKIP=$sk python3 bench.py --steps 3 --warmup 1 --no-cpu --no-parity --e2e-steps 0; done; grep -o '"ms_chain_match": [0-9.]*' $OUT/ph*.log ;;
+        phases) for sk in 4 8 16 2 0; do run ph$sk 200 env SDG_FU_SKIP=$sk python3 bench.py --steps 3 --warmup 1 --no-cpu --no-parity --no-gather --e2e-steps 0; done; for sk in 2 0; do run phold$sk 200 env SDG_FU_OLDDQ=1 SDG_FU_SKIP=$sk python3 bench.py --steps 3 --warmup 1 --no-cpu --no-parity --no-gather --e2e-steps 0; done; grep -o '"ms_chain_match": [0-9.]*' $OUT/ph*.log ;;
         cpubase) run cpubase 900 python3 scripts/cpu_baselines.py --threads 16 ;;
         c4prof) run c4prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/c4prof" -o run --output-format csv -- python3 scripts/bench_configs.py --only c4 ;;
         c4test) run c4test 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -s --timeout 300 --timeout-method thread -p no:cacheprovider -k c4 ;;
