@@ -71,6 +71,7 @@ for s in "$@"; do
         s3sel) run s3t 600 python3 -u -m pytest tests/test_gpu_seq3.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider && run s3tb 600 env SDG_S3_BRANCH=1 python3 -u -m pytest tests/test_gpu_seq3.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "shapes or within" && run s3sel 600 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && run s3br 600 env SDG_S3_BRANCH=1 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && run s3sel16 600 env SDG_S3_G=16 python3 scripts/bench_configs.py --only c3md --c3-steps 3 ;;
         mrbench) run mrbench 600 env SDG_BENCH_BACKEND=gloo SDG_BENCH_SHARE_GPU=1 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --events 30000000 --no-cpu ;;
         wps) for r in 1 2; do run w8_$r 300 env SDG_FU_WPS=8 python3 bench.py --steps 10 --warmup 2 --no-cpu --no-parity --no-gather --e2e-steps 0 && run w6_$r 300 env SDG_FU_WPS=6 python3 bench.py --steps 10 --warmup 2 --no-cpu --no-parity --no-gather --e2e-steps 0; done; grep -h "^{" $OUT/w*.log | python3 -c "import json,sys; [print(json.loads(l)['ms_per_step'], json.loads(l)['roofline']['kernel_ms']['ms_chain_match']) for l in sys.stdin]" ;;
+        cskip) run cskt 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_robust.py tests/test_fallbacks.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider && for r in 1 2; do run ck_$r 300 python3 bench.py --steps 10 --warmup 2 --no-cpu --no-gather --e2e-steps 0 && run nk_$r 300 env SDG_FU_NOSKIP=1 python3 bench.py --steps 10 --warmup 2 --no-cpu --no-parity --no-gather --e2e-steps 0; done; grep -h "^{" $OUT/ck_*.log $OUT/nk_*.log | python3 -c "import json,sys; [print(json.loads(l)['ms_per_step'], json.loads(l)['roofline']['kernel_ms']['ms_chain_match'], json.loads(l).get('parity',{}).get('bit_exact')) for l in sys.stdin]" ;;
         *) echo "unknown step $s" ;;
     esac
 done

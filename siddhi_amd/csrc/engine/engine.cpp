@@ -2026,6 +2026,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         a.fu_skip = skip ? atoi(skip) : 0;
         static const bool old_dq = getenv("SDG_FU_OLDDQ") != nullptr;  // A/B: the monotone-deque pass
         if (old_dq) a.fu_skip |= 64;
+        static const bool no_cskip = getenv("SDG_FU_NOSKIP") != nullptr;  // A/B: chunk-summary skipping in the deque
+        if (no_cskip) a.fu_skip |= 128;
         a.fu_mode = getenv("SDG_FU_NODEQUE") ? DQ_OFF : a.deque_mode;
         a.deque_mode = DQ_OFF;
         a.bstart = b_start;

@@ -14,6 +14,8 @@
 // chain_carry_k: partials carried in from the previous batch scan the new batch's key segment.
 #include <hip/hip_runtime.h>
 
+#include <limits>
+
 #include "../engine/eval.h"
 #include "kernels.h"
 #include "wave.h"
@@ -900,7 +902,7 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
     __shared__ uint16_t s_row[FU_ROWS];
     __shared__ uint8_t s_lk[FU_ROWS];
     __shared__ uint16_t s_res[FU_ROWS];  // per position: e2 position | R_NONE | R_CARRY | R_OVF
-    __shared__ uint16_t wc[NW][256];
+    __shared__ __align__(16) uint16_t wc[NW][256];  // regrouping counters; then the deque chunks' summaries
     __shared__ uint16_t lstart[256], lend[256];
     __shared__ uint32_t wcnt[3][FU_PT][NW];
     __shared__ unsigned long long bbase[3];
@@ -1093,6 +1095,25 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
             cx[i] = s_x[sw(q)];
             crow[i] = s_row[sw(q)];
         }
+        // chunk summaries (stack mode, ordering comparisons): per FU_DQ-position chunk the extreme value that could
+        // complete a pending partial -- the max when "x beats y" grows with x, else the min; NaN rows never complete
+        // one. A continuation skips a whole chunk of its key when the summary cannot beat its deque's top: pops only
+        // ever take the top, so no row of the chunk changes the deque but expiry, which the chunk's last ts applies.
+        // (wc is free after the regrouping: 512 chunks x 8 B)
+        const bool mono = stack && (m.gt != m.lt) && !m.ne && !(a.fu_skip & 128);
+        const bool use_max = left == m.gt;
+        T* s_cs = reinterpret_cast<T*>(&wc[0][0]);
+        static_assert(FU_ROWS / FU_DQ * sizeof(int64_t) <= sizeof(wc), "chunk summaries fit the regrouping counters");
+        if (mono) {
+            T ext = use_max ? std::numeric_limits<T>::lowest() : std::numeric_limits<T>::max();
+#pragma unroll
+            for (int i = 0; i < FU_DQ; ++i) {
+                const T x = SAME ? C::get(cx[i]) : C::get(cvt(cx[i], kind, (uint8_t)K));
+                if (p0 + i < nr && x == x) ext = use_max ? (x > ext ? x : ext) : (x < ext ? x : ext);
+            }
+            if (p0 < FU_ROWS) s_cs[t] = ext;
+        }
+        __syncthreads();
 #pragma unroll
         for (int i = 0; i < FU_DQ; ++i) {
             const int q = p0 + i;
@@ -1115,7 +1136,30 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
         // continuation over the key's following positions (no pushes) until the deque drains
         // software-pipelined: row q + 1 is read from LDS while row q is processed (the step's branches depend on
         // the row, so without this every step waits out an LDS round trip)
-        if (pe < cur_end && pend) {
+        if (pe < cur_end && pend && mono) {
+            int q = pe;  // chunk-aligned (pe = p0 + FU_DQ)
+#pragma unroll 1
+            while (q < cur_end && pend) {
+                if (q + FU_DQ <= cur_end) {  // a whole chunk of this key
+                    const T cs = s_cs[q / FU_DQ];
+                    if (!(left ? cmp_m(m, cs, ytop) : cmp_m(m, ytop, cs))) {
+                        const uint32_t tl = s_ts[sw(q + FU_DQ - 1)];  // the chunk's last (latest) row
+                        while (pend && (uint64_t)(tl - tf) > within_u) {
+                            pend &= pend - 1;
+                            if (pend) tf = s_ts[sw(p0 + __builtin_ctz(pend))];
+                        }
+                        q += FU_DQ;
+                        continue;
+                    }
+                }
+                const int qe = min(cur_end, q + FU_DQ);
+#pragma unroll 1
+                for (; q < qe && pend; ++q) {
+                    const int64_t xr = s_x[sw(q)];
+                    step(q, s_ts[sw(q)], SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K)));
+                }
+            }
+        } else if (pe < cur_end && pend) {
             uint32_t tn = s_ts[sw(pe)];
             int64_t xn = s_x[sw(pe)];
 #pragma unroll 1
