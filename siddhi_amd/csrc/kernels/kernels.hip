@@ -24,6 +24,7 @@ __device__ __forceinline__ uint32_t digit_of(uint32_t k, int shift, uint32_t mas
 // per-tile digit histogram: counts[tile * nb + d]
 // kcheck (first pass only): keys >= K (device-resident batches whose ids did not come from this engine) set
 // *kflag; every later kernel masks its key-derived indices, so such a batch fails the flush without a fault
+template <int RX_TILE, int RX_THREADS>
 __global__ __launch_bounds__(RX_THREADS) void rx_hist(const uint32_t* __restrict__ keys, int64_t n, int shift,
                                                       uint32_t mask, int nb, uint32_t* __restrict__ counts,
                                                       uint32_t kcheck, int* __restrict__ kflag) {
@@ -165,7 +166,11 @@ struct RxPass {
 // LDS ops of one wave are in order, so no block barrier while counting). Then per digit: prefix over waves
 // and the tile's digit starts; each column is staged in LDS in digit order and written out as coalesced runs
 // (keys and original rows together as one 8-byte word).
-__global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {  // 4 waves/SIMD: 2 blocks per CU
+// Tiles: 8192 rows x 512 threads (2 blocks per CU) or 16384 x 1024 (one block per CU, 154 KB of LDS): both 4
+// waves/SIMD and 16 rows per lane; the larger tile doubles the average bucket run each tile writes (a 256-bucket
+// pass writes runs of 64 rows instead of 32: fewer partial cache lines for the u8 / u32 columns).
+template <int RX_TILE, int RX_THREADS>
+__global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
     constexpr int R = RX_TILE / RX_THREADS;  // 16 elements per lane
     constexpr int NW = RX_THREADS / 64;
     __shared__ uint16_t wc[NW][1 << RX_MAXBITS];  // per-wave digit counts (<= 1024), then per-wave digit bases
@@ -628,7 +633,31 @@ __global__ __launch_bounds__(256) void nfa_commit_k(uint8_t* __restrict__ cur, u
 
 }  // namespace
 
-static int64_t rx_ntiles(int64_t n) { return n <= 0 ? 1 : (n + RX_TILE - 1) / RX_TILE; }
+// SDG_RX_TILE=8192 / 16384: the radix tile (A/B); the workspace is sized for the smaller one
+static int rx_tile() {
+    static const int t = [] {
+        const char* e = getenv("SDG_RX_TILE");
+        return e && atoi(e) == RX_TILE_BIG ? RX_TILE_BIG : e && atoi(e) == RX_TILE ? RX_TILE : RX_TILE_DEFAULT;
+    }();
+    return t;
+}
+static int64_t rx_ntiles(int64_t n, int tile = RX_TILE) { return n <= 0 ? 1 : (n + tile - 1) / tile; }
+static void launch_rx_hist(int64_t nt, hipStream_t stream, const uint32_t* keys, int64_t n, int shift, uint32_t mask,
+                           int nb, uint32_t* counts, uint32_t kcheck, int* kflag) {
+    if (rx_tile() == RX_TILE_BIG)
+        hipLaunchKernelGGL((rx_hist<RX_TILE_BIG, RX_THREADS_BIG>), dim3((unsigned)nt), dim3(RX_THREADS_BIG), 0, stream,
+                           keys, n, shift, mask, nb, counts, kcheck, kflag);
+    else
+        hipLaunchKernelGGL((rx_hist<RX_TILE, RX_THREADS>), dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, keys, n,
+                           shift, mask, nb, counts, kcheck, kflag);
+}
+static void launch_rx_scatter(int64_t nt, hipStream_t stream, const RxPass& rp) {
+    if (rx_tile() == RX_TILE_BIG)
+        hipLaunchKernelGGL((rx_scatter<RX_TILE_BIG, RX_THREADS_BIG>), dim3((unsigned)nt), dim3(RX_THREADS_BIG), 0,
+                           stream, rp);
+    else
+        hipLaunchKernelGGL((rx_scatter<RX_TILE, RX_THREADS>), dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, rp);
+}
 
 size_t keygroup_workspace(int64_t n, int32_t K, int32_t ncols, const uint8_t* widths) {
     int64_t nt = rx_ntiles(n);
@@ -664,7 +693,7 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
     if (kbits == 0) kbits = 1;
     int npass = (kbits + RX_MAXBITS - 1) / RX_MAXBITS;
     int bits = (kbits + npass - 1) / npass;
-    int64_t nt = rx_ntiles(a.n);
+    int64_t nt = rx_ntiles(a.n, rx_tile());
     int ng = (int)((nt + KG_GROUP - 1) / KG_GROUP);
     if (marks) (void)hipEventRecord(marks[0], stream);
     for (int p = 0; p < npass; ++p) {
@@ -674,8 +703,8 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
         uint32_t mask = (uint32_t)nb - 1;
         const uint32_t* kin = p == 0 ? a.keys : a.tmp_keys[(p - 1) & 1];
         bool last = p == npass - 1;
-        hipLaunchKernelGGL(rx_hist, dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, kin, a.n, shift, mask, nb, a.counts,
-                           p == 0 && a.key_flag ? (uint32_t)a.K : 0u, a.key_flag);
+        launch_rx_hist(nt, stream, kin, a.n, shift, mask, nb, a.counts, p == 0 && a.key_flag ? (uint32_t)a.K : 0u,
+                       a.key_flag);
         int64_t gk = (int64_t)ng * nb;
         hipLaunchKernelGGL(rx_p1, dim3((unsigned)((gk + 255) / 256)), dim3(256), 0, stream, a.counts, (int)nt, nb, a.gsum);
         hipLaunchKernelGGL(rx_p2, dim3(1), dim3(256), 0, stream, a.gsum, ng, nb, a.tot);
@@ -702,7 +731,7 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
         rp.bits = b;
         rp.mono_col = -1;
         rp.ts32_col = -1;
-        hipLaunchKernelGGL(rx_scatter, dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, rp);
+        launch_rx_scatter(nt, stream, rp);
     }
     if (marks) (void)hipEventRecord(marks[2], stream);
     (void)hipMemsetAsync(a.seg_start, 0, (size_t)a.K * 4, stream);
@@ -746,11 +775,10 @@ void bucketize(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, uint
                int seg_rows, hipStream_t stream, hipEvent_t* marks) {
     const int nb = 1 << bits;
     const uint32_t mask = (uint32_t)nb - 1;
-    const int64_t nt = rx_ntiles(a.n);
+    const int64_t nt = rx_ntiles(a.n, rx_tile());
     const int ng = (int)((nt + KG_GROUP - 1) / KG_GROUP);
     if (marks) (void)hipEventRecord(marks[0], stream);
-    hipLaunchKernelGGL(rx_hist, dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, a.keys, a.n, 0, mask, nb, a.counts,
-                       a.key_flag ? (uint32_t)a.K : 0u, a.key_flag);
+    launch_rx_hist(nt, stream, a.keys, a.n, 0, mask, nb, a.counts, a.key_flag ? (uint32_t)a.K : 0u, a.key_flag);
     const int64_t gk = (int64_t)ng * nb;
     hipLaunchKernelGGL(rx_p1, dim3((unsigned)((gk + 255) / 256)), dim3(256), 0, stream, a.counts, (int)nt, nb, a.gsum);
     hipLaunchKernelGGL(rx_p2, dim3(1), dim3(256), 0, stream, a.gsum, ng, nb, a.tot);
@@ -781,7 +809,7 @@ void bucketize(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, uint
     rp.ts_base = a.ts_base;
     rp.lkey_out = a.lkey_out;
     rp.lkey_shift = bits;
-    hipLaunchKernelGGL(rx_scatter, dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, rp);
+    launch_rx_scatter(nt, stream, rp);
     if (marks) (void)hipEventRecord(marks[2], stream);
     hipLaunchKernelGGL(bk_plan, dim3(1), dim3(256), 0, stream, a.tot, a.n, nb, seg_rows, bstart, bseg);
     if (marks) (void)hipEventRecord(marks[3], stream);
