@@ -194,6 +194,8 @@ typedef struct sdg_stats {
     int64_t carry_out;         /* chain path: partials the last flush carries into the next */
     int64_t arena_slots;       /* generic NFA: per-key arenas allocated after the last flush (queries summed); keys
                                   whose state the reference destroys down to their start seeds give theirs back */
+    int64_t sched_exact_passes; /* scheduler simulation: exact passes run (0 when the device reruns reproduced the
+                                   optimistic pass's model changes, SchedSim::confirm) */
 } sdg_stats;
 int sdg_last_stats(sdg_engine* e, sdg_stats* out);
 

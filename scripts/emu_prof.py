@@ -66,9 +66,9 @@ def main():
     if rc:
         raise SystemExit(L.emu_error().decode())
     print("%s %d keys, %d events: flush %.2f s, %d matches; scheduler passes (us): optimistic %d rerun %d exact %d,"
-          " reordered %d taken %d" % (args.config, args.keys, n, dt, L.emu_num_out(h, 0), L.emu_sched_stat(2),
+          " reordered %d taken %d exact passes %d" % (args.config, args.keys, n, dt, L.emu_num_out(h, 0), L.emu_sched_stat(2),
                                        L.emu_sched_stat(3), L.emu_sched_stat(4), L.emu_sched_stat(0),
-                                       L.emu_sched_stat(1)))
+                                       L.emu_sched_stat(1), L.emu_sched_stat(6)))
     L.emu_destroy(h)
     # samples -> functions
     cnt = collections.Counter()

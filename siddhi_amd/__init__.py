@@ -86,7 +86,7 @@ class Stats(ctypes.Structure):
                 ("sched_host_keys", ctypes.c_int64), ("sched_rerun_keys", ctypes.c_int64),
                 ("ms_nfa_kernel", ctypes.c_double), ("ms_sched_host", ctypes.c_double),
                 ("arena_growths", ctypes.c_int64), ("carry_in", ctypes.c_int64), ("carry_out", ctypes.c_int64),
-                ("arena_slots", ctypes.c_int64)]
+                ("arena_slots", ctypes.c_int64), ("sched_exact_passes", ctypes.c_int64)]
 
 
 _lib = None

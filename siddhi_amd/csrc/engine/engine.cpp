@@ -992,10 +992,23 @@ const uint32_t* device_key_ids(sdg_engine* e, QueryRt& q, const void* col, int k
         HIPCHECK(hipMemcpyAsync(pairs.data(), d_pairs, cnt * 8, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipMemcpyAsync(vals.data(), d_vals, cnt * 8, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
-        std::vector<uint32_t> order(cnt);
+        // new keys in order of their first row (pairs: first row << 32 | slot; first rows are distinct): an LSD
+        // radix sort of the indices on the first row, 8 bits a pass (passes whose digit is constant skipped)
+        std::vector<uint32_t> order(cnt), tmp(cnt);
         for (uint32_t i = 0; i < cnt; ++i) order[i] = i;
-        std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return pairs[a] < pairs[b]; });
+        for (int sh = 32; sh < 64; sh += 8) {
+            size_t hist[257] = {};
+            for (uint64_t i = 0; i < cnt; ++i) ++hist[((pairs[i] >> sh) & 0xFF) + 1];
+            bool one = false;
+            for (int d = 0; d < 256 && !one; ++d) one = hist[d + 1] == cnt;
+            if (one) continue;
+            for (int d = 0; d < 256; ++d) hist[d + 1] += hist[d];
+            for (uint64_t j = 0; j < cnt; ++j) tmp[hist[(pairs[order[j]] >> sh) & 0xFF]++] = order[j];
+            order.swap(tmp);
+        }
         std::vector<uint32_t> slots(cnt);
+        q.keydict.reserve(K0 + cnt);  // one rehash, not ~log2(cnt) of them
+        q.keystr.reserve(K0 + cnt);
         for (uint64_t j = 0; j < cnt; ++j) {
             const uint32_t i = order[j];
             const uint32_t id = (uint32_t)(K0 + j);
@@ -1097,7 +1110,9 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                      e->stream_types.size() <= (size_t)MV_MAX_STREAMS;
     for (const PushChunk* c : parts) dev_mixed &= c->stream == -2 && !c->device && c->cols.size() <= (size_t)MV_MAX_ATTRS;
     if (dev_mixed) {
+        hp.mark("parts");
         nrows = mixed_view(e, q, parts, part_pos, n, &d_ts, &d_qs, d_cols, d_nulls, &d_vpos);
+        hp.mark("mixed_view");
         if (partitioned) {
             if (q.string_keys) d_key = q.st_key.as<uint32_t>();
             else d_key = device_key_ids(e, q, q.kt_vals_in.as<int64_t>(), VK_I64, nrows);
@@ -1908,7 +1923,13 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 read_logs(false);
             }
             q.runs.clear();
-            q.sim.simulate(e->bc, logs, q.key_hash, kr, take, res);
+            // the exact pass only when the reruns did not reproduce the optimistic pass's model changes
+            // (SDG_SCHED_EXACT: always, A/B)
+            static const bool sched_exact = getenv("SDG_SCHED_EXACT") != nullptr;
+            if (sched_exact || !q.sim.confirm(logs, res)) {
+                q.sim.simulate(e->bc, logs, q.key_hash, kr, take, res);
+                e->stats.sched_exact_passes += 1;
+            }
             hp.mark("sched_simulate_exact");
             for (auto& r : q.runs) {
                 if (r->overflow())
@@ -2546,6 +2567,7 @@ int do_flush(sdg_engine* e) {
     e->stats.arena_slots = 0;
     e->stats.fused_ovf = 0;
     e->stats.sched_fires = e->stats.sched_shifted = e->stats.sched_host_keys = e->stats.sched_rerun_keys = 0;
+    e->stats.sched_exact_passes = 0;
     // a flush consumes its batch whether or not it succeeds: a failing query must not make the next flush
     // replay the events onto the queries that already committed them. The batch's positions and its clock are
     // consumed with it: queries that committed before a failing one hold carries, arenas and scheduler state

@@ -269,7 +269,6 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
     prof.lap(0);
     hash_ = &key_hash;
     out = Result{};
-    out.rank.reserve(logs.size() / 4 + 16);
     constexpr size_t NONE = ~size_t(0);
     enum : uint8_t { DEV = 0, PENDING = 1, HOST = 2 };  // the key's history so far: its device run / a device fire
                                                       // the scheduler has not made yet / stepped on the host
@@ -280,6 +279,7 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
         bool touched = false;
         KeyRun* run = nullptr;
         int32_t fh = -1, ft = -1;            // the scheduler's fires of this key so far (list in `fl`)
+        uint32_t nshift = 0;                 // its device fires accepted as shifted
     };
     struct FN {
         nfa::TimerFire f;
@@ -287,6 +287,16 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
         uint32_t rank;  // the fire's rank among the fires of its position
     };
     std::vector<FN> fl;
+    // optimistic pass: every model change, tagged with the key it was made for (confirm() checks reruns by them)
+    struct KOp {
+        uint32_t key;
+        Op op;
+    };
+    std::vector<KOp> kops;
+    if (optimistic) kops.reserve(logs.size());
+    auto rec = [&](uint32_t key, uint32_t g, uint8_t kind, int sch, int64_t t) {
+        if (optimistic) kops.push_back(KOp{key, Op{g, kind, (uint8_t)sch, t}});
+    };
     // keys: dense ids; the table covers every key with records, rows or a queued state
     size_t nkeys = (size_t)std::max<int64_t>(rows.K, 0);
     for (const SchedState& S : work_.sc) nkeys = std::max(nkeys, S.ks.size());
@@ -310,16 +320,20 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
         return (logs[i].type == nfa::LOG_PUSH && logs[i].origin == nfa::ORIGIN_EVENT) || logs[i].type == nfa::LOG_PURGE;
     };
     std::vector<size_t> evp;  // pushes made while processing events, applied at their positions
+    size_t nfire_logs = 0;
     for (size_t i = 0; i < logs.size();) {
         size_t j = i;
         while (j < logs.size() && logs[j].key == logs[i].key) ++j;
         KC& c = K(logs[i].key);
         c.i = i;
         c.e = j;
-        for (size_t x = i; x < j; ++x)
+        for (size_t x = i; x < j; ++x) {
             if (is_evpush(x)) evp.push_back(x);
+            nfire_logs += logs[x].type == nfa::LOG_FIRE;
+        }
         i = j;
     }
+    out.rank.reserve(nfire_logs + nfire_logs / 4 + 16);  // ~ one entry per fire (grows if the scheduler fires more)
     prof.lap(9);
     {  // by position, stable: sort (position + 1, record index) packed in one word (no record loads in the sort)
         std::vector<uint64_t> pk(evp.size());
@@ -409,6 +423,7 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
         ++out.n_fires;
         KC& c = K(key);
         add_fire(c, nfa::TimerFire{g, sch, clock}, rk);
+        rec(key, g, OP_FIRE, sch, clock);
         if (c.mode != HOST) {
             const size_t f = next_fire(c);
             bool ok = f != NONE && logs[f].sched == sch && (int64_t)logs[f].g <= (int64_t)g;
@@ -425,15 +440,23 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
             if (ok) {
                 for (size_t x = f + 1; x < end; ++x) {
                     const SchedLog& L = logs[x];
-                    if (L.type == nfa::LOG_POP) pop(L.sched, key);
-                    else if (L.type == nfa::LOG_PUSH) notify(L.sched, key, L.t);
+                    if (L.type == nfa::LOG_POP) {
+                        pop(L.sched, key);
+                        rec(key, g, OP_POP, L.sched, 0);
+                    } else if (L.type == nfa::LOG_PUSH) {
+                        notify(L.sched, key, L.t);
+                        rec(key, g, OP_NOTIFY, L.sched, L.t);
+                    }
                 }
                 // Scheduler.sendTimerEvents pops every queued time <= currentTime in this one fire. A device fire
                 // made at an earlier clock may have left some of them (only the optimistic pass accepts such a
                 // fire, c.reordered): without this the model would fire the key again at the next advance -- a
                 // fire the reference never makes, which the rerun would then execute
                 while (queued(sch, key) && head(sch, key) <= clock) pop(sch, key);
-                if (logs[f].g != g) ++out.n_shifted;
+                if (logs[f].g != g) {
+                    ++out.n_shifted;
+                    ++c.nshift;
+                }
                 out.rank.put(rank_key(logs[f].g, sch, key), Slot{g, rk});
                 c.i = end + 1;
                 c.mode = DEV;
@@ -470,8 +493,17 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
         return x >= bc.G ? bc.G : (int64_t)bc.nadv[x];
     };
     size_t ep = 0;
-    for (; ep < evp.size() && posof(evp[ep]) < 0; ++ep)  // an unpartitioned query's init at start
-        if (K(logs[evp[ep]].key).mode == DEV) notify(logs[evp[ep]].sched, logs[evp[ep]].key, logs[evp[ep]].t);
+    for (; ep < evp.size() && posof(evp[ep]) < 0; ++ep) {  // an unpartitioned query's init at start
+        const SchedLog& L = logs[evp[ep]];
+        if (K(L.key).mode != DEV) continue;
+        if (L.type == nfa::LOG_PURGE) {
+            purge(L.key);
+            rec(L.key, L.g, OP_PURGE, 0, 0);
+        } else {
+            notify(L.sched, L.key, L.t);
+            rec(L.key, L.g, OP_NOTIFY, L.sched, L.t);
+        }
+    }
     int64_t g = 0;
     std::vector<std::pair<int64_t, uint32_t>> W;
     prof.lap(1);
@@ -563,8 +595,13 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
             const SchedLog& L = logs[evp[ep]];
             const uint8_t m = kc[L.key].mode;
             if (m != DEV && !(optimistic && m == PENDING)) continue;
-            if (L.type == nfa::LOG_PURGE) purge(L.key);
-            else notify(L.sched, L.key, L.t);
+            if (L.type == nfa::LOG_PURGE) {
+                purge(L.key);
+                rec(L.key, L.g, OP_PURGE, 0, 0);
+            } else {
+                notify(L.sched, L.key, L.t);
+                rec(L.key, L.g, OP_NOTIFY, L.sched, L.t);
+            }
         }
         ++g;
         prof.lap(5);
@@ -577,9 +614,27 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
         }
         out.fire_off.push_back(0);
         for (uint32_t k : out.reordered) {
-            for (int32_t x = kc[k].fh; x >= 0; x = fl[x].next) out.fires.push_back(fl[x].f);
+            for (int32_t x = kc[k].fh; x >= 0; x = fl[x].next) {
+                out.fires.push_back(fl[x].f);
+                out.fire_rank.push_back(fl[x].rank);
+            }
             out.fire_off.push_back((uint32_t)out.fires.size());
         }
+        // the reordered keys' model changes, grouped by key (stable), and the shifted fires of the others
+        std::vector<int32_t> rd(nkeys, -1);  // dense (not kc[].rd): the ops are in time order, keys at random
+        for (size_t d = 0; d < out.reordered.size(); ++d) rd[out.reordered[d]] = (int32_t)d;
+        out.trace_off.assign(out.reordered.size() + 1, 0);
+        for (const KOp& o : kops)
+            if (rd[o.key] >= 0) ++out.trace_off[rd[o.key] + 1];
+        for (size_t d = 0; d < out.reordered.size(); ++d) out.trace_off[d + 1] += out.trace_off[d];
+        out.trace.resize(out.trace_off.back());
+        {
+            std::vector<uint32_t> wp(out.trace_off.begin(), out.trace_off.end() - 1);
+            for (const KOp& o : kops)
+                if (rd[o.key] >= 0) out.trace[wp[rd[o.key]]++] = o.op;
+        }
+        for (uint32_t k : touched)
+            if (rd[k] < 0) out.n_shifted_kept += kc[k].nshift;
         prof.lap(6);
         prof.print("optimistic", logs.size(), evp.size(), out.n_fires);
         return;
@@ -602,6 +657,51 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
     std::sort(out.taken.begin(), out.taken.end());
     prof.lap(6);
     prof.print("exact", logs.size(), evp.size(), out.n_fires);
+}
+
+bool SchedSim::confirm(const std::vector<nfa::SchedLog>& logs, Result& res) const {
+    using nfa::SchedLog;
+    std::vector<Op> got;
+    size_t i = 0;
+    for (size_t d = 0; d < res.reordered.size(); ++d) {
+        const uint32_t key = res.reordered[d];
+        i = std::lower_bound(logs.begin() + i, logs.end(), key,
+                             [](const SchedLog& L, uint32_t k) { return L.key < k; }) - logs.begin();
+        size_t j = i;
+        while (j < logs.size() && logs[j].key == key) ++j;
+        // the changes the exact pass would make for the key if every fire of its new run is consistent
+        got.clear();
+        for (size_t x = i; x < j; ++x) {
+            const SchedLog& L = logs[x];
+            if (L.type == nfa::LOG_PUSH && L.origin == nfa::ORIGIN_EVENT) {
+                got.push_back(Op{L.g, OP_NOTIFY, L.sched, L.t});
+            } else if (L.type == nfa::LOG_PURGE) {
+                got.push_back(Op{L.g, OP_PURGE, 0, 0});
+            } else if (L.type == nfa::LOG_FIRE) {
+                got.push_back(Op{L.g, OP_FIRE, L.sched, L.t});
+                size_t y = x + 1;
+                for (; y < j && logs[y].type != nfa::LOG_FIRE_END; ++y) {
+                    if (logs[y].type == nfa::LOG_POP) got.push_back(Op{L.g, OP_POP, logs[y].sched, 0});
+                    else if (logs[y].type == nfa::LOG_PUSH) got.push_back(Op{L.g, OP_NOTIFY, logs[y].sched, logs[y].t});
+                }
+                if (y == j) return false;  // a fire without its end record
+                x = y;
+            } else {
+                return false;  // a pop / scheduler push outside a fire: not a shape the comparison covers
+            }
+        }
+        const size_t b = res.trace_off[d], e = res.trace_off[d + 1];
+        if (got.size() != e - b || !std::equal(got.begin(), got.end(), res.trace.begin() + b)) return false;
+        i = j;
+    }
+    for (size_t d = 0; d < res.reordered.size(); ++d)  // the reruns' fires sit at the scheduler's positions now
+        for (uint32_t x = res.fire_off[d]; x < res.fire_off[d + 1]; ++x) {
+            const nfa::TimerFire& f = res.fires[x];
+            res.rank.put(rank_key(f.g, f.sched, res.reordered[d]), Slot{f.g, res.fire_rank[x]});
+        }
+    res.n_shifted = res.n_shifted_kept;
+    res.taken.clear();
+    return true;
 }
 
 namespace {

@@ -84,8 +84,7 @@ class SchedSim {
         void reserve(size_t n) {
             size_t c = 16;
             while (c < 2 * n) c <<= 1;
-            keys_.assign(c, EMPTY);
-            vals_.assign(c, Slot{0, 0});
+            e_.assign(c, E{EMPTY, Slot{0, 0}});
             n_ = 0;
             has_empty_key_ = false;
         }
@@ -95,57 +94,67 @@ class SchedSim {
                 empty_val_ = v;
                 return;
             }
-            if (2 * (n_ + 1) > keys_.size()) grow();
-            size_t i = at(k);
-            if (keys_[i] == EMPTY) {
-                keys_[i] = k;
+            if (2 * (n_ + 1) > e_.size()) grow();
+            E& x = e_[at(k)];
+            if (x.k == EMPTY) {
+                x.k = k;
                 ++n_;
             }
-            vals_[i] = v;
+            x.v = v;
         }
         const Slot* find(uint64_t k) const {
             if (k == EMPTY) return has_empty_key_ ? &empty_val_ : nullptr;
-            if (keys_.empty()) return nullptr;
-            const size_t i = at(k);
-            return keys_[i] == k ? &vals_[i] : nullptr;
+            if (e_.empty()) return nullptr;
+            const E& x = e_[at(k)];
+            return x.k == k ? &x.v : nullptr;
         }
         void clear() { reserve(0); }
         bool empty() const { return n_ == 0 && !has_empty_key_; }
 
        private:
         static constexpr uint64_t EMPTY = ~0ull;
-        std::vector<uint64_t> keys_;
-        std::vector<Slot> vals_;
+        struct E {  // key and value side by side: one cache line per probe
+            uint64_t k;
+            Slot v;
+        };
+        std::vector<E> e_;
         size_t n_ = 0;
         bool has_empty_key_ = false;
         Slot empty_val_{0, 0};
         size_t at(uint64_t k) const {  // the key's slot or the empty slot where it would go
-            const size_t m = keys_.size() - 1;
+            const size_t m = e_.size() - 1;
             size_t i = (size_t)((k ^ (k >> 29)) * 0xBF58476D1CE4E5B9ull >> 17) & m;
-            while (keys_[i] != EMPTY && keys_[i] != k) i = (i + 1) & m;
+            while (e_[i].k != EMPTY && e_[i].k != k) i = (i + 1) & m;
             return i;
         }
         void grow() {
-            std::vector<uint64_t> ok;
-            std::vector<Slot> ov;
-            ok.swap(keys_);
-            ov.swap(vals_);
-            const size_t c = std::max<size_t>(16, 2 * ok.size());
-            keys_.assign(c, EMPTY);
-            vals_.assign(c, Slot{0, 0});
-            for (size_t i = 0; i < ok.size(); ++i)
-                if (ok[i] != EMPTY) {
-                    const size_t j = at(ok[i]);
-                    keys_[j] = ok[i];
-                    vals_[j] = ov[i];
-                }
+            std::vector<E> o;
+            o.swap(e_);
+            e_.assign(std::max<size_t>(16, 2 * o.size()), E{EMPTY, Slot{0, 0}});
+            for (const E& x : o)
+                if (x.k != EMPTY) e_[at(x.k)] = x;
         }
+    };
+    // one change the pass made to the scheduler model on behalf of a key (confirm() compares them)
+    enum : uint8_t { OP_NOTIFY = 0, OP_POP = 1, OP_PURGE = 2, OP_FIRE = 3 };
+    struct Op {
+        uint32_t g;      // position (OP_FIRE and the fire's pops / pushes: the scheduler's fire position)
+        uint8_t kind;
+        uint8_t sched;
+        int64_t t;       // OP_NOTIFY: notify time; OP_FIRE: the clock; else 0
+        bool operator==(const Op& o) const { return g == o.g && kind == o.kind && sched == o.sched && t == o.t; }
     };
     struct Result {
         std::vector<uint32_t> taken;                         // keys run on the host (their device run is void)
         // optimistic pass: keys whose device run the scheduler reordered (and their fire lists in its order)
         std::vector<uint32_t> reordered, fire_off;
         std::vector<nfa::TimerFire> fires;
+        std::vector<uint32_t> fire_rank;                     // [fires] each fire's rank among its position's fires
+        // optimistic pass: per reordered key (trace_off like fire_off), the model changes the pass made for it:
+        // its device run's event pushes, each scheduler fire (OP_FIRE) and the fire's records it applied
+        std::vector<Op> trace;
+        std::vector<uint32_t> trace_off;
+        int64_t n_shifted_kept = 0;                          // shifted fires of keys not reordered
         RankMap rank;                                        // (position in the key's run, scheduler, key) -> slot
         int64_t n_fires = 0, n_shifted = 0;
     };
@@ -167,6 +176,13 @@ class SchedSim {
     void simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& logs, const std::vector<int32_t>& key_hash,
                   const KeyRows& rows, const std::function<KeyRun*(uint32_t)>& take_over, Result& out,
                   bool optimistic = false);
+    // after the optimistic pass `res` and the device rerun of res.reordered (logs: the merged logs, by key): true
+    // when every rerun key's new log makes exactly the model changes the optimistic pass made for it (same event
+    // pushes, same fires at the same positions and clocks, same records inside each fire). The exact pass would
+    // then retrace the optimistic one -- same model, every fire consistent, no host replay -- so its result is
+    // res with the rerun keys' fires ranked at their own (now the scheduler's) positions, which confirm() writes.
+    // false: run the exact pass.
+    bool confirm(const std::vector<nfa::SchedLog>& logs, Result& res) const;
     void commit() { std::swap(cur_, work_); }  // work_ is rebuilt from cur_ by the next simulate()
     // snapshot / restore of the committed scheduler states (sdg_snapshot): every key's queue and HashMap entry
     void save(std::vector<uint8_t>& out) const;

@@ -105,7 +105,7 @@ BatchClock batch_clock(Emu* e) {
     return bc;
 }
 
-size_t reordered_ = 0, taken_ = 0;
+size_t reordered_ = 0, taken_ = 0, exact_passes_ = 0;
 double us_[3] = {0, 0, 0};
 int g_reclaim = 0;      // emu_set_reclaim: every idle key goes through its idle record after each run (nfa.h to_idle)
 int64_t idles_ = 0;     // keys rebuilt from an idle record (all flushes)
@@ -376,7 +376,10 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
         }
         reordered_ = res.reordered.size();
         auto t2 = std::chrono::steady_clock::now();
-        q.sim.simulate(bc, all, q.key_hash, kr, take, res);
+        if (getenv("SDG_SCHED_EXACT") || !q.sim.confirm(all, res)) {
+            q.sim.simulate(bc, all, q.key_hash, kr, take, res);
+            ++exact_passes_;
+        }
         auto t3 = std::chrono::steady_clock::now();
         us_[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
         us_[1] += std::chrono::duration<double, std::micro>(t2 - t1).count();
@@ -530,7 +533,8 @@ int emu_flush(void* h) {
 }
 
 int64_t emu_sched_stat(int which) {
-    return which == 0 ? (int64_t)reordered_ : which == 1 ? (int64_t)taken_ : which == 5 ? growths_ : (int64_t)us_[which - 2];
+    return which == 0 ? (int64_t)reordered_ : which == 1 ? (int64_t)taken_ : which == 5 ? growths_
+         : which == 6 ? (int64_t)exact_passes_ : (int64_t)us_[which - 2];
 }
 int emu_num_queries(void* h) { return (int)((Emu*)h)->qs.size(); }
 const char* emu_query_name(void* h, int q) { return ((Emu*)h)->qs[q]->hq.name.c_str(); }

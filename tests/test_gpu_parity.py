@@ -611,6 +611,7 @@ def test_c4_vs_oracle(keys, oracle_built):
     assert len(ots) > 1000
     assert sum(s.sched_shifted for s in stats) > 0  # the collapse did delay fires
     assert sum(s.sched_rerun_keys for s in stats) > 0  # and reordered some keys' fires (device rerun)
-    print("C4 %d keys: rerun %d, host %d" % (keys, sum(s.sched_rerun_keys for s in stats),
-                                              sum(s.sched_host_keys for s in stats)))
+    print("C4 %d keys: rerun %d, host %d, exact passes %d" % (keys, sum(s.sched_rerun_keys for s in stats),
+                                                                sum(s.sched_host_keys for s in stats),
+                                                                sum(s.sched_exact_passes for s in stats)))
     assert np.array_equal(gts, ots) and np.array_equal(gvals.T, ovals) and not gnulls.any()
