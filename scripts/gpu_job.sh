@@ -75,6 +75,8 @@ for s in "$@"; do
         rxab) run rxt 900 env SDG_RX_TILE=16384 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_seq3.py tests/test_fallbacks.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider && for r in 1 2; do run rb_$r 300 env SDG_RX_TILE=16384 python3 bench.py --steps 10 --warmup 2 --no-cpu --no-gather --e2e-steps 0 && run rs_$r 300 env SDG_RX_TILE=8192 python3 bench.py --steps 10 --warmup 2 --no-cpu --no-parity --no-gather --e2e-steps 0; done && grep -h "^{" $OUT/rb_*.log $OUT/rs_*.log | python3 -c "import json,sys; [print(json.loads(l)['ms_per_step'], json.loads(l)['roofline']['kernel_ms']['ms_kg_scatter'], json.loads(l)['roofline']['kernel_ms']['ms_chain_match'], json.loads(l).get('parity',{}).get('bit_exact')) for l in sys.stdin]" && run rc5b 600 env SDG_RX_TILE=16384 python3 bench.py --config c5 --c5-shard 0/8 --steps 3 --warmup 1 --no-gather && run rc5s 600 env SDG_RX_TILE=8192 python3 bench.py --config c5 --c5-shard 0/8 --steps 3 --warmup 1 --no-gather && run rxw 180 env SDG_RX_TILE=16384 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/rxw" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-parity --no-gather --e2e-steps 0 ;;
         c4hp) run c4hp 600 env SDG_HOST_PROF=1 python3 scripts/bench_configs.py --only c4 ;;
         c4ab) run c4t 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_select.py -m gpu -x -q -s --timeout 300 --timeout-method thread -p no:cacheprovider -k "c4 or absent or collision" && run c4new 600 python3 scripts/bench_configs.py --only c4 && run c4hp 600 env SDG_HOST_PROF=1 python3 scripts/bench_configs.py --only c4 && run c4exact 600 env SDG_SCHED_EXACT=1 python3 scripts/bench_configs.py --only c4 ;;
+        c3rx) for r in 1 2; do run c3b_$r 300 env SDG_RX_TILE=16384 python3 scripts/bench_configs.py --only c3md --c3-steps 3 && run c3s_$r 300 env SDG_RX_TILE=8192 python3 scripts/bench_configs.py --only c3md --c3-steps 3; done && run c3rxprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/c3rxprof" -o run --output-format csv -- python3 scripts/bench_configs.py --only c3md --c3-steps 2 --warmup 1 && grep -h "^{" $OUT/c3b_*.log $OUT/c3s_*.log ;;
+        emab) run emt 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_robust.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider && for r in 1 2; do run e8_$r 300 python3 bench.py --steps 10 --warmup 2 --no-cpu --no-gather --e2e-steps 0 && run e6_$r 300 env SDG_FU_WPS=6 python3 bench.py --steps 10 --warmup 2 --no-cpu --no-parity --no-gather --e2e-steps 0; done && grep -h "^{" $OUT/e8_*.log $OUT/e6_*.log | python3 -c "import json,sys; [print(json.loads(l)['ms_per_step'], json.loads(l)['roofline']['kernel_ms']['ms_kg_scatter'], json.loads(l)['roofline']['kernel_ms']['ms_chain_match'], json.loads(l).get('parity',{}).get('bit_exact')) for l in sys.stdin]" && i=0 && for c in "FETCH_SIZE" "WRITE_SIZE"; do i=$((i+1)); run pmc$i 180 rocprofv3 --pmc $c --kernel-trace -d "$OUT/pmc$i" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-parity --no-gather --e2e-steps 0; done ;;
         *) echo "unknown step $s" ;;
     esac
 done

@@ -691,7 +691,20 @@ bool SchedSim::confirm(const std::vector<nfa::SchedLog>& logs, Result& res) cons
             }
         }
         const size_t b = res.trace_off[d], e = res.trace_off[d + 1];
-        if (got.size() != e - b || !std::equal(got.begin(), got.end(), res.trace.begin() + b)) return false;
+        if (got.size() != e - b || !std::equal(got.begin(), got.end(), res.trace.begin() + b)) {
+            if (std::getenv("SDG_SCHED_PROF")) {  // diagnostics: the first difference
+                size_t x = 0;
+                while (x < got.size() && b + x < e && got[x] == res.trace[b + x]) ++x;
+                auto pr = [](const char* w, const Op* o) {
+                    if (o) std::fprintf(stderr, "  %s g %u kind %d sched %d t %lld\n", w, o->g, o->kind, o->sched, (long long)o->t);
+                    else std::fprintf(stderr, "  %s (none)\n", w);
+                };
+                std::fprintf(stderr, "[sched confirm] key %u differs at op %zu of %zu / %zu\n", key, x, got.size(), e - b);
+                pr("rerun", x < got.size() ? &got[x] : nullptr);
+                pr("trace", b + x < e ? &res.trace[b + x] : nullptr);
+            }
+            return false;
+        }
         i = j;
     }
     for (size_t d = 0; d < res.reordered.size(); ++d)  // the reruns' fires sit at the scheduler's positions now

@@ -1278,27 +1278,37 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
     {
         const int64_t* c0p = n_out >= 1 ? (const int64_t*)a.cols[in0.b] : nullptr;
         const int64_t* c1p = n_out >= 2 ? (const int64_t*)a.cols[in1.b] : nullptr;
-        uint32_t op[FU_PT], oq[FU_PT];
-        int64_t v0[FU_PT], v1[FU_PT];
-#pragma unroll
-        for (int k = 0; k < FU_PT; ++k)
-            if (slot[k] != NOSLOT) {
-                op[k] = a.orig[lo + prow[k]];
-                oq[k] = a.orig[lo + qrow[k]];
-                if (fast && n_out >= 1) v0[k] = c0p[lo + (in0.a == 0 ? prow[k] : qrow[k])];
-                if (fast && n_out >= 2) v1[k] = c1p[lo + (in1.a == 0 ? prow[k] : qrow[k])];
-            }
         int64_t* const ov0 = a.out_vals;
         int64_t* const ov1 = a.out_vals + a.out_cap;
+        // FU_EH rounds at a time: their loads, then their stores. All FU_PT rounds at once needs 24 more VGPRs than
+        // the 8-waves-per-SIMD build has (64): it spilled the values to scratch and waited on every load (r3zb)
+        constexpr int FU_EH = W >= 8 ? 2 : FU_PT;
 #pragma unroll
-        for (int k = 0; k < FU_PT; ++k)
-            if (slot[k] != NOSLOT) {
-                a.out_ts[slot[k]] = tbase + (int64_t)s_ts[sw(res[k])];
-                a.out_emit_seq[slot[k]] = a.seq_base + (int64_t)oq[k];
-                a.out_first_seq[slot[k]] = a.seq_base + (int64_t)op[k];
-                if (fast && n_out >= 1) ov0[slot[k]] = v0[k];
-                if (fast && n_out >= 2) ov1[slot[k]] = v1[k];
+        for (int h = 0; h < FU_PT; h += FU_EH) {
+            uint32_t op[FU_EH], oq[FU_EH];
+            int64_t v0[FU_EH], v1[FU_EH];
+#pragma unroll
+            for (int i = 0; i < FU_EH; ++i) {
+                const int k = h + i;
+                if (slot[k] != NOSLOT) {
+                    op[i] = a.orig[lo + prow[k]];
+                    oq[i] = a.orig[lo + qrow[k]];
+                    if (fast && n_out >= 1) v0[i] = c0p[lo + (in0.a == 0 ? prow[k] : qrow[k])];
+                    if (fast && n_out >= 2) v1[i] = c1p[lo + (in1.a == 0 ? prow[k] : qrow[k])];
+                }
             }
+#pragma unroll
+            for (int i = 0; i < FU_EH; ++i) {
+                const int k = h + i;
+                if (slot[k] != NOSLOT) {
+                    a.out_ts[slot[k]] = tbase + (int64_t)s_ts[sw(res[k])];
+                    a.out_emit_seq[slot[k]] = a.seq_base + (int64_t)oq[i];
+                    a.out_first_seq[slot[k]] = a.seq_base + (int64_t)op[i];
+                    if (fast && n_out >= 1) ov0[slot[k]] = v0[i];
+                    if (fast && n_out >= 2) ov1[slot[k]] = v1[i];
+                }
+            }
+        }
     }
     uint32_t nm[FU_PT];
 #pragma unroll
