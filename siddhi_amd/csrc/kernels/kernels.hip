@@ -159,6 +159,8 @@ struct RxPass {
     const int64_t* ts_base;
     uint8_t* lkey_out;        // non-null: u8 keys >> lkey_shift here instead of keys_out
     int lkey_shift;
+    int ntiles;               // tiles; the grid is rounded up to a multiple of 8 (XCD remap)
+    int xcd;                  // 1: XCD-aware tile order
 };
 
 // stable tile scatter. Tile element e = w * 1024 + r * 64 + lane belongs to wave w (16 rounds r), so a wave
@@ -179,11 +181,18 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
     __shared__ uint8_t sdig[RX_TILE];  // digit of each staged element: its destination is gbase + rank in the run
     __shared__ uint64_t stage[RX_TILE];
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    const int64_t base = (int64_t)blockIdx.x * RX_TILE;
+    // XCD-aware tile order: the hardware deals consecutive block ids round-robin to the 8 XCDs; virtual tile v gives
+    // each XCD a contiguous run of tiles. A digit's runs of consecutive tiles are adjacent in the output, so the
+    // cache line where one tile's run ends and the next one's begins is completed in one XCD's L2 instead of being
+    // written back partially by two
+    const uint32_t G8 = gridDim.x / 8;
+    const uint32_t tile = a.xcd ? (blockIdx.x & 7u) * G8 + (blockIdx.x >> 3) : blockIdx.x;
+    if ((int)tile >= a.ntiles) return;  // block-uniform: the rounding of the grid
+    const int64_t base = (int64_t)tile * RX_TILE;
     const int64_t tile_n = min((int64_t)RX_TILE, a.n - base);
     const int64_t wbase = base + w * (R * 64);
     for (int d = t; d < a.nb; d += RX_THREADS) {
-        gbase[d] = a.offsets[(int64_t)blockIdx.x * a.nb + d];
+        gbase[d] = a.offsets[(int64_t)tile * a.nb + d];
 #pragma unroll
         for (int v = 0; v < NW; ++v) wc[v][d] = 0;
     }
@@ -651,12 +660,16 @@ static void launch_rx_hist(int64_t nt, hipStream_t stream, const uint32_t* keys,
         hipLaunchKernelGGL((rx_hist<RX_TILE, RX_THREADS>), dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, keys, n,
                            shift, mask, nb, counts, kcheck, kflag);
 }
-static void launch_rx_scatter(int64_t nt, hipStream_t stream, const RxPass& rp) {
+static void launch_rx_scatter(int64_t nt, hipStream_t stream, RxPass rp) {
+    static const bool no_xcd = getenv("SDG_RX_NOXCD") != nullptr;  // A/B: tiles in block order
+    rp.ntiles = (int)nt;
+    rp.xcd = !no_xcd;
+    const int64_t grid = no_xcd ? nt : (nt + 7) / 8 * 8;
     if (rx_tile() == RX_TILE_BIG)
-        hipLaunchKernelGGL((rx_scatter<RX_TILE_BIG, RX_THREADS_BIG>), dim3((unsigned)nt), dim3(RX_THREADS_BIG), 0,
+        hipLaunchKernelGGL((rx_scatter<RX_TILE_BIG, RX_THREADS_BIG>), dim3((unsigned)grid), dim3(RX_THREADS_BIG), 0,
                            stream, rp);
     else
-        hipLaunchKernelGGL((rx_scatter<RX_TILE, RX_THREADS>), dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, rp);
+        hipLaunchKernelGGL((rx_scatter<RX_TILE, RX_THREADS>), dim3((unsigned)grid), dim3(RX_THREADS), 0, stream, rp);
 }
 
 size_t keygroup_workspace(int64_t n, int32_t K, int32_t ncols, const uint8_t* widths) {
