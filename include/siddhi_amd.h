@@ -69,6 +69,11 @@ typedef struct sdg_opts {
 #define SDG_FORCE_GENERIC 2    /* run every query on the generic keyed-NFA kernel (testing: both kernels on one query) */
 #define SDG_NO_FUSED 4         /* chain path: always key-sort with the full radix (testing: both chain kernels on one query) */
 #define SDG_NO_SEQ3 8          /* sequences of the seq3 shape on the generic keyed NFA instead (testing: both kernels) */
+#define SDG_SCHED_EXACT 16     /* absent states: always run the scheduler's exact pass, even when the device reruns
+                                  reproduce the optimistic pass (testing: pins the exact pass against the oracle) */
+#define SDG_SCHED_HOST 32      /* absent states: no optimistic pass / device rerun; the exact pass runs over the
+                                  ideal-order device run and replays every key it orders differently on the host
+                                  (testing: pins the host replay KeyRun against the oracle) */
 
 typedef struct sdg_out {
     int64_t n;                 /* output events */

@@ -217,13 +217,13 @@ class InputHandler:
 
 class SiddhiAppRuntime:
     def __init__(self, app_text, device=0, batch_capacity=0, compile_only=False, force_generic=False, fused=True,
-                 max_partials=0, seq3=True):
+                 max_partials=0, seq3=True, sched_exact=False, sched_host=False):
         L = load_library()
         self._L = L
         h = ctypes.c_void_p()
         opts = _Opts(device, batch_capacity, max_partials,
                      (1 if compile_only else 0) | (2 if force_generic else 0) | (0 if fused else 4) |
-                     (0 if seq3 else 8))
+                     (0 if seq3 else 8) | (16 if sched_exact else 0) | (32 if sched_host else 0))
         _check(L.sdg_compile(app_text.encode(), ctypes.byref(opts), ctypes.byref(h)))
         self._h = h
         self._compile_only = compile_only

@@ -340,6 +340,8 @@ struct sdg_engine {
     bool force_generic = false;
     bool no_fused = false;
     bool no_seq3 = false;        // SDG_NO_SEQ3 / SDG_FORCE_GENERIC: seq3-shaped sequences on the generic NFA
+    bool sched_exact = false;    // SDG_SCHED_EXACT (flag or env): the scheduler's exact pass always runs
+    bool sched_host = false;     // SDG_SCHED_HOST: exact pass over the first run, diverged keys replayed on the host
     uint64_t app_hash = 0;       // FNV-1a of the app text: a snapshot restores only into the app it came from
     std::vector<uint8_t> snap;   // the last sdg_snapshot's bytes (valid until the next snapshot / destroy)
     std::vector<Stage> stage;    // per stream: host pushes staged in HBM (see stage_push)
@@ -1893,7 +1895,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 return r;
             };
             SchedSim::Result res;
-            for (int tries = 0;; ++tries) {
+            for (int tries = 0; !e->sched_host; ++tries) {
                 q.sim.simulate(e->bc, logs, q.key_hash, kr, take, res, true);
                 hp.mark("sched_simulate_optimistic");
                 q.reordered = res.reordered;
@@ -1924,9 +1926,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             }
             q.runs.clear();
             // the exact pass only when the reruns did not reproduce the optimistic pass's model changes
-            // (SDG_SCHED_EXACT: always, A/B)
-            static const bool sched_exact = getenv("SDG_SCHED_EXACT") != nullptr;
-            if (sched_exact || !q.sim.confirm(logs, res)) {
+            // (SDG_SCHED_EXACT: always; SDG_SCHED_HOST: no optimistic pass, so always)
+            if (e->sched_exact || e->sched_host || !q.sim.confirm(logs, res)) {
                 q.sim.simulate(e->bc, logs, q.key_hash, kr, take, res);
                 e->stats.sched_exact_passes += 1;
             }
@@ -3017,6 +3018,8 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             e->force_generic = (opts->flags & SDG_FORCE_GENERIC) != 0;
             e->no_fused = (opts->flags & SDG_NO_FUSED) != 0;
             e->no_seq3 = (opts->flags & (SDG_NO_SEQ3 | SDG_FORCE_GENERIC)) != 0;
+            e->sched_exact = (opts->flags & SDG_SCHED_EXACT) != 0 || getenv("SDG_SCHED_EXACT") != nullptr;
+            e->sched_host = (opts->flags & SDG_SCHED_HOST) != 0;
         }
         if (opts && opts->max_partials > 0) {
             if (opts->max_partials > 4096) throw CompileError(SDG_ERR_ARG, "max_partials must be <= 4096");

@@ -8,9 +8,10 @@ TAG = {sa.INT: "i", sa.LONG: "l", sa.FLOAT: "f", sa.DOUBLE: "d", sa.BOOL: "b", s
 
 
 class ProductAdapter:
-    def __init__(self, app, force_generic=False, fused=True, max_partials=0, seq3=True):
+    def __init__(self, app, force_generic=False, fused=True, max_partials=0, seq3=True, **kw):
         self.rt = sa.SiddhiAppRuntime(app, force_generic=force_generic, fused=fused, max_partials=max_partials,
-                                      seq3=seq3)
+                                      seq3=seq3, **kw)
+        self.stats = []  # sdg_stats of every flush
         self.handlers = {}
         self.records = []
 
@@ -40,6 +41,7 @@ class ProductAdapter:
 
     def flush(self):
         self.rt.flush(deliver=False)
+        self.stats.append(self.rt.stats())
         for q, (name, target, types, names) in enumerate(self.rt._queries):
             types, ts, vals, nulls = self.rt.raw_outputs(q)
             def dec(t, v):

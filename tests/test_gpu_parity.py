@@ -573,8 +573,8 @@ def test_failed_flush_consumes_its_batch(oracle_built):
 
 
 # ---- absent states on the device (C4): timers, the global scheduler, host replays -----------------------------
-def product_c4(c, end, batches=3):
-    rt = sa.SiddhiAppRuntime(w.C4_APP)
+def product_c4(c, end, batches=3, **kw):
+    rt = sa.SiddhiAppRuntime(w.C4_APP, **kw)
     try:
         assert rt.query_paths() == [1]
         idx = np.array([rt._L.sdg_stream_index(rt._h, s.encode()) for s in w.C4_STREAMS], dtype=np.int32)
