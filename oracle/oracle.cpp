@@ -400,6 +400,125 @@ struct JHashMap {
     }
 };
 
+// PartitionState.partitionKeys (PartitionRuntimeImpl.java:423) is a java.util.concurrent.ConcurrentHashMap
+// <String, Long>; PartitionStreamReceiver.send(ComplexEvent) (:274-283) walks getPartitionKeys() = new
+// HashSet<>(partitionKeys.keySet()) (PartitionRuntimeImpl.java:404-407). Both iteration orders, JDK 8, single-threaded:
+//   ConcurrentHashMap: table of 16 on the first put (initTable); putVal appends a new key at the TAIL of its bin;
+//     after a put that makes count >= sizeCtl (0.75 n) the table doubles (addCount -> transfer); a put that walked
+//     >= 8 nodes of a bin calls treeifyBin, which on a table < 64 presizes instead (tryPresize(n << 1): doubles
+//     until tableSizeFor(3n + 1) <= sizeCtl). transfer splits a list bin by its `lastRun`: the maximal tail whose
+//     nodes all go to one side keeps its order and heads that side; every node before it is PREPENDED to its side
+//     (so their order reverses). Iteration: bins 0..n-1, each bin's list in order. Tree bins (>= 8 keys in one bin
+//     of a table >= 64) are not modelled: such a bin throws.
+//   HashSet(Collection c): new HashMap(max((int)(c.size() / .75f) + 1, 16)) (capacity tableSizeFor of that), then
+//     add() of every key in the CHM's iteration order; HashMap.putVal appends at the tail of its bin (no resize
+//     happens below 0.75 load; a bin reaching 9 keys would treeify and is not modelled: throws).
+struct JavaCHM {
+    struct Node {
+        int32_t hash;  // spread(h) = (h ^ h >>> 16) & 0x7fffffff
+        std::string key;
+    };
+    std::vector<std::vector<Node>> table;
+    int64_t count = 0, sizeCtl = 0;
+    static int32_t spread(const std::string& k) {
+        int32_t h = java_string_hash(k);
+        return (h ^ (int32_t)((uint32_t)h >> 16)) & 0x7fffffff;
+    }
+    static int64_t tableSizeFor(int64_t c) {
+        int64_t n = 1;
+        while (n < c) n <<= 1;
+        return n;
+    }
+    void transfer() {  // ConcurrentHashMap.transfer, one thread
+        const size_t n = table.size();
+        std::vector<std::vector<Node>> nt(2 * n);
+        for (size_t i = 0; i < n; ++i) {
+            std::vector<Node>& f = table[i];
+            if (f.empty()) continue;
+            size_t lastRun = 0;
+            bool runBit = (f[0].hash & (int32_t)n) != 0;
+            for (size_t p = 1; p < f.size(); ++p) {
+                const bool b = (f[p].hash & (int32_t)n) != 0;
+                if (b != runBit) { runBit = b; lastRun = p; }
+            }
+            std::vector<Node> ln, hn;  // built front to back: the lastRun tail, then the prefix prepended
+            std::vector<Node>& run = runBit ? hn : ln;
+            run.assign(f.begin() + lastRun, f.end());
+            for (size_t p = 0; p < lastRun; ++p) {
+                std::vector<Node>& side = (f[p].hash & (int32_t)n) ? hn : ln;
+                side.insert(side.begin(), f[p]);
+            }
+            nt[i] = std::move(ln);
+            nt[i + n] = std::move(hn);
+        }
+        table.swap(nt);
+        sizeCtl = (int64_t)(2 * n) - (int64_t)(n >> 1);  // 0.75 * 2n
+    }
+    void put(const std::string& k) {  // putVal(k, v, false) then addCount
+        if (table.empty()) {
+            table.assign(16, {});
+            sizeCtl = 12;
+        }
+        const int32_t h = spread(k);
+        std::vector<Node>& bin = table[(table.size() - 1) & (uint32_t)h];
+        int binCount = 0;
+        bool found = false;
+        if (!bin.empty()) {
+            binCount = 1;
+            for (size_t p = 0;; ++binCount, ++p) {
+                if (bin[p].hash == h && bin[p].key == k) { found = true; break; }
+                if (p + 1 == bin.size()) { bin.push_back(Node{h, k}); break; }
+            }
+        } else {
+            bin.push_back(Node{h, k});
+        }
+        if (binCount >= 8) {  // treeifyBin
+            if (table.size() < 64) {  // tryPresize(n << 1)
+                const int64_t c = tableSizeFor(3 * (int64_t)table.size() + 1);
+                while (!(c <= sizeCtl)) transfer();
+            } else {
+                throw OracleError("partition key order: a ConcurrentHashMap tree bin (not modelled)");
+            }
+        }
+        if (found) return;
+        if (++count >= sizeCtl) transfer();
+    }
+    void remove(const std::string& k) {  // replaceNode(k, null, null): unlinked, the table never shrinks
+        if (table.empty()) return;
+        const int32_t h = spread(k);
+        std::vector<Node>& bin = table[(table.size() - 1) & (uint32_t)h];
+        for (size_t p = 0; p < bin.size(); ++p)
+            if (bin[p].hash == h && bin[p].key == k) {
+                bin.erase(bin.begin() + p);
+                --count;
+                return;
+            }
+    }
+    // new HashSet<>(keySet()) iterated
+    std::vector<std::string> hashset_order() const {
+        int64_t cap = tableSizeFor(std::max<int64_t>((int64_t)((float)count / 0.75f) + 1, 16));
+        std::vector<std::vector<const Node*>> hs((size_t)cap);
+        for (const auto& bin : table)
+            for (const Node& nd : bin) {
+                auto& b = hs[(size_t)(nd.hash & (int32_t)(cap - 1))];
+                b.push_back(&nd);
+                if (b.size() >= 9) {  // putVal's treeifyBin: a table < 64 resizes (order-preserving split)
+                    if (cap >= 64) throw OracleError("partition key order: a HashMap tree bin (not modelled)");
+                    std::vector<std::vector<const Node*>> nt((size_t)cap * 2);
+                    for (const auto& ob : hs)
+                        for (const Node* x : ob) nt[(size_t)(x->hash & (int32_t)(2 * cap - 1))].push_back(x);
+                    hs.swap(nt);
+                    cap *= 2;
+                }
+            }
+        std::vector<std::string> out;
+        out.reserve((size_t)count);
+        for (const auto& b : hs)
+            for (const Node* x : b) out.push_back(x->key);
+        return out;
+    }
+};
+
 // ------------------------------------------------------------------------------------------------
 struct Engine;
 struct Ctx {
@@ -1772,6 +1891,7 @@ struct PartitionRt {
     int index = 0;
     std::vector<int> queries;
     std::unordered_map<std::string, int64_t> keys;  // PartitionState.partitionKeys: key -> currentTime at its last event
+    JavaCHM keyOrder;                                // the same keys in the ConcurrentHashMap's iteration order
     bool purge = false;
     int64_t purge_interval = 0, purge_idle = 0;
     int64_t first_init = INT64_MIN;                 // currentTime of the partition's first initPartition
@@ -1791,7 +1911,7 @@ struct AppRt {
     std::vector<std::unique_ptr<PartitionRt>> partitions;
     // per stream: ordered subscribers (receivers of top-level queries, partition receivers)
     struct Sub {
-        int kind;  // 0 receiver, 1 partition receiver
+        int kind;  // 0 receiver, 1 partition receiver, 2 partition receiver of a stream without a partition key
         Receiver* r = nullptr;
         PartitionRt* p = nullptr;
     };
@@ -2597,6 +2717,18 @@ void AppRt::deliverStream(int stream, const SEv& ev) {
             eng.ctx.key.clear();
             sub.r->receive(ev);
             eng.ctx = outer;
+        } else if (sub.kind == 2) {
+            // PartitionStreamReceiver.send(ComplexEvent) (:274-283): a stream with no partition executor goes to
+            // every key of getPartitionKeys() (PartitionRuntimeImpl.java:404-407), in that HashSet's order; no
+            // initPartition, no partitionKeys.put (the keys' purge clocks do not move)
+            auto it = innerSubs.find({sub.p->index, stream});
+            if (it == innerSubs.end()) continue;
+            for (const std::string& key : sub.p->keyOrder.hashset_order()) {
+                eng.ctx.has_key = true;
+                eng.ctx.key = key;
+                for (Receiver* r : it->second) r->receive(ev);
+            }
+            eng.ctx = outer;
         } else {
             PartitionRt* p = sub.p;
             for (auto& w : p->with) {
@@ -2642,6 +2774,7 @@ void AppRt::deliverStream(int stream, const SEv& ev) {
                     if (it != p->keys.end() && p->first_init != INT64_MIN && now >= p->first_init + p->purge_interval &&
                         it->second + p->purge_idle < now) {
                         p->keys.erase(it);
+                        p->keyOrder.remove(key);
                         for (int qi : p->queries) queries[qi]->purgeKey(key);
                     }
                 }
@@ -2650,6 +2783,7 @@ void AppRt::deliverStream(int stream, const SEv& ev) {
                     if (p->first_init == INT64_MIN) p->first_init = now;
                 }
                 p->keys[key] = now;
+                p->keyOrder.put(key);  // partitionKeys.put: a new key, or a walk along its bin (treeifyBin)
                 auto it = innerSubs.find({p->index, stream});
                 if (it != innerSubs.end())
                     for (Receiver* r : it->second) r->receive(ev);
@@ -2753,10 +2887,15 @@ static void build_app(orc_engine* e, const char* text) {
                 rt.subs[si].push_back(s);
             }
         }
-        // inner streams without a partition key are broadcast in the reference; not supported here
+        // streams of the partition's queries without a partition key: PartitionRuntimeImpl.addPartitionReceiver
+        // (:290-304) subscribes a PartitionStreamReceiver with no executors, which broadcasts (kind 2)
         for (auto& kv : rt.innerSubs)
-            if (kv.first.first == (int)pi && std::find(streamsSeen.begin(), streamsSeen.end(), kv.first.second) == streamsSeen.end())
-                throw OracleError("unsupported: un-partitioned stream used inside a partition");
+            if (kv.first.first == (int)pi && std::find(streamsSeen.begin(), streamsSeen.end(), kv.first.second) == streamsSeen.end()) {
+                AppRt::Sub s;
+                s.kind = 2;
+                s.p = p;
+                rt.subs[kv.first.second].push_back(s);
+            }
     }
 }
 

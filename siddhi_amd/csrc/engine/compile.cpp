@@ -176,9 +176,9 @@ class QC {
         p.partitioned = q_.partition_index >= 0;
         detect_chain(root);
         for (int ka : h_.key_attr)
-            if (ka == -2) {  // an event may go to several keys (one view row each): the generic NFA
+            if (ka == -2 || ka == -3) {  // an event may go to several keys (one view row each): the generic NFA
                 p.chain = 0;
-                h_.chain_reason = "range partition";
+                h_.chain_reason = ka == -2 ? "range partition" : "a stream without a partition key (broadcast)";
             }
         if (p.has_post) {  // the selector's post pass reads every record's key: the generic NFA writes it
             p.chain = 0;
@@ -950,8 +950,15 @@ class QC {
                 h_.key_kind[i] = (uint8_t)def.attrs[ai].type;
                 found = true;
             }
-            if (!found)
-                throw CompileError(SDG_ERR_UNSUPPORTED, "stream '" + def.id + "' used in a partition without a key");
+            if (!found) {
+                // no partition executor for this stream: PartitionStreamReceiver.send(ComplexEvent) (:274-283)
+                // delivers each of its events to every key the partition has initialised, in getPartitionKeys()
+                // order (keyorder.h), without initPartition
+                if (part.purge)
+                    throw CompileError(SDG_ERR_UNSUPPORTED, "@purge with a stream that has no partition key ('" + def.id + "')");
+                h_.key_attr[i] = -3;
+                h_.key_kind[i] = 0;
+            }
         }
     }
 
@@ -985,6 +992,22 @@ std::vector<HostQuery> compile_app(const sql::App& app, Interner& strings) {
         HostQuery h;
         QC(app, q, strings, h).run();
         out.push_back(std::move(h));
+    }
+    // a stream without a partition key goes to every key of the PARTITION (PartitionRuntimeImpl.partitionKeys: the
+    // keys any of its queries' keyed streams delivered). The engine keeps the key set per query, so every keyed
+    // stream of the partition's queries must be a keyed stream of the broadcasting query too
+    for (const auto& h : out) {
+        if (std::find(h.key_attr.begin(), h.key_attr.end(), -3) == h.key_attr.end()) continue;
+        for (const auto& g : out) {
+            if (g.partition != h.partition) continue;
+            for (size_t i = 0; i < g.streams.size(); ++i) {
+                if (g.key_attr[i] == -3) continue;
+                const int hp = h.stream_pos(g.streams[i]);
+                if (hp < 0 || h.key_attr[hp] == -3)
+                    throw CompileError(SDG_ERR_UNSUPPORTED, "query '" + h.name + "' broadcasts a stream without a partition key "
+                                       "but does not read the partition's keyed stream '" + app.streams[g.streams[i]].id + "'");
+            }
+        }
     }
     // a query output consumed by another query (query chaining) is not on the device path
     for (const auto& h : out)

@@ -37,7 +37,8 @@ struct HostQuery {
     std::vector<int> streams;                          // app stream index, receiver (first appearance) order
     std::vector<std::pair<std::string, uint8_t>> cols; // physical column (attribute name, kind)
     std::vector<std::vector<int>> col_attr;            // [query stream][column] -> attribute index or -1
-    std::vector<int> key_attr;                         // [query stream] partition key attribute (-1: none, -2: ranges)
+    std::vector<int> key_attr;                         // [query stream] partition key attribute (-1: none, -2: ranges,
+                                                       //  -3: no key in the partition: broadcast to every key)
     struct RangeKey {
         Prog cond;                                     // over the stream's event (OP_LOAD slot 0, physical columns)
         uint32_t label;                                // interned label: the partition key when cond holds

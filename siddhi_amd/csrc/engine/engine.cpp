@@ -19,6 +19,7 @@
 #include "../kernels/kernels.h"
 #include "../siddhiql/parser.h"
 #include "compile.h"
+#include "keyorder.h"
 #include "keyrun.h"
 #include "hostpar.h"
 #include "sched.h"
@@ -227,6 +228,10 @@ struct QueryRt {
     HostPin kt_ret;
     std::unordered_map<std::string, uint32_t> keydict;
     std::vector<std::string> keystr;                // keydict id -> key text (numeric keys)
+    // a stream of the query without a partition key (key_attr -3): its events go to every key the partition has
+    // initialised, in getPartitionKeys() order (keyorder.h); host batch assembly only
+    bool broadcast = false;
+    PartitionKeyOrder korder;
     // absent states: the scheduler simulation, per-key HashMap hashes, double-buffered arenas, the run's log
     SchedSim sim;
     std::vector<int32_t> key_hash;
@@ -485,7 +490,7 @@ bool seq3_spec_(const HostQuery& h, Seq3Spec& s, int& why) {
     if (P.chain || !P.seq || P.n_states != 3 || P.n_sched || P.purge || P.has_post) return why = 1, false;
     if (h.streams.size() != 1 || P.n_cols < 1 || P.n_cols > S3_MAX_COLS || P.n_out > S3_MAX_OUT) return why = 2, false;
     for (int x : h.key_attr)
-        if (x == -2) return why = 3, false;  // range partitions
+        if (x == -2 || x == -3) return why = 3, false;  // range partitions, broadcast streams
     const StateRow &r0 = P.st[0], &r1 = P.st[1], &r2 = P.st[2];
     if (r0.kind != PK_STREAM || !r0.is_start || r0.next != 1 || r0.next_every != 0 || (r0.within_every != -1 && r0.within_every != 0) ||
         r0.callback != -1)
@@ -1063,11 +1068,11 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     const void* d_cols[MAX_COLS] = {};
     const uint8_t* d_nulls[MAX_COLS] = {};
     int64_t nrows = 0;
-    const bool ranged = std::find(h.key_attr.begin(), h.key_attr.end(), -2) != h.key_attr.end();
-    const uint8_t* d_vrank = nullptr;
-    bool zero_copy = parts.size() == 1 && parts[0]->device && !multi_stream && parts[0]->stream >= 0;
+    const bool ranged = std::find(h.key_attr.begin(), h.key_attr.end(), -2) != h.key_attr.end() || q.broadcast;
+    const uint32_t* d_vrank = nullptr;
+    bool zero_copy = parts.size() == 1 && parts[0]->device && !multi_stream && parts[0]->stream >= 0 && !q.broadcast;
     // several staged host pushes of the query's one stream: consecutive rows of the stream's staging
-    bool staged_run = !zero_copy && !multi_stream && !parts.empty();
+    bool staged_run = !zero_copy && !multi_stream && !parts.empty() && !q.broadcast;
     for (size_t i = 0; i < parts.size() && staged_run; ++i)
         staged_run = parts[i]->device && parts[i]->stage_off >= 0 && parts[i]->stream == parts[0]->stream &&
                      (i == 0 || parts[i]->stage_off == parts[i - 1]->stage_off + parts[i - 1]->n);
@@ -1107,7 +1112,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         nrows = n;
     }
     // mixed pushes only (C4's interleaved streams): the view is built on the device from the raw slot rows
-    bool dev_mixed = !zero_copy && !parts.empty() && !ranged && !getenv("SDG_NO_DEVMIX") &&
+    bool dev_mixed = !zero_copy && !parts.empty() && !ranged && !q.broadcast && !getenv("SDG_NO_DEVMIX") &&
                      (!partitioned || q.string_keys || q.key_class != KC_NONE) &&
                      e->stream_types.size() <= (size_t)MV_MAX_STREAMS;
     for (const PushChunk* c : parts) dev_mixed &= c->stream == -2 && !c->device && c->cols.size() <= (size_t)MV_MAX_ATTRS;
@@ -1128,7 +1133,23 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         std::vector<std::vector<uint8_t>> cols(nc), nulls(nc);
         std::vector<bool> any_null(nc, false);
         std::vector<uint32_t> vpos;
-        std::vector<uint8_t> vrank;  // range partitions: the range each view row came from (its delivery sub-order)
+        std::vector<uint32_t> vrank;  // range partitions: the range each view row came from; broadcast rows: the key's
+                                      // rank in getPartitionKeys() order (the delivery sub-order)
+        // partitionKeys.put of a keyed row (broadcast queries): the key set and order the next broadcast row sees
+        auto key_seen = [&](uint32_t key) {
+            if (!q.broadcast) return;
+            while (q.key_hash.size() <= (size_t)key) {
+                const size_t k = q.key_hash.size();
+                q.key_hash.push_back(java_spread_hash(q.string_keys ? e->strings.strs[k] : q.keystr[k]));
+            }
+            q.korder.add(key, q.key_hash[key]);
+        };
+        auto bcast_order = [&]() -> const std::vector<uint32_t>& {
+            const std::vector<uint32_t>& o = q.korder.order();
+            if (o.size() >= ((size_t)1 << 23))
+                throw CompileError(SDG_ERR_CAPACITY, "a broadcast to more than 2^23 partition keys");
+            return o;
+        };
         ts.reserve(n);
         vpos.reserve(n);
         for (int k = 0; k < nc; ++k) cols[k].reserve((size_t)n * width_of(P.col_kind[k]));
@@ -1139,7 +1160,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 struct VRow {
                     int64_t r;
                     uint32_t key;
-                    uint8_t rank, qpos;
+                    uint32_t rank;
+                    uint8_t qpos;
                 };
                 std::vector<VRow> vr;
                 vr.reserve((size_t)c->n);
@@ -1160,12 +1182,16 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                     if (partitioned && h.key_attr[qpos] == -2) {  // one view row per range that holds, in range order
                         const auto& rs = h.key_ranges[qpos];
                         for (size_t x = 0; x < rs.size(); ++x)
-                            if (range_holds(h, rs[x], qpos, *c, r, true)) vr.push_back({r, rs[x].label, (uint8_t)x, (uint8_t)qpos});
+                            if (range_holds(h, rs[x], qpos, *c, r, true)) vr.push_back({r, rs[x].label, (uint32_t)x, (uint8_t)qpos});
+                    } else if (partitioned && h.key_attr[qpos] == -3) {  // one view row per initialised key, in order
+                        const std::vector<uint32_t>& o = bcast_order();
+                        for (size_t x = 0; x < o.size(); ++x) vr.push_back({r, o[x], (uint32_t)x, (uint8_t)qpos});
                     } else if (partitioned) {
                         const int ai = h.key_attr[qpos];
                         if (!c->nulls[ai].empty() && c->nulls[ai][r]) continue;  // null partition key: dropped
                         uint32_t key = 0;
                         if (!slot_key(e, q, qpos, ((const int64_t*)c->cols[ai].data())[r], &key)) continue;
+                        key_seen(key);
                         vr.push_back({r, key, 0, (uint8_t)qpos});
                     } else {
                         vr.push_back({r, 0, 0, (uint8_t)qpos});
@@ -1217,8 +1243,17 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                         if (range_holds(h, rs[x], qpos, *c, r, false)) {
                             keys.push_back(rs[x].label);
                             kept.push_back(r);
-                            vrank.push_back((uint8_t)x);
+                            vrank.push_back((uint32_t)x);
                         }
+            } else if (partitioned && h.key_attr[qpos] == -3) {  // one view row per initialised key (a chunk of one
+                all = false;                                      // stream: the key set is the same for all its rows)
+                const std::vector<uint32_t>& o = bcast_order();
+                for (int64_t r = 0; r < c->n; ++r)
+                    for (size_t x = 0; x < o.size(); ++x) {
+                        keys.push_back(o[x]);
+                        kept.push_back(r);
+                        vrank.push_back((uint32_t)x);
+                    }
             } else if (partitioned) {
                 keys.reserve(keys.size() + (size_t)c->n);
                 const uint8_t kk = h.key_kind[qpos];
@@ -1237,11 +1272,12 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                         continue;
                     }
                     keys.push_back(key);
+                    key_seen(key);
                     if (!all) kept.push_back(r);
                 }
             }
             const size_t m = all ? (size_t)c->n : kept.size();
-            if (ranged && h.key_attr[qpos] != -2) vrank.resize(base + m, 0);
+            if (ranged && h.key_attr[qpos] != -2 && h.key_attr[qpos] != -3) vrank.resize(base + m, 0);
             if (all) ts.insert(ts.end(), c->ts.begin(), c->ts.begin() + c->n);
             else for (int64_t r : kept) ts.push_back(c->ts[r]);
             if (all) for (int64_t r = 0; r < c->n; ++r) vpos.push_back((uint32_t)(part_pos[pi] + r));
@@ -1290,8 +1326,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             if (nrows) HIPCHECK(hipMemcpyAsync((void*)d_key, keys.data(), nrows * 4, hipMemcpyHostToDevice, st));
         }
         if (ranged) {
-            d_vrank = (const uint8_t*)q.st_vrank.ensure(cnt);
-            if (nrows) HIPCHECK(hipMemcpyAsync((void*)d_vrank, vrank.data(), nrows, hipMemcpyHostToDevice, st));
+            d_vrank = (const uint32_t*)q.st_vrank.ensure(cnt * 4);
+            if (nrows) HIPCHECK(hipMemcpyAsync((void*)d_vrank, vrank.data(), nrows * 4, hipMemcpyHostToDevice, st));
         }
         for (int k = 0; k < nc; ++k) {
             int w = width_of(P.col_kind[k]);
@@ -1334,7 +1370,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     // ---- 2. key grouping ---------------------------------------------------------------------------------
     const int64_t* v_ts = d_ts;
     const uint8_t* v_qs = d_qs;
-    const uint8_t* v_vrank = d_vrank;
+    const uint32_t* v_vrank = d_vrank;
     const uint32_t* v_key = nullptr;
     const uint32_t* v_seg = nullptr;
     const uint32_t* v_orig = d_vpos;  // partitioned: replaced by orig_sorted (positions when d_vpos is set)
@@ -1369,7 +1405,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             a.src[c] = d_ts; a.dst[c] = q.so_ts.ensure(nrows * 8); a.width[c] = 8; v_ts = (const int64_t*)a.dst[c]; ++c;
         }
         if (d_qs) { a.src[c] = d_qs; a.dst[c] = q.so_qs.ensure(nrows); a.width[c] = 1; v_qs = (const uint8_t*)a.dst[c]; ++c; }
-        if (d_vrank) { a.src[c] = d_vrank; a.dst[c] = q.so_vrank.ensure(nrows); a.width[c] = 1; v_vrank = (const uint8_t*)a.dst[c]; ++c; }
+        if (d_vrank) { a.src[c] = d_vrank; a.dst[c] = q.so_vrank.ensure(nrows * 4); a.width[c] = 4; v_vrank = (const uint32_t*)a.dst[c]; ++c; }
         for (int k = 0; k < nc; ++k) {
             if (c >= MAX_COLS + 2) throw CompileError(SDG_ERR_UNSUPPORTED, "too many columns");
             int w = width_of(P.col_kind[k]);
@@ -1868,6 +1904,10 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 r->pos.resize(m);
                 for (int64_t p = 0; p < m; ++p) r->pos[p] = (uint32_t)kr.pos(b + p);
                 if (m) HIPCHECK(hipMemcpy(r->ts.data(), v_ts + b, m * 8, hipMemcpyDeviceToHost));
+                if (v_vrank) {
+                    r->vrank.resize(m);
+                    if (m) HIPCHECK(hipMemcpy(r->vrank.data(), v_vrank + b, m * 4, hipMemcpyDeviceToHost));
+                }
                 r->has_qs = multi_stream;
                 if (multi_stream) {
                     r->qs.resize(m);
@@ -2694,6 +2734,9 @@ struct SnapR {
     }
 };
 constexpr uint64_t SNAP_MAGIC = 0x31504e5347445353ull;  // "SSDGSNP1"
+}  // namespace
+void sdg::PartitionKeyOrder::throw_corrupt() { throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (partition keys)"); }
+namespace {
 
 void snapshot(sdg_engine* e, std::vector<uint8_t>& out) {
     out.clear();
@@ -2730,6 +2773,7 @@ void snapshot(sdg_engine* e, std::vector<uint8_t>& out) {
         w.put<uint64_t>(q.keystr.size());
         for (auto& x : q.keystr) w.str(x);
         w.vec(q.key_hash);
+        if (q.broadcast) q.korder.save(w);
         // generic NFA: layout + both arena copies + the committed-copy bits
         w.put(q.L);
         w.put<int64_t>(q.arena_keys);
@@ -2799,6 +2843,7 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
         uint64_t in = 0;
         std::vector<std::string> keystr;
         std::vector<int32_t> key_hash;
+        PartitionKeyOrder korder;
         nfa::Layout L{};
         int64_t arena_keys = 0;
         View arena, arena2, cur_bits, last_seen, agg;
@@ -2845,6 +2890,7 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
         g.keystr.resize(nks);
         for (auto& x : g.keystr) x = r.str();
         r.vec(g.key_hash);
+        if (e->qs[qi]->broadcast) g.korder.load(r);
         g.L = r.get<nfa::Layout>();
         g.arena_keys = r.get<int64_t>();
         if (g.arena_keys < 0) throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (arena keys)");
@@ -2934,6 +2980,7 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
         q.kt_synced = 0;
         for (size_t i = 0; i < q.keystr.size(); ++i) q.keydict[q.keystr[i]] = (uint32_t)i;
         q.key_hash = std::move(g.key_hash);
+        q.korder = std::move(g.korder);
         q.L = g.L;
         q.arena_keys = g.arena_keys;
         if (q.arena_keys > 0) {
@@ -3043,6 +3090,7 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             q->hq = std::move(h);
             if (e->force_generic) q->hq.plan.chain = 0;
             const Plan& P = q->hq.plan;
+            q->broadcast = std::find(q->hq.key_attr.begin(), q->hq.key_attr.end(), -3) != q->hq.key_attr.end();
             q->L = nfa::make_layout(P.n_states, std::max(P.n_cols, 1), e->max_partials, P.n_sched);
             q->sim.setup(P.n_sched, P.partitioned, !P.playback);
             e->any_sched |= P.n_sched > 0;
@@ -3071,7 +3119,7 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
         for (auto& q : e->qs) {
             const HostQuery& h = q->hq;
             const bool ranged = std::find(h.key_attr.begin(), h.key_attr.end(), -2) != h.key_attr.end();
-            const bool ok = h.streams.size() == 1 && !ranged &&
+            const bool ok = h.streams.size() == 1 && !ranged && !q->broadcast &&
                             (!h.plan.partitioned || q->string_keys || q->key_class != KC_NONE);
             if (!ok)
                 for (int s2 : h.streams) e->stage_ok[s2] = 0;

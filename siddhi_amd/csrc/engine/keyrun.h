@@ -18,6 +18,7 @@ struct KeyRun {
     std::vector<int64_t> ts;
     std::vector<uint8_t> qs;
     std::vector<uint32_t> pos;                       // batch position of each row
+    std::vector<uint32_t> vrank;                     // the rows' delivery ranks (range / broadcast rows), or empty
     std::vector<std::vector<uint8_t>> cols, nulls;   // per physical column: raw values / null flags
     bool has_qs = false;
     // outputs (same record layout as the device's)
@@ -57,7 +58,7 @@ struct KeyRun {
             nptr_[k] = nulls[k].empty() ? nullptr : nulls[k].data();
         }
         ev_ = nfa::KeyEvents{ts.data(), has_qs ? qs.data() : nullptr, pos.data(), cptr_, nptr_, 0, (int64_t)ts.size(),
-                             seq_base, 0};
+                             seq_base, 0, vrank.empty() ? nullptr : vrank.data()};
         need_init_ = nfa::key_begin(c_, ev_);
         p_ = 0;
     }

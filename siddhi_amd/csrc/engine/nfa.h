@@ -1341,8 +1341,11 @@ struct KeyEvents {
     const uint8_t* const* nulls;
     int64_t b, e, seq_base;
     int64_t pos_off;          // batch position of view row 0 (row p: pos_off + (orig ? orig[p] : p))
-    const uint8_t* vrank = nullptr;  // range partitions: the range a row came from -- one event sent to several keys
-                                     // is processed key after key in range order (PartitionStreamReceiver.receive)
+    const uint32_t* vrank = nullptr;  // range partitions: the range a row came from; a stream without a partition key:
+                                      // the key's rank in getPartitionKeys() order -- one event sent to several keys
+                                      // is processed key after key in that order (PartitionStreamReceiver.receive /
+                                      // send(ComplexEvent) :274-283); < 2^23
+
 };
 
 // one key's batch run, in steps (the device composes them in run_key; the host scheduler simulation steps a key

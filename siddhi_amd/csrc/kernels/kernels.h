@@ -230,7 +230,8 @@ struct NfaArgs {
     int64_t n;
     const int64_t* ts;                // sorted view
     const uint8_t* qstream;           // nullptr: single stream 0
-    const uint8_t* vrank;             // range partitions: the range of each view row (nullptr: none)
+    const uint32_t* vrank;            // range partitions: the range of each view row; broadcast rows: the key's
+                                      // rank in getPartitionKeys() order (nullptr: none)
     const uint32_t* seg_start;        // [K] (nullptr: unpartitioned, K == 1, one segment [0, n))
     const uint32_t* seg_end;
     int32_t K;

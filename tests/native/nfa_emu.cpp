@@ -441,7 +441,8 @@ void* emu_create(const char* text, int max_partials) {
             if (P.has_post)  // the selector's post pass runs on the device only (order.hip select_post)
                 throw std::runtime_error("selector post pass (aggregators / having) is device-only");
             for (int ka : q->hq.key_attr)
-                if (ka == -2) throw std::runtime_error("range partitions: the engine's batch assembly only");
+                if (ka == -2 || ka == -3)
+                    throw std::runtime_error("range partitions / broadcast streams: the engine's batch assembly only");
             if (P.purge) throw std::runtime_error("@purge: the engine's kernel arguments only");
             if (P.n_list_cols) throw std::runtime_error("multi-value selections: the engine's poll only");
             q->L = nfa::make_layout(P.n_states, std::max(P.n_cols, 1), e->ns, P.n_sched);

@@ -15,6 +15,11 @@ def part(q):
     return "@app:playback " + DEFS + "partition with (key of S, key of T) begin " + q + " end;"
 
 
+def part_s(q):
+    """a partition keyed on S only: T has no partition key, so each T event goes to every key (broadcast)"""
+    return "@app:playback " + DEFS + "partition with (key of S) begin " + q + " end;"
+
+
 def flat(q):
     return "@app:playback " + DEFS + q
 
@@ -256,3 +261,21 @@ SELECT_APPS["multi_value"] = part(
 SELECT_APPS["multi_value_seq"] = part(
     "@info(name='q') from every e1=S[price>20], e2=T[price>e1.price]+, e3=S[price<e2[last].price] "
     "select e1.id as a, e2.volume as vols, e3.id as c insert into O;")
+
+
+# ---- a stream without a partition key inside a partition (PartitionStreamReceiver.send(ComplexEvent) :274-283):
+# T events reach every key S initialised, in getPartitionKeys() order ----
+BCAST_APPS = {
+    "bc_pattern": part_s("@info(name='q') from every e1=S[price>20] -> e2=T[price>e1.price] within 50 milliseconds "
+                         "select e1.id as a, e2.id as b insert into O;"),
+    "bc_count": part_s("@info(name='q') from every e1=S[price>50 and volume>10] -> e2=T[price<40]<1:> -> "
+                       "e3=T[volume<=70] select e3.id as a, e2[0].id as b, e1.id as c insert into O;"),
+    "bc_sequence": part_s("@info(name='q') from every e1=S[price>20], e2=T[price>e1.price] "
+                          "select e1.id as a, e2.id as b insert into O;"),
+    "bc_absent": part_s("@info(name='q') from every e1=S[price>60] -> not T[price>e1.price] for 20 milliseconds "
+                        "select e1.id as a insert into O;"),
+    "bc_logical": part_s("@info(name='q') from every (e1=S[price>30] and e2=T[price>40]) -> e3=S[price>e1.price] "
+                         "select e1.id as a, e2.id as b, e3.id as c insert into O;"),
+    "bc_only_t": part_s("@info(name='q') from every e1=T[price>90] -> e2=S[price>e1.price] "
+                        "select e1.id as a, e2.id as b insert into O;"),
+}

@@ -1,0 +1,62 @@
+"""A stream without a partition key inside a partition, on the GPU: the engine expands each
+of its events into one view row per initialised key, ranked in getPartitionKeys() order (keyorder.h), and the
+generic keyed NFA runs them. Bit-exact against the oracle (whose key order tests/test_broadcast_order.py pins against
+a transliteration of the JDK 8 classes), over >= 1000 keys, in one and several flushes."""
+import pytest
+
+import synth
+from oracle_rt import Oracle
+from product_rt import ProductAdapter
+from test_broadcast_order import APP, keysets
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", sorted(synth.BCAST_APPS))
+@pytest.mark.parametrize("batches", [1, 3])
+def test_broadcast_apps_vs_oracle(name, batches, oracle_built):
+    app = synth.BCAST_APPS[name]
+    tr = synth.trace(6000, keys=1000, seed=41, two_streams=True)
+    o = Oracle(app)
+    try:
+        ref = synth.run(o, tr)
+    finally:
+        o.close()
+    p = ProductAdapter(app)
+    try:
+        assert p.rt.query_paths() == [1]
+        got = synth.run(p, tr, batches)
+    finally:
+        p.close()
+    assert len(ref) > 100, (name, len(ref))
+    assert got == ref, name
+
+
+def test_broadcast_key_order_through_resizes(oracle_built):
+    """the order test's trace (9 colliding keys first, then 4500 keys, re-puts, a broadcast at 11 key-set sizes)"""
+    import numpy as np
+    keys = keysets(0)
+    rng = np.random.default_rng(10)
+    rows, eid, ts, sent = [], 0, 1000, []
+    stops = {5, 9, 11, 12, 13, 40, 100, 700, 1500, 3000, len(keys)}
+    for i, k in enumerate(keys):
+        rows.append(("S", ts, [eid, k, -1.0])); eid += 1; sent.append(k)
+        if rng.random() < 0.3:
+            rows.append(("S", ts, [eid, sent[int(rng.integers(0, len(sent)))], -1.0])); eid += 1
+        if i + 1 in stops:
+            for k2 in sent:
+                rows.append(("S", ts, [eid, k2, 2.0])); eid += 1
+            rows.append(("T", ts, [eid, "ignored", 0.0])); eid += 1
+        ts += 1
+    o = Oracle(APP)
+    try:
+        ref = synth.run(o, rows)
+    finally:
+        o.close()
+    for batches in (1, 4):
+        p = ProductAdapter(APP)
+        try:
+            got = synth.run(p, rows, batches)
+        finally:
+            p.close()
+        assert len(ref) > 10_000 and got == ref, batches
