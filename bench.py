@@ -226,10 +226,11 @@ def cpu_baseline_sharded(cols, syms, sample, threads):
 
 
 def ordered_gather_leg(rt, step_push, n, dev, dist, rank, world):
-    """C5's ordered result gather: one batch's match records exported device-to-device (sdg_export_device), sorted
-    on each rank's GPU, sent to rank 0 over RCCL (send/recv) and merged there into the single delivery order of the
-    combined stream: (event time, rank, position of the emitting event in its rank's stream, ordinal). The
-    combined stream interleaves the ranks' events by time, ties by rank. Rank 0 checks the merged order."""
+    """The ordered result gather of one batch: each rank's match records exported device-to-device already in its
+    delivery order (sdg_export_ordered: the engine's device ordering pass), sent to rank 0 over RCCL (send/recv) and
+    merged there into the single delivery order of the combined stream: (event time, rank, position of the emitting
+    event in its rank's stream, ordinal) -- a rank's delivery order is already sorted by event time, so the merge is
+    one stable device sort of the concatenated runs by time. Rank 0 checks the merged order."""
     import torch
     from siddhi_amd import shard
     step_push()
@@ -239,19 +240,18 @@ def ordered_gather_leg(rt, step_push, n, dev, dist, rank, world):
     t_seq = torch.empty(cap, dtype=torch.int64, device=dev)
     t_sub = torch.empty(cap, dtype=torch.int64, device=dev)
     t_vals = torch.empty((2, cap), dtype=torch.int64, device=dev)
-    cnt = rt.export_device(0, cap, t_ts.data_ptr(), t_seq.data_ptr(), t_sub.data_ptr(), t_vals.data_ptr())
-    recs = {"ts": t_ts[:cnt], "seq": t_seq[:cnt], "sub": t_sub[:cnt],
-            "rank": torch.full((cnt,), rank, dtype=torch.int64, device=dev), "vals": t_vals[:, :cnt]}
     key = ["ts", "rank", "seq", "sub"]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    cnt = rt.export_ordered(0, cap, t_ts.data_ptr(), t_seq.data_ptr(), t_sub.data_ptr(), t_vals.data_ptr())
+    recs = {"ts": t_ts[:cnt], "seq": t_seq[:cnt], "sub": t_sub[:cnt],
+            "rank": torch.full((cnt,), rank, dtype=torch.int64, device=dev), "vals": t_vals[:, :cnt]}
     if dist is None:
-        order = shard.lexsort([recs[k] for k in key])
-        merged = {k: v[..., order] for k, v in recs.items()}
+        merged = recs
     else:
-        merged = shard.ordered_gather(dist, rank, world, recs, key)
+        merged = shard.ordered_gather(dist, rank, world, recs, key, presorted=True)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -274,7 +274,42 @@ def ordered_gather_leg(rt, step_push, n, dev, dist, rank, world):
         raise RuntimeError("ordered gather: merged records are not in delivery order")
     return {"records": total, "ms": dt * 1000.0, "bytes_to_rank0": int((total - cnt) * 8 * 6),
             "key": "(event ts, rank, event position in its rank's stream, ordinal)", "ordered": True,
-            "path": "sdg_export_device -> per-rank device sort -> RCCL send/recv to rank 0 -> merge"}
+            "path": "sdg_export_ordered (per-rank device ordering) -> RCCL send/recv to rank 0 -> stable device "
+                    "sort of the concatenated runs by time (shard.merge_runs)"}
+
+
+def c5_cpu_baseline(sh, nkeys=100_000):
+    """The oracle (one core, count-only) on a bounded sample of this rank's C5 shard: the events of `nkeys` of its keys
+    in the first global batch (keys are independent: the same per-key streams the GPU processes)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from oracle_rt import Oracle, lib
+    from siddhi_amd import workloads as w
+    skeys, smap = sh.sample(nkeys)
+    g0, g1 = sh.global_range(0)
+    ev = sh.sample_events(smap, len(skeys), g0, g1)
+    o = Oracle(w.C2_APP)
+    L = lib()
+    L.orc_count_only(o.h, 1)
+    oid = np.array([L.orc_intern(o.h, ("S%08d" % k).encode()) for k in skeys], dtype=np.int64)
+    n = len(ev["ts"])
+    slots = np.empty((n, 4), dtype=np.int64)
+    slots[:, 0] = ev["id"]
+    slots[:, 1] = oid[ev["sym"]]
+    slots[:, 2] = ev["price"].view(np.int64)
+    slots[:, 3] = ev["volume"]
+    strm = np.full(n, o.stream("StockStream"), dtype=np.int32)
+    ts = np.ascontiguousarray(ev["ts"])
+    offs = np.arange(n, dtype=np.int64) * 4
+    t = time.perf_counter()
+    rc = L.orc_send_batch(o.h, n, strm.ctypes.data, ts.ctypes.data, offs.ctypes.data, slots.ctypes.data, None)
+    dt = time.perf_counter() - t
+    m = L.orc_output_count(o.h)
+    o.close()
+    if rc != 0:
+        raise RuntimeError("oracle failed")
+    return {"value": n / dt, "unit": "events/s", "cores": 1, "kind": "port",
+            "sample": "%d events of %d of this rank's keys in global batch 0 (%.2f s, %d matches), oracle restatement"
+                      % (n, len(skeys), dt, m)}
 
 
 def run_c5(args, rank, world, local, dist):
@@ -311,15 +346,37 @@ def run_c5(args, rank, world, local, dist):
                                                                 cols["price"].data_ptr(), cols["volume"].data_ptr()])
         return n
 
-    def step(j):
+    # the ordered result gather is part of the C5 step: the flush's records leave the engine already in delivery
+    # order (sdg_export_ordered), go to rank 0 over RCCL (send/recv) and are merged there on e2id (the global position
+    # of the emitting event: unique across ranks; shard.merge_runs)
+    gcap = args.c5_batch // 2 + (1 << 20)
+    g_ts = torch.empty(gcap, dtype=torch.int64, device=dev)
+    g_seq, g_sub = torch.empty_like(g_ts), torch.empty_like(g_ts)
+    g_vals = torch.empty((2, gcap), dtype=torch.int64, device=dev)
+    last_merged = [None]
+
+    def gather():
+        cnt = rt.export_ordered(0, gcap, g_ts.data_ptr(), g_seq.data_ptr(), g_sub.data_ptr(), g_vals.data_ptr())
+        recs = {"e2": g_vals[1, :cnt], "e1": g_vals[0, :cnt], "ts": g_ts[:cnt]}
+        if dist is None:
+            merged = recs
+        else:
+            merged = shard.ordered_gather(dist, rank, world, recs, ["e2", "e1"], presorted=True, first_key_unique=True)
+        last_merged[0] = merged
+        return cnt
+
+    def step(j, with_gather=True):
         n = push(j)
         rt.flush(deliver=False)
-        rt.discard()
         st = rt.stats()
         if dist is not None:  # batch-boundary match-count all-gather (global output offsets)
             cnt = torch.tensor([st.matches], dtype=torch.int64, device=dev)
             allc = [torch.empty_like(cnt) for _ in range(world)]
             dist.all_gather(allc, cnt)
+        if with_gather and not args.no_gather:
+            gather()
+        else:
+            rt.discard()
         return n, st
 
     log("C5: warm-up (%d flushes)" % args.warmup)
@@ -328,12 +385,20 @@ def run_c5(args, rank, world, local, dist):
     keys_k = ["ms_kg_hist", "ms_kg_prefix", "ms_kg_scatter", "ms_chain_carry", "ms_chain_match", "ms_chain_emit"]
     acc = {k: 0.0 for k in keys_k}
     events = matches = carries = 0
+    t_flush = 0.0
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for j in range(args.warmup, nsteps):
-        n, st = step(j)
+        tf = time.perf_counter()
+        n, st = step(j, with_gather=False)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        t_flush += time.perf_counter() - tf  # (the flush phase; then the gather of the same batch)
+        if not args.no_gather:
+            gather()
         events += n
         matches += st.matches
         carries += st.carry_in
@@ -345,9 +410,9 @@ def run_c5(args, rank, world, local, dist):
     elapsed = time.perf_counter() - t0
     tot_events, tot_matches = events, matches
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, t_flush], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, t_flush = float(t[0].item()), float(t[1].item())
         v = torch.tensor([events, matches], dtype=torch.int64, device=dev)
         dist.all_reduce(v)
         tot_events, tot_matches = int(v[0].item()), int(v[1].item())
@@ -366,56 +431,43 @@ def run_c5(args, rank, world, local, dist):
         "dtype": "f64",
         "data": "synthetic (splitmix64 C5 generator on the GPU, siddhi_amd/c5.py), device-resident",
         "config": {"workload": "C5: C2 query, %d events / 10^8 keys key-hash sharded over %d GPU(s)%s, batches of "
-                               "%d rank events" % (args.c5_events, sworld, "" if sworld == world else
-                                                   " (shard %d of %d measured on this GPU)" % (srank, sworld),
-                                                   args.c5_batch),
+                               "%d rank events; a step = flush + ordered result gather to rank 0" % (
+                                   args.c5_events, sworld, "" if sworld == world else
+                                   " (shard %d of %d measured on this GPU)" % (srank, sworld), args.c5_batch),
                    "keys_this_rank": sh.n_keys, "events_per_rank_step": events / K, "matches_per_step": tot_matches / K,
                    "carried_partials_per_rank_step": carries / K,
                    "parallelism": "key-hash shards x%d" % sworld, "path": "radix key sort + chain kernels"},
+        "without_gather": {"value": tot_events / t_flush, "ms_per_step": t_flush * 1000.0 / K},
+        "gather": None if args.no_gather else {
+            "ms_per_step": (elapsed - t_flush) * 1000.0 / K, "inside_step": True,
+            "records_per_rank_step": matches / K,
+            "key": "(e2id = global position of the emitting event, e1id)",
+            "path": "sdg_export_ordered (device ordering) -> RCCL send/recv to rank 0 -> stable device sort of the "
+                    "concatenated runs on e2id (shard.merge_runs)"},
         "roofline": {"bound": "hbm", "kernel": names.get(dom, dom), "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "algorithmic_bytes_per_launch": step_bytes,
-                     "step_frac": step_bytes / (elapsed / K) / 1e9 / HBM_PEAK_GBS, "kernel_ms": per_kernel},
+                     "step_frac": step_bytes / (t_flush / K) / 1e9 / HBM_PEAK_GBS, "kernel_ms": per_kernel},
         "cpu_baseline": None,
     }
-    del batches
+    tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(tpath):  # PMC HBM bytes per launch of the dominant kernel at this batch size, if measured
+        ent = json.load(open(tpath)).get("c5", {}).get(names.get(dom, dom).split(" ")[0])
+        if ent and ent.get("events_per_launch") == args.c5_batch:
+            out["roofline"]["traffic"] = ent["fetch_bytes"] + ent["write_bytes"]
+    if rank == 0 and last_merged[0] is not None:  # the last step's merged records are in delivery order
+        e2, e1 = last_merged[0]["e2"], last_merged[0]["e1"]
+        ok = bool(((e2[1:] > e2[:-1]) | ((e2[1:] == e2[:-1]) & (e1[1:] > e1[:-1]))).all().item()) \
+            if e2.numel() > 1 else True
+        if not ok:
+            raise RuntimeError("C5 ordered gather: merged records are not in delivery order")
+        out["gather"]["ordered"] = True
+        out["gather"]["records_merged_last_step"] = int(e2.numel())
+    last_merged[0] = None
+    del batches, g_ts, g_seq, g_sub, g_vals
     torch.cuda.empty_cache()
-    if not args.no_gather and nsteps < nb:
-        log("C5: ordered result gather of batch %d (outside the timed region)" % nsteps)
-        cols, n = sh.generate(nsteps)
-        rt.push_device("StockStream", n, cols["ts"].data_ptr(), [cols["id"].data_ptr(), cols["sym"].data_ptr(),
-                                                                cols["price"].data_ptr(), cols["volume"].data_ptr()])
-        rt.flush(deliver=False)
-        del cols
-        m = int(rt.stats().matches)
-        t_ts = torch.empty(max(m, 1), dtype=torch.int64, device=dev)
-        t_seq, t_sub = torch.empty_like(t_ts), torch.empty_like(t_ts)
-        t_vals = torch.empty((2, max(m, 1)), dtype=torch.int64, device=dev)
-        rt.export_device(0, max(m, 1), t_ts.data_ptr(), t_seq.data_ptr(), t_sub.data_ptr(), t_vals.data_ptr())
-        recs = {"e2": t_vals[1, :m].contiguous(), "e1": t_vals[0, :m].contiguous(), "ts": t_ts[:m]}
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        tg = time.perf_counter()
-        if dist is None:
-            order = shard.lexsort([recs["e2"], recs["e1"]])
-            merged = {k: v[order] for k, v in recs.items()}
-        else:
-            merged = shard.ordered_gather(dist, rank, world, recs, ["e2", "e1"])
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - tg
-        if rank == 0:
-            e2, e1 = merged["e2"], merged["e1"]
-            ok = bool(((e2[1:] > e2[:-1]) | ((e2[1:] == e2[:-1]) & (e1[1:] > e1[:-1]))).all().item()) \
-                if e2.numel() > 1 else True
-            if not ok:
-                raise RuntimeError("C5 ordered gather: merged records are not in delivery order")
-            out["ordered_gather"] = {"records": int(e2.numel()), "ms": dt * 1000.0, "ordered": True,
-                                     "key": "(e2id = global position of the emitting event, e1id)",
-                                     "path": "sdg_export_device -> per-rank device sort -> RCCL send/recv to rank 0 "
-                                             "-> G-way merge (shard.merge_runs)"}
-        del t_ts, t_seq, t_sub, t_vals, recs, merged
-        torch.cuda.empty_cache()
+    if rank == 0 and not args.no_cpu:
+        out["cpu_baseline"] = c5_cpu_baseline(sh, args.c5_sample)
     if not args.no_parity:
         log("C5: oracle sample of this rank's shard (%d keys)" % args.c5_sample)
         sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -522,6 +574,22 @@ def main():
     ap.add_argument("--c5-shard", default=None,
                     help="C5 on one process: run shard R/W (rank R of a W-GPU run) instead of this process's rank")
     args = ap.parse_args()
+
+    # --gpus N is honoured: without a launcher (no WORLD_SIZE in the environment) this process starts the N ranks
+    # itself -- torch.distributed.run as a CHILD process, before anything here touches the GPU -- and exits with its
+    # status; under a launcher the world size must agree with --gpus
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        import socket
+        import subprocess
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        log("starting %d ranks: %s" % (args.gpus, " ".join(cmd)))
+        raise SystemExit(subprocess.call(cmd))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%s" % (args.gpus, os.environ.get("WORLD_SIZE")))
 
     import torch
     rank = int(os.environ.get("RANK", "0"))
@@ -652,15 +720,16 @@ def main():
                      "step_frac": step_bytes / (ms_per_step / 1000.0) / 1e9 / HBM_PEAK_GBS,
                      "kernel_ms": per_kernel},
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
-        log("cpu baseline (oracle, 1 thread, %d events)" % min(args.cpu_sample, n))
-        rate, cm, dt = cpu_baseline(cols, syms, min(args.cpu_sample, n))
+    if rank == 0 and not args.no_cpu:  # (at N > 1: rank 0's shard, a third of the sample, after the timed region)
+        cs = min(args.cpu_sample if world == 1 else args.cpu_sample // 3, n)
+        log("cpu baseline (oracle, 1 thread, %d events)" % cs)
+        rate, cm, dt = cpu_baseline(cols, syms, cs)
         out["cpu_baseline"] = {"value": rate, "unit": "events/s", "cores": 1, "kind": "port",
-                               "sample": "first %d events of the C2 stream (%.1f s, %d matches), oracle restatement"
-                                         % (min(args.cpu_sample, n), dt, cm)}
+                               "sample": "first %d events of %s C2 stream (%.1f s, %d matches), oracle restatement"
+                                         % (cs, "the" if world == 1 else "rank 0's", dt, cm)}
         thr = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
         log("cpu baseline, key-sharded over %d threads" % thr)
-        srate, scm, sdt = cpu_baseline_sharded(cols, syms, min(args.cpu_sample, n), thr)
+        srate, scm, sdt = cpu_baseline_sharded(cols, syms, cs, thr)
         if scm != cm:
             raise RuntimeError("key-sharded CPU baseline disagrees with the single-thread run: %d vs %d" % (scm, cm))
         out["cpu_baseline_sharded"] = {"value": srate, "unit": "events/s", "cores": thr, "kind": "port",

@@ -102,7 +102,13 @@ int sdg_query_path(sdg_engine* e, int query);
 #define SDG_Q_PARTITIONED 1    /* partition with (...): keys are independent, the query shards by key hash */
 #define SDG_Q_TIMERS 2         /* absent states: the reference's Scheduler collapses due timers across ALL keys
                                   (Scheduler.java:75-98), so key shards on different GPUs would change the result */
+#define SDG_Q_BROADCAST 4      /* a stream of the query has no partition key: its events go to every key of the partition
+                                  in one global key order (PartitionStreamReceiver.java:274-283), across shards */
 int sdg_query_flags(sdg_engine* e, int query);
+/* how a partitioned query keys a stream (PartitionStreamReceiver / ValuePartitionExecutor): the attribute index of a
+ * value partition, -2 range partitions, -3 no key (broadcast), -1 the query does not read the stream or is not
+ * partitioned. A multi-GPU router shards the stream's events by the hash of that attribute's toString. */
+int sdg_query_key_attr(sdg_engine* e, int query, int stream);
 const char* sdg_query_name(sdg_engine* e, int query);
 const char* sdg_query_target(sdg_engine* e, int query);
 int sdg_query_output_schema(sdg_engine* e, int query, int32_t* n_attrs, const int32_t** types,
@@ -158,6 +164,10 @@ int sdg_discard(sdg_engine* e);
  * states (their timer matches are ordered on the host). */
 int sdg_export_device(sdg_engine* e, int query, int64_t cap, int64_t* n_out, int64_t* d_ts, int64_t* d_seq,
                       int64_t* d_sub, int64_t* d_vals);
+/* sdg_export_device with the records already in delivery order ((event_seq, sub) ascending, put in order on the
+ * device by the same pass sdg_poll uses): each rank's export is a sorted run, so a multi-GPU gather only merges */
+int sdg_export_ordered(sdg_engine* e, int query, int64_t cap, int64_t* n_out, int64_t* d_ts, int64_t* d_seq,
+                       int64_t* d_sub, int64_t* d_vals);
 
 /* SiddhiAppRuntime.snapshot() / restore(byte[]) (core/SiddhiAppRuntimeImpl.java:677-737): every partial match,
  * carried partial, timer queue, aggregator and key dictionary of the engine, after flushing what was pushed. The

@@ -145,6 +145,8 @@ def load_library():
     L.sdg_snapshot.argtypes = [P, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(I64)]
     L.sdg_restore.argtypes = [P, ctypes.c_char_p, I64]
     L.sdg_export_device.argtypes = [P, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), P, P, P, P]
+    L.sdg_export_ordered.argtypes = [P, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), P, P, P, P]
+    L.sdg_query_key_attr.argtypes = [P, I32, I32]
     L.sdg_last_stats.argtypes = [P, ctypes.POINTER(Stats)]
     _lib = L
     return L
@@ -227,6 +229,7 @@ class SiddhiAppRuntime:
         _check(L.sdg_compile(app_text.encode(), ctypes.byref(opts), ctypes.byref(h)))
         self._h = h
         self._compile_only = compile_only
+        self._app_text = app_text
         self.playback = "@app:playback" in app_text.replace(" ", "").lower()
         import re as _re
         m = _re.search(r"@app:name\(\s*['\"]([^'\"]*)['\"]", app_text)
@@ -285,8 +288,19 @@ class SiddhiAppRuntime:
 
     # --- engine ----------------------------------------------------------------------------------------
     def query_flags(self):
-        """per query: SDG_Q_PARTITIONED (1) | SDG_Q_TIMERS (2)"""
+        """per query: SDG_Q_PARTITIONED (1) | SDG_Q_TIMERS (2) | SDG_Q_BROADCAST (4)"""
         return [self._L.sdg_query_flags(self._h, q) for q in range(len(self._queries))]
+
+    def app_stream_ids(self):
+        """the app's defined stream ids, in definition order"""
+        import re as _re
+        return [s for s in _re.findall(r"define\s+stream\s+([A-Za-z_]\w*)", self._app_text, flags=_re.I)
+                if self._L.sdg_stream_index(self._h, s.encode()) >= 0]
+
+    def query_key_attr(self, q, stream_id):
+        """how query q keys stream_id: attribute index of its value partition, -2 ranges, -3 no key (broadcast), -1
+        not read / not partitioned (sdg_query_key_attr)"""
+        return self._L.sdg_query_key_attr(self._h, q, self._L.sdg_stream_index(self._h, stream_id.encode()))
 
     def query_paths(self):
         """device path per query: 0 chain kernel, 1 generic keyed NFA, 2 register sequence kernel (seq3)"""
@@ -459,6 +473,13 @@ class SiddhiAppRuntime:
         d_vals: [n_out][cap]); unordered -- delivery order is (seq, sub). Returns the record count."""
         n = ctypes.c_int64()
         _check(self._L.sdg_export_device(self._h, q, cap, ctypes.byref(n), d_ts, d_seq, d_sub, d_vals))
+        return n.value
+
+    def export_ordered(self, q, cap, d_ts, d_seq, d_sub, d_vals):
+        """export_device with the records already in delivery order ((seq, sub) ascending, ordered on the device):
+        a rank's sorted run for the multi-GPU merge. Returns the record count."""
+        n = ctypes.c_int64()
+        _check(self._L.sdg_export_ordered(self._h, q, cap, ctypes.byref(n), d_ts, d_seq, d_sub, d_vals))
         return n.value
 
     def stats(self):

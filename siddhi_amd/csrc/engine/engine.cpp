@@ -232,6 +232,8 @@ struct QueryRt {
     // initialised, in getPartitionKeys() order (keyorder.h); host batch assembly only
     bool broadcast = false;
     PartitionKeyOrder korder;
+    bool ranked = false;  // range partitions or broadcast rows: delivery ranks in bits 40..62 of `sub`
+    int sub_bits() const { return ranked ? 64 : 48; }
     // absent states: the scheduler simulation, per-key HashMap hashes, double-buffered arenas, the run's log
     SchedSim sim;
     std::vector<int32_t> key_hash;
@@ -2316,7 +2318,7 @@ void drain(sdg_engine* e, QueryRt& q) {
         void* work = q.ord_ws.ensure(wb);
         uint32_t* perm = nullptr;
         order_records((const int64_t*)q.o_emit.p, (const int64_t*)q.o_first.p, n, q.emit_base,
-                      q.sub_is_seq ? q.emit_base - (1ll << 40) : 0, work, wb, &perm, st);
+                      q.sub_is_seq ? q.emit_base - (1ll << 40) : 0, q.sub_bits(), work, wb, &perm, st);
         int64_t* gts = (int64_t*)q.g_ts.ensure((size_t)n * 8);
         int64_t* gem = (int64_t*)q.g_emit.ensure((size_t)n * 8);
         int64_t* gv = (int64_t*)q.g_vals.ensure((size_t)std::max(na, 1) * n * 8);
@@ -3091,6 +3093,7 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             if (e->force_generic) q->hq.plan.chain = 0;
             const Plan& P = q->hq.plan;
             q->broadcast = std::find(q->hq.key_attr.begin(), q->hq.key_attr.end(), -3) != q->hq.key_attr.end();
+            q->ranked = q->broadcast || std::find(q->hq.key_attr.begin(), q->hq.key_attr.end(), -2) != q->hq.key_attr.end();
             q->L = nfa::make_layout(P.n_states, std::max(P.n_cols, 1), e->max_partials, P.n_sched);
             q->sim.setup(P.n_sched, P.partitioned, !P.playback);
             e->any_sched |= P.n_sched > 0;
@@ -3190,7 +3193,15 @@ int sdg_num_queries(sdg_engine* e) { return e ? (int)e->qs.size() : 0; }
 int sdg_query_flags(sdg_engine* e, int q) {
     if (!e || q < 0 || q >= (int)e->qs.size()) return -1;
     const Plan& P = e->qs[q]->hq.plan;
-    return (P.partitioned ? SDG_Q_PARTITIONED : 0) | (P.n_sched > 0 ? SDG_Q_TIMERS : 0);
+    return (P.partitioned ? SDG_Q_PARTITIONED : 0) | (P.n_sched > 0 ? SDG_Q_TIMERS : 0) |
+           (e->qs[q]->broadcast ? SDG_Q_BROADCAST : 0);
+}
+int sdg_query_key_attr(sdg_engine* e, int q, int stream) {
+    if (!e || q < 0 || q >= (int)e->qs.size()) return -1;
+    const HostQuery& h = e->qs[q]->hq;
+    const int qp = h.stream_pos(stream);
+    if (qp < 0 || !h.plan.partitioned) return -1;
+    return h.key_attr[qp];
 }
 int sdg_query_path(sdg_engine* e, int q) {
     if (!e || q < 0 || q >= (int)e->qs.size()) return -1;
@@ -3570,8 +3581,9 @@ int sdg_poll_list(sdg_engine* e, int qi, int attr, int32_t* cap, int32_t* elem_t
     return SDG_OK;
 }
 
-int sdg_export_device(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_t* d_ts, int64_t* d_seq,
-                      int64_t* d_sub, int64_t* d_vals) {
+namespace {
+int export_records(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_t* d_ts, int64_t* d_seq, int64_t* d_sub,
+                   int64_t* d_vals, bool ordered) {
     if (!e || qi < 0 || qi >= (int)e->qs.size() || !n_out) return fail(SDG_ERR_ARG, "bad export arguments");
     return guarded([&]() {
         QueryRt& q = *e->qs[qi];
@@ -3585,7 +3597,19 @@ int sdg_export_device(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_
                                                               std::to_string(n) + " records");
         hipStream_t st = e->stream;
         const int na = q.hq.plan.n_user_out;
-        if (n > 0) {
+        if (n > 0 && ordered) {  // the delivery-order pass of drain(), gathering straight into the caller's buffers
+            const size_t wb = order_workspace(n);
+            void* work = q.ord_ws.ensure(wb);
+            uint32_t* perm = nullptr;
+            order_records((const int64_t*)q.o_emit.p, (const int64_t*)q.o_first.p, n, q.emit_base,
+                          q.sub_is_seq ? q.emit_base - (1ll << 40) : 0, q.sub_bits(), work, wb, &perm, st);
+            gather_i64((const int64_t*)q.o_ts.p, perm, n, d_ts, st);
+            gather_i64((const int64_t*)q.o_emit.p, perm, n, d_seq, st);
+            gather_i64((const int64_t*)q.o_first.p, perm, n, d_sub, st);
+            for (int j = 0; j < na; ++j)
+                gather_i64((const int64_t*)q.o_vals.p + (size_t)j * q.out_cap, perm, n, d_vals + (size_t)j * cap, st);
+            HIPCHECK(hipStreamSynchronize(st));
+        } else if (n > 0) {
             HIPCHECK(hipMemcpyAsync(d_ts, q.o_ts.p, n * 8, hipMemcpyDeviceToDevice, st));
             HIPCHECK(hipMemcpyAsync(d_seq, q.o_emit.p, n * 8, hipMemcpyDeviceToDevice, st));
             HIPCHECK(hipMemcpyAsync(d_sub, q.o_first.p, n * 8, hipMemcpyDeviceToDevice, st));
@@ -3597,6 +3621,16 @@ int sdg_export_device(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_
         q.polled = true;
         return SDG_OK;
     });
+}
+}  // namespace
+
+int sdg_export_device(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_t* d_ts, int64_t* d_seq,
+                      int64_t* d_sub, int64_t* d_vals) {
+    return export_records(e, qi, cap, n_out, d_ts, d_seq, d_sub, d_vals, false);
+}
+int sdg_export_ordered(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_t* d_ts, int64_t* d_seq,
+                       int64_t* d_sub, int64_t* d_vals) {
+    return export_records(e, qi, cap, n_out, d_ts, d_seq, d_sub, d_vals, true);
 }
 
 int sdg_last_stats(sdg_engine* e, sdg_stats* out) {

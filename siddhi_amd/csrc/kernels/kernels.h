@@ -383,10 +383,11 @@ void nfa_slots_assign(const SlotPool& sp, const uint32_t* seg_start, const uint3
 void nfa_commit_slots(const SlotPool& sp, uint8_t* cur, uint8_t* ran, int64_t slots, hipStream_t st);
 
 // delivery order of n match records (order.hip): perm = the record indices sorted by (emit - emit_base as u32,
-// sub - sub_bias as a 48-bit key); work = order_workspace(n) bytes
+// sub - sub_bias as a sub_bits-bit key: 48, or 64 when a delivery rank sits in bits 40..62 -- range partitions and
+// broadcast rows); work = order_workspace(n) bytes
 size_t order_workspace(int64_t n);
-void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t emit_base, int64_t sub_bias, void* work,
-                   size_t work_bytes, uint32_t** perm_out, hipStream_t stream);
+void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t emit_base, int64_t sub_bias, int sub_bits,
+                   void* work, size_t work_bytes, uint32_t** perm_out, hipStream_t stream);
 void gather_i64(const int64_t* src, const uint32_t* perm, int64_t n, int64_t* dst, hipStream_t stream);
 void gather_u32(const uint32_t* src, const uint32_t* perm, int64_t n, uint32_t* dst, hipStream_t stream);
 void gather_u8(const uint8_t* src, const uint32_t* perm, int64_t n, uint8_t* dst, hipStream_t stream);

@@ -37,7 +37,7 @@ void temp_sizes(int64_t n, size_t& a, size_t& b) {
     uint32_t* k32 = nullptr;
     uint32_t* v = nullptr;
     a = b = 0;
-    rocprim::radix_sort_pairs(nullptr, a, k64, k64, v, v, (size_t)n, 0, 48);
+    rocprim::radix_sort_pairs(nullptr, a, k64, k64, v, v, (size_t)n, 0, 64);
     rocprim::radix_sort_pairs(nullptr, b, k32, k32, v, v, (size_t)n, 0, 32);
 }
 
@@ -51,8 +51,8 @@ size_t order_workspace(int64_t n) {
     return sort_tmp + (size_t)n * (16 + 8 + 8) + 1024;
 }
 
-void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t emit_base, int64_t sub_bias, void* work,
-                   size_t work_bytes, uint32_t** perm_out, hipStream_t stream) {
+void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t emit_base, int64_t sub_bias, int sub_bits,
+                   void* work, size_t work_bytes, uint32_t** perm_out, hipStream_t stream) {
     if (n <= 0) return;
     size_t a = 0, b = 0;
     temp_sizes(n, a, b);
@@ -70,7 +70,7 @@ void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t e
     const unsigned grid = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(order_keys_k, dim3(grid), dim3(256), 0, stream, emit, sub, n, emit_base, sub_bias, ek0, sk0, ix0);
     // by the ordinal, then (stable) by the emitting event
-    rocprim::radix_sort_pairs(tmp, a, sk0, sk1, ix0, ix1, (size_t)n, 0, 48, stream);
+    rocprim::radix_sort_pairs(tmp, a, sk0, sk1, ix0, ix1, (size_t)n, 0, sub_bits, stream);
     hipLaunchKernelGGL(gather_k<uint32_t>, dim3(grid), dim3(256), 0, stream, ek0, ix1, n, ek1);
     rocprim::radix_sort_pairs(tmp, b, ek1, ek0, ix1, ix0, (size_t)n, 0, 32, stream);
     *perm_out = ix0;

@@ -25,16 +25,30 @@ def owner(key, world):
     return key_hash(key) % world
 
 
-def route(keys, world):
-    """rank of each event, for an array/list of partition key values"""
-    cache = {}
-    out = np.empty(len(keys), dtype=np.int32)
-    for i, k in enumerate(keys):
+def route(keys, world, cache=None):
+    """rank of each event, for an array/list of partition key values (PartitionStreamReceiver.receive(Event[])
+    :176-216 routes a batch key by key; here the batch is split by owner at once): each distinct key's toString is
+    hashed once (np.unique + a per-router cache), then the ranks are gathered back to the rows"""
+    if world == 1:
+        return np.zeros(len(keys), dtype=np.int32)
+    cache = {} if cache is None else cache
+    arr = np.asarray(keys)
+    if arr.dtype == object or arr.ndim != 1:
+        out = np.empty(len(keys), dtype=np.int32)
+        for i, k in enumerate(keys):
+            r = cache.get(k)
+            if r is None:
+                r = cache[k] = owner(k, world)
+            out[i] = r
+        return out
+    uniq, inv = np.unique(arr, return_inverse=True)
+    ranks = np.empty(len(uniq), dtype=np.int32)
+    for j, k in enumerate(uniq.tolist()):
         r = cache.get(k)
         if r is None:
             r = cache[k] = owner(k, world)
-        out[i] = r
-    return out
+        ranks[j] = r
+    return ranks[inv]
 
 
 def merge(parts):
@@ -52,16 +66,25 @@ def lexsort(keys):
 
 
 def merge_runs(runs, key):
-    """G-way merge of sorted runs (dicts of torch tensors, records along the last dim) by their 1-D `key` column:
-    record i of run r lands at  i + sum_{r' < r} #{x in run r' : x <= v} + sum_{r' > r} #{x in run r' : x < v}
-    (binary searches into the other runs), so equal keys keep run order, then their order inside the run. Linear
-    in the records (times log of a run), no re-sort of the concatenation."""
+    """G-way merge of sorted runs (dicts of torch tensors, records along the last dim) by their 1-D `key` column;
+    equal keys keep run order, then their order inside the run. Large merges: the runs concatenated in run order and
+    ONE stable device radix sort of the key relative to its minimum (32-bit when the span fits: 4 digit passes), so
+    ties keep exactly that order; small ones: each record's slot from binary searches into the other runs."""
     import torch
     runs = [r for r in runs if r[key].numel() > 0]
     if not runs:
         return None
     if len(runs) == 1:
         return runs[0]
+    total = sum(int(r[key].numel()) for r in runs)
+    if total >= (1 << 20):
+        cat = {k: torch.cat([r[k] for r in runs], dim=-1) for k in runs[0]}
+        kv = cat[key]
+        lo = kv.min()
+        span = int((kv.max() - lo).item())
+        rel = (kv - lo).to(torch.int32) if span < (1 << 31) else kv - lo
+        perm = torch.sort(rel, stable=True).indices
+        return {k: v[..., perm] for k, v in cat.items()}
     dev = runs[0][key].device
     total = sum(int(r[key].numel()) for r in runs)
     out = {k: torch.empty(list(v.shape[:-1]) + [total], dtype=v.dtype, device=dev) for k, v in runs[0].items()}
@@ -76,19 +99,28 @@ def merge_runs(runs, key):
     return out
 
 
-def ordered_gather(dist, rank, world, cols, key_names):
+def ordered_gather(dist, rank, world, cols, key_names, presorted=False, first_key_unique=False):
     """Ordered result gather: `cols` maps names to this rank's record tensors (1-D [n], or 2-D
     [m, n] with records along the last dim) on the communication device. Every rank sorts its records by
     `key_names` on its device, the run lengths are all-gathered, and each rank's sorted run goes to rank 0
     point-to-point (send/recv: RCCL over xGMI with the nccl backend, gloo on CPU), where the G runs are merged on the
     first key (merge_runs: records of different ranks with equal first keys keep rank order, which is the
     tie-break every caller's key implies -- either the first key is unique across ranks, e.g. the global position of
-    the emitting event, or the rank is the next key). Returns the merged dict on rank 0, None elsewhere."""
+    the emitting event, or the rank is the next key). presorted: the records already are in `key_names` order (an
+    sdg_export_ordered run), no local sort. Returns the merged dict on rank 0, None elsewhere."""
     import torch
+    # the merge orders by key_names[0], then rank, then each run's own order: that equals key_names order only if
+    # the first key is unique across ranks or the rank is the next key
+    if not (len(key_names) == 1 or key_names[1] == "rank" or first_key_unique):
+        raise ValueError("ordered_gather merges on %r then rank: pass first_key_unique=True or put 'rank' second"
+                         % key_names[0])
     names = sorted(cols)
     ref = cols[key_names[0]]
-    order = lexsort([cols[k] for k in key_names])
-    mine = {k: cols[k][..., order].contiguous() for k in names}
+    if presorted:
+        mine = {k: cols[k].contiguous() for k in names}
+    else:
+        order = lexsort([cols[k] for k in key_names])
+        mine = {k: cols[k][..., order].contiguous() for k in names}
     n = torch.tensor([ref.numel()], dtype=torch.int64, device=ref.device)
     counts = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(counts, n)
@@ -114,32 +146,59 @@ def ordered_gather(dist, rank, world, cols, key_names):
     return merged
 
 
-Q_PARTITIONED, Q_TIMERS = 1, 2
+Q_PARTITIONED, Q_TIMERS, Q_BROADCAST = 1, 2, 4
 
 
 class ShardedAppRuntime:
     """One rank's share of a Siddhi app on an N-GPU node: partitioned queries are key-hash sharded
     (rank r processes the events whose partition key hashes to r, `owner`), unpartitioned queries run as replicas
-    on rank 0. N > 1 is refused with OperationNotSupportedException for queries with absent states: the reference's
-    Scheduler collapses the due timers of ALL partition keys into one TreeMultimap per clock advance
-    (Scheduler.java:75-98, only the first state per due time fires), so which fires it delays depends on keys that
-    would live on other GPUs -- sharding them would silently change the matches (7,857 vs 9,790).
-    Such an app runs on one GPU (world 1), where the engine reproduces the collapse exactly."""
+    on rank 0. Each stream is routed by the partition attribute the ENGINE compiled for it (sdg_query_key_attr), so
+    the router and the queries cannot disagree; a stream keyed by different attributes in different partitions
+    cannot be routed by one key and is refused. Also refused at N > 1, with OperationNotSupportedException:
+      * absent states: the reference's Scheduler collapses the due timers of ALL partition keys into one
+        TreeMultimap per clock advance (Scheduler.java:75-98, only the first state per due time fires), so which
+        fires it delays depends on keys that would live on other GPUs (BASELINE.md C4: 7,857 vs 9,790);
+      * a stream without a partition key (PartitionStreamReceiver.send(ComplexEvent) :274-283): its events go to
+        every key of the partition in ONE global key order that interleaves the ranks' keys;
+      * range partitions: an event may belong to several ranges (keys), so it has no single owner.
+    Such apps run on one GPU (world 1), where the engine reproduces the reference exactly."""
 
     def __init__(self, app_text, rank, world, device=0, key_attr=None, **kw):
         import siddhi_amd as sa
         self.rank, self.world = rank, world
         self.rt = sa.SiddhiAppRuntime(app_text, device=device, **kw)
         flags = self.rt.query_flags()
-        if world > 1 and any(f & Q_TIMERS for f in flags):
-            names = [q[0] for q, f in zip(self.rt._queries, flags) if f & Q_TIMERS]
+        names = [q[0] for q in self.rt._queries]
+
+        def refuse(msg):
             self.rt.shutdown()
-            raise sa.OperationNotSupportedException(
-                "queries %s have absent states: the reference's scheduler orders timers across all partition keys "
-                "(Scheduler.java:75-98), so they cannot be key-sharded over %d GPUs; run the app on one GPU" % (names, world))
+            raise sa.OperationNotSupportedException(msg)
+        if world > 1:
+            timers = [n for n, f in zip(names, flags) if f & Q_TIMERS]
+            if timers:
+                refuse("queries %s have absent states: the reference's scheduler orders timers across all partition "
+                       "keys (Scheduler.java:75-98), so they cannot be key-sharded over %d GPUs; run the app on one GPU"
+                       % (timers, world))
+            bcast = [n for n, f in zip(names, flags) if f & Q_BROADCAST]
+            if bcast:
+                refuse("queries %s read a stream without a partition key: its events reach every key in one global "
+                       "key order (PartitionStreamReceiver.java:274-283); run the app on one GPU" % bcast)
         self.sharded = all(f & Q_PARTITIONED for f in flags)
         self.replica = not self.sharded  # an unpartitioned query: every event, on rank 0 only
-        self.key_attr = key_attr or {}    # stream id -> index of its partition attribute
+        # stream id -> the partition attribute every partitioned query reading it keys it by
+        self.key_attr = {}
+        for s in self.rt.app_stream_ids():
+            attrs = {self.rt.query_key_attr(q, s) for q in range(len(names))} - {-1}
+            if not attrs:
+                continue
+            if world > 1 and (len(attrs) > 1 or min(attrs) < 0):
+                refuse("stream '%s' is keyed by %s in different partitions (or by ranges): its events have no single "
+                       "owner GPU" % (s, sorted(attrs)))
+            self.key_attr[s] = attrs.pop()
+        for s, a in (key_attr or {}).items():  # a caller's statement of the keys must agree with the engine's
+            if self.key_attr.get(s, a) != a:
+                refuse("key_attr[%r] = %d, but the app partitions it by attribute %d" % (s, a, self.key_attr[s]))
+        self._cache = {}
 
     def mine(self, stream_id, row):
         """whether this rank processes the event"""
@@ -147,11 +206,34 @@ class ShardedAppRuntime:
             return True
         if self.replica:
             return self.rank == 0
-        return owner(row[self.key_attr[stream_id]], self.world) == self.rank
+        ai = self.key_attr.get(stream_id)
+        if ai is None:  # no partitioned query reads the stream
+            return self.rank == 0
+        return owner(row[ai], self.world) == self.rank
 
     def send(self, stream_id, ts, row):
         if self.mine(stream_id, row):
             self.rt.getInputHandler(stream_id).send(ts, row)
+
+    def send_columns(self, stream_id, ts, columns, key_values=None):
+        """a columnar batch (InputHandler.send per row, in order): this rank's rows, routed at once. key_values:
+        the key attribute's values as the app sees them (e.g. strings when `columns` hold sdg_intern ids); default
+        the key column itself"""
+        ts = np.asarray(ts)
+        if self.world == 1:
+            mask = slice(None)
+        elif self.replica or stream_id not in self.key_attr:
+            if self.rank != 0:
+                return 0
+            mask = slice(None)
+        else:
+            kv = columns[self.key_attr[stream_id]] if key_values is None else key_values
+            mask = route(kv, self.world, self._cache) == self.rank
+        cols = [np.ascontiguousarray(np.asarray(c)[mask]) for c in columns]
+        sel = np.ascontiguousarray(ts[mask])
+        if len(sel):
+            self.rt.getInputHandler(stream_id).send_columns(sel, cols)
+        return len(sel)
 
     def shutdown(self):
         self.rt.shutdown()

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../siddhi_amd/csrc/engine/compile.h"
+#include "../../siddhi_amd/csrc/engine/keyorder.h"
 #include "../../siddhi_amd/csrc/engine/nfa.h"
 #include "../../siddhi_amd/csrc/engine/keyrun.h"
 #include "../../siddhi_amd/csrc/engine/sched.h"
@@ -27,6 +28,9 @@ using namespace sdg;
 namespace {
 
 std::string g_err;
+}  // namespace
+void sdg::PartitionKeyOrder::throw_corrupt() { throw std::runtime_error("corrupt key order"); }
+namespace {
 
 int width_of(uint8_t kind) {
     switch (kind) {
@@ -57,6 +61,8 @@ struct EmuQuery {
     std::vector<std::vector<uint8_t>> arenas;
     SchedSim sim;
     std::vector<Out> outs;
+    bool bcast = false;              // a stream without a partition key: rows to every key, in korder order
+    PartitionKeyOrder korder;
 };
 
 struct Emu {
@@ -117,13 +123,23 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
     const int nc = P.n_cols;
     std::vector<const Ev*> rows;
     std::vector<int> rkey;
-    std::vector<uint32_t> rpos;
+    std::vector<uint32_t> rpos, rrank;
     for (int64_t g = 0; g < bc.G; ++g) {
         const Ev& ev = e->pending[g];
         if (ev.stream < 0) continue;
         int qpos = h.stream_pos(ev.stream);
         if (qpos < 0) continue;
         int key = 0;
+        if (P.partitioned && h.key_attr[qpos] == -3) {  // every initialised key, in getPartitionKeys() order
+            const std::vector<uint32_t>& o = q.korder.order();
+            for (size_t x = 0; x < o.size(); ++x) {
+                rows.push_back(&ev);
+                rkey.push_back((int)o[x]);
+                rpos.push_back((uint32_t)g);
+                rrank.push_back((uint32_t)x);
+            }
+            continue;
+        }
         if (P.partitioned) {
             int ai = h.key_attr[qpos];
             if (ev.nulls[ai]) continue;  // null partition key: dropped
@@ -134,10 +150,12 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
                 q.key_hash.push_back(java_spread_hash(kt));
             }
             key = it->second;
+            if (q.bcast) q.korder.add((uint32_t)key, q.key_hash[key]);
         }
         rows.push_back(&ev);
         rkey.push_back(key);
         rpos.push_back((uint32_t)g);
+        rrank.push_back(0);
     }
     const int64_t n = (int64_t)rows.size();
     const int K = P.partitioned ? (int)q.keys.size() : 1;
@@ -147,7 +165,7 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return rkey[a] < rkey[b]; });
     std::vector<int64_t> ts(std::max<int64_t>(n, 1));
     std::vector<uint8_t> qs(std::max<int64_t>(n, 1));
-    std::vector<uint32_t> gpos(std::max<int64_t>(n, 1));
+    std::vector<uint32_t> gpos(std::max<int64_t>(n, 1)), vrank(std::max<int64_t>(n, 1));
     std::vector<std::vector<uint8_t>> cols(nc), nulls(nc);
     std::vector<const void*> cptr(MAX_COLS, nullptr);
     std::vector<const uint8_t*> nptr(MAX_COLS, nullptr);
@@ -164,6 +182,7 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
         ts[p] = ev.ts;
         qs[p] = (uint8_t)qpos;
         gpos[p] = rpos[order[p]];
+        vrank[p] = rrank[order[p]];
         for (int k = 0; k < nc; ++k) {
             int ai = h.col_attr[qpos][k];
             int w = width_of(P.col_kind[k]);
@@ -234,7 +253,7 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
         c.fires = fires;
         c.nfires = nfires;
         nfa::KeyEvents kev{ts.data(), qs.data(), gpos.data(), cptr.data(), nptr.data(), seg_b.size() > k ? seg_b[k] : 0,
-                           seg_e.size() > k ? seg_e[k] : 0, e->seq, 0};
+                           seg_e.size() > k ? seg_e[k] : 0, e->seq, 0, q.bcast ? vrank.data() : nullptr};
         if (kev.b > kev.e) kev.b = kev.e;
         nfa::run_key(c, kev);
         if (c.ovf()) {
@@ -333,6 +352,7 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
                 r->ts.push_back(ts[p]);
                 r->qs.push_back(qs[p]);
                 r->pos.push_back(gpos[p]);
+                if (q.bcast) r->vrank.push_back(vrank[p]);
             }
             r->has_qs = true;
             r->cols.resize(nc);
@@ -440,9 +460,10 @@ void* emu_create(const char* text, int max_partials) {
             const Plan& P = q->hq.plan;
             if (P.has_post)  // the selector's post pass runs on the device only (order.hip select_post)
                 throw std::runtime_error("selector post pass (aggregators / having) is device-only");
-            for (int ka : q->hq.key_attr)
-                if (ka == -2 || ka == -3)
-                    throw std::runtime_error("range partitions / broadcast streams: the engine's batch assembly only");
+            for (int ka : q->hq.key_attr) {
+                if (ka == -2) throw std::runtime_error("range partitions: the engine's batch assembly only");
+                if (ka == -3) q->bcast = true;
+            }
             if (P.purge) throw std::runtime_error("@purge: the engine's kernel arguments only");
             if (P.n_list_cols) throw std::runtime_error("multi-value selections: the engine's poll only");
             q->L = nfa::make_layout(P.n_states, std::max(P.n_cols, 1), e->ns, P.n_sched);

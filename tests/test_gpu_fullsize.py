@@ -16,8 +16,8 @@ def test_c3_full_config_vs_sharded_oracle(query, oracle_built):
     """C3 at its config size: 10^6 long keys x 100 events = 10^8 events in one flush"""
     c = w.c3_columns(1_000_000)
     app = w.C3_APP.replace("<2:5>", query)
-    rt = sa.SiddhiAppRuntime(app)
-    try:
+    rt = sa.SiddhiAppRuntime(app, batch_capacity=len(c["ts"]) + 1)  # one flush (an auto-flush would deliver to
+    try:                                                              # callbacks, of which there are none here)
         assert rt.query_paths() == [2]
         rt.getInputHandler("S").send_columns(c["ts"], [c["id"], c["key"], c["price"], c["volume"]])
         rt.flush(deliver=False)

@@ -58,7 +58,7 @@ def _rank_main(rank, world, port, out_dir):
                 "gseq": torch.tensor([p[0] for p in part], dtype=torch.int64),
                 "ord": torch.tensor([p[1] for p in part], dtype=torch.int64),
                 "rank": torch.full((len(part),), rank, dtype=torch.int64),
-                "idx": torch.arange(len(part), dtype=torch.int64)}, ["gseq", "ord"])
+                "idx": torch.arange(len(part), dtype=torch.int64)}, ["gseq", "ord"], first_key_unique=True)
             if rank == 0:
                 merged = shard.merge(parts)
                 tensor_merged = [parts[r][i][2] for r, i in zip(g["rank"].tolist(), g["idx"].tolist())]
@@ -128,3 +128,40 @@ def test_sharded_runtime_refuses_absent_states_at_n_gt_1():
     assert mine == [k for k in keys if shard.owner(k, 4) == 1]
     r1 = shard.ShardedAppRuntime(w.C1_APP, 1, 2, compile_only=True)
     assert r1.replica and not r1.mine("StockStream", [0, "IBM", 1.0, 1])
+
+
+def test_sharded_runtime_routes_by_the_engines_partition_attribute():
+    """the router takes each stream's key attribute from the engine (sdg_query_key_attr), refuses a
+    caller's key_attr that disagrees, a stream keyed by two attributes, range partitions and broadcast streams at
+    N > 1, and routes columnar batches at once (route over the distinct keys)"""
+    import numpy as np
+    import siddhi_amd as sa
+    import synth
+    from siddhi_amd import workloads as w
+    s = shard.ShardedAppRuntime(w.C2_APP, 1, 4, compile_only=True)
+    assert s.key_attr == {"StockStream": 1}
+    assert s.rt.query_key_attr(0, "StockStream") == 1
+    with pytest.raises(sa.OperationNotSupportedException):
+        shard.ShardedAppRuntime(w.C2_APP, 1, 4, compile_only=True, key_attr={"StockStream": 0})
+    two = ("define stream S (id long, a string, b string); partition with (a of S) begin @info(name='q1') "
+           "from every e1=S -> e2=S select e1.id as x insert into O1; end; partition with (b of S) begin "
+           "@info(name='q2') from every e1=S -> e2=S select e1.id as x insert into O2; end;")
+    assert shard.ShardedAppRuntime(two, 0, 1, compile_only=True).key_attr  # one GPU: fine
+    with pytest.raises(sa.OperationNotSupportedException):
+        shard.ShardedAppRuntime(two, 0, 2, compile_only=True)
+    bc = synth.BCAST_APPS["bc_pattern"]
+    assert sa.SiddhiAppRuntime(bc, compile_only=True).query_flags() == [shard.Q_PARTITIONED | shard.Q_BROADCAST]
+    assert sa.SiddhiAppRuntime(bc, compile_only=True).query_key_attr(0, "T") == -3
+    with pytest.raises(sa.OperationNotSupportedException):
+        shard.ShardedAppRuntime(bc, 0, 2, compile_only=True)
+    keys = np.array(["S%05d" % k for k in np.random.default_rng(3).integers(0, 5000, 20000)])
+    r = shard.route(keys, 4)
+    assert r.tolist() == [shard.owner(k, 4) for k in keys.tolist()]
+    ints = np.random.default_rng(4).integers(-10**12, 10**12, 5000)
+    assert shard.route(ints, 3).tolist() == [shard.owner(int(k), 3) for k in ints.tolist()]
+
+
+def test_ordered_gather_checks_its_merge_precondition():
+    import torch
+    with pytest.raises(ValueError):
+        shard.ordered_gather(None, 0, 1, {"a": torch.zeros(3), "b": torch.zeros(3)}, ["a", "b"])
