@@ -248,10 +248,11 @@ def ordered_gather_leg(rt, step_push, n, dev, dist, rank, world):
     cnt = rt.export_ordered(0, cap, t_ts.data_ptr(), t_seq.data_ptr(), t_sub.data_ptr(), t_vals.data_ptr())
     recs = {"ts": t_ts[:cnt], "seq": t_seq[:cnt], "sub": t_sub[:cnt],
             "rank": torch.full((cnt,), rank, dtype=torch.int64, device=dev), "vals": t_vals[:, :cnt]}
+    gph = {"export": time.perf_counter() - t0, "transfer": 0.0, "merge": 0.0}
     if dist is None:
         merged = recs
     else:
-        merged = shard.ordered_gather(dist, rank, world, recs, key, presorted=True)
+        merged = shard.ordered_gather(dist, rank, world, recs, key, presorted=True, timings=gph)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -272,7 +273,8 @@ def ordered_gather_leg(rt, step_push, n, dev, dist, rank, world):
         ok = bool(less.all().item())
     if not ok:
         raise RuntimeError("ordered gather: merged records are not in delivery order")
-    return {"records": total, "ms": dt * 1000.0, "bytes_to_rank0": int((total - cnt) * 8 * 6),
+    return {"records": total, "ms": dt * 1000.0, "rank0_ms": {k: v * 1000.0 for k, v in gph.items()},
+            "bytes_to_rank0": int((total - cnt) * 8 * 6),
             "key": "(event ts, rank, event position in its rank's stream, ordinal)", "ordered": True,
             "path": "sdg_export_ordered (per-rank device ordering) -> RCCL send/recv to rank 0 -> stable device "
                     "sort of the concatenated runs by time (shard.merge_runs)"}
@@ -355,17 +357,23 @@ def run_c5(args, rank, world, local, dist):
     g_vals = torch.empty((2, gcap), dtype=torch.int64, device=dev)
     last_merged = [None]
 
+    gph = {"export": 0.0, "transfer": 0.0, "merge": 0.0}
+
     def gather():
+        t = time.perf_counter()
         cnt = rt.export_ordered(0, gcap, g_ts.data_ptr(), g_seq.data_ptr(), g_sub.data_ptr(), g_vals.data_ptr())
         recs = {"e2": g_vals[1, :cnt], "e1": g_vals[0, :cnt], "ts": g_ts[:cnt]}
+        gph["export"] += time.perf_counter() - t
         if dist is None:
             merged = recs
         else:
-            merged = shard.ordered_gather(dist, rank, world, recs, ["e2", "e1"], presorted=True, first_key_unique=True)
+            merged = shard.ordered_gather(dist, rank, world, recs, ["e2", "e1"], presorted=True, first_key_unique=True,
+                                          timings=gph)
         last_merged[0] = merged
         return cnt
 
-    def step(j, with_gather=True):
+    def step(j):
+        """one flush (its records stay on the device for the gather that follows)"""
         n = push(j)
         rt.flush(deliver=False)
         st = rt.stats()
@@ -373,15 +381,17 @@ def run_c5(args, rank, world, local, dist):
             cnt = torch.tensor([st.matches], dtype=torch.int64, device=dev)
             allc = [torch.empty_like(cnt) for _ in range(world)]
             dist.all_gather(allc, cnt)
-        if with_gather and not args.no_gather:
-            gather()
-        else:
+        if args.no_gather:
             rt.discard()
         return n, st
 
     log("C5: warm-up (%d flushes)" % args.warmup)
     for j in range(args.warmup):
         step(j)
+        if not args.no_gather:
+            gather()
+    for k in gph:
+        gph[k] = 0.0
     keys_k = ["ms_kg_hist", "ms_kg_prefix", "ms_kg_scatter", "ms_chain_carry", "ms_chain_match", "ms_chain_emit"]
     acc = {k: 0.0 for k in keys_k}
     events = matches = carries = 0
@@ -392,7 +402,7 @@ def run_c5(args, rank, world, local, dist):
     t0 = time.perf_counter()
     for j in range(args.warmup, nsteps):
         tf = time.perf_counter()
-        n, st = step(j, with_gather=False)
+        n, st = step(j)
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
@@ -441,6 +451,7 @@ def run_c5(args, rank, world, local, dist):
         "gather": None if args.no_gather else {
             "ms_per_step": (elapsed - t_flush) * 1000.0 / K, "inside_step": True,
             "records_per_rank_step": matches / K,
+            "rank0_ms_per_step": {k: v * 1000.0 / K for k, v in gph.items()},
             "key": "(e2id = global position of the emitting event, e1id)",
             "path": "sdg_export_ordered (device ordering) -> RCCL send/recv to rank 0 -> stable device sort of the "
                     "concatenated runs on e2id (shard.merge_runs)"},
@@ -467,7 +478,7 @@ def run_c5(args, rank, world, local, dist):
     del batches, g_ts, g_seq, g_sub, g_vals
     torch.cuda.empty_cache()
     if rank == 0 and not args.no_cpu:
-        out["cpu_baseline"] = c5_cpu_baseline(sh, args.c5_sample)
+        out["cpu_baseline"] = c5_cpu_baseline(sh)
     if not args.no_parity:
         log("C5: oracle sample of this rank's shard (%d keys)" % args.c5_sample)
         sys.path.insert(0, os.path.join(REPO, "tests"))

@@ -99,7 +99,7 @@ def merge_runs(runs, key):
     return out
 
 
-def ordered_gather(dist, rank, world, cols, key_names, presorted=False, first_key_unique=False):
+def ordered_gather(dist, rank, world, cols, key_names, presorted=False, first_key_unique=False, timings=None):
     """Ordered result gather: `cols` maps names to this rank's record tensors (1-D [n], or 2-D
     [m, n] with records along the last dim) on the communication device. Every rank sorts its records by
     `key_names` on its device, the run lengths are all-gathered, and each rank's sorted run goes to rank 0
@@ -107,7 +107,8 @@ def ordered_gather(dist, rank, world, cols, key_names, presorted=False, first_ke
     first key (merge_runs: records of different ranks with equal first keys keep rank order, which is the
     tie-break every caller's key implies -- either the first key is unique across ranks, e.g. the global position of
     the emitting event, or the rank is the next key). presorted: the records already are in `key_names` order (an
-    sdg_export_ordered run), no local sort. Returns the merged dict on rank 0, None elsewhere."""
+    sdg_export_ordered run), no local sort. timings: a dict whose "transfer" / "merge" entries get this call's seconds
+    added (device-synchronised). Returns the merged dict on rank 0, None elsewhere."""
     import torch
     # the merge orders by key_names[0], then rank, then each run's own order: that equals key_names order only if
     # the first key is unique across ranks or the rank is the next key
@@ -130,6 +131,9 @@ def ordered_gather(dist, rank, world, cols, key_names, presorted=False, first_ke
             for k in names:
                 dist.send(mine[k], dst=0)
         return None
+    import time
+    torch.cuda.synchronize() if ref.is_cuda else None
+    t0 = time.perf_counter()
     runs = [mine]
     for r in range(1, world):
         if counts[r] == 0:
@@ -140,7 +144,13 @@ def ordered_gather(dist, rank, world, cols, key_names, presorted=False, first_ke
             run[k] = torch.empty(shape, dtype=cols[k].dtype, device=ref.device)
             dist.recv(run[k], src=r)
         runs.append(run)
+    torch.cuda.synchronize() if ref.is_cuda else None
+    t1 = time.perf_counter()
     merged = merge_runs(runs, key_names[0])
+    torch.cuda.synchronize() if ref.is_cuda else None
+    if timings is not None:
+        timings["transfer"] = timings.get("transfer", 0.0) + t1 - t0
+        timings["merge"] = timings.get("merge", 0.0) + time.perf_counter() - t1
     if merged is None:
         return {k: mine[k] for k in names}
     return merged
