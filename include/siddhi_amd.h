@@ -69,6 +69,8 @@ typedef struct sdg_opts {
 #define SDG_FORCE_GENERIC 2    /* run every query on the generic keyed-NFA kernel (testing: both kernels on one query) */
 #define SDG_NO_FUSED 4         /* chain path: always key-sort with the full radix (testing: both chain kernels on one query) */
 #define SDG_NO_SEQ3 8          /* sequences of the seq3 shape on the generic keyed NFA instead (testing: both kernels) */
+#define SDG_NO_SORTED 64       /* chain path past the fused bucket matcher: the lane deque kernels instead of the
+                                  LDS-staged sorted-view matcher (testing: both kernels on one query) */
 #define SDG_SCHED_EXACT 16     /* absent states: always run the scheduler's exact pass, even when the device reruns
                                   reproduce the optimistic pass (testing: pins the exact pass against the oracle) */
 #define SDG_SCHED_HOST 32      /* absent states: no optimistic pass / device rerun; the exact pass runs over the
@@ -211,6 +213,9 @@ typedef struct sdg_stats {
                                   whose state the reference destroys down to their start seeds give theirs back */
     int64_t sched_exact_passes; /* scheduler simulation: exact passes run (0 when the device reruns reproduced the
                                    optimistic pass's model changes, SchedSim::confirm) */
+    int32_t sorted_view;       /* chain path: 1 the LDS-staged sorted-view matcher ran (carried partials folded into
+                                  the key sort), 0 otherwise */
+    int32_t reserved0;
 } sdg_stats;
 int sdg_last_stats(sdg_engine* e, sdg_stats* out);
 

@@ -86,7 +86,8 @@ class Stats(ctypes.Structure):
                 ("sched_host_keys", ctypes.c_int64), ("sched_rerun_keys", ctypes.c_int64),
                 ("ms_nfa_kernel", ctypes.c_double), ("ms_sched_host", ctypes.c_double),
                 ("arena_growths", ctypes.c_int64), ("carry_in", ctypes.c_int64), ("carry_out", ctypes.c_int64),
-                ("arena_slots", ctypes.c_int64), ("sched_exact_passes", ctypes.c_int64)]
+                ("arena_slots", ctypes.c_int64), ("sched_exact_passes", ctypes.c_int64),
+                ("sorted_view", ctypes.c_int32), ("reserved0", ctypes.c_int32)]
 
 
 _lib = None
@@ -219,13 +220,14 @@ class InputHandler:
 
 class SiddhiAppRuntime:
     def __init__(self, app_text, device=0, batch_capacity=0, compile_only=False, force_generic=False, fused=True,
-                 max_partials=0, seq3=True, sched_exact=False, sched_host=False):
+                 max_partials=0, seq3=True, sched_exact=False, sched_host=False, sorted_view=True):
         L = load_library()
         self._L = L
         h = ctypes.c_void_p()
         opts = _Opts(device, batch_capacity, max_partials,
                      (1 if compile_only else 0) | (2 if force_generic else 0) | (0 if fused else 4) |
-                     (0 if seq3 else 8) | (16 if sched_exact else 0) | (32 if sched_host else 0))
+                     (0 if seq3 else 8) | (16 if sched_exact else 0) | (32 if sched_host else 0) |
+                     (0 if sorted_view else 64))
         _check(L.sdg_compile(app_text.encode(), ctypes.byref(opts), ctypes.byref(h)))
         self._h = h
         self._compile_only = compile_only

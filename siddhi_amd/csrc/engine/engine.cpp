@@ -349,6 +349,7 @@ struct sdg_engine {
     bool no_seq3 = false;        // SDG_NO_SEQ3 / SDG_FORCE_GENERIC: seq3-shaped sequences on the generic NFA
     bool sched_exact = false;    // SDG_SCHED_EXACT (flag or env): the scheduler's exact pass always runs
     bool sched_host = false;     // SDG_SCHED_HOST: exact pass over the first run, diverged keys replayed on the host
+    bool no_sorted = false;      // SDG_NO_SORTED: the radix chain path keeps the lane deque kernels
     uint64_t app_hash = 0;       // FNV-1a of the app text: a snapshot restores only into the app it came from
     std::vector<uint8_t> snap;   // the last sdg_snapshot's bytes (valid until the next snapshot / destroy)
     std::vector<Stage> stage;    // per stream: host pushes staged in HBM (see stage_push)
@@ -1365,10 +1366,29 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                            ((ps.scan_mode == SCAN_CONST || ps.scan_mode == SCAN_E1) && ps.scan_col < nc && !d_nulls[ps.scan_col]);
         try_fused = !pa.generic && typed && ps.scan_col >= 0 && ps.scan_col < nc;
     }
+    // sorted-view matcher (chain.hip chain_sorted_k) on the radix path: the shapes of the fused matcher without the
+    // key-count limit; the carried partials fold into the key sort (their values must not be null: none of the
+    // query's columns may hold nulls)
+    bool sorted_now = false;
+    if (P.chain && partitioned && !multi_stream && nrows > 0 && !e->no_sorted && P.n_states == 2 && nc >= 1 &&
+        P.fast[0].kind != FP_NONE && !q.carry_nullable && nrows + q.carry[q.cur].n < ((int64_t)1 << 31) &&
+        (int64_t)K < ((int64_t)1 << 31)) {
+        ChainArgs pa;
+        std::memset(&pa, 0, sizeof pa);
+        bool nulls = false;
+        for (int k = 0; k < nc; ++k) nulls |= d_nulls[k] != nullptr;
+        chain_staging(h, pa, false);
+        const ChainSpec& ps = pa.sp;
+        const bool typed = ps.scan_mode == SCAN_TRUE || ps.scan_mode == SCAN_CONST || ps.scan_mode == SCAN_E1;
+        sorted_now = !nulls && !pa.generic && typed && ps.scan_col >= 0 && ps.scan_col < nc;
+    }
     e->stats.fused = 0;
     const bool carry_nullable0 = q.carry_nullable;
     // returns false when the fused path found its precondition broken (nothing of the batch is committed then)
     auto run = [&](bool fused) -> bool {
+    const bool sorted = !fused && sorted_now && P.chain;
+    // sorted view rows: the batch plus the carried partials folded in as leading rows of their keys
+    const int64_t nv = nrows + (sorted ? q.carry[q.cur].n : 0);
     // ---- 2. key grouping ---------------------------------------------------------------------------------
     const int64_t* v_ts = d_ts;
     const uint8_t* v_qs = d_qs;
@@ -1392,7 +1412,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         KeyGroupArgs a;
         std::memset(&a, 0, sizeof a);
         a.ts32_col = -1;
-        a.n = nrows;
+        a.n = nv;
         a.K = (int32_t)K;
         a.keys = d_key;
         a.key_flag = zero_copy ? flags + 4 : nullptr;  // caller-supplied device ids: range-check against K
@@ -1404,14 +1424,14 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         if (ts_by_orig) {
             v_ts = nullptr;
         } else {
-            a.src[c] = d_ts; a.dst[c] = q.so_ts.ensure(nrows * 8); a.width[c] = 8; v_ts = (const int64_t*)a.dst[c]; ++c;
+            a.src[c] = d_ts; a.dst[c] = q.so_ts.ensure(nv * 8); a.width[c] = 8; v_ts = (const int64_t*)a.dst[c]; ++c;
         }
         if (d_qs) { a.src[c] = d_qs; a.dst[c] = q.so_qs.ensure(nrows); a.width[c] = 1; v_qs = (const uint8_t*)a.dst[c]; ++c; }
         if (d_vrank) { a.src[c] = d_vrank; a.dst[c] = q.so_vrank.ensure(nrows * 4); a.width[c] = 4; v_vrank = (const uint32_t*)a.dst[c]; ++c; }
         for (int k = 0; k < nc; ++k) {
             if (c >= MAX_COLS + 2) throw CompileError(SDG_ERR_UNSUPPORTED, "too many columns");
             int w = width_of(P.col_kind[k]);
-            a.src[c] = d_cols[k]; a.dst[c] = q.so_cols[k].ensure(nrows * w); a.width[c] = (uint8_t)w;
+            a.src[c] = d_cols[k]; a.dst[c] = q.so_cols[k].ensure(nv * w); a.width[c] = (uint8_t)w;
             v_cols[k] = a.dst[c];
             ++c;
             if (d_nulls[k]) {
@@ -1421,9 +1441,17 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             }
         }
         a.ncols = c;
-        keygroup_bind(a, q.kg_counts.ensure(keygroup_workspace(nrows, (int32_t)K, a.ncols, a.width)));
-        a.keys_sorted = (uint32_t*)q.so_key.ensure(nrows * 4);
-        a.orig_sorted = (uint32_t*)q.so_orig.ensure(nrows * 4);
+        if (sorted && q.carry[q.cur].n > 0) {  // the carried partials as prefix rows (ts, then each column's slots)
+            const QueryRt::Carry& ci = q.carry[q.cur];
+            a.pre_n = ci.n;
+            a.pre_keys = ci.key.as<uint32_t>();
+            a.pre_src[0] = ci.ts.p;
+            for (int k = 0; k < nc; ++k) a.pre_src[1 + k] = ci.vals.as<int64_t>() + (size_t)k * ci.cap;
+        }
+        a.no_segments = sorted;
+        keygroup_bind(a, q.kg_counts.ensure(keygroup_workspace(nv, (int32_t)K, a.ncols, a.width)));
+        a.keys_sorted = (uint32_t*)q.so_key.ensure(nv * 4);
+        a.orig_sorted = (uint32_t*)q.so_orig.ensure(nv * 4);
         a.seg_start = (uint32_t*)q.seg.ensure((size_t)K * 4);
         a.seg_end = (uint32_t*)q.kg_gsum.ensure((size_t)K * 4);
         if (fused) {
@@ -2039,7 +2067,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     a.plan = q.d_plan.as<Plan>();
     a.code = q.d_code.as<Instr>();
     a.consts = q.d_consts.as<int64_t>();
-    a.n = nrows;
+    a.n = nv;
+    a.fold = sorted;
     a.ts = v_ts;
     a.ts32 = v_ts32;
     a.ts_base = v_ts32 ? d_ts : nullptr;
@@ -2101,9 +2130,14 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         a.lbits = std::max(0, kbits - bbits);
         a.seg_start = a.seg_end = nullptr;
     }
-    if ((a.deque_mode != DQ_OFF || fused) && nrows > 0) {
+    if (sorted) {  // chain_sorted_k: deque / forward scans in LDS blocks, the rest of a cut run in chain_sovf_k
+        a.fu_mode = a.deque_mode;
+        a.deque_mode = DQ_OFF;
+        a.seg_start = a.seg_end = nullptr;
+    }
+    if ((a.deque_mode != DQ_OFF || fused || sorted) && nrows > 0) {
         a.mq = (uint32_t*)q.o_mq.ensure((size_t)nrows * 4);
-        a.ovf_rows = (uint32_t*)q.o_ovf.ensure((size_t)nrows * 4);
+        a.ovf_rows = (uint32_t*)q.o_ovf.ensure((size_t)nv * 4);
         a.ovf_count = (unsigned long long*)q.o_ovfc.ensure(8);
         HIPCHECK(hipMemsetAsync(a.ovf_count, 0, 8, st));
     }
@@ -2142,7 +2176,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     };
     dbg_sync("bucketize / staging");
     ev_record(e->ev[3], st);  // after the buffer (re)allocations above: they stall the stream, not the kernels
-    chain_carry(a, d_a, st);
+    if (!sorted) chain_carry(a, d_a, st);  // (sorted: the carried partials are rows of the view)
     dbg_sync("chain_carry_k");
     ev_record(e->ev[8], st);
     if (fused) {
@@ -2187,6 +2221,12 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         ev_record(e->ev[9], st);
         chain_fovf(a, d_a, st);
         dbg_sync("chain_fovf_k");
+    } else if (sorted) {
+        chain_sorted(a, d_a, st);
+        dbg_sync("chain_sorted_k");
+        ev_record(e->ev[9], st);
+        chain_sovf(a, d_a, st);
+        dbg_sync("chain_sovf_k");
     } else if (a.deque_mode != DQ_OFF && nrows > 0) {
         chain_deque(a, d_a, st);
         ev_record(e->ev[9], st);
@@ -2204,7 +2244,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     hovf = 0;
     HIPCHECK(hipMemcpyAsync(hc, counters, 16, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipMemcpyAsync(hf, flags, 32, hipMemcpyDeviceToHost, st));
-    if (fused) HIPCHECK(hipMemcpyAsync(&hovf, a.ovf_count, 8, hipMemcpyDeviceToHost, st));
+    if (fused || sorted) HIPCHECK(hipMemcpyAsync(&hovf, a.ovf_count, 8, hipMemcpyDeviceToHost, st));
     hp.mark("tail_enqueue");
     HIPCHECK(hipStreamSynchronize(st));
     hp.mark("sync_wait");
@@ -2215,7 +2255,13 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         q.carry_nullable = carry_nullable0;
         return false;
     }
+    if (sorted && hf[3]) {  // a block's staged span over 2^32 ms: the lane deque kernels
+        sorted_now = false;
+        q.carry_nullable = carry_nullable0;
+        return false;
+    }
     e->stats.fused = fused ? 1 : e->stats.fused;
+    e->stats.sorted_view = sorted ? 1 : 0;
     e->stats.fused_ovf += (int64_t)hovf;
     float ms_kg = 0, ms_m = 0;
     ev_elapsed(&ms_kg, e->ev[0], e->ev[1]);
@@ -2240,7 +2286,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     e->stats.ms_chain_match += t;
     ev_elapsed(&t, e->ev[9], e->ev[2]);
     e->stats.ms_chain_emit += t;
-    e->stats.deque = a.deque_mode;
+    e->stats.deque = sorted ? a.fu_mode : a.deque_mode;
     e->stats.events += nrows;
     if (hf[0]) {
         e->stats.overflow += 1;
@@ -2271,7 +2317,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     };
     // rerun on the radix path (fused precondition broken), or on the generic NFA (chain precondition broken)
     for (int attempt = 0; !run(try_fused && attempt == 0); ++attempt)
-        if (attempt >= 2) throw DeviceError("query '" + h.name + "': no matcher path accepted the batch");
+        if (attempt >= 3) throw DeviceError("query '" + h.name + "': no matcher path accepted the batch");
 }
 
 // read the last flush's match records back (pinned staging) and append them to the query's delivery backlog in
@@ -2611,6 +2657,7 @@ int do_flush(sdg_engine* e) {
     e->stats.fused_ovf = 0;
     e->stats.sched_fires = e->stats.sched_shifted = e->stats.sched_host_keys = e->stats.sched_rerun_keys = 0;
     e->stats.sched_exact_passes = 0;
+    e->stats.sorted_view = 0;
     // a flush consumes its batch whether or not it succeeds: a failing query must not make the next flush
     // replay the events onto the queries that already committed them. The batch's positions and its clock are
     // consumed with it: queries that committed before a failing one hold carries, arenas and scheduler state
@@ -3069,6 +3116,7 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             e->no_seq3 = (opts->flags & (SDG_NO_SEQ3 | SDG_FORCE_GENERIC)) != 0;
             e->sched_exact = (opts->flags & SDG_SCHED_EXACT) != 0 || getenv("SDG_SCHED_EXACT") != nullptr;
             e->sched_host = (opts->flags & SDG_SCHED_HOST) != 0;
+            e->no_sorted = (opts->flags & SDG_NO_SORTED) != 0 || getenv("SDG_NO_SORTED") != nullptr;
         }
         if (opts && opts->max_partials > 0) {
             if (opts->max_partials > 4096) throw CompileError(SDG_ERR_ARG, "max_partials must be <= 4096");

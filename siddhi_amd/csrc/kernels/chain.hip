@@ -1406,6 +1406,446 @@ size_t chain_lds_bytes(const ChainArgs& a) {
     return b + (size_t)CM_EPT * CM_THREADS * 4;
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Sorted-view matcher (the radix path's counterpart of chain_fused_k, for key counts past the bucket path): the view
+// is fully key-sorted (keygroup), so a block stages FU_ROWS consecutive sorted rows -- FU_OWN own rows plus a halo --
+// coalesced into LDS and every key's run is already contiguous: no regrouping, run boundaries are key changes. The
+// same chunked monotone deque (chain_deque_k), then the matches emitted straight from the block (no mq
+// round trip through HBM, no separate emission kernel).
+// Carried partials of the previous batch are FOLDED into the view (a.fold): the first radix pass read them as leading
+// rows (orig = SV_CARRIED | carry index), so the stable sort puts them at the start of their key's run. They are not
+// events: no deque step, no e1 filter; each resolves with a forward scan over the run (their order among themselves
+// is the arbitrary carry-out order, which a forward scan does not depend on). No separate carry kernel.
+// A partial whose run is cut by the staged rows (the key continues past the halo) goes to chain_sovf_k, which scans
+// the rest of the run in HBM; one whose run ends in the batch is carried.
+constexpr uint32_t SV_CARRIED = 0x80000000u;   // orig flag / s_key flag of a folded carried partial
+constexpr uint32_t SV_KEY = 0x7FFFFFFFu;
+__device__ __forceinline__ int64_t sv_seq(const ChainArgs& a, uint32_t o) {
+    return (a.fold && (o & SV_CARRIED)) ? a.cin_seq[o & SV_KEY] : a.seq_base + (int64_t)o;
+}
+
+template <int K, bool SAME>
+__global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs* __restrict__ pa) {
+    using C = KT<K>;
+    using T = typename C::T;
+    constexpr int NW = FU_THREADS / 64;
+    constexpr int WROWS = FU_ROWS / NW;
+    const ChainArgs& a = *pa;
+    const ChainSpec& sp = a.sp;
+    __shared__ uint32_t s_ts[FU_ROWS];   // ts - the block's smallest staged ts
+    __shared__ int64_t s_x[FU_ROWS];
+    __shared__ uint32_t s_key[FU_ROWS];  // key | SV_CARRIED for a folded carried partial
+    __shared__ uint16_t s_res[FU_ROWS];  // per position: e2 position | R_NONE | R_CARRY | R_OVF
+    __shared__ uint32_t wcnt[3][FU_PT][NW];
+    __shared__ unsigned long long bbase[3];
+    __shared__ int64_t wmin[NW], wmax[NW];
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const uint32_t G8 = gridDim.x / 8;  // XCD-aware block order: neighbouring blocks (shared halo rows) on one XCD
+    const uint32_t v = (blockIdx.x & 7u) * G8 + (blockIdx.x >> 3);
+    const int64_t lo = (int64_t)v * FU_OWN;
+    if (lo >= a.n) return;  // block-uniform: the rounding of the grid
+    const int own = (int)min((int64_t)FU_OWN, a.n - lo);
+    const int nr = (int)min((int64_t)FU_ROWS, a.n - lo);
+    const int col = sp.scan_col;
+    const uint8_t kind = sp.scan_col_kind;
+    const void* xcol = a.cols[col];
+    // ---- stage: coalesced loads -------------------------------------------------------------------------------
+    uint32_t rkey[FU_PT];
+    int64_t rts[FU_PT], rx[FU_PT];
+    int64_t tmn = INT64_MAX, tmx = INT64_MIN;
+#pragma unroll
+    for (int r = 0; r < FU_PT; ++r) {
+        const int row = w * WROWS + r * 64 + lane;
+        const int64_t g = lo + min(row, nr - 1);
+        const uint32_t o = a.orig[g];
+        rkey[r] = (a.key[g] & SV_KEY) | ((a.fold && (o & SV_CARRIED)) ? SV_CARRIED : 0u);
+        rts[r] = a.ts[g];
+        rx[r] = kind == VK_F64 || kind == VK_I64 ? ((const int64_t*)xcol)[g] : load_col(xcol, kind, g);
+        tmn = min(tmn, rts[r]);
+        tmx = max(tmx, rts[r]);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        tmn = min(tmn, (int64_t)__shfl_xor(tmn, d));
+        tmx = max(tmx, (int64_t)__shfl_xor(tmx, d));
+    }
+    if (lane == 0) {
+        wmin[w] = tmn;
+        wmax[w] = tmx;
+    }
+    __syncthreads();
+    int64_t tbase = wmin[0], tlast = wmax[0];
+#pragma unroll
+    for (int x = 1; x < NW; ++x) {
+        tbase = min(tbase, wmin[x]);
+        tlast = max(tlast, wmax[x]);
+    }
+    if (tlast - tbase > (int64_t)0xFFFFFFFF) {  // staged span does not fit the u32 offsets: the host reruns the
+        if (t == 0) atomicOr(&a.flags[3], 1);     // batch on the lane deque path
+        return;                                   // block-uniform
+    }
+#pragma unroll
+    for (int r = 0; r < FU_PT; ++r) {
+        const int row = w * WROWS + r * 64 + lane;
+        if (row < nr) {
+            s_ts[sw(row)] = (uint32_t)(rts[r] - tbase);
+            s_x[sw(row)] = rx[r];
+            s_key[sw(row)] = rkey[r];
+            s_res[sw(row)] = R_NONE;
+        }
+    }
+    // the key of the first row past the staged ones: a run cut at the staged end continues in HBM (R_OVF) only if
+    // that row is of the same key; else the key's rows of this batch end there (R_CARRY)
+    const uint32_t next_key = lo + nr < a.n ? (a.key[lo + nr] & SV_KEY) : 0xFFFFFFFFu;
+    __syncthreads();
+    // per-key time order (the chain path's precondition): own positions against their predecessor
+#pragma unroll
+    for (int r = 0; r < FU_PT; ++r) {
+        const int pos = r * FU_THREADS + t;
+        if (pos >= own) continue;
+        const uint32_t kp = s_key[sw(pos)];
+        if (kp & SV_CARRIED) continue;  // (a carried partial has no successor constraint among carried ones)
+        int64_t pk, pt;
+        if (pos > 0) {
+            pk = s_key[sw(pos - 1)] & SV_KEY;
+            pt = (int64_t)s_ts[sw(pos - 1)];
+        } else if (lo > 0) {
+            pk = a.key[lo - 1] & SV_KEY;
+            pt = a.ts[lo - 1] - tbase;
+        } else {
+            continue;
+        }
+        if (pk == (kp & SV_KEY) && pt > (int64_t)s_ts[sw(pos)]) atomicOr(&a.flags[1], 1);
+    }
+    const CmpMask m = cmp_mask(sp.scan_mode == SCAN_TRUE ? OP_ALWAYS : sp.scan_op);
+    const bool left = sp.scan_e2_left;
+    const uint64_t within_u = sp.has_within ? (uint64_t)sp.within_ms : ~0ull;
+    const FastPred& f0 = sp.f0;
+    const bool f0_on_x = a.f0_on_x;
+    const bool f0_typed = f0_on_x && SAME && f0.t == K;
+    const CmpMask m0 = cmp_mask(f0.op);
+    const T k0 = C::get(f0.konst);
+    const T kc = C::get(sp.scan_konst);
+    const bool stream_e1 = sp.scan_mode == SCAN_E1;
+    const bool e1_is_x = stream_e1 && sp.e1_col == col && sp.e1_col_kind == kind;
+    auto xval = [&](int64_t xr) -> T { return SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K)); };
+    auto c0_at = [&](int pos, int64_t xr, T xv) -> bool {
+        if (f0_typed) return cmp_m(m0, xv, k0);
+        if (f0_on_x) return cmp(f0.op, f0.t, cvt(xr, kind, f0.t), f0.konst);
+        ChainAcc acc{&a, View{}, lo + pos, -1, -1};
+        return f0.kind == FP_TRUE ? true : fast_pass(f0, acc);
+    };
+    // where a pending partial of key k goes when its run leaves the staged rows at position q (q = the first
+    // position not of the run): the key's end in this batch (carry) or the HBM continuation (overflow scan)
+    auto off_res = [&](int q, uint32_t k) -> uint16_t {
+        return (q < nr || next_key != (k & SV_KEY)) ? R_CARRY : R_OVF;
+    };
+    if (a.fu_mode != DQ_OFF) {
+        // ---- monotone-deque pass (as chain_fused_k): lane t owns positions [FU_DQ t, FU_DQ (t + 1)) ----------
+        const bool stack = a.fu_mode == DQ_STACK;
+        const int p0 = t * FU_DQ;
+        uint32_t pend = 0, tf = 0;
+        T ytop = T(0);
+        auto step = [&](int q, uint32_t tq, T x) {
+            while (pend && (uint64_t)(tq - tf) > within_u) {  // expireEvents: the expired prefix
+                pend &= pend - 1;
+                if (pend) tf = s_ts[sw(p0 + __builtin_ctz(pend))];
+            }
+            if (stack) {
+                while (pend && (left ? cmp_m(m, x, ytop) : cmp_m(m, ytop, x))) {
+                    const int tp = 31 - __builtin_clz(pend);
+                    s_res[sw(p0 + tp)] = (uint16_t)q;
+                    pend &= ~(1u << tp);
+                    if (pend) ytop = xval(s_x[sw(p0 + 31 - __builtin_clz(pend))]);
+                }
+            } else if (pend && (left ? cmp_m(m, x, kc) : cmp_m(m, kc, x))) {
+                for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = (uint16_t)q;
+            }
+        };
+        const int pe = min(p0 + FU_DQ, own);  // (FU_OWN is a multiple of FU_DQ: a chunk is all own rows or none)
+        uint32_t cur = p0 < own ? (s_key[sw(p0)] & SV_KEY) : 0u;
+        for (int q = p0; q < pe; ++q) {
+            const uint32_t kq = s_key[sw(q)];
+            if ((kq & SV_KEY) != cur) {  // the previous key's run ended inside the chunk: its partials are carried
+                for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = R_CARRY;
+                cur = kq & SV_KEY;
+            }
+            if (kq & SV_CARRIED) continue;  // a carried partial: resolved by its forward scan below
+            const uint32_t tq = s_ts[sw(q)];
+            const int64_t xr = s_x[sw(q)];
+            const T x = xval(xr);
+            step(q, tq, x);
+            if (c0_at(q, xr, x) && (!stack || x == x)) {  // e1: visible from the next row on
+                if (!pend) tf = tq;
+                pend |= 1u << (q - p0);
+                ytop = x;
+            }
+        }
+        // continuation over the key's following positions until the deque drains
+        int q = pe;
+        for (; pend && q < nr && (s_key[sw(q)] & SV_KEY) == cur; ++q) step(q, s_ts[sw(q)], xval(s_x[sw(q)]));
+        if (pend) {
+            const uint16_t rr = off_res(q, cur);
+            for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = rr;
+        }
+    }
+    // ---- forward scans: carried partials (and every candidate without a deque mode) -------------------------
+#pragma unroll 1
+    for (int k = 0; k < FU_PT; ++k) {
+        const int pos = k * FU_THREADS + t;
+        if (pos >= own) continue;
+        const uint32_t kp = s_key[sw(pos)];
+        const bool carried = (kp & SV_CARRIED) != 0;
+        if (!carried && a.fu_mode != DQ_OFF) continue;
+        const int64_t xr = s_x[sw(pos)];
+        const T xv = xval(xr);
+        if (!carried && !c0_at(pos, xr, xv)) continue;
+        T y = kc;
+        CmpMask mm = m;
+        if (stream_e1) {
+            if (e1_is_x) {
+                y = xv;
+            } else {
+                const int64_t p = lo + pos;
+                if (a.nulls[sp.e1_col] && a.nulls[sp.e1_col][p]) mm = CmpMask{false, false, false, false};
+                y = C::get(cvt(load_col(a.cols[sp.e1_col], sp.e1_col_kind, p), sp.e1_col_kind, (uint8_t)K));
+            }
+        }
+        const uint32_t t0 = s_ts[sw(pos)];
+        uint16_t out = R_NONE;
+        int q = pos + 1;
+        for (; q < nr; ++q) {
+            const uint32_t kq = s_key[sw(q)];
+            if ((kq & SV_KEY) != (kp & SV_KEY)) break;
+            if (kq & SV_CARRIED) continue;  // another carried partial: not an event
+            if ((uint64_t)(s_ts[sw(q)] - t0) > within_u) { out = R_NONE; q = -1; break; }  // isExpired: dead
+            const T x = xval(s_x[sw(q)]);
+            if (left ? cmp_m(mm, x, y) : cmp_m(mm, y, x)) { out = (uint16_t)q; q = -1; break; }
+        }
+        if (q >= 0) out = off_res(q, kp);
+        s_res[sw(pos)] = out;
+    }
+    __syncthreads();
+    // ---- counts, one reservation per block and counter ----------------------------------------------------
+    uint32_t res[FU_PT];
+    const uint64_t lt = lanemask_lt();
+#pragma unroll
+    for (int k = 0; k < FU_PT; ++k) {
+        const int pos = k * FU_THREADS + t;
+        const uint16_t r16 = pos < own ? s_res[sw(pos)] : R_NONE;
+        const uint32_t out = r16 == R_NONE ? MQ_NONE : r16 == R_CARRY ? MQ_CARRY : r16 == R_OVF ? MQ_OVF : (uint32_t)r16;
+        res[k] = out;
+        const uint64_t bm = __ballot(out < MQ_OVF), bc = __ballot(out == MQ_CARRY), bo = __ballot(out == MQ_OVF);
+        if (lane == 0) {
+            wcnt[0][k][w] = (uint32_t)__popcll(bm);
+            wcnt[1][k][w] = (uint32_t)__popcll(bc);
+            wcnt[2][k][w] = (uint32_t)__popcll(bo);
+        }
+    }
+    __syncthreads();
+    if (t < 3) {
+        uint32_t run = 0;
+        for (int k = 0; k < FU_PT; ++k)
+            for (int x = 0; x < NW; ++x) {
+                const uint32_t c = wcnt[t][k][x];
+                wcnt[t][k][x] = run;
+                run += c;
+            }
+        unsigned long long* ctr = t == 0 ? a.out_count : t == 1 ? a.carry_count : a.ovf_count;
+        bbase[t] = run ? atomicAdd(ctr, (unsigned long long)run) : 0ull;
+    }
+    __syncthreads();
+    // ---- emit matches (loads of a group of rounds, then its stores: see chain_fused_k) ---------------------
+    constexpr uint32_t NOSLOT = 0xFFFFFFFFu;
+    uint32_t slot[FU_PT];
+    bool any_co = false;
+#pragma unroll
+    for (int k = 0; k < FU_PT; ++k) {
+        const uint32_t out = res[k];
+        const uint64_t bm = __ballot(out < MQ_OVF);
+        slot[k] = NOSLOT;
+        any_co |= out == MQ_CARRY || out == MQ_OVF;
+        if (out < MQ_OVF) {
+            const uint64_t sl = bbase[0] + wcnt[0][k][w] + (uint32_t)__popcll(bm & lt);
+            if (sl >= (uint64_t)a.out_cap) atomicOr(&a.flags[0], 1);
+            else slot[k] = (uint32_t)sl;
+        }
+    }
+    const int n_out = sp.n_out;
+    Instr in0 = {}, in1 = {};
+    if (n_out >= 1) in0 = load_instr(&sp.out_ins[0]);
+    if (n_out >= 2) in1 = load_instr(&sp.out_ins[1]);
+    auto plain8 = [&](const Instr& in) {
+        return (in.c == 0 || in.c == -1) && in.a < 2 && (in.k == VK_I64 || in.k == VK_F64) && !a.nulls[in.b];
+    };
+    const bool fast = n_out <= 2 && (n_out < 1 || plain8(in0)) && (n_out < 2 || plain8(in1));
+    const int jfrom = fast ? n_out : 0;
+    {
+        const int64_t* c0p = n_out >= 1 ? (const int64_t*)a.cols[in0.b] : nullptr;
+        const int64_t* c1p = n_out >= 2 ? (const int64_t*)a.cols[in1.b] : nullptr;
+        int64_t* const ov0 = a.out_vals;
+        int64_t* const ov1 = a.out_vals + a.out_cap;
+        constexpr int EH = 2;
+#pragma unroll
+        for (int h = 0; h < FU_PT; h += EH) {
+            uint32_t op[EH], oq[EH];
+            int64_t v0[EH], v1[EH];
+#pragma unroll
+            for (int i = 0; i < EH; ++i) {
+                const int k = h + i;
+                if (slot[k] != NOSLOT) {
+                    const int pos = k * FU_THREADS + t;
+                    op[i] = a.orig[lo + pos];
+                    oq[i] = a.orig[lo + res[k]];
+                    if (fast && n_out >= 1) v0[i] = c0p[lo + (in0.a == 0 ? pos : (int)res[k])];
+                    if (fast && n_out >= 2) v1[i] = c1p[lo + (in1.a == 0 ? pos : (int)res[k])];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < EH; ++i) {
+                const int k = h + i;
+                if (slot[k] != NOSLOT) {
+                    a.out_ts[slot[k]] = tbase + (int64_t)s_ts[sw(res[k])];
+                    a.out_emit_seq[slot[k]] = a.seq_base + (int64_t)oq[i];
+                    a.out_first_seq[slot[k]] = sv_seq(a, op[i]);
+                    if (fast && n_out >= 1) ov0[slot[k]] = v0[i];
+                    if (fast && n_out >= 2) ov1[slot[k]] = v1[i];
+                }
+            }
+        }
+    }
+    uint32_t nm[FU_PT];
+#pragma unroll
+    for (int k = 0; k < FU_PT; ++k) nm[k] = 0;
+    for (int j = jfrom; j < n_out; ++j) {
+        const Instr in = load_instr(&sp.out_ins[j]);
+        const bool ok = (in.c == 0 || in.c == -1) && in.a < 2;
+        const void* cp = a.cols[in.b];
+        const uint8_t* np = a.nulls[in.b];
+        int64_t* const ov = a.out_vals + (int64_t)j * a.out_cap;
+#pragma unroll
+        for (int k = 0; k < FU_PT; ++k) {
+            if (slot[k] == NOSLOT) continue;
+            const int64_t r = lo + (in.a == 0 ? k * FU_THREADS + t : (int)res[k]);
+            ov[slot[k]] = ok ? load_col(cp, in.k, r) : 0;
+            if (!ok || (np && np[r])) nm[k] |= 1u << j;
+        }
+    }
+    if (a.write_nulls) {
+#pragma unroll
+        for (int k = 0; k < FU_PT; ++k)
+            if (slot[k] != NOSLOT) a.out_nulls[slot[k]] = nm[k];
+    }
+    // ---- carries / overflow rows --------------------------------------------------------------------------
+    if (__ballot(any_co) == 0) return;  // wave-uniform
+#pragma unroll 1
+    for (int k = 0; k < FU_PT; ++k) {
+        const uint32_t out = res[k];
+        const uint64_t bc = __ballot(out == MQ_CARRY), bo = __ballot(out == MQ_OVF);
+        if (out != MQ_CARRY && out != MQ_OVF) continue;
+        const int64_t p = lo + k * FU_THREADS + t;
+        if (out == MQ_CARRY) {
+            const int64_t cs = (int64_t)bbase[1] + wcnt[1][k][w] + __popcll(bc & lt);
+            if (cs >= a.carry_cap) atomicOr(&a.flags[0], 1);
+            else emit_carry(a, View{}, cs, p, a.key[p] & SV_KEY, sv_seq(a, a.orig[p]));
+        } else {
+            const int64_t os = (int64_t)bbase[2] + wcnt[2][k][w] + __popcll(bo & lt);
+            if (os < a.n) a.ovf_rows[os] = (uint32_t)p;
+        }
+    }
+}
+
+// sorted view: partials whose key's run continues past the staged rows of their block. One wave per partial
+// (CW_PER_WAVE per wave) scans the run's remaining rows 64 at a time; the block then emits the matches and carries.
+template <int K>
+__device__ int64_t sv_wave_scan(const ChainArgs& a, int64_t p, uint32_t kp, int64_t ts0, int64_t k, uint8_t op) {
+    using C = KT<K>;
+    const typename C::T y = C::get(k);
+    const ChainSpec& sp = a.sp;
+    const int col = sp.scan_col;
+    const uint8_t kind = sp.scan_col_kind;
+    const bool left = sp.scan_e2_left, always = op == OP_ALWAYS;
+    const uint64_t within_u = sp.has_within ? (uint64_t)sp.within_ms : ~0ull;
+    const CmpMask m = cmp_mask(op);
+    const int lane = lane_id();
+    for (int64_t q0 = p + 1; q0 < a.n; q0 += 64) {
+        const int64_t q = q0 + lane;
+        bool stop = false, hit = false, end = false;
+        if (q >= a.n || (a.key[q] & SV_KEY) != kp) {
+            end = true;  // the key's rows of this batch end: carried
+        } else if (!(a.fold && (a.orig[q] & SV_CARRIED))) {
+            if ((uint64_t)(a.ts[q] - ts0) > within_u) stop = true;  // isExpired at this event of the key
+            else if (always) hit = true;
+            else hit = left ? cmp_m(m, C::get(cvt(load_col(a.cols[col], kind, q), kind, (uint8_t)K)), y)
+                            : cmp_m(m, y, C::get(cvt(load_col(a.cols[col], kind, q), kind, (uint8_t)K)));
+        }
+        const uint64_t bh = __ballot(hit), bs = __ballot(stop), be = __ballot(end);
+        const uint64_t any = bh | bs | be;
+        if (any) {
+            const int l = __ffsll((unsigned long long)any) - 1;
+            return ((bh >> l) & 1u) ? q0 + l : ((bs >> l) & 1u) ? -1 : -2;
+        }
+    }
+    return -2;
+}
+
+__global__ __launch_bounds__(256, 8) void chain_sovf_k(const ChainArgs* __restrict__ pa) {
+    const ChainArgs& a = *pa;
+    const ChainSpec& sp = a.sp;
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const int64_t total = (int64_t)*a.ovf_count;
+    // grid-stride over groups of 4 x CW_PER_WAVE partials (block-uniform bounds: block_reserve2 needs every thread)
+    for (int64_t g0 = (int64_t)blockIdx.x * 4 * CW_PER_WAVE; g0 < total; g0 += (int64_t)gridDim.x * 4 * CW_PER_WAVE) {
+        const int64_t c_base = g0 + (int64_t)w * CW_PER_WAVE;
+        int64_t mine = -1;
+        for (int i = 0; i < CW_PER_WAVE; ++i) {
+            const int64_t c = c_base + i;
+            if (c >= total) break;  // wave-uniform
+            const int64_t p = a.ovf_rows[c];
+            const uint32_t kp = a.key[p] & SV_KEY;
+            int64_t k = sp.scan_konst;
+            uint8_t op = sp.scan_op;
+            if (sp.scan_mode == SCAN_TRUE) {
+                op = OP_ALWAYS;
+            } else if (sp.scan_mode == SCAN_E1) {
+                if (a.nulls[sp.e1_col] && a.nulls[sp.e1_col][p]) op = OP_NEVER;
+                else k = cvt(load_col(a.cols[sp.e1_col], sp.e1_col_kind, p), sp.e1_col_kind, sp.scan_t);
+            }
+            int64_t r;
+            switch (sp.scan_t) {
+                case VK_I32: r = sv_wave_scan<VK_I32>(a, p, kp, a.ts[p], k, op); break;
+                case VK_I64: r = sv_wave_scan<VK_I64>(a, p, kp, a.ts[p], k, op); break;
+                case VK_F32: r = sv_wave_scan<VK_F32>(a, p, kp, a.ts[p], k, op); break;
+                case VK_F64: r = sv_wave_scan<VK_F64>(a, p, kp, a.ts[p], k, op); break;
+                case VK_BOOL: r = sv_wave_scan<VK_BOOL>(a, p, kp, a.ts[p], k, op); break;
+                default: r = sv_wave_scan<VK_STR>(a, p, kp, a.ts[p], k, op); break;
+            }
+            if (lane == i) mine = r;
+        }
+        const int64_t c = c_base + lane;
+        const bool valid = lane < CW_PER_WAVE && c < total;
+        const bool has = valid && mine >= 0, carry = valid && mine == -2;
+        int64_t slot, cs;
+        block_reserve2<256>(has, carry, a.out_count, a.carry_count, &slot, &cs);
+        if (valid) {
+            const int64_t p = a.ovf_rows[c];
+            if (has) {
+                if (slot >= a.out_cap) {
+                    atomicOr(&a.flags[0], 1);
+                } else {
+                    ChainAcc acc{&a, View{}, p, -1, -1};
+                    emit_match<false>(a, acc, slot, mine, a.key[p] & SV_KEY, sv_seq(a, a.orig[p]), nullptr, 0);
+                }
+            }
+            if (carry) {
+                if (cs >= a.carry_cap) atomicOr(&a.flags[0], 1);
+                else emit_carry(a, View{}, cs, p, a.key[p] & SV_KEY, sv_seq(a, a.orig[p]));
+            }
+        }
+        __syncthreads();  // block_reserve2's shared words are reused by the next group
+    }
+}
+
 void chain_match(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
     if (a.n <= 0) return;
     const dim3 grid((unsigned)((a.n + CM_TILE - 1) / CM_TILE));
@@ -1489,6 +1929,32 @@ void chain_fused(const ChainArgs& a, const ChainArgs* d_a, int64_t grid, hipStre
         default: FU_LAUNCH(VK_STR); break;
     }
 #undef FU_LAUNCH
+}
+
+void chain_sorted(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
+    if (a.n <= 0) return;
+    const int64_t grid = ((a.n + FU_OWN - 1) / FU_OWN + 7) / 8 * 8;  // rounded for the XCD remap
+    const dim3 g((unsigned)grid), b(FU_THREADS);
+    const bool same = a.sp.scan_col_kind == a.sp.scan_t;
+#define SV_LAUNCH(KK)                                                                    \
+    do {                                                                                 \
+        if (same) hipLaunchKernelGGL((chain_sorted_k<KK, true>), g, b, 0, stream, d_a);  \
+        else hipLaunchKernelGGL((chain_sorted_k<KK, false>), g, b, 0, stream, d_a);     \
+    } while (0)
+    switch (a.sp.scan_t) {
+        case VK_I32: SV_LAUNCH(VK_I32); break;
+        case VK_I64: SV_LAUNCH(VK_I64); break;
+        case VK_F32: SV_LAUNCH(VK_F32); break;
+        case VK_F64: SV_LAUNCH(VK_F64); break;
+        case VK_BOOL: SV_LAUNCH(VK_BOOL); break;
+        default: SV_LAUNCH(VK_STR); break;
+    }
+#undef SV_LAUNCH
+}
+
+void chain_sovf(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
+    if (a.n <= 0) return;
+    hipLaunchKernelGGL(chain_sovf_k, dim3(2048), dim3(256), 0, stream, d_a);  // grid-stride over ovf_count
 }
 
 void chain_fovf(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {

@@ -53,6 +53,13 @@ struct KeyGroupArgs {
     int32_t ts32_col = -1;
     const int64_t* ts_base = nullptr;
     uint8_t* lkey_out = nullptr;
+    // prefix rows (keygroup, the sorted-view matcher's folded carries): rows [0, pre_n) of the input are read from
+    // pre_keys / pre_src (8-byte slots per row; a narrower column takes the slot's low bytes), rows [pre_n, n) from
+    // keys / src; a prefix row's orig is 0x80000000 | its index. n counts both
+    int64_t pre_n = 0;
+    const uint32_t* pre_keys = nullptr;
+    const void* pre_src[MAX_COLS + 2] = {};
+    int32_t no_segments = 0;          // keygroup: skip seg_start / seg_end (the sorted-view matcher finds runs by key)
 };
 // bytes of workspace for n events; fills the workspace pointers of `a` from `base`
 size_t keygroup_workspace(int64_t n, int32_t K, int32_t ncols, const uint8_t* widths);
@@ -183,6 +190,8 @@ struct ChainArgs {
     int32_t fu_mode;                  // chain_fused_k: DQ_STACK / DQ_ALL -> chunked deque pass, DQ_OFF -> forward scans
     int32_t fu_skip;                  // SDG_FU_SKIP (phase timing only, results invalid): 1 scan, 2 emit, 4 stop
                                       // after the loads, 8 stop after the LDS regrouping
+    int32_t fold;                     // chain_sorted_k: the carried partials are rows of the sorted view (orig =
+                                      // 0x80000000 | carry index; keygroup's prefix rows), no chain_carry pass
 };
 enum DequeMode : int32_t { DQ_OFF = 0, DQ_STACK = 1, DQ_ALL = 2 };
 constexpr uint32_t MQ_NONE = 0xFFFFFFFFu, MQ_CARRY = 0xFFFFFFFEu, MQ_OVF = 0xFFFFFFFDu;
@@ -196,6 +205,10 @@ void chain_deque(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
 // kernel arguments are read from a device copy (d_a) of `a`: the struct is too large to index as a kernarg
 void chain_match(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
 void chain_carry(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
+// sorted-view matcher (radix path): LDS-staged blocks of FU_ROWS sorted rows, chunked deque + forward scans, matches
+// emitted in the kernel; chain_sovf then resolves the partials whose key continues past their block's staged rows
+void chain_sorted(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
+void chain_sovf(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
 
 // ---- fused bucket matcher -------------------------------------------------------------------------------
 // One block per segment of FU_OWN rows of one bucket: the segment plus FU_HALO following rows of the bucket

@@ -24,18 +24,20 @@ __device__ __forceinline__ uint32_t digit_of(uint32_t k, int shift, uint32_t mas
 // per-tile digit histogram: counts[tile * nb + d]
 // kcheck (first pass only): keys >= K (device-resident batches whose ids did not come from this engine) set
 // *kflag; every later kernel masks its key-derived indices, so such a batch fails the flush without a fault
+// prefix rows (keygroup's pre_n): rows [0, pre_n) take their keys from pre_keys, the rest from keys[i - pre_n]
 template <int RX_TILE, int RX_THREADS>
 __global__ __launch_bounds__(RX_THREADS) void rx_hist(const uint32_t* __restrict__ keys, int64_t n, int shift,
                                                       uint32_t mask, int nb, uint32_t* __restrict__ counts,
-                                                      uint32_t kcheck, int* __restrict__ kflag) {
+                                                      uint32_t kcheck, int* __restrict__ kflag,
+                                                      const uint32_t* __restrict__ pre_keys, int64_t pre_n) {
     __shared__ uint32_t h[1 << RX_MAXBITS];
     for (int d = threadIdx.x; d < nb; d += RX_THREADS) h[d] = 0;
     __syncthreads();
     int64_t base = (int64_t)blockIdx.x * RX_TILE;
-    if (base + RX_TILE <= n && (((uintptr_t)(keys + base)) & 15) == 0) {
+    if (base + RX_TILE <= n && base >= pre_n && (((uintptr_t)(keys + base - pre_n)) & 15) == 0) {
         // full, 16-B aligned tile: 4 keys per load, every load of the thread in flight before the atomics
         constexpr int V = RX_TILE / RX_THREADS / 4;
-        const uint4* kv = reinterpret_cast<const uint4*>(keys + base);
+        const uint4* kv = reinterpret_cast<const uint4*>(keys + base - pre_n);
         uint4 x[V];
 #pragma unroll
         for (int r = 0; r < V; ++r) x[r] = kv[r * RX_THREADS + threadIdx.x];
@@ -52,7 +54,7 @@ __global__ __launch_bounds__(RX_THREADS) void rx_hist(const uint32_t* __restrict
         for (int r = 0; r < RX_TILE / RX_THREADS; ++r) {
             int64_t i = base + r * RX_THREADS + threadIdx.x;
             if (i < n) {
-                const uint32_t k = keys[i];
+                const uint32_t k = i < pre_n ? pre_keys[i] : keys[i - pre_n];
                 if (kcheck && k >= kcheck) *kflag = 1;
                 atomicAdd(&h[digit_of(k, shift, mask)], 1u);
             }
@@ -161,6 +163,9 @@ struct RxPass {
     int lkey_shift;
     int ntiles;               // tiles; the grid is rounded up to a multiple of 8 (XCD remap)
     int xcd;                  // 1: XCD-aware tile order
+    int64_t pre_n;            // first pass only: prefix rows [0, pre_n) from pre_keys / pre_src (8-byte slots), the
+    const uint32_t* pre_keys; // others from keys_in / src at i - pre_n; a prefix row's orig is 0x80000000 | i
+    const void* pre_src[MAX_COLS + 2];
 };
 
 // stable tile scatter. Tile element e = w * 1024 + r * 64 + lane belongs to wave w (16 rounds r), so a wave
@@ -171,7 +176,7 @@ struct RxPass {
 // Tiles: 8192 rows x 512 threads (2 blocks per CU) or 16384 x 1024 (one block per CU, 154 KB of LDS): both 4
 // waves/SIMD and 16 rows per lane; the larger tile doubles the average bucket run each tile writes (a 256-bucket
 // pass writes runs of 64 rows instead of 32: fewer partial cache lines for the u8 / u32 columns).
-template <int RX_TILE, int RX_THREADS>
+template <int RX_TILE, int RX_THREADS, bool PRE>
 __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
     constexpr int R = RX_TILE / RX_THREADS;  // 16 elements per lane
     constexpr int NW = RX_THREADS / 64;
@@ -204,7 +209,7 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int64_t i = wbase + r * 64 + lane;
-        kreg[r] = i < a.n ? a.keys_in[i] : 0u;
+        kreg[r] = i < a.n ? (PRE && i < a.pre_n ? a.pre_keys[i] : a.keys_in[i - (PRE ? a.pre_n : 0)]) : 0u;
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -268,10 +273,13 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
         for (int r = 0; r < R; ++r) {
             const int64_t i = wbase + r * 64 + lane;
             uint64_t x = 0;
-            if (i < a.n) {
-                if (wd == 8) x = ((const uint64_t*)src)[i];
-                else if (wd == 4) x = ((const uint32_t*)src)[i];
-                else x = ((const uint8_t*)src)[i];
+            if (PRE && i < a.pre_n) {
+                x = ((const uint64_t*)a.pre_src[c])[i];  // an 8-byte slot: the store keeps the column's low bytes
+            } else if (i < a.n) {
+                const int64_t j = i - (PRE ? a.pre_n : 0);
+                if (wd == 8) x = ((const uint64_t*)src)[j];
+                else if (wd == 4) x = ((const uint32_t*)src)[j];
+                else x = ((const uint8_t*)src)[j];
             }
             v[r] = x;
         }
@@ -280,7 +288,11 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int64_t i = wbase + r * 64 + lane;
-        cur[r] = (uint64_t)kreg[r] | ((uint64_t)(a.orig_in ? (i < a.n ? a.orig_in[i] : 0u) : (uint32_t)i) << 32);
+        uint32_t o;
+        if (PRE && i < a.pre_n) o = 0x80000000u | (uint32_t)i;
+        else if (a.orig_in) o = i < a.n ? a.orig_in[i - (PRE ? a.pre_n : 0)] : 0u;
+        else o = (uint32_t)(i - (PRE ? a.pre_n : 0));
+        cur[r] = (uint64_t)kreg[r] | ((uint64_t)o << 32);
     }
     for (int c = -1; c < a.ncols; ++c) {
 #pragma unroll
@@ -652,24 +664,32 @@ static int rx_tile() {
 }
 static int64_t rx_ntiles(int64_t n, int tile = RX_TILE) { return n <= 0 ? 1 : (n + tile - 1) / tile; }
 static void launch_rx_hist(int64_t nt, hipStream_t stream, const uint32_t* keys, int64_t n, int shift, uint32_t mask,
-                           int nb, uint32_t* counts, uint32_t kcheck, int* kflag) {
+                           int nb, uint32_t* counts, uint32_t kcheck, int* kflag, const uint32_t* pre_keys = nullptr,
+                           int64_t pre_n = 0) {
     if (rx_tile() == RX_TILE_BIG)
         hipLaunchKernelGGL((rx_hist<RX_TILE_BIG, RX_THREADS_BIG>), dim3((unsigned)nt), dim3(RX_THREADS_BIG), 0, stream,
-                           keys, n, shift, mask, nb, counts, kcheck, kflag);
+                           keys, n, shift, mask, nb, counts, kcheck, kflag, pre_keys, pre_n);
     else
         hipLaunchKernelGGL((rx_hist<RX_TILE, RX_THREADS>), dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, keys, n,
-                           shift, mask, nb, counts, kcheck, kflag);
+                           shift, mask, nb, counts, kcheck, kflag, pre_keys, pre_n);
 }
 static void launch_rx_scatter(int64_t nt, hipStream_t stream, RxPass rp) {
     static const bool no_xcd = getenv("SDG_RX_NOXCD") != nullptr;  // A/B: tiles in block order
     rp.ntiles = (int)nt;
     rp.xcd = !no_xcd;
     const int64_t grid = no_xcd ? nt : (nt + 7) / 8 * 8;
-    if (rx_tile() == RX_TILE_BIG)
-        hipLaunchKernelGGL((rx_scatter<RX_TILE_BIG, RX_THREADS_BIG>), dim3((unsigned)grid), dim3(RX_THREADS_BIG), 0,
+    if (rp.pre_n > 0) {  // (the large tile only: prefix rows exist on the sorted-view path alone)
+        if (rx_tile() == RX_TILE_BIG)
+            hipLaunchKernelGGL((rx_scatter<RX_TILE_BIG, RX_THREADS_BIG, true>), dim3((unsigned)grid), dim3(RX_THREADS_BIG),
+                               0, stream, rp);
+        else
+            hipLaunchKernelGGL((rx_scatter<RX_TILE, RX_THREADS, true>), dim3((unsigned)grid), dim3(RX_THREADS), 0, stream, rp);
+    } else if (rx_tile() == RX_TILE_BIG) {
+        hipLaunchKernelGGL((rx_scatter<RX_TILE_BIG, RX_THREADS_BIG, false>), dim3((unsigned)grid), dim3(RX_THREADS_BIG), 0,
                            stream, rp);
-    else
-        hipLaunchKernelGGL((rx_scatter<RX_TILE, RX_THREADS>), dim3((unsigned)grid), dim3(RX_THREADS), 0, stream, rp);
+    } else {
+        hipLaunchKernelGGL((rx_scatter<RX_TILE, RX_THREADS, false>), dim3((unsigned)grid), dim3(RX_THREADS), 0, stream, rp);
+    }
 }
 
 size_t keygroup_workspace(int64_t n, int32_t K, int32_t ncols, const uint8_t* widths) {
@@ -717,7 +737,7 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
         const uint32_t* kin = p == 0 ? a.keys : a.tmp_keys[(p - 1) & 1];
         bool last = p == npass - 1;
         launch_rx_hist(nt, stream, kin, a.n, shift, mask, nb, a.counts, p == 0 && a.key_flag ? (uint32_t)a.K : 0u,
-                       a.key_flag);
+                       a.key_flag, p == 0 ? a.pre_keys : nullptr, p == 0 ? a.pre_n : 0);
         int64_t gk = (int64_t)ng * nb;
         hipLaunchKernelGGL(rx_p1, dim3((unsigned)((gk + 255) / 256)), dim3(256), 0, stream, a.counts, (int)nt, nb, a.gsum);
         hipLaunchKernelGGL(rx_p2, dim3(1), dim3(256), 0, stream, a.gsum, ng, nb, a.tot);
@@ -744,13 +764,20 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
         rp.bits = b;
         rp.mono_col = -1;
         rp.ts32_col = -1;
+        if (p == 0 && a.pre_n > 0) {
+            rp.pre_n = a.pre_n;
+            rp.pre_keys = a.pre_keys;
+            for (int c = 0; c < a.ncols; ++c) rp.pre_src[c] = a.pre_src[c];
+        }
         launch_rx_scatter(nt, stream, rp);
     }
     if (marks) (void)hipEventRecord(marks[2], stream);
-    (void)hipMemsetAsync(a.seg_start, 0, (size_t)a.K * 4, stream);
-    (void)hipMemsetAsync(a.seg_end, 0, (size_t)a.K * 4, stream);
-    hipLaunchKernelGGL(rx_segments, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, stream, a.keys_sorted, a.n,
-                       (uint32_t)a.K, a.seg_start, a.seg_end);
+    if (!a.no_segments) {
+        (void)hipMemsetAsync(a.seg_start, 0, (size_t)a.K * 4, stream);
+        (void)hipMemsetAsync(a.seg_end, 0, (size_t)a.K * 4, stream);
+        hipLaunchKernelGGL(rx_segments, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, stream, a.keys_sorted, a.n,
+                           (uint32_t)a.K, a.seg_start, a.seg_end);
+    }
     if (marks) (void)hipEventRecord(marks[3], stream);
 }
 

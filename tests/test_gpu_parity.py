@@ -303,10 +303,14 @@ def test_generic_nfa_many_keys_on_gpu(seq3, oracle_built):
 FUSED_SHAPES = {"gt", "ge", "lt", "le_flipped", "const", "no_filter", "ne_const", "cross_col"}
 
 
-@pytest.mark.parametrize("fused", [True, False])
+SORTED_SHAPES = FUSED_SHAPES | {"int_gt_nowithin"}  # the sorted-view matcher: typed scans, no nulls, any key count
+
+
+@pytest.mark.parametrize("path", ["fused", "sorted", "lane"])
 @pytest.mark.parametrize("name", sorted(synth.CHAIN_APPS))
 @pytest.mark.parametrize("shape", ["k5_b1", "k200_b4", "desc_b3", "nan_b2"])
-def test_chain_shapes_on_gpu(name, shape, fused, oracle_built):
+def test_chain_shapes_on_gpu(name, shape, path, oracle_built):
+    fused = path == "fused"
     app, deque = synth.CHAIN_APPS[name]
     seed = zlib.crc32((name + shape).encode()) % 1000
     if shape == "k5_b1":
@@ -322,13 +326,15 @@ def test_chain_shapes_on_gpu(name, shape, fused, oracle_built):
         ref = synth.run(o, tr)
     finally:
         o.close()
-    p = ProductAdapter(app, fused=fused)
+    p = ProductAdapter(app, fused=fused, sorted_view=path != "lane")
     try:
         assert p.rt.query_paths() == [0]
         got = synth.run(p, tr, batches)
         st = p.rt.stats()
         if not fused:
             assert st.fused == 0 and st.deque == deque
+            # the sorted-view matcher (nan_b2: null prices -> the lane kernels)
+            assert st.sorted_view == (path == "sorted" and name in SORTED_SHAPES and shape != "nan_b2")
         elif name in FUSED_SHAPES and shape != "nan_b2":  # nan_b2: nulls in the scanned column -> radix path
             assert st.fused == 1
     finally:
@@ -451,26 +457,31 @@ def test_c2_bench_regime_vs_oracle(flushes, oracle_built):
     assert np.all(np.diff(gseq) >= 0)  # delivery order: by emitting event
 
 
-def test_radix_path_million_keys_vs_oracle(oracle_built):
+@pytest.mark.parametrize("sorted_view", [True, False])
+def test_radix_path_million_keys_vs_oracle(sorted_view, oracle_built):
     """C2's query over 2^20 long partition keys (past the fused path's 2^16: the full radix key sort + chain
-    kernels), 3M events in two batches at a rate that puts each key's ~3 events inside one window; every match
-    against the oracle, in delivery order"""
+    kernels), 3M events in three batches at a rate that puts each key's ~3 events inside one window; every match
+    against the oracle, in delivery order. sorted_view: the LDS-staged sorted-view matcher with the carried partials
+    folded into the key sort (else the lane deque kernels + the carry pass)"""
     keys = 1 << 20
     n = 3_000_000
     app = ("@app:playback define stream S (id long, key long, price double, volume int); partition with (key of S) "
            "begin @info(name = 'query1') from every e1=S[price>20] -> e2=S[price>e1.price] within 1 sec "
            "select e1.id as e1id, e2.id as e2id insert into M; end;")
     cols = w.c2_columns(n, keys=keys, per_ms=20_000)
-    rt = sa.SiddhiAppRuntime(app)
+    rt = sa.SiddhiAppRuntime(app, sorted_view=sorted_view)
+    carried = 0
     try:
         assert rt.query_paths() == [0]
         h = rt.getInputHandler("S")
         parts = []
-        for lo, hi in ((0, n // 2), (n // 2, n)):
+        for lo, hi in ((0, n // 3), (n // 3, 2 * n // 3), (2 * n // 3, n)):
             h.send_columns(cols["ts"][lo:hi], [cols["id"][lo:hi], cols["key"][lo:hi], cols["price"][lo:hi],
                                               cols["volume"][lo:hi]])
             rt.flush(deliver=False)
-            assert rt.stats().fused == 0 and rt.stats().path == 0
+            st = rt.stats()
+            assert st.fused == 0 and st.path == 0 and st.sorted_view == sorted_view
+            carried += st.carry_in
             parts.append(rt.poll_arrays(0))
     finally:
         rt.shutdown()
@@ -478,7 +489,7 @@ def test_radix_path_million_keys_vs_oracle(oracle_built):
     gvals = np.concatenate([p[1] for p in parts], axis=1)
     ots, ovals, _ = oracle_batch_rows(app, "S", cols["ts"], [cols["id"], cols["key"], cols["price"].view(np.int64),
                                                               cols["volume"]], 2)
-    assert len(ots) > 300_000
+    assert len(ots) > 300_000 and carried > 10_000
     assert np.array_equal(gts, ots) and np.array_equal(gvals.T, ovals)
 
 
