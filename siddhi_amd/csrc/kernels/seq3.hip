@@ -104,8 +104,52 @@ __device__ __forceinline__ bool s3_pass(const S3Pred& f, const S3Ev<NC>& e1, con
                                                                      (f.kind == FP_CONST ? 1u << 16 : 0u), x, z);
 }
 
-template <int NC, int S3_G, bool F64, bool SEL>
-__global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
+// Per-query specialisation: a predicate's operands as compile-time codes (src * 8 + col; -1: FP_TRUE for the first
+// operand / the constant for the second; -2: resolved at run time by s3_get). With fixed codes an operand is one
+// register (no masked-OR pick over the columns, no per-operand source switch) -- the uniform operand dispatch was
+// most of the ~600 instructions per row. F64 only.
+template <int CODE, int NC>
+__device__ __forceinline__ int64_t s3_fx(const S3Ev<NC>& e1, const S3Ev<NC>& ef, const S3Ev<NC>& el, const S3Ev<NC>& y) {
+    constexpr int src = CODE / 8, c = CODE % 8;
+    static_assert(c < NC, "operand column");
+    if constexpr (src == S3_E1) return e1.v[c];
+    else if constexpr (src == S3_E2F) return ef.v[c];
+    else if constexpr (src == S3_E2L) return el.v[c];
+    else return y.v[c];
+}
+template <int CODE>
+__device__ __forceinline__ bool s3_fx_null(uint32_t nm, uint32_t yn) {
+    constexpr int src = CODE / 8, c = CODE % 8;
+    if constexpr (src == S3_E1) return (nm >> c) & 1u;
+    else if constexpr (src == S3_E2F) return (nm >> (8 + c)) & 1u;
+    else if constexpr (src == S3_E2L) return (nm >> (16 + c)) & 1u;
+    else return (yn >> c) & 1u;
+}
+template <bool F64, int FA, int FB, int NC>
+__device__ __forceinline__ bool s3_pass_x(const S3Pred& f, const S3Ev<NC>& e1, const S3Ev<NC>& ef, const S3Ev<NC>& el,
+                                          const S3Ev<NC>& y, uint32_t nm, uint32_t yn) {
+    if constexpr (FA == -2) {
+        return s3_pass<F64>(f, e1, ef, el, y, nm, yn);
+    } else if constexpr (FA == -1) {
+        return true;
+    } else {
+        static_assert(F64, "fixed operands: the double-compare variant");
+        if (s3_fx_null<FA>(nm, yn)) return false;
+        const int64_t x = s3_fx<FA>(e1, ef, el, y);
+        int64_t z;
+        if constexpr (FB == -1) {
+            z = f.konst;
+        } else {
+            if (s3_fx_null<FB>(nm, yn)) return false;
+            z = s3_fx<FB>(e1, ef, el, y);
+        }
+        return cmpT<double>(f.op, bits_f64(x), bits_f64(z));
+    }
+}
+
+template <int NC, int S3_G, bool F64, bool SEL, int FA0 = -2, int FA1 = -2, int FB1 = -2, int FA2 = -2, int FB2 = -2,
+          int W = 1>
+__global__ __launch_bounds__(64, W) void seq3_k(const Seq3Args* __restrict__ pa) {
     const Seq3Args& a = *pa;
     const Seq3Spec& sp = a.sp;
     extern __shared__ __align__(16) uint8_t s3_lds[];
@@ -199,7 +243,7 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
             hasQ = hasQ && (d < 0 ? -d : d) <= within;
         }
         // e3 (first in the receiver's order)
-        const bool em = hasP && s3_pass<F64>(sp.f[2], P1, PF, PL, y, pn, ynn);
+        const bool em = hasP && s3_pass_x<F64, FA2, FB2>(sp.f[2], P1, PF, PL, y, pn, ynn);
         const uint64_t m = __ballot(em);
         if (m) {
             if (em) {
@@ -225,7 +269,7 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
         const bool qfirst = cnt == 0;
         QF.set_if(qfirst, y);
         const uint32_t qn2 = qfirst ? ((qn & ~0xFF00u) | (ynn << 8)) : qn;
-        const bool adv = hasQ && !(em && same) && n1 >= mn && s3_pass<F64>(sp.f[1], Q1, QF, y, y, qn2, ynn);
+        const bool adv = hasQ && !(em && same) && n1 >= mn && s3_pass_x<F64, FA1, FB1>(sp.f[1], Q1, QF, y, y, qn2, ynn);
         const bool keep = adv && n1 != mx;  // kept at e2 too: one object
         const uint32_t pn2 = (qn2 & 0xFFFFu) | (ynn << 16);
         P1.set_if(adv, Q1);
@@ -235,7 +279,7 @@ __global__ __launch_bounds__(64) void seq3_k(const Seq3Args* __restrict__ pa) {
         pts = adv ? qts : pts;
         QL.set_if(keep, y);
         // e1: the every-seed starts a partial when e2's list is still empty
-        const bool fresh = act && !keep && s3_pass<F64>(sp.f[0], y, y, y, y, 0u, ynn);
+        const bool fresh = act && !keep && s3_pass_x<F64, FA0, -1>(sp.f[0], y, y, y, y, 0u, ynn);
         Q1.set_if(fresh, y);
         qts = fresh ? yt : qts;
         qn = fresh ? ynn : keep ? pn2 : qn;
@@ -395,6 +439,37 @@ void seq3_run(const Seq3Args& a, const Seq3Args* d_a, hipStream_t stream) {
         if (f.kind == FP_TRUE) continue;
         f64 &= f.t == VK_F64 && f.a.kind == VK_F64 && (f.kind == FP_CONST || f.b.kind == VK_F64);
     }
+    // the predicates' operand codes (s3_pass_x): a kernel compiled for them when the query is the C3 form
+    // (e1 = S[x > c], e2 = S[x > e1.x], e3 = S[x < e2[last].x] over a double column x, two columns)
+    auto code = [](const S3Operand& o) { return o.src < 0 ? -9 : (int)o.src * 8 + (int)o.col; };
+    const S3Pred &f0 = a.sp.f[0], &f1 = a.sp.f[1], &f2 = a.sp.f[2];
+    static const bool no_fix = getenv("SDG_S3_NOFIX") != nullptr;  // A/B: the run-time operand dispatch
+    int fx = -1;  // column of x in a C3-form query
+    if (f64 && sel && !no_fix && a.sp.nc == 2 && !g16 && f0.kind == FP_CONST && f1.kind == FP_SLOT && f2.kind == FP_SLOT) {
+        const int x = f0.a.col;
+        if (code(f0.a) == S3_Y * 8 + x && code(f1.a) == S3_Y * 8 + x && code(f1.b) == S3_E1 * 8 + x &&
+            code(f2.a) == S3_Y * 8 + x && code(f2.b) == S3_E2L * 8 + x && x < 2)
+            fx = x;
+    }
+    // waves per SIMD the fixed kernels are compiled for (A/B SDG_S3_W=3: <= 168 VGPRs instead of ~190)
+    static const char* ws = getenv("SDG_S3_W");
+    const bool w3 = ws && atoi(ws) == 3;
+#define S3_FIX(X)                                                                                                  \
+    do {                                                                                                           \
+        if (w3) hipLaunchKernelGGL((seq3_k<2, 8, true, true, S3_Y * 8 + X, S3_Y * 8 + X, S3_E1 * 8 + X, S3_Y * 8 + X,  \
+                                           S3_E2L * 8 + X, 3>), dim3(grid), dim3(64), lds, stream, d_a);            \
+        else hipLaunchKernelGGL((seq3_k<2, 8, true, true, S3_Y * 8 + X, S3_Y * 8 + X, S3_E1 * 8 + X, S3_Y * 8 + X,     \
+                                        S3_E2L * 8 + X, 1>), dim3(grid), dim3(64), lds, stream, d_a);               \
+    } while (0)
+    if (fx == 0) {
+        S3_FIX(0);
+        return;
+    }
+    if (fx == 1) {
+        S3_FIX(1);
+        return;
+    }
+#undef S3_FIX
 #define S3_LAUNCH(NC_, G_)                                                                              \
     do {                                                                                                \
         if (f64 && sel) hipLaunchKernelGGL((seq3_k<NC_, G_, true, true>), dim3(grid), dim3(64), lds, stream, d_a);  \
