@@ -206,7 +206,8 @@ typedef struct sdg_stats {
                                   scheduler simulation, log read-back and host replays between them */
     double ms_sched_host;      /* host ms: scheduler simulation passes, log read-back, host replays */
     int64_t arena_growths;     /* generic NFA: times a key ran out of partial-match slots and the arenas doubled
-                                  (the batch reran from its start; max_partials is the starting size, 4096 the cap) */
+                                  (the batch reran from its start; max_partials is the starting size, 4096 the
+                                  device cap -- a key past it spills to the host, spilled_keys) */
     int64_t carry_in;          /* chain path: partials carried into the last flush from the one before */
     int64_t carry_out;         /* chain path: partials the last flush carries into the next */
     int64_t arena_slots;       /* generic NFA: per-key arenas allocated after the last flush (queries summed); keys
@@ -215,7 +216,8 @@ typedef struct sdg_stats {
                                    optimistic pass's model changes, SchedSim::confirm) */
     int32_t sorted_view;       /* chain path: 1 the LDS-staged sorted-view matcher ran (carried partials folded into
                                   the key sort), 0 otherwise */
-    int32_t reserved0;
+    int32_t spilled_keys;      /* generic NFA: partition keys the last flush moved to the host because they outgrew
+                                  the device arena's 4096 partial matches (they run there from then on) */
 } sdg_stats;
 int sdg_last_stats(sdg_engine* e, sdg_stats* out);
 

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <numeric>
 #include <string>
@@ -290,6 +291,18 @@ struct QueryRt {
     DevBuf slot_of, idle_rec, slot_key, init_from, releasable, idle_out, free_slots, pool_ctr;
     HostPin pool_ret;
     nfa::Layout L{};
+    // spilled keys: a partition key that outgrows the device arena's largest layout (4096 partial matches) goes on
+    // on the host from its batch-start state, in an arena of 32-bit indices that doubles whenever the key needs
+    // more (KeyRunT<int32_t>); the device skips it from then on (KH_HOST in its arena head, or slot_of -3 for
+    // reclaiming queries). Its records of the flush that overflowed are dropped (q.taken) for the host run's.
+    struct Spilled {
+        nfa::Layout L{};
+        std::vector<uint8_t> arena;
+        int64_t purge_last = INT64_MIN;  // @purge: the key's last activity reading (PurgeIn::last)
+    };
+    std::map<uint32_t, Spilled> spill;
+    std::vector<std::unique_ptr<KeyRunT<int32_t>>> spill_runs;  // the last flush's host runs of spilled keys
+    DevBuf d_ovf;                                               // overflowed keys: [0] count, [1..] keys
     // the register sequence kernel (seq3.hip) instead of the generic NFA: its per-key state, SoA with stride s3_kcap
     bool seq3 = false;
     Seq3Spec s3{};
@@ -770,6 +783,194 @@ int64_t mixed_view(sdg_engine* e, QueryRt& q, const std::vector<const PushChunk*
     *d_vpos = opos;
     (void)n;
     return rows;
+}
+
+// ---- spilled keys (QueryRt::spill) ---------------------------------------------------------------------------
+// the flush's sorted view, as the generic NFA kernel reads it
+struct SpillView {
+    const int64_t* ts;
+    const uint8_t* qs;        // nullptr: single stream
+    const uint32_t* vrank;
+    const uint32_t* orig;     // view row -> batch position - pos_off (nullptr: identity)
+    int64_t pos_off;
+    const uint32_t* seg_b;    // nullptr: unpartitioned (one key, every row)
+    const uint32_t* seg_e;
+    int64_t K;
+    int64_t n;
+    const void* const* cols;
+    const uint8_t* const* nulls;
+    int nc;
+};
+
+// Takes the keys that overflowed the device's largest layout over to the host (their batch-start state, migrated
+// into a 32-bit layout of twice the slots), then runs every spilled key's rows of this flush there
+// (KeyRunT<int32_t>, the same nfa.h code), doubling a key's layout and rerunning it from its batch-start state
+// whenever it outgrows it. The runs' records join the device's in drain().
+void spill_keys(sdg_engine* e, QueryRt& q, const std::vector<uint32_t>& fresh, const SpillView& v,
+                const nfa::TimerIn& T, int64_t purge_from, int64_t purge_idle) {
+    const Plan& P = q.hq.plan;
+    const int64_t kb = q.L.bytes;
+    const int ncols = std::max(P.n_cols, 1);
+    HIPCHECK(hipStreamSynchronize(e->stream));
+    for (uint32_t k : fresh) {
+        std::vector<uint8_t> start((size_t)kb, 0);  // the key's committed state (zeros: fresh)
+        int64_t s = k;
+        uint8_t from = 0;
+        if (q.reclaim) {
+            int32_t so = -1;
+            HIPCHECK(hipMemcpy(&so, q.slot_of.as<int32_t>() + k, 4, hipMemcpyDeviceToHost));
+            if (so < 0) throw DeviceError("spilled key without an arena slot");
+            s = so;
+            HIPCHECK(hipMemcpy(&from, q.init_from.as<uint8_t>() + s, 1, hipMemcpyDeviceToHost));
+        }
+        if (from == 0) {
+            uint8_t cur = 0;
+            HIPCHECK(hipMemcpy(&cur, q.cur_bits.as<uint8_t>() + s, 1, hipMemcpyDeviceToHost));
+            const uint8_t* committed = (cur ? q.arena2.as<uint8_t>() : q.arena.as<uint8_t>()) + s * kb;
+            HIPCHECK(hipMemcpy(start.data(), committed, (size_t)kb, hipMemcpyDeviceToHost));
+        } else if (from == 2) {  // rebuilt from its idle record, as the kernel did
+            const int ib = nfa::idle_bytes(P.n_states);
+            std::vector<uint8_t> rec((size_t)ib);
+            HIPCHECK(hipMemcpy(rec.data(), q.idle_rec.as<uint8_t>() + (int64_t)k * ib, (size_t)ib, hipMemcpyDeviceToHost));
+            nfa::CtxT<true> c;
+            c.P = &P;
+            c.L = q.L;
+            c.base = start.data();
+            nfa::from_idle(c, rec.data());
+        }
+        QueryRt::Spilled& sp = q.spill[k];
+        sp.L = nfa::make_layout<int32_t>(P.n_states, ncols, 2 * q.L.ns, P.n_sched);
+        sp.arena.assign((size_t)sp.L.bytes, 0);
+        nfa::CtxT<true, int32_t> d;
+        d.P = &P;
+        d.L = sp.L;
+        d.base = sp.arena.data();
+        nfa::migrate_key<int16_t>(d, start.data(), q.L);
+        if (P.purge) {
+            int64_t ls = 0;
+            HIPCHECK(hipMemcpy(&ls, q.last_seen_bak.as<int64_t>() + k, 8, hipMemcpyDeviceToHost));
+            sp.purge_last = ls ^ INT64_MIN;
+        }
+        e->stats.spilled_keys += 1;
+    }
+    if (!v.ts && v.n > 0) throw DeviceError("spilled keys: the batch view has no timestamps");
+    for (auto& kv : q.spill) {
+        const uint32_t k = kv.first;
+        QueryRt::Spilled& sp = kv.second;
+        int64_t b = 0, en = v.n;
+        if (v.seg_b) {
+            if ((int64_t)k >= v.K) continue;  // no rows in this flush (nothing runs without rows: no timers)
+            uint32_t be[2];
+            HIPCHECK(hipMemcpy(&be[0], v.seg_b + k, 4, hipMemcpyDeviceToHost));
+            HIPCHECK(hipMemcpy(&be[1], v.seg_e + k, 4, hipMemcpyDeviceToHost));
+            b = be[0];
+            en = be[1];
+        }
+        const int64_t m = en - b;
+        if (m <= 0) continue;
+        // the key's rows (view order = its time order)
+        KeyRunT<int32_t> rows;
+        rows.ts.resize(m);
+        rows.pos.resize(m);
+        HIPCHECK(hipMemcpy(rows.ts.data(), v.ts + b, (size_t)m * 8, hipMemcpyDeviceToHost));
+        if (v.orig) {
+            std::vector<uint32_t> o(m);
+            HIPCHECK(hipMemcpy(o.data(), v.orig + b, (size_t)m * 4, hipMemcpyDeviceToHost));
+            for (int64_t p = 0; p < m; ++p) rows.pos[p] = (uint32_t)(v.pos_off + o[p]);
+        } else {
+            for (int64_t p = 0; p < m; ++p) rows.pos[p] = (uint32_t)(v.pos_off + b + p);
+        }
+        if (v.vrank) {
+            rows.vrank.resize(m);
+            HIPCHECK(hipMemcpy(rows.vrank.data(), v.vrank + b, (size_t)m * 4, hipMemcpyDeviceToHost));
+        }
+        rows.has_qs = v.qs != nullptr;
+        if (v.qs) {
+            rows.qs.resize(m);
+            HIPCHECK(hipMemcpy(rows.qs.data(), v.qs + b, (size_t)m, hipMemcpyDeviceToHost));
+        }
+        rows.cols.resize(v.nc);
+        rows.nulls.resize(v.nc);
+        for (int c = 0; c < v.nc; ++c) {
+            const int w = width_of(P.col_kind[c]);
+            rows.cols[c].resize((size_t)m * w);
+            HIPCHECK(hipMemcpy(rows.cols[c].data(), (const uint8_t*)v.cols[c] + b * w, (size_t)m * w, hipMemcpyDeviceToHost));
+            if (v.nulls[c]) {
+                rows.nulls[c].resize(m);
+                HIPCHECK(hipMemcpy(rows.nulls[c].data(), v.nulls[c] + b, (size_t)m, hipMemcpyDeviceToHost));
+            }
+        }
+        for (;;) {
+            std::unique_ptr<KeyRunT<int32_t>> r(new KeyRunT<int32_t>());
+            r->key = k;
+            r->arena = sp.arena;  // batch-start state (kept until the run succeeds)
+            r->ts = rows.ts;
+            r->pos = rows.pos;
+            r->vrank = rows.vrank;
+            r->qs = rows.qs;
+            r->has_qs = rows.has_qs;
+            r->cols = rows.cols;
+            r->nulls = rows.nulls;
+            if (P.purge) {
+                const nfa::PurgeIn pin{e->bc.clk.data(), purge_from, purge_idle, sp.purge_last};
+                r->start(&P, q.hq.code.data(), q.hq.consts.data(), sp.L, T, e->seq, &pin);
+            } else {
+                r->start(&P, q.hq.code.data(), q.hq.consts.data(), sp.L, T, e->seq);
+            }
+            r->rows_before(INT64_MAX);
+            if (!r->arena_overflow()) {
+                if (r->overflow()) throw DeviceError("spilled key: host run sink overflow");
+                sp.arena.swap(r->arena);
+                if (P.purge) sp.purge_last = r->purge_last();
+                q.spill_runs.push_back(std::move(r));
+                break;
+            }
+            if (sp.L.ns >= (1 << 22))
+                throw CompileError(SDG_ERR_CAPACITY, "query '" + q.hq.name + "': a partition key holds more than " +
+                                                         std::to_string(sp.L.ns) + " live partial matches");
+            const nfa::Layout Ln = nfa::make_layout<int32_t>(P.n_states, ncols, 2 * sp.L.ns, P.n_sched);
+            std::vector<uint8_t> na((size_t)Ln.bytes, 0);
+            nfa::CtxT<true, int32_t> d;
+            d.P = &P;
+            d.L = Ln;
+            d.base = na.data();
+            nfa::migrate_key<int32_t>(d, sp.arena.data(), sp.L);
+            sp.arena.swap(na);
+            sp.L = Ln;
+        }
+    }
+}
+
+// after the flush's commit: the device skips the newly spilled keys from now on (reclaiming queries: the key's
+// slot returns to the pool and slot_of says -3; others: KH_HOST in both copies of the key's arena head)
+void mark_spilled(sdg_engine* e, QueryRt& q, const std::vector<uint32_t>& keys, const SlotPool& sp) {
+    HIPCHECK(hipStreamSynchronize(e->stream));
+    if (q.reclaim) {
+        unsigned int top = 0;
+        HIPCHECK(hipMemcpy(&top, sp.counters, 4, hipMemcpyDeviceToHost));
+        for (uint32_t k : keys) {
+            int32_t s = -1;
+            HIPCHECK(hipMemcpy(&s, sp.slot_of + k, 4, hipMemcpyDeviceToHost));
+            if (s >= 0) {
+                HIPCHECK(hipMemcpy(sp.free_slots + top, &s, 4, hipMemcpyHostToDevice));
+                ++top;
+            }
+            const int32_t host = -3;
+            HIPCHECK(hipMemcpy(sp.slot_of + k, &host, 4, hipMemcpyHostToDevice));
+        }
+        HIPCHECK(hipMemcpy(sp.counters, &top, 4, hipMemcpyHostToDevice));
+        return;
+    }
+    const int64_t kb = q.L.bytes;
+    for (uint32_t k : keys) {
+        for (uint8_t* base : {q.arena.as<uint8_t>(), q.arena2.as<uint8_t>()}) {
+            if (!base) continue;
+            int32_t f = 0;
+            HIPCHECK(hipMemcpy(&f, base + (int64_t)k * kb, 4, hipMemcpyDeviceToHost));
+            f = (f & ~1) | 2 | nfa::KH_HOST;
+            HIPCHECK(hipMemcpy(base + (int64_t)k * kb, &f, 4, hipMemcpyHostToDevice));
+        }
+    }
 }
 
 // A chain query moving to the generic NFA: its carried partials (e1 events still pending at the end of the last
@@ -1782,8 +1983,20 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         };
         int hf[8];
         unsigned long long hc[2];
+        // keys past the largest device layout go on on the host (QueryRt::spill); queries with timers (the
+        // scheduler simulation owns their host runs) or @purge aggregators (per-record reset flags) still refuse
+        const bool can_spill = !timers && !q.purge_agg;
+        constexpr int32_t OVF_CAP = 4096;
+        std::vector<uint32_t> spill_new;  // keys whose run overflowed the largest layout in this flush (sorted)
+        if (can_spill) {
+            uint32_t* ob = (uint32_t*)q.d_ovf.ensure((size_t)(OVF_CAP + 1) * 4);
+            a.ovf_count = (unsigned int*)ob;
+            a.ovf_keys = ob + 1;
+            a.ovf_cap = OVF_CAP;
+        }
         // one launch; returns false when a growable buffer (outputs, scheduler log) overflowed
         auto launch = [&](bool first) -> bool {
+            if (a.ovf_count) HIPCHECK(hipMemsetAsync(a.ovf_count, 0, 4, st));
             if (first && q.purge_agg) HIPCHECK(hipMemsetAsync(a.agg_reset, 0, (size_t)q.arena_keys, st));
             if (first) {
                 HIPCHECK(hipMemsetAsync(counters, 0, 16, st));
@@ -1809,7 +2022,21 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 HIPCHECK(hipMemsetAsync(flags, 0, 32, st));
                 return false;
             }
-            if (hf[2]) {
+            spill_new.clear();
+            if (hf[2] && can_spill) {  // the keys that overflowed: the host takes them over (spill_keys below)
+                unsigned int no = 0;
+                HIPCHECK(hipMemcpy(&no, a.ovf_count, 4, hipMemcpyDeviceToHost));
+                if (no == 0 || no > (unsigned)OVF_CAP)
+                    throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': " + std::to_string(no) + " partition keys "
+                                                             "exceeded " + std::to_string(q.L.ns) + " live partial matches "
+                                                             "in one flush (at most " + std::to_string(OVF_CAP) +
+                                                             " can move to the host at once)");
+                spill_new.resize(no);
+                HIPCHECK(hipMemcpy(spill_new.data(), a.ovf_keys, (size_t)no * 4, hipMemcpyDeviceToHost));
+                std::sort(spill_new.begin(), spill_new.end());
+                spill_new.erase(std::unique(spill_new.begin(), spill_new.end()), spill_new.end());
+                HIPCHECK(hipMemsetAsync(flags + 2, 0, 4, st));
+            } else if (hf[2]) {
                 e->stats.overflow += 1;
                 throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': a partition key exceeded max_partials (" +
                                                          std::to_string(q.L.ns) + " live partial matches, or as many queued "
@@ -1852,6 +2079,14 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         q.last_seq_base = e->seq;
         q.emit_base = e->seq;
         q.sub_is_seq = false;
+        q.spill_runs.clear();
+        if (can_spill && (!spill_new.empty() || !q.spill.empty())) {
+            spill_keys(e, q, spill_new, SpillView{v_ts, multi_stream ? v_qs : nullptr, v_vrank, v_orig, a.pos_off,
+                                                  partitioned ? v_seg : nullptr, partitioned ? v_segend : nullptr,
+                                                  partitioned ? (int64_t)K : 1, nrows, v_cols, v_nulls, nc},
+                       a.T, a.purge_from, a.purge_idle);
+            q.taken = spill_new;  // their device records of this flush are void (the host runs replace them)
+        }
         if (timers) {
             const auto t_sched = std::chrono::steady_clock::now();
             double k_before = e->stats.ms_nfa_kernel;
@@ -2027,6 +2262,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         }
         if (q.reclaim) nfa_commit_slots(slot_pool(), q.cur_bits.as<uint8_t>(), q.ran_bits.as<uint8_t>(), q.arena_keys, st);
         else nfa_commit(q.cur_bits.as<uint8_t>(), q.ran_bits.as<uint8_t>(), q.arena_keys, st);
+        if (!spill_new.empty()) mark_spilled(e, q, spill_new, slot_pool());
         e->stats.arena_slots += q.arena_keys;
         ev_record(e->ev[2], st);
         HIPCHECK(hipStreamSynchronize(st));
@@ -2339,7 +2575,11 @@ void drain(sdg_engine* e, QueryRt& q) {
             (void)hipStreamSynchronize(e->stream);
         }
     } tail_reset{e, q};
-    if (n <= 0) return;
+    // host runs whose records join the device's: scheduler replays (timers) and spilled keys
+    std::vector<const KeyOut*> hruns;
+    for (auto& r : q.runs) hruns.push_back(r.get());
+    for (auto& r : q.spill_runs) hruns.push_back(r.get());
+    if (n <= 0 && hruns.empty()) return;
     const int na = q.hq.plan.n_out;  // every column of the records (hidden selector columns included)
     const bool post = q.hq.plan.has_post;
     uint8_t* hb = (uint8_t*)q.h_rb.ensure((size_t)n * (28 + 8 * (size_t)na));
@@ -2358,7 +2598,7 @@ void drain(sdg_engine* e, QueryRt& q) {
     const void* src_nulls = q.o_nulls.p;
     const void* src_key = q.o_key.p;
     const void* src_flags = q.o_flags.p;
-    const bool dev_order = !q.last_timers && n > 1;
+    const bool dev_order = !q.last_timers && n > 1 && hruns.empty();
     if (dev_order) {
         const size_t wb = order_workspace(n);
         void* work = q.ord_ws.ensure(wb);
@@ -2394,30 +2634,32 @@ void drain(sdg_engine* e, QueryRt& q) {
     }
     std::vector<uint32_t> okey;
     std::vector<uint8_t> oround, oflags;
-    if (q.purge_agg) {  // (no timers: purge with aggregators excludes absent states, so no host replay records)
-        oflags.resize(n);
-        HIPCHECK(hipMemcpyAsync(oflags.data(), src_flags, n, hipMemcpyDeviceToHost, st));
-    }
-    if (q.last_timers || post) {  // keys: the aggregators' state, and for timer matches: drop the records of keys
-        okey.resize(n);            // replayed on the host, order the fires
-        HIPCHECK(hipMemcpyAsync(okey.data(), src_key, n * 4, hipMemcpyDeviceToHost, st));
-    }
-    if (q.last_timers) {
-        if (!q.reordered.empty()) {  // and the first run's records of the keys rerun with the scheduler's order
-            oround.resize(n);
-            HIPCHECK(hipMemcpyAsync(oround.data(), q.o_round.p, n, hipMemcpyDeviceToHost, st));
+    if (n > 0) {  // (a flush whose records all come from host runs reads nothing back)
+        if (q.purge_agg) {  // (no timers: purge with aggregators excludes absent states, so no host replay records)
+            oflags.resize(n);
+            HIPCHECK(hipMemcpyAsync(oflags.data(), src_flags, n, hipMemcpyDeviceToHost, st));
         }
+        if (q.last_timers || post || !q.taken.empty()) {  // keys: the aggregators' state, the records of keys the
+            okey.resize(n);                                 // host replayed (dropped), timer matches' fire order
+            HIPCHECK(hipMemcpyAsync(okey.data(), src_key, n * 4, hipMemcpyDeviceToHost, st));
+        }
+        if (q.last_timers) {
+            if (!q.reordered.empty()) {  // and the first run's records of the keys rerun with the scheduler's order
+                oround.resize(n);
+                HIPCHECK(hipMemcpyAsync(oround.data(), q.o_round.p, n, hipMemcpyDeviceToHost, st));
+            }
+        }
+        HIPCHECK(hipMemcpyAsync(ts, src_ts, n * 8, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(emit, src_emit, n * 8, hipMemcpyDeviceToHost, st));
+        if (src_first) HIPCHECK(hipMemcpyAsync(first, src_first, n * 8, hipMemcpyDeviceToHost, st));
+        if (q.nulls_valid) HIPCHECK(hipMemcpyAsync(nulls, src_nulls, n * 4, hipMemcpyDeviceToHost, st));
+        for (int j = 0; j < na; ++j)
+            HIPCHECK(hipMemcpyAsync(vals + (size_t)j * n, src_vals + (size_t)j * vstride, n * 8, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
     }
-    HIPCHECK(hipMemcpyAsync(ts, src_ts, n * 8, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipMemcpyAsync(emit, src_emit, n * 8, hipMemcpyDeviceToHost, st));
-    if (src_first) HIPCHECK(hipMemcpyAsync(first, src_first, n * 8, hipMemcpyDeviceToHost, st));
-    if (q.nulls_valid) HIPCHECK(hipMemcpyAsync(nulls, src_nulls, n * 4, hipMemcpyDeviceToHost, st));
-    for (int j = 0; j < na; ++j)
-        HIPCHECK(hipMemcpyAsync(vals + (size_t)j * n, src_vals + (size_t)j * vstride, n * 8, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
     // records already in delivery order on the device, nothing to drop, rank or aggregate: the columns join the
     // backlog as they are (a memcpy per column instead of a per-record walk)
-    if (dev_order && !post && q.runs.empty()) {
+    if (dev_order && !post) {
         const int nu = q.hq.plan.n_user_out + q.hq.plan.n_list_cols;
         const size_t b = q.acc_ts.size();
         q.acc_ts.resize(b + n);
@@ -2450,14 +2692,14 @@ void drain(sdg_engine* e, QueryRt& q) {
     if (!q.nulls_valid) std::memset(nulls, 0, (size_t)n * 4);
     // the host replays' records join the device's (same layout, after them)
     int64_t nh = 0;
-    for (auto& r : q.runs) nh += (int64_t)r->count;
+    for (const KeyOut* r : hruns) nh += (int64_t)r->count;
     std::vector<int64_t> hts, hemit, hfirst, hvals;
     std::vector<uint32_t> hnulls, hkey;
     if (nh) {
         hts.reserve(nh); hemit.reserve(nh); hfirst.reserve(nh); hnulls.reserve(nh); hkey.reserve(nh);
         hvals.resize((size_t)na * nh);
         int64_t x = 0;
-        for (auto& r : q.runs) {
+        for (const KeyOut* r : hruns) {
             const int64_t cap = (int64_t)r->o_ts.size();
             for (unsigned long long i = 0; i < r->count; ++i, ++x) {
                 hts.push_back(r->o_ts[i]);
@@ -2480,8 +2722,8 @@ void drain(sdg_engine* e, QueryRt& q) {
     std::vector<int64_t> ord;  // < n: device record, >= n: host record n + i
     ord.reserve(n + nh);
     for (int64_t i = 0; i < n; ++i) {
+        if (!q.taken.empty() && std::binary_search(q.taken.begin(), q.taken.end(), okey[i])) continue;
         if (q.last_timers) {
-            if (std::binary_search(q.taken.begin(), q.taken.end(), okey[i])) continue;
             if (!oround.empty() && oround[i] == 0 && std::binary_search(q.reordered.begin(), q.reordered.end(), okey[i]))
                 continue;
             slot(emit[i], first[i], okey[i]);
@@ -2597,6 +2839,7 @@ void drain(sdg_engine* e, QueryRt& q) {
         ++o;
     }
     q.runs.clear();
+    q.spill_runs.clear();
 }
 
 // the batch clock (sched.h BatchClock): playback = TimestampGeneratorImpl.setCurrentTimestamp per position (an
@@ -2846,6 +3089,14 @@ void snapshot(sdg_engine* e, std::vector<uint8_t>& out) {
                 w.dev(q.pool_ctr.p, 4, st);
             }
         }
+        // spilled keys: their host arenas (32-bit layouts)
+        w.put<uint64_t>(q.spill.size());
+        for (const auto& kv : q.spill) {
+            w.put<uint32_t>(kv.first);
+            w.put<int32_t>(kv.second.L.ns);
+            w.put<int64_t>(kv.second.purge_last);
+            w.vec(kv.second.arena);
+        }
         w.put<int64_t>(q.purge_first);
         if (P.purge && q.arena_keys > 0) w.dev(q.last_seen.p, (size_t)q.arena_keys * 8, st);
         // selector aggregators per key
@@ -2903,6 +3154,7 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
         int64_t s3_kcap = 0;
         View s3_hdr, s3_pn, s3_qn, s3_vals, s3_ts;
         SchedSim sim;
+        std::map<uint32_t, QueryRt::Spilled> spill;
     };
     const int64_t seq = r.get<int64_t>();
     const int64_t clock = r.get<int64_t>();
@@ -2970,6 +3222,18 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
                     throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (arena slots)");
             }
         }
+        const uint64_t nsp = r.get<uint64_t>();
+        if (nsp > (uint64_t)(r.end - r.p) / 16) throw CompileError(SDG_ERR_ARG, "snapshot is truncated");
+        for (uint64_t i = 0; i < nsp; ++i) {
+            const uint32_t k = r.get<uint32_t>();
+            const int32_t sns = r.get<int32_t>();
+            if (sns <= 0 || sns > (1 << 22)) throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (spilled key)");
+            QueryRt::Spilled& sp = g.spill[k];
+            sp.L = nfa::make_layout<int32_t>(P.n_states, std::max(P.n_cols, 1), sns, P.n_sched);
+            sp.purge_last = r.get<int64_t>();
+            r.vec(sp.arena);
+            if ((int64_t)sp.arena.size() != sp.L.bytes) throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (spilled key)");
+        }
         g.purge_first = r.get<int64_t>();
         if (P.purge && g.arena_keys > 0) g.last_seen = view();
         g.agg_keys = r.get<int64_t>();
@@ -3002,6 +3266,8 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
         Plan& P = q.hq.plan;
         Stage& g = stg[qi];
         P.chain = g.chain;
+        q.spill.swap(g.spill);
+        q.spill_runs.clear();
         q.replay_carries = g.replay;
         q.carry_nullable = g.nullable;
         const int nc = std::max(P.n_cols, 1);
@@ -3638,6 +3904,9 @@ int export_records(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_t* 
         if (e->compile_only) throw DeviceError("engine was compiled with SDG_COMPILE_ONLY");
         if (!q.acc_ts.empty()) throw CompileError(SDG_ERR_ARG, "earlier results are still queued on the host: sdg_poll first");
         if (q.last_timers) throw CompileError(SDG_ERR_UNSUPPORTED, "device export of timer (absent-state) matches");
+        if (!q.spill.empty())
+            throw CompileError(SDG_ERR_UNSUPPORTED, "device export of a query with partition keys spilled to the host "
+                                                    "(their records are host-side): use sdg_poll");
         if (q.hq.plan.has_post) throw CompileError(SDG_ERR_UNSUPPORTED, "device export of aggregated / having outputs");
         const int64_t n = q.polled ? 0 : q.out_n;
         *n_out = n;

@@ -1,7 +1,9 @@
-// One partition key's NFA (nfa.h, the same code the gfx950 kernel runs) executed on the host and stepped by the
-// scheduler simulation (sched.h): when the reference's global scheduler orders a key's timer fires differently
-// from the key's own device run in a way that changes its result, the simulation replays that key from its
-// batch-start state with the exact order of events and fires, and keeps stepping it in lockstep.
+// One partition key's NFA (nfa.h, the same code the gfx950 kernel runs) executed on the host, for two callers:
+//   * the scheduler simulation (sched.h): when the reference's global scheduler orders a key's timer fires
+//     differently from the key's own device run in a way that changes its result, the simulation replays that key
+//     from its batch-start state with the exact order of events and fires, and keeps stepping it in lockstep;
+//   * spilled keys (engine.cpp): a key that outgrows the device arena's 4096 partial matches continues on the host
+//     in an arena of 32-bit indices (KeyRunT<int32_t>) that doubles whenever the key needs more.
 #pragma once
 #include <stdint.h>
 
@@ -11,8 +13,16 @@
 
 namespace sdg {
 
-struct KeyRun {
+// a host run's match records (same record layout as the device's)
+struct KeyOut {
     uint32_t key = 0;
+    std::vector<int64_t> o_ts, o_vals, o_seq, o_sub;
+    std::vector<uint32_t> o_nulls, o_key;
+    unsigned long long count = 0;
+};
+
+template <class IX>
+struct KeyRunT : KeyOut {
     std::vector<uint8_t> arena;                      // batch-start state, then the run's state
     // the key's rows in this batch (time order), as the sorted view holds them
     std::vector<int64_t> ts;
@@ -21,10 +31,6 @@ struct KeyRun {
     std::vector<uint32_t> vrank;                     // the rows' delivery ranks (range / broadcast rows), or empty
     std::vector<std::vector<uint8_t>> cols, nulls;   // per physical column: raw values / null flags
     bool has_qs = false;
-    // outputs (same record layout as the device's)
-    std::vector<int64_t> o_ts, o_vals, o_seq, o_sub;
-    std::vector<uint32_t> o_nulls, o_key;
-    unsigned long long count = 0;
     std::vector<nfa::SchedLog> log;
     unsigned long long lcount = 0;
     size_t lread = 0;
@@ -79,13 +85,14 @@ struct KeyRun {
         if (T.G > 0) c_.clock = T.clk[T.G - 1];
     }
     bool overflow() { return c_.ovf() || flags_[0] || flags_[5]; }
+    bool arena_overflow() { return c_.ovf(); }
     int64_t next_row_pos() const { return p_ < (int64_t)ts.size() ? (int64_t)pos[p_] : -1; }
     int64_t purge_last() const { return c_.purge.last; }  // the key's last activity after the replay (@purge)
 
    private:
     const Plan* P_ = nullptr;
     int n_out_ = 0, ncols_ = 0;
-    nfa::CtxT<true> c_;
+    nfa::CtxT<true, IX> c_;
     nfa::KeyEvents ev_{};
     const void* cptr_[MAX_COLS] = {};
     const uint8_t* nptr_[MAX_COLS] = {};
@@ -122,5 +129,6 @@ struct KeyRun {
         }
     }
 };
+using KeyRun = KeyRunT<int16_t>;
 
 }  // namespace sdg

@@ -48,28 +48,35 @@ struct Layout {
 };
 
 struct KHead {
-    int32_t flags;       // bit0 overflow, bit1 key initialised
+    int32_t flags;       // bit0 overflow, bit1 key initialised, bit2 (KH_HOST) the host runs the key (spilled)
     int32_t se_free, nd_free, rc_free;
     int32_t se_used, nd_used, rc_used;
     uint32_t kseq;       // scheduler log records written by this key in the current run
     int32_t screate;     // scheduler states created by this key (creation order, live-mode tie break)
     int32_t pad;
 };
+constexpr int32_t KH_HOST = 4;
 
-struct PState {
+// IX: the arena's object index type -- int16_t on the device (compact arenas, <= 4096 partials per key), int32_t
+// for the keys the host takes over when they outgrow that (spilled keys, engine.cpp)
+template <class IX>
+struct PStateT {
     uint8_t changed, initialized, success, start_reset, active, started, returned, pad;
     int64_t last_sched;    // AbsentStreamPreState.lastScheduledTime
-    int16_t pn, nw;
-    int16_t pad2[2];
+    IX pn, nw;
+    IX pad2[2];
     int64_t last_arrival;  // AbsentLogicalPreStateProcessor.LogicalStreamPreState.lastArrivalTime
 };
+using PState = PStateT<int16_t>;
 
 // one scheduler's notify-time FIFO of one key (Scheduler.SchedulerState.toNotifyQueue)
-struct TQ {
+template <class IX>
+struct TQT {
     int64_t earliest;  // first batch position at which the current head may fire (ideal mode)
     int32_t created;   // KHead::screate when this scheduler state was (re)created
-    int16_t h, n;
+    IX h, n;
 };
+using TQ = TQT<int16_t>;
 
 // scheduler log (device -> host scheduler simulation): every fire a key run performs and every notify time it
 // pushes, in the key's order (kseq)
@@ -116,28 +123,38 @@ struct PurgeIn {
     int64_t last;                 // the key's currentTime at its last event (INT64_MIN: none yet); updated by the run
 };
 
-struct SE {
-    int16_t free_next;
+template <class IX>
+struct SET {
+    IX free_next;
     uint8_t type, mark;
     int32_t pad;
     int64_t ts;
-    // int16_t slot[n_states] follows
+    // IX slot[n_states] follows
 };
 
-struct Node {
-    int16_t rec, next, free_next;
+template <class IX>
+struct NodeT {
+    IX rec, next, free_next;
     uint8_t mark, pad;
 };
 
-struct Rec {
+template <class IX>
+struct RecT {
     uint32_t nullmask;
     uint8_t mark, pad;
-    int16_t free_next;
+    IX free_next;
     int64_t ts;
     // int64_t vals[n_cols] follows
 };
 
+template <class IX = int16_t>
 inline Layout make_layout(int n_states, int n_cols, int ns, int n_sched = 0) {
+    using SE = SET<IX>;
+    using Node = NodeT<IX>;
+    using Rec = RecT<IX>;
+    using PState = PStateT<IX>;
+    using TQ = TQT<IX>;
+    constexpr int W = (int)sizeof(IX);
     Layout L;
     L.ns = ns;
     L.nn = ns * 4;
@@ -147,17 +164,17 @@ inline Layout make_layout(int n_states, int n_cols, int ns, int n_sched = 0) {
     L.n_cols = n_cols;
     L.n_sched = n_sched;
     L.qcap = n_sched ? ns : 0;
-    L.se_bytes = (int32_t)((sizeof(SE) + 2 * n_states + 7) & ~7);
+    L.se_bytes = (int32_t)((sizeof(SE) + W * n_states + 7) & ~7);
     L.rc_bytes = (int32_t)(sizeof(Rec) + 8 * n_cols);
     int64_t o = sizeof(KHead);
     L.off_ps = o;
     o += (int64_t)sizeof(PState) * n_states;
     L.off_pend = o;
-    o += (int64_t)2 * L.lcap * n_states;
+    o += (int64_t)W * L.lcap * n_states;
     L.off_newe = o;
-    o += (int64_t)2 * L.lcap * n_states;
+    o += (int64_t)W * L.lcap * n_states;
     L.off_ret = o;  // StateEvents one processAndReturn call returns (emitted after its loop)
-    o += (int64_t)2 * L.lcap;
+    o += (int64_t)W * L.lcap;
     o = (o + 7) & ~7;
     L.off_tq = o;
     o += (int64_t)sizeof(TQ) * n_sched;
@@ -174,14 +191,14 @@ inline Layout make_layout(int n_states, int n_cols, int ns, int n_sched = 0) {
     return L;
 }
 
-template <bool TM>
+template <bool TM, class IX = int16_t>
 struct CtxT;
 
 // bytecode accessor over a StateEvent (StateEvent.getStreamEvent(int[]) + attribute)
-template <bool TM>
+template <bool TM, class IX = int16_t>
 struct SEAccT {
-    CtxT<TM>* c;
-    int16_t se;
+    CtxT<TM, IX>* c;
+    IX se;
     SDG_HD void load(int slot, int col, int chain, uint8_t kind, int64_t* v, bool* null);
     SDG_HD bool slot_empty(int slot, int chain);
     SDG_HD void agg(int, int64_t* v, bool* n) { *v = 0; *n = true; }  // aggregators: the post pass only
@@ -189,8 +206,13 @@ struct SEAccT {
 
 // TM: the query has absent states (timer code compiled in); without them the kernel keeps its registers for
 // the plain processors
-template <bool TM>
+template <bool TM, class IX>
 struct CtxT {
+    using SE = SET<IX>;
+    using Node = NodeT<IX>;
+    using Rec = RecT<IX>;
+    using PState = PStateT<IX>;
+    using TQ = TQT<IX>;
     const Plan* P;
     const Instr* code;
     const int64_t* consts;
@@ -230,10 +252,10 @@ struct CtxT {
     // ---- arena access ------------------------------------------------------------------------------------
     SDG_HD KHead& head() { return *(KHead*)base; }
     SDG_HD PState& ps(int p) { return ((PState*)(base + L.off_ps))[p]; }
-    SDG_HD int16_t* pend(int p) { return (int16_t*)(base + L.off_pend) + (int64_t)p * L.lcap; }
-    SDG_HD int16_t* newe(int p) { return (int16_t*)(base + L.off_newe) + (int64_t)p * L.lcap; }
+    SDG_HD IX* pend(int p) { return (IX*)(base + L.off_pend) + (int64_t)p * L.lcap; }
+    SDG_HD IX* newe(int p) { return (IX*)(base + L.off_newe) + (int64_t)p * L.lcap; }
     SDG_HD SE& se(int i) { return *(SE*)(base + L.off_se + (int64_t)i * L.se_bytes); }
-    SDG_HD int16_t* slots(int i) { return (int16_t*)((uint8_t*)&se(i) + sizeof(SE)); }
+    SDG_HD IX* slots(int i) { return (IX*)((uint8_t*)&se(i) + sizeof(SE)); }
     SDG_HD Node& nd(int i) { return ((Node*)(base + L.off_nd))[i]; }
     SDG_HD Rec& rc(int i) { return *(Rec*)(base + L.off_rc + (int64_t)i * L.rc_bytes); }
     SDG_HD TQ& tq(int s) { return ((TQ*)(base + L.off_tq))[s]; }
@@ -246,9 +268,9 @@ struct CtxT {
         KHead& h = head();
         h.flags = 0;
         h.se_used = h.nd_used = h.rc_used = 0;
-        for (int i = 0; i < L.ns; ++i) se(i).free_next = (int16_t)(i + 1 < L.ns ? i + 1 : NIL);
-        for (int i = 0; i < L.nn; ++i) nd(i).free_next = (int16_t)(i + 1 < L.nn ? i + 1 : NIL);
-        for (int i = 0; i < L.nr; ++i) rc(i).free_next = (int16_t)(i + 1 < L.nr ? i + 1 : NIL);
+        for (int i = 0; i < L.ns; ++i) se(i).free_next = (IX)(i + 1 < L.ns ? i + 1 : NIL);
+        for (int i = 0; i < L.nn; ++i) nd(i).free_next = (IX)(i + 1 < L.nn ? i + 1 : NIL);
+        for (int i = 0; i < L.nr; ++i) rc(i).free_next = (IX)(i + 1 < L.nr ? i + 1 : NIL);
         h.se_free = 0;
         h.nd_free = 0;
         h.rc_free = 0;
@@ -269,33 +291,33 @@ struct CtxT {
         }
     }
 
-    SDG_HD int16_t se_alloc() {
+    SDG_HD IX se_alloc() {
         KHead& h = head();
         if (h.se_free == NIL) { set_ovf(); return NIL; }
-        int16_t i = (int16_t)h.se_free;
+        IX i = (IX)h.se_free;
         h.se_free = se(i).free_next;
         h.se_used++;
         SE& s = se(i);
         s.type = T_CURRENT;
         s.ts = -1;
-        int16_t* sl = slots(i);
+        IX* sl = slots(i);
         for (int k = 0; k < L.n_states; ++k) sl[k] = NIL;
         return i;
     }
-    SDG_HD int16_t nd_alloc(int16_t rec) {
+    SDG_HD IX nd_alloc(IX rec) {
         KHead& h = head();
         if (h.nd_free == NIL) { set_ovf(); return NIL; }
-        int16_t i = (int16_t)h.nd_free;
+        IX i = (IX)h.nd_free;
         h.nd_free = nd(i).free_next;
         h.nd_used++;
         nd(i).rec = rec;
         nd(i).next = NIL;
         return i;
     }
-    SDG_HD int16_t rc_alloc() {
+    SDG_HD IX rc_alloc() {
         KHead& h = head();
         if (h.rc_free == NIL) { set_ovf(); return NIL; }
-        int16_t i = (int16_t)h.rc_free;
+        IX i = (IX)h.rc_free;
         h.rc_free = rc(i).free_next;
         h.rc_used++;
         return i;
@@ -308,15 +330,15 @@ struct CtxT {
         for (int i = 0; i < L.nr; ++i) rc(i).mark = 0;
         for (int p = 0; p < L.n_states; ++p) {
             for (int l = 0; l < 2; ++l) {
-                int16_t* lst = l ? newe(p) : pend(p);
+                IX* lst = l ? newe(p) : pend(p);
                 int n = l ? ps(p).nw : ps(p).pn;
                 for (int j = 0; j < n; ++j) {
-                    int16_t s = lst[j];
+                    IX s = lst[j];
                     if (se(s).mark) continue;
                     se(s).mark = 1;
-                    int16_t* sl = slots(s);
+                    IX* sl = slots(s);
                     for (int k = 0; k < L.n_states; ++k)
-                        for (int16_t x = sl[k]; x != NIL && !nd(x).mark; x = nd(x).next) {
+                        for (IX x = sl[k]; x != NIL && !nd(x).mark; x = nd(x).next) {
                             nd(x).mark = 1;
                             rc(nd(x).rec).mark = 1;
                         }
@@ -328,36 +350,36 @@ struct CtxT {
         h.se_used = h.nd_used = h.rc_used = 0;
         for (int i = L.ns - 1; i >= 0; --i) {
             if (se(i).mark) { h.se_used++; continue; }
-            se(i).free_next = (int16_t)h.se_free;
+            se(i).free_next = (IX)h.se_free;
             h.se_free = i;
         }
         for (int i = L.nn - 1; i >= 0; --i) {
             if (nd(i).mark) { h.nd_used++; continue; }
-            nd(i).free_next = (int16_t)h.nd_free;
+            nd(i).free_next = (IX)h.nd_free;
             h.nd_free = i;
         }
         for (int i = L.nr - 1; i >= 0; --i) {
             if (rc(i).mark) { h.rc_used++; continue; }
-            rc(i).free_next = (int16_t)h.rc_free;
+            rc(i).free_next = (IX)h.rc_free;
             h.rc_free = i;
         }
     }
 
     // ---- StateEvent helpers ------------------------------------------------------------------------------
-    SDG_HD int16_t clone(int16_t o) {  // StateEventCloner.copyStateEvent: slots shared
-        int16_t n = se_alloc();
+    SDG_HD IX clone(IX o) {  // StateEventCloner.copyStateEvent: slots shared
+        IX n = se_alloc();
         if (n == NIL) return NIL;
         SE& a = se(n);
         SE& b = se(o);
         a.type = b.type;
         a.ts = b.ts;
-        int16_t* sa = slots(n);
-        int16_t* sb = slots(o);
+        IX* sa = slots(n);
+        IX* sb = slots(o);
         for (int k = 0; k < L.n_states; ++k) sa[k] = sb[k];
         return n;
     }
-    SDG_HD int16_t chain_at(int16_t s, int pos, int idx) {  // StateEvent.getStreamEvent(int[])
-        int16_t e = slots(s)[pos];
+    SDG_HD IX chain_at(IX s, int pos, int idx) {  // StateEvent.getStreamEvent(int[])
+        IX e = slots(s)[pos];
         if (e == NIL) return NIL;
         if (idx >= 0) {
             for (int i = 1; i <= idx; ++i) {
@@ -376,20 +398,20 @@ struct CtxT {
             return e;
         }
         int len = 0;
-        for (int16_t x = e; x != NIL; x = nd(x).next) ++len;
+        for (IX x = e; x != NIL; x = nd(x).next) ++len;
         int k = len + idx;
         if (k < 0) return NIL;
         for (int i = 0; i < k; ++i) e = nd(e).next;
         return e;
     }
-    SDG_HD void add_event(int16_t s, int pos, int16_t node) {
-        int16_t a = slots(s)[pos];
+    SDG_HD void add_event(IX s, int pos, IX node) {
+        IX a = slots(s)[pos];
         if (a == NIL) { slots(s)[pos] = node; return; }
         while (nd(a).next != NIL) a = nd(a).next;
         nd(a).next = node;
     }
-    SDG_HD void remove_last_event(int16_t s, int pos) {
-        int16_t a = slots(s)[pos];
+    SDG_HD void remove_last_event(IX s, int pos) {
+        IX a = slots(s)[pos];
         if (a == NIL) return;
         while (nd(a).next != NIL) {
             if (nd(nd(a).next).next == NIL) { nd(a).next = NIL; return; }
@@ -458,13 +480,13 @@ struct CtxT {
     SDG_HD int64_t tq_pop(int sch) {
         TQ& q = tq(sch);
         const int64_t t = tqt(sch)[q.h];
-        q.h = (int16_t)((q.h + 1) % L.qcap);
+        q.h = (IX)((q.h + 1) % L.qcap);
         q.n--;
         return t;
     }
     // StreamEventFactory.newInstance(): timestamp -1, every attribute null
-    SDG_HD int16_t empty_node() {
-        int16_t r = rc_alloc();
+    SDG_HD IX empty_node() {
+        IX r = rc_alloc();
         if (r == NIL) return NIL;
         rc(r).ts = -1;
         rc(r).nullmask = 0xFFFFFFFFu;
@@ -485,19 +507,19 @@ struct CtxT {
     }
 
     // ---- list helpers ------------------------------------------------------------------------------------
-    SDG_HD void push(int16_t* lst, int16_t& n, int16_t v) {
+    SDG_HD void push(IX* lst, IX& n, IX v) {
         if (n >= L.lcap) { set_ovf(); return; }
         lst[n++] = v;
     }
-    SDG_HD static void erase(int16_t* lst, int16_t& n, int j) {
+    SDG_HD static void erase(IX* lst, IX& n, int j) {
         for (int i = j; i + 1 < n; ++i) lst[i] = lst[i + 1];
         --n;
     }
     SDG_HD void pend_push_newe(int p) {  // newAndEvery.sort(eventTimeComparator) + pending.addAll + clear
         PState& s = ps(p);
-        int16_t* nw = newe(p);
+        IX* nw = newe(p);
         for (int i = 1; i < s.nw; ++i) {  // stable insertion sort; ts == -1 sorts last
-            int16_t v = nw[i];
+            IX v = nw[i];
             int64_t tv = se(v).ts;
             int j = i - 1;
             while (j >= 0) {
@@ -509,22 +531,22 @@ struct CtxT {
             }
             nw[j + 1] = v;
         }
-        int16_t* pd = pend(p);
+        IX* pd = pend(p);
         for (int i = 0; i < s.nw; ++i) push(pd, s.pn, nw[i]);
         s.nw = 0;
     }
 
     // ---- filters / selector ------------------------------------------------------------------------------
-    SDG_HD bool filter(int p, int16_t s) {
+    SDG_HD bool filter(int p, IX s) {
         const StateRow& r = P->st[p];
         const FastPred& f = P->fast[p];
-        SEAccT<TM> acc{this, s};
+        SEAccT<TM, IX> acc{this, s};
         if (f.kind == FP_TRUE) return true;
         if (f.kind != FP_NONE) return fast_pass(f, acc);
         return pass(code, r.filter, consts, acc, stk, stride);
     }
 
-    SDG_HD void emit(int16_t s) {  // QuerySelector.processNoGroupBy for one StateEvent (insert current events)
+    SDG_HD void emit(IX s) {  // QuerySelector.processNoGroupBy for one StateEvent (insert current events)
         // (timer emissions: cur_seq = the position of the fire, cur_sub negative -- before that event's own)
         if (se(s).type != T_CURRENT) return;
         unsigned long long slot = reserve(emit_count);
@@ -540,7 +562,7 @@ struct CtxT {
         emit_key[slot] = key;
         if (emit_round) emit_round[slot] = round;
         uint32_t nm = 0;
-        SEAccT<TM> acc{this, s};
+        SEAccT<TM, IX> acc{this, s};
         for (int j = 0; j < P->n_out; ++j) {
             int64_t v;
             bool nl;
@@ -552,11 +574,11 @@ struct CtxT {
     }
 
     // ---- pre-state processors ----------------------------------------------------------------------------
-    SDG_HD bool is_expired(int16_t s, int64_t now) {
+    SDG_HD bool is_expired(IX s, int64_t now) {
         if (!P->has_within) return false;
         for (int i = 0; i < P->n_states; ++i) {
             if (!P->st[i].is_start) continue;
-            int16_t e = slots(s)[i];
+            IX e = slots(s)[i];
             if (e != NIL) {
                 int64_t d = rc(nd(e).rec).ts - now;
                 if (d < 0) d = -d;
@@ -566,7 +588,7 @@ struct CtxT {
         return false;
     }
 
-    SDG_HD void add_state(int p, int16_t s) {
+    SDG_HD void add_state(int p, IX s) {
         // iterative: a count state with min 0 forwards at once (CountPreStateProcessor.addState :97-125 ->
         // CountPostStateProcessor.processMinCountReached), which may reach another such state. The every clone of
         // each level is pushed before the forward chain continues: the chain only touches lists of later states,
@@ -618,9 +640,9 @@ struct CtxT {
         set_ovf();
     }
 
-    SDG_HD void add_every_state(int p, int16_t s) {
+    SDG_HD void add_every_state(int p, IX s) {
         const StateRow& r = P->st[p];
-        int16_t c = clone(s);
+        IX c = clone(s);
         if (c == NIL) return;
         se(c).type = T_CURRENT;
         if (r.kind == PK_LOGICAL && (TM && r.absent)) {  // AbsentLogicalPreStateProcessor.addEveryState :99-118
@@ -647,7 +669,7 @@ struct CtxT {
         const StateRow& r = P->st[p];
         PState& st = ps(p);
         if (r.is_start && (!st.initialized || r.next_every >= 0 || (r.seq && r.next >= 0 && is_absent(r.next)))) {
-            int16_t s = se_alloc();
+            IX s = se_alloc();
             if (s == NIL) return;
             add_state(p, s);
             st.initialized = 1;
@@ -696,16 +718,16 @@ struct CtxT {
 
     SDG_HD void expire_events(int p, int64_t now) {  // :326-361
         PState& st = ps(p);
-        int16_t expired = NIL;
-        int16_t* pd = pend(p);
+        IX expired = NIL;
+        IX* pd = pend(p);
         while (st.pn > 0 && is_expired(pd[0], now)) {
-            int16_t s = pd[0];
+            IX s = pd[0];
             erase(pd, st.pn, 0);
             if (se(s).type != T_EXPIRED) { se(s).type = T_EXPIRED; expired = s; }
         }
-        int16_t* nw = newe(p);
+        IX* nw = newe(p);
         for (int j = 0; j < st.nw;) {
-            int16_t s = nw[j];
+            IX s = nw[j];
             if (is_expired(s, now)) {
                 erase(nw, st.nw, j);
                 if (se(s).type != T_EXPIRED) { se(s).type = T_EXPIRED; expired = s; }
@@ -728,7 +750,7 @@ struct CtxT {
     }
 
     // ---- post-state processors ---------------------------------------------------------------------------
-    SDG_HD void post_stream(int p, int16_t s) {  // StreamPostStateProcessor.process :64-83
+    SDG_HD void post_stream(int p, IX s) {  // StreamPostStateProcessor.process :64-83
         const StateRow& r = P->st[p];
         ps(p).changed = 1;
         se(s).ts = rc(nd(slots(s)[p]).rec).ts;
@@ -737,7 +759,7 @@ struct CtxT {
         if (r.next_every >= 0) add_every_state(r.next_every, s);
         if (r.callback >= 0) start_state_reset(r.callback);
     }
-    SDG_HD void count_min_reached(int p, int16_t s) {  // CountPostStateProcessor.processMinCountReached
+    SDG_HD void count_min_reached(int p, IX s) {  // CountPostStateProcessor.processMinCountReached
         const StateRow& r = P->st[p];
         if (r.selector_after) {
             ps(p).changed = 1;
@@ -746,9 +768,9 @@ struct CtxT {
         if (r.next >= 0) add_state(r.next, s);
         if (r.next_every >= 0) add_every_state(r.next_every, s);
     }
-    SDG_HD void post_count(int p, int16_t s) {  // CountPostStateProcessor.process :39-79
+    SDG_HD void post_count(int p, IX s) {  // CountPostStateProcessor.process :39-79
         const StateRow& r = P->st[p];
-        int16_t e = slots(s)[p];
+        IX e = slots(s)[p];
         int n = 1;
         while (nd(e).next != NIL) { ++n; e = nd(e).next; }
         ps(p).success = 1;
@@ -763,7 +785,7 @@ struct CtxT {
             if (n == r.max_count) ps(p).changed = 1;
         }
     }
-    SDG_HD bool partner_can_proceed(int q, int16_t s) {  // AbsentLogicalPreStateProcessor.partnerCanProceed :353-388
+    SDG_HD bool partner_can_proceed(int q, IX s) {  // AbsentLogicalPreStateProcessor.partnerCanProceed :353-388
         const StateRow& r = P->st[q];
         PState& st = ps(q);
         if (r.seq && r.next_every < 0 && st.last_arrival > 0) return false;
@@ -778,7 +800,7 @@ struct CtxT {
         }
         return slots(s)[q] != NIL;
     }
-    SDG_HD void post_absent(int p, int16_t s) {  // AbsentStreamPostStateProcessor.process :36-56
+    SDG_HD void post_absent(int p, IX s) {  // AbsentStreamPostStateProcessor.process :36-56
         const StateRow& r = P->st[p];
         ps(p).changed = 1;
         const int64_t ts = rc(nd(slots(s)[p]).rec).ts;
@@ -788,7 +810,7 @@ struct CtxT {
         ps(p).last_sched = ts + r.waiting_ms;  // updateLastArrivalTime :68-78
         notify_at(r.sched, ps(p).last_sched);
     }
-    SDG_HD void post_logical(int p, int16_t s) {  // LogicalPostStateProcessor.process :59-87
+    SDG_HD void post_logical(int p, IX s) {  // LogicalPostStateProcessor.process :59-87
         const StateRow& r = P->st[p];
         if ((TM && r.absent)) {  // AbsentLogicalPostStateProcessor.process :37-49
             ps(p).changed = 1;
@@ -807,7 +829,7 @@ struct CtxT {
             if (P->st[r.partner].selector_after && r.last == r.partner) ps(r.partner).returned = 1;
         }
     }
-    SDG_HD void post(int p, int16_t s) {
+    SDG_HD void post(int p, IX s) {
         switch (P->st[p].kind) {
             case PK_COUNT: post_count(p, s); break;
             case PK_LOGICAL: post_logical(p, s); break;
@@ -819,7 +841,7 @@ struct CtxT {
     }
 
     // process(StateEvent): filters then post
-    SDG_HD void process_se(int p, int16_t s) {
+    SDG_HD void process_se(int p, IX s) {
         ps(p).changed = 0;
         if (filter(p, s)) post(p, s);
     }
@@ -828,20 +850,20 @@ struct CtxT {
     // (StateMultiProcessStreamReceiver.processAndClear :47-68), so they are collected first
     // AbsentLogicalPreStateProcessor.processAndReturn :262-319: a matching event removes the absence candidate; it
     // never returns a match itself
-    SDG_HD void alogic_process_and_return(int p, int16_t rec) {
+    SDG_HD void alogic_process_and_return(int p, IX rec) {
         const StateRow& r = P->st[p];
         PState& st = ps(p);
         if (!st.active) return;
-        int16_t* pd = pend(p);
+        IX* pd = pend(p);
         for (int j = 0; j < st.pn;) {
             if (ovf()) return;
-            const int16_t s = pd[j];
+            const IX s = pd[j];
             if (r.logical_or && slots(s)[r.partner] != NIL) {
                 erase(pd, st.pn, j);
                 continue;
             }
-            const int16_t cur = slots(s)[p];
-            const int16_t n = nd_alloc(rec);
+            const IX cur = slots(s)[p];
+            const IX n = nd_alloc(rec);
             if (n == NIL) return;
             slots(s)[p] = n;
             process_se(p, s);
@@ -853,7 +875,7 @@ struct CtxT {
                 removed = true;
                 if (r.seq) {  // partner's pending list .remove(stateEvent): first occurrence
                     PState& qs = ps(r.partner);
-                    int16_t* qp = pend(r.partner);
+                    IX* qp = pend(r.partner);
                     for (int i = 0; i < qs.pn; ++i)
                         if (qp[i] == s) { erase(qp, qs.pn, i); break; }
                 }
@@ -870,7 +892,7 @@ struct CtxT {
         }
     }
 
-    SDG_HD void process_and_return(int p, int16_t rec, bool selector) {
+    SDG_HD void process_and_return(int p, IX rec, bool selector) {
         const StateRow& r = P->st[p];
         PState& st = ps(p);
         if (r.kind == PK_LOGICAL && (TM && r.absent)) {
@@ -883,19 +905,19 @@ struct CtxT {
             if (!st.active) return;
             selector = false;
         }
-        int16_t* pd = pend(p);
+        IX* pd = pend(p);
         const int last = r.last;
-        int16_t* ret = (int16_t*)(base + L.off_ret);
+        IX* ret = (IX*)(base + L.off_ret);
         int nret = 0;
         for (int j = 0; j < st.pn;) {
             if (ovf()) return;
-            int16_t s = pd[j];
+            IX s = pd[j];
             if (r.kind == PK_COUNT) {  // :60-66
                 if ((p + 1 < L.n_states && slots(s)[p + 1] != NIL) || (p + 2 < L.n_states && slots(s)[p + 2] != NIL)) {
                     erase(pd, st.pn, j);
                     continue;
                 }
-                int16_t n = nd_alloc(rec);
+                IX n = nd_alloc(rec);
                 if (n == NIL) return;
                 add_event(s, p, n);
                 st.success = 0;
@@ -904,11 +926,11 @@ struct CtxT {
                     erase(pd, st.pn, j);
                     continue;
                 }
-                int16_t n = nd_alloc(rec);
+                IX n = nd_alloc(rec);
                 if (n == NIL) return;
                 slots(s)[p] = n;
             } else {
-                int16_t n = nd_alloc(rec);
+                IX n = nd_alloc(rec);
                 if (n == NIL) return;
                 slots(s)[p] = n;
             }
@@ -950,7 +972,7 @@ struct CtxT {
 
     // ---- timers ------------------------------------------------------------------------------------------
     // AbsentStreamPreStateProcessor.sendEvent :238-254
-    SDG_HD void absent_send(int p, int16_t s) {
+    SDG_HD void absent_send(int p, IX s) {
         const StateRow& r = P->st[p];
         if (r.selector_after) emit(s);
         if (r.next >= 0) add_state(r.next, s);
@@ -966,18 +988,18 @@ struct CtxT {
         bool initialize = r.is_start && st.nw == 0 && st.pn == 0;
         if (initialize && r.seq && r.next_every < 0 && st.last_sched > 0) initialize = false;
         if (initialize) {
-            const int16_t s = se_alloc();
+            const IX s = se_alloc();
             if (s == NIL) return;
             add_state(p, s);
         } else if (r.seq && st.nw != 0) {
             reset_state(p);
         }
         update_state(p);
-        int16_t* pd = pend(p);
-        int16_t* ret = (int16_t*)(base + L.off_ret);
+        IX* pd = pend(p);
+        IX* ret = (IX*)(base + L.off_ret);
         int nret = 0;
         for (int j = 0; j < st.pn;) {
-            const int16_t s = pd[j];
+            const IX s = pd[j];
             if (is_expired(s, now)) {
                 erase(pd, st.pn, j);
                 if (r.within_every >= 0 && r.next_every != p) {
@@ -1011,7 +1033,7 @@ struct CtxT {
         }
     }
     // AbsentLogicalPreStateProcessor.sendEvent :230-250
-    SDG_HD void alogic_send(int p, int16_t s) {
+    SDG_HD void alogic_send(int p, IX s) {
         const StateRow& r = P->st[p];
         if (r.selector_after) emit(s);
         if (r.next >= 0) add_state(r.next, s);
@@ -1031,32 +1053,32 @@ struct CtxT {
         bool not_processed = true;
         if (now >= st.last_arrival + r.waiting_ms) {
             if (r.is_start && r.seq && st.nw == 0 && st.pn == 0) {
-                const int16_t s = se_alloc();
+                const IX s = se_alloc();
                 if (s == NIL) return;
                 add_state(p, s);
             } else if (r.seq && st.nw != 0) {
                 reset_state(p);
             }
             update_state(p);
-            int16_t expired = NIL;
-            int16_t* pd = pend(p);
-            int16_t* ret = (int16_t*)(base + L.off_ret);
+            IX expired = NIL;
+            IX* pd = pend(p);
+            IX* ret = (IX*)(base + L.off_ret);
             int nret = 0;
             for (int j = 0; j < st.pn;) {
-                const int16_t s = pd[j];
+                const IX s = pd[j];
                 if (is_expired(s, now)) {  // within
                     expired = s;
                     erase(pd, st.pn, j);
                     continue;
                 }
-                const int16_t own = slots(s)[p];
+                const IX own = slots(s)[p];
                 const bool passed = own == NIL ? now >= se(s).ts + r.waiting_ms
                                                : now >= rc(nd(own).rec).ts + r.waiting_ms;  // waitingTimePassed
                 if (passed) {
                     erase(pd, st.pn, j);
                     const bool partner_in = slots(s)[r.partner] != NIL;
                     if (r.logical_or && !partner_in) {  // OR partner not received
-                        const int16_t n = empty_node();
+                        const IX n = empty_node();
                         if (n == NIL) return;
                         add_event(s, p, n);
                         if (nret >= L.lcap) { set_ovf(); return; }
@@ -1065,7 +1087,7 @@ struct CtxT {
                         if (nret >= L.lcap) { set_ovf(); return; }
                         ret[nret++] = s;
                     } else if (!r.logical_or) {  // AND partner not received: let it proceed
-                        const int16_t n = empty_node();
+                        const IX n = empty_node();
                         if (n == NIL) return;
                         add_event(s, p, n);
                     }
@@ -1187,7 +1209,7 @@ struct CtxT {
         absent_gc();
     }
 
-    SDG_HD void on_event(int qs, int16_t rec, int64_t ts) {
+    SDG_HD void on_event(int qs, IX rec, int64_t ts) {
         const RecvRow& rv = P->recv[qs];
         // stabilizeStates (state/receiver/*ProcessStreamReceiver.java)
         for (int i = 0; i < P->n_expire; ++i) expire_events(P->expire_seq[i], ts);
@@ -1218,8 +1240,8 @@ struct CtxT {
 constexpr int IDLE_PER_STATE = 12;  // 8 PState flag bytes, int16 pending / newAndEvery seed counts
 SDG_HD int idle_bytes(int n_states) { return (4 + IDLE_PER_STATE * n_states + 15) & ~15; }
 
-template <bool TM>
-SDG_HD bool to_idle(CtxT<TM>& c, uint8_t* rec) {
+template <bool TM, class IX>
+SDG_HD bool to_idle(CtxT<TM, IX>& c, uint8_t* rec) {
     if (c.ovf()) return false;
     KHead& h = c.head();
     if (!(h.flags & 2)) return false;
@@ -1227,16 +1249,16 @@ SDG_HD bool to_idle(CtxT<TM>& c, uint8_t* rec) {
     if (h.nd_used || h.rc_used) return false;
     int entries = 0;
     for (int p = 0; p < c.L.n_states; ++p) {
-        const PState& st = c.ps(p);
+        const auto& st = c.ps(p);
         if (st.last_sched || st.last_arrival) return false;
         if (!c.P->st[p].is_start && (st.pn || st.nw)) return false;
         for (int l = 0; l < 2; ++l) {
-            const int16_t* lst = l ? c.newe(p) : c.pend(p);
+            const IX* lst = l ? c.newe(p) : c.pend(p);
             const int n = l ? st.nw : st.pn;
             for (int j = 0; j < n; ++j) {
-                const SE& e = c.se(lst[j]);
+                const auto& e = c.se(lst[j]);
                 if (e.type != T_CURRENT || e.ts != -1) return false;
-                const int16_t* sl = c.slots(lst[j]);
+                const IX* sl = c.slots(lst[j]);
                 for (int k = 0; k < c.L.n_states; ++k)
                     if (sl[k] != NIL) return false;
             }
@@ -1247,30 +1269,30 @@ SDG_HD bool to_idle(CtxT<TM>& c, uint8_t* rec) {
     *(int32_t*)rec = h.flags;
     for (int p = 0; p < c.L.n_states; ++p) {
         uint8_t* r = rec + 4 + IDLE_PER_STATE * p;
-        const PState& st = c.ps(p);
+        const auto& st = c.ps(p);
         const uint8_t* f = &st.changed;  // the 8 flag bytes: changed .. pad
         for (int b = 0; b < 8; ++b) r[b] = f[b];
-        *(int16_t*)(r + 8) = st.pn;
-        *(int16_t*)(r + 10) = st.nw;
+        *(int16_t*)(r + 8) = (int16_t)st.pn;  // (reclaiming device queries only: int16 counts)
+        *(int16_t*)(r + 10) = (int16_t)st.nw;
     }
     return true;
 }
 
-template <bool TM>
-SDG_HD void from_idle(CtxT<TM>& c, const uint8_t* rec) {
+template <bool TM, class IX>
+SDG_HD void from_idle(CtxT<TM, IX>& c, const uint8_t* rec) {
     c.arena_init();
     c.head().flags = *(const int32_t*)rec;
     for (int p = 0; p < c.L.n_states; ++p) {
         const uint8_t* r = rec + 4 + IDLE_PER_STATE * p;
         const int16_t pn = *(const int16_t*)(r + 8), nw = *(const int16_t*)(r + 10);
         if (!c.P->st[p].is_start) continue;  // destroyed: fresh (arena_init)
-        PState& st = c.ps(p);
+        auto& st = c.ps(p);
         uint8_t* f = &st.changed;
         for (int b = 0; b < 8; ++b) f[b] = r[b];
         for (int l = 0; l < 2; ++l) {
             const int n = l ? nw : pn;
             for (int j = 0; j < n; ++j) {
-                const int16_t s = c.se_alloc();
+                const IX s = c.se_alloc();
                 if (s == NIL) return;
                 if (l) c.push(c.newe(p), st.nw, s);
                 else c.push(c.pend(p), st.pn, s);
@@ -1279,12 +1301,13 @@ SDG_HD void from_idle(CtxT<TM>& c, const uint8_t* rec) {
     }
 }
 
-// one key's committed arena into a larger layout (more partial-match slots, same states / columns / schedulers):
+// one key's committed arena into a larger layout (more partial-match slots, same states / columns / schedulers),
+// possibly of a wider index type (SIX: the source's -- a key the host takes over moves from int16 to int32 indices):
 // header, processor states, the lists (re-strided), timer queues (unrolled to start at 0) and every pool object at
 // its index; the free lists are then rebuilt by a mark-sweep in the new layout (the lists are the only roots
 // between batches), which also frees the new slots
-template <bool TM>
-SDG_HD void migrate_key(CtxT<TM>& d, const uint8_t* src, const Layout& Ls) {
+template <class SIX = int16_t, bool TM, class IX>
+SDG_HD void migrate_key(CtxT<TM, IX>& d, const uint8_t* src, const Layout& Ls) {
     const Layout& Ld = d.L;
     uint8_t* dst = d.base;
     for (int64_t i = 0; i < Ld.bytes; ++i) dst[i] = 0;
@@ -1292,42 +1315,75 @@ SDG_HD void migrate_key(CtxT<TM>& d, const uint8_t* src, const Layout& Ls) {
     if (!(sh->flags & 2)) return;  // never initialised: stays zero (= fresh)
     d.head() = *sh;
     for (int p = 0; p < Ld.n_states; ++p) {
-        d.ps(p) = ((const PState*)(src + Ls.off_ps))[p];
-        const int16_t* sp = (const int16_t*)(src + Ls.off_pend) + (int64_t)p * Ls.lcap;
-        const int16_t* sn = (const int16_t*)(src + Ls.off_newe) + (int64_t)p * Ls.lcap;
-        for (int j = 0; j < d.ps(p).pn; ++j) d.pend(p)[j] = sp[j];
-        for (int j = 0; j < d.ps(p).nw; ++j) d.newe(p)[j] = sn[j];
+        const PStateT<SIX>& sp0 = ((const PStateT<SIX>*)(src + Ls.off_ps))[p];
+        auto& dp = d.ps(p);
+        dp.changed = sp0.changed;
+        dp.initialized = sp0.initialized;
+        dp.success = sp0.success;
+        dp.start_reset = sp0.start_reset;
+        dp.active = sp0.active;
+        dp.started = sp0.started;
+        dp.returned = sp0.returned;
+        dp.last_sched = sp0.last_sched;
+        dp.last_arrival = sp0.last_arrival;
+        dp.pn = sp0.pn;
+        dp.nw = sp0.nw;
+        const SIX* sp = (const SIX*)(src + Ls.off_pend) + (int64_t)p * Ls.lcap;
+        const SIX* sn = (const SIX*)(src + Ls.off_newe) + (int64_t)p * Ls.lcap;
+        for (int j = 0; j < dp.pn; ++j) d.pend(p)[j] = sp[j];
+        for (int j = 0; j < dp.nw; ++j) d.newe(p)[j] = sn[j];
     }
     for (int q = 0; q < Ld.n_sched; ++q) {
-        TQ t = ((const TQ*)(src + Ls.off_tq))[q];
+        const TQT<SIX>& t = ((const TQT<SIX>*)(src + Ls.off_tq))[q];
         const int64_t* st = (const int64_t*)(src + Ls.off_tqt) + (int64_t)q * Ls.qcap;
         for (int j = 0; j < t.n; ++j) d.tqt(q)[j] = st[(t.h + j) % Ls.qcap];
-        t.h = 0;
-        d.tq(q) = t;
+        auto& dt = d.tq(q);
+        dt.earliest = t.earliest;
+        dt.created = t.created;
+        dt.h = 0;
+        dt.n = t.n;
     }
-    for (int i = 0; i < Ls.ns; ++i)
-        for (int b = 0; b < Ls.se_bytes; ++b) ((uint8_t*)&d.se(i))[b] = src[Ls.off_se + (int64_t)i * Ls.se_bytes + b];
-    for (int i = 0; i < Ls.nn; ++i) d.nd(i) = ((const Node*)(src + Ls.off_nd))[i];
-    for (int i = 0; i < Ls.nr; ++i)
-        for (int b = 0; b < Ls.rc_bytes; ++b) ((uint8_t*)&d.rc(i))[b] = src[Ls.off_rc + (int64_t)i * Ls.rc_bytes + b];
+    for (int i = 0; i < Ls.ns; ++i) {  // (every index is < the source's pool sizes: it fits the destination's type)
+        const SET<SIX>& se = *(const SET<SIX>*)(src + Ls.off_se + (int64_t)i * Ls.se_bytes);
+        auto& de = d.se(i);
+        de.type = se.type;
+        de.mark = se.mark;
+        de.ts = se.ts;
+        const SIX* ss = (const SIX*)((const uint8_t*)&se + sizeof(SET<SIX>));
+        IX* ds = d.slots(i);
+        for (int k = 0; k < Ld.n_states; ++k) ds[k] = (IX)ss[k];
+    }
+    for (int i = 0; i < Ls.nn; ++i) {
+        const NodeT<SIX>& n = ((const NodeT<SIX>*)(src + Ls.off_nd))[i];
+        d.nd(i).rec = n.rec;
+        d.nd(i).next = n.next;
+    }
+    for (int i = 0; i < Ls.nr; ++i) {
+        const RecT<SIX>& r = *(const RecT<SIX>*)(src + Ls.off_rc + (int64_t)i * Ls.rc_bytes);
+        auto& dr = d.rc(i);
+        dr.nullmask = r.nullmask;
+        dr.ts = r.ts;
+        const int64_t* sv = (const int64_t*)((const uint8_t*)&r + sizeof(RecT<SIX>));
+        for (int c = 0; c < Ld.n_cols; ++c) d.vals(i)[c] = sv[c];
+    }
     d.head().flags &= ~1;
     d.gc();
 }
 
-template <bool TM>
-SDG_HD void SEAccT<TM>::load(int slot, int col, int chain, uint8_t kind, int64_t* v, bool* null) {
+template <bool TM, class IX>
+SDG_HD void SEAccT<TM, IX>::load(int slot, int col, int chain, uint8_t kind, int64_t* v, bool* null) {
     (void)kind;
     *v = 0;
     *null = true;
     if (slot < 0 || slot >= c->L.n_states) return;
-    int16_t e = c->chain_at(se, slot, chain);
+    IX e = c->chain_at(se, slot, chain);
     if (e == NIL) return;
-    int16_t r = c->nd(e).rec;
+    IX r = c->nd(e).rec;
     *v = c->vals(r)[col];
     *null = (c->rc(r).nullmask >> col) & 1u;
 }
-template <bool TM>
-SDG_HD bool SEAccT<TM>::slot_empty(int slot, int chain) {
+template <bool TM, class IX>
+SDG_HD bool SEAccT<TM, IX>::slot_empty(int slot, int chain) {
     if (slot < 0 || slot >= c->L.n_states) return true;
     return c->chain_at(se, slot, chain) == NIL;
 }
@@ -1351,8 +1407,8 @@ struct KeyEvents {
 // one key's batch run, in steps (the device composes them in run_key; the host scheduler simulation steps a key
 // itself when it has to take it over, sched.h): initPartition on the key's first event ever (unpartitioned
 // queries: before position 0, as SiddhiAppRuntime.start does), each row through the receiver, timer fires between
-template <bool TM>
-SDG_HD bool key_begin(CtxT<TM>& c, const KeyEvents& ev) {  // returns need_init (a partitioned first-seen key)
+template <bool TM, class IX>
+SDG_HD bool key_begin(CtxT<TM, IX>& c, const KeyEvents& ev) {  // returns need_init (a partitioned first-seen key)
     const Plan* P = c.P;
     c.seq_base = ev.seq_base;
     c.fsched = -1;
@@ -1375,8 +1431,8 @@ SDG_HD bool key_begin(CtxT<TM>& c, const KeyEvents& ev) {  // returns need_init 
 }
 SDG_HD int64_t key_pos(const KeyEvents& ev, int64_t p) { return ev.pos_off + (ev.orig ? (int64_t)ev.orig[p] : p); }
 // row p (fires due before it have run); returns false when the key overflowed
-template <bool TM>
-SDG_HD bool key_row(CtxT<TM>& c, const KeyEvents& ev, int64_t p, bool& need_init) {
+template <bool TM, class IX>
+SDG_HD bool key_row(CtxT<TM, IX>& c, const KeyEvents& ev, int64_t p, bool& need_init) {
     const Plan* P = c.P;
     const int64_t g = key_pos(ev, p);
     c.pos = g;
@@ -1400,9 +1456,9 @@ SDG_HD bool key_row(CtxT<TM>& c, const KeyEvents& ev, int64_t p, bool& need_init
         need_init = false;
     }
     c.maybe_gc();
-    int16_t r = c.rc_alloc();
+    IX r = c.rc_alloc();
     if (r == NIL) return false;
-    Rec& rec = c.rc(r);
+    auto& rec = c.rc(r);
     const int64_t ts = ev.ts[p];
     rec.ts = ts;
     int64_t* v = c.vals(r);
@@ -1418,8 +1474,8 @@ SDG_HD bool key_row(CtxT<TM>& c, const KeyEvents& ev, int64_t p, bool& need_init
     if (TM && P->n_sched) c.absent_gc();
     return !c.ovf();
 }
-template <bool TM>
-SDG_HD void run_key(CtxT<TM>& c, const KeyEvents& ev) {
+template <bool TM, class IX>
+SDG_HD void run_key(CtxT<TM, IX>& c, const KeyEvents& ev) {
     bool need_init = key_begin(c, ev);
     for (int64_t p = ev.b; p < ev.e && !c.ovf(); ++p) {
         c.fire_until(key_pos(ev, p));  // TimeChangeListener.onTimeChange runs before the event is processed

@@ -294,6 +294,10 @@ struct NfaArgs {
     int32_t nlist;
     const uint32_t* fire_off;
     const nfa::TimerFire* fires;
+    // keys whose run overflowed the arena (the host takes them over when the layout is at its largest)
+    uint32_t* ovf_keys;               // [ovf_cap] (nullptr: not recorded)
+    unsigned int* ovf_count;
+    int32_t ovf_cap;
 };
 // ---- register sequence kernel (seq3.hip): SEQUENCE `every e1=S[f1], e2=S[f2]<m:n>, e3=S[f3]` ------------------
 // Per partition key the reference holds at most one partial waiting at e2 (Q) and one at e3 (P; the same object as Q

@@ -365,6 +365,15 @@ __global__ __launch_bounds__(256) void rx_segments(const uint32_t* __restrict__ 
 #endif
 // one lane per key: the key's arena is private to the lane, so the state machine runs without atomics; only
 // the output slot and log reservations are shared
+// a key's run overflowed its arena: the flag the host checks, and the key on the list it takes spilled keys from
+__device__ __forceinline__ void note_overflow(const NfaArgs& a, int64_t k) {
+    atomicOr(&a.flags[2], 1);
+    if (a.ovf_keys) {
+        const unsigned i = atomicAdd(a.ovf_count, 1u);
+        if (i < (unsigned)a.ovf_cap) a.ovf_keys[i] = (uint32_t)k;
+    }
+}
+
 template <bool TM>
 __global__ __launch_bounds__(256, TM ? 1 : SDG_NFA_MINB) void nfa_k(const NfaArgs* __restrict__ pa) {
     // arguments from a device copy: indexing a by-value kernel argument (cols[col]) makes the compiler copy the
@@ -400,6 +409,7 @@ __global__ __launch_bounds__(256, TM ? 1 : SDG_NFA_MINB) void nfa_k(const NfaArg
         if (a.cur[s]) src = a.arena2 + s * kb;
         else dst = a.arena2 + s * kb;
     }
+    if (!from && (((const nfa::KHead*)src)->flags & nfa::KH_HOST)) return;  // a spilled key: the host runs it
     if (!a.list && b >= e && P->partitioned) {
         // no event of this key: it runs only for its queued timers (initPartition happens at a first event)
         const nfa::KHead* h = (const nfa::KHead*)src;
@@ -455,7 +465,7 @@ __global__ __launch_bounds__(256, TM ? 1 : SDG_NFA_MINB) void nfa_k(const NfaArg
     if (a.last_seen) a.last_seen[k] = c.purge.last ^ INT64_MIN;
     if (a.agg_reset && c.purge_pending) a.agg_reset[k] = 1;
     if (a.releasable) a.releasable[s] = nfa::to_idle(c, a.idle_out + s * a.idle_bytes) ? 1 : 0;
-    if (c.ovf()) atomicOr(&a.flags[2], 1);
+    if (c.ovf()) note_overflow(a, k);
 }
 
 // The same state machine with each key's arena staged in LDS (nfa_k walks it in HBM: one lane per key, every
@@ -515,7 +525,8 @@ __global__ __launch_bounds__(64) void nfa_lds_k(const NfaArgs* __restrict__ pa, 
             if (a.cur[s]) src = a.arena2 + s * kb;
             else dst = a.arena2 + s * kb;
         }
-        if (!a.list && b >= e && P->partitioned) {
+        if (!from && (((const nfa::KHead*)src)->flags & nfa::KH_HOST)) active = false;  // spilled: the host runs it
+        if (active && !a.list && b >= e && P->partitioned) {
             // no event of this key: it runs only for its queued timers (initPartition happens at a first event)
             const nfa::KHead* h = (const nfa::KHead*)src;
             if (!(h->flags & 2) || P->n_sched == 0) {
@@ -581,7 +592,7 @@ __global__ __launch_bounds__(64) void nfa_lds_k(const NfaArgs* __restrict__ pa, 
         ovf = c.ovf();
         if (dst != src) a.ran[s] = 1;
     }
-    if (ovf) atomicOr(&a.flags[2], 1);
+    if (ovf) note_overflow(a, k);
     __syncthreads();
     // write back into the working copy
     for (uint64_t m = __ballot(active); m; m &= m - 1) {
@@ -612,7 +623,8 @@ __device__ __forceinline__ bool has_rows(const uint32_t* seg_start, const uint32
 __global__ __launch_bounds__(256) void nfa_slots_need_k(SlotPool sp, const uint32_t* __restrict__ seg_start,
                                                         const uint32_t* __restrict__ seg_end, int64_t K) {
     const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const bool need = k < K && sp.slot_of[k] < 0 && has_rows(seg_start, seg_end, k);
+    // (-1 never seen, -2 idle: a slot for a key with rows; -3: spilled, the host runs it)
+    const bool need = k < K && (sp.slot_of[k] == -1 || sp.slot_of[k] == -2) && has_rows(seg_start, seg_end, k);
     const uint64_t m = __ballot(need);
     if (m && lane_id() == __ffsll((unsigned long long)m) - 1) atomicAdd(&sp.counters[1], (unsigned)__popcll(m));
 }
@@ -621,7 +633,7 @@ __global__ __launch_bounds__(256) void nfa_slots_assign_k(SlotPool sp, const uin
     const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (k >= K) return;
     const int32_t cur = sp.slot_of[k];
-    if (cur >= 0 || !has_rows(seg_start, seg_end, k)) return;
+    if ((cur != -1 && cur != -2) || !has_rows(seg_start, seg_end, k)) return;
     const unsigned top = atomicSub(&sp.counters[0], 1u);  // (the host grew the pool to cover every such key)
     const int32_t s = sp.free_slots[top - 1];
     sp.slot_of[k] = s;

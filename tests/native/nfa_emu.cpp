@@ -63,6 +63,11 @@ struct EmuQuery {
     std::vector<Out> outs;
     bool bcast = false;              // a stream without a partition key: rows to every key, in korder order
     PartitionKeyOrder korder;
+    struct Spilled {                 // as QueryRt::spill: keys past the device's 4096 partials, 32-bit arenas
+        nfa::Layout L{};
+        std::vector<uint8_t> arena;
+    };
+    std::map<uint32_t, Spilled> spill;
 };
 
 struct Emu {
@@ -115,7 +120,8 @@ size_t reordered_ = 0, taken_ = 0, exact_passes_ = 0;
 double us_[3] = {0, 0, 0};
 int g_reclaim = 0;      // emu_set_reclaim: every idle key goes through its idle record after each run (nfa.h to_idle)
 int64_t idles_ = 0;     // keys rebuilt from an idle record (all flushes)
-int64_t growths_ = 0;  // arena doublings (all flushes)  // cumulative: optimistic pass, reruns, exact pass (microseconds)  // last flush's scheduler statistics (tests)
+int64_t growths_ = 0;
+int64_t spills_ = 0;    // keys moved to a 32-bit host arena (all flushes)  // arena doublings (all flushes)  // cumulative: optimistic pass, reruns, exact pass (microseconds)  // last flush's scheduler statistics (tests)
 
 int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
     HostQuery& h = q.hq;
@@ -222,41 +228,89 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
         grow(o_nulls, cap); grow(o_key, cap);
         unsigned long long count = 0, lcount = 0;
         int flags[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        nfa::CtxT<true> c;
-        c.P = &P;
-        c.code = h.code.data();
-        c.consts = h.consts.data();
-        c.L = q.L;
-        c.base = q.arenas[k].data();
-        c.stk = stk.data();
-        c.stride = 1;
-        c.emit_ts = o_ts.data();
-        c.emit_vals = o_vals.data();
-        c.emit_nulls = o_nulls.data();
-        c.emit_seq = o_seq.data();
-        c.emit_sub = o_sub.data();
-        c.emit_key = o_key.data();
-        c.emit_round = nullptr;
-        c.round = 0;
-        c.emit_count = &count;
-        c.emit_cap = cap;
-        c.flags = flags;
-        c.key = k;
-        c.T.G = bc.G;
-        c.T.clk = bc.clk.data();
-        c.T.nadv = bc.nadv.data();
-        c.T.clock0 = bc.clock0;
-        c.T.live = !e->app.playback;
-        c.T.log = q.sim.active() ? logs.data() : nullptr;
-        c.T.log_count = &lcount;
-        c.T.log_cap = (int64_t)logs.size();
-        c.fires = fires;
-        c.nfires = nfires;
+        auto setup = [&](auto& c, const nfa::Layout& L, uint8_t* base) {
+            count = lcount = 0;
+            std::fill(flags, flags + 8, 0);
+            c.P = &P;
+            c.code = h.code.data();
+            c.consts = h.consts.data();
+            c.L = L;
+            c.base = base;
+            c.stk = stk.data();
+            c.stride = 1;
+            c.emit_ts = o_ts.data();
+            c.emit_vals = o_vals.data();
+            c.emit_nulls = o_nulls.data();
+            c.emit_seq = o_seq.data();
+            c.emit_sub = o_sub.data();
+            c.emit_key = o_key.data();
+            c.emit_round = nullptr;
+            c.round = 0;
+            c.emit_count = &count;
+            c.emit_cap = cap;
+            c.flags = flags;
+            c.key = k;
+            c.T.G = bc.G;
+            c.T.clk = bc.clk.data();
+            c.T.nadv = bc.nadv.data();
+            c.T.clock0 = bc.clock0;
+            c.T.live = !e->app.playback;
+            c.T.log = q.sim.active() ? logs.data() : nullptr;
+            c.T.log_count = &lcount;
+            c.T.log_cap = (int64_t)logs.size();
+            c.fires = fires;
+            c.nfires = nfires;
+        };
         nfa::KeyEvents kev{ts.data(), qs.data(), gpos.data(), cptr.data(), nptr.data(), seg_b.size() > k ? seg_b[k] : 0,
                            seg_e.size() > k ? seg_e[k] : 0, e->seq, 0, q.bcast ? vrank.data() : nullptr};
         if (kev.b > kev.e) kev.b = kev.e;
-        nfa::run_key(c, kev);
-        if (c.ovf()) {
+        nfa::CtxT<true> c;
+        auto spilled = q.spill.find(k);
+        if (spilled == q.spill.end()) {
+            setup(c, q.L, q.arenas[k].data());
+            nfa::run_key(c, kev);
+            // as the engine: a key past the largest device layout goes on on the host in a 32-bit layout of twice
+            // the slots (queries without timers), from its batch-start state
+            if (c.ovf() && q.L.ns >= 4096 && P.n_sched == 0 && !(P.purge && P.n_agg > 0)) {
+                EmuQuery::Spilled& sp = q.spill[k];
+                sp.L = nfa::make_layout<int32_t>(P.n_states, std::max(nc, 1), 2 * q.L.ns, P.n_sched);
+                sp.arena.assign((size_t)sp.L.bytes, 0);
+                nfa::CtxT<true, int32_t> d;
+                d.P = &P;
+                d.L = sp.L;
+                d.base = sp.arena.data();
+                nfa::migrate_key<int16_t>(d, backup[k].data(), q.L);
+                q.arenas[k] = backup[k];
+                ++spills_;
+                spilled = q.spill.find(k);
+            }
+        }
+        if (spilled != q.spill.end()) {
+            EmuQuery::Spilled& sp = spilled->second;
+            for (;;) {
+                std::vector<uint8_t> work = sp.arena;  // batch-start state
+                nfa::CtxT<true, int32_t> c32;
+                setup(c32, sp.L, work.data());
+                nfa::run_key(c32, kev);
+                if (!c32.ovf()) {
+                    sp.arena.swap(work);
+                    break;
+                }
+                if (sp.L.ns >= (1 << 22)) {
+                    g_err = "query '" + h.name + "': partial-match arena overflow (spilled key)";
+                    return 3;
+                }
+                const nfa::Layout Ln = nfa::make_layout<int32_t>(P.n_states, std::max(nc, 1), 2 * sp.L.ns, P.n_sched);
+                std::vector<uint8_t> na((size_t)Ln.bytes, 0);
+                nfa::CtxT<true, int32_t> d;
+                d.P = &P;
+                d.L = Ln;
+                d.base = na.data();
+                nfa::migrate_key<int32_t>(d, sp.arena.data(), sp.L);
+                sp.arena.swap(na);
+                sp.L = Ln;
+            }
+        } else if (c.ovf()) {
             g_err = "query '" + h.name + "': partial-match arena overflow";
             arena_ovf = true;
             return 3;
@@ -275,7 +329,7 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
         klog[k].assign(logs.begin(), logs.begin() + (int64_t)lcount);
         // as the engine's reclaiming queries: a key that ends idle keeps only its idle record; its arena is rebuilt
         // from it (here at once, on the device at the key's next batch -- the same state)
-        if (g_reclaim && P.partitioned && P.n_sched == 0 && !P.purge) {
+        if (g_reclaim && P.partitioned && P.n_sched == 0 && !P.purge && spilled == q.spill.end()) {
             std::vector<uint8_t> rec((size_t)nfa::idle_bytes(P.n_states));
             if (nfa::to_idle(c, rec.data())) {
                 std::fill(q.arenas[k].begin(), q.arenas[k].end(), 0);
@@ -556,7 +610,7 @@ int emu_flush(void* h) {
 
 int64_t emu_sched_stat(int which) {
     return which == 0 ? (int64_t)reordered_ : which == 1 ? (int64_t)taken_ : which == 5 ? growths_
-         : which == 6 ? (int64_t)exact_passes_ : (int64_t)us_[which - 2];
+         : which == 6 ? (int64_t)exact_passes_ : which == 7 ? spills_ : (int64_t)us_[which - 2];
 }
 int emu_num_queries(void* h) { return (int)((Emu*)h)->qs.size(); }
 const char* emu_query_name(void* h, int q) { return ((Emu*)h)->qs[q]->hq.name.c_str(); }

@@ -78,6 +78,54 @@ def test_host_nfa_500_deep_descending_run(batches, oracle_built, emu_built):
     assert L.emu_sched_stat(5) - g0 >= 5  # 16 -> 512 slots at least
 
 
+def spill_trace(depth=6000, tail=600, seed=5, keys=("k0",), step=0.01):
+    """`depth` slowly descending prices on each key of `keys` (every partial stays pending: more than the device's
+    4096 partial matches per key), a lighter key k9 alongside, then a noisy tail that completes them"""
+    rng = np.random.default_rng(seed)
+    out, i = [], 0
+    for d in range(depth):
+        for k in keys:
+            out.append(("S", 1000 + i // 8, [i, k, float(100.0 - step * d), int(rng.integers(0, 100))]))
+            i += 1
+        if d % 10 == 0:
+            out.append(("S", 1000 + i // 8, [i, "k9", float(np.round(rng.uniform(20, 110), 2)), 1]))
+            i += 1
+    for _ in range(tail):
+        k = keys[int(rng.integers(0, len(keys)))] if rng.random() < 0.8 else "k9"
+        out.append(("S", 1000 + i // 8, [i, k, float(np.round(rng.uniform(20, 110), 2)), int(rng.integers(0, 100))]))
+        i += 1
+    return out
+
+
+@pytest.mark.parametrize("batches", [1, 4])
+def test_host_nfa_spills_key_past_4096_partials(batches, oracle_built, emu_built):
+    """a key with 6000 pending partials outgrows the device layout's 4096: it moves to a 32-bit host arena (nfa.h
+    migrate_key<int16_t> into make_layout<int32_t>) and goes on there, oracle-equal"""
+    tr = spill_trace()
+    ref = oracle_rows(DEEP, tr, batches)
+    L = emu_lib()
+    s0 = L.emu_sched_stat(7)
+    e = EmuAdapter(DEEP, max_partials=1024)
+    try:
+        got = synth.run(e, tr, batches)
+    finally:
+        e.close()
+    assert len(ref) > 5000 and got == ref
+    assert L.emu_sched_stat(7) - s0 == 1  # k0 spilled once (and stayed on the host)
+
+
+def test_host_nfa_spilled_key_doubles_its_host_arena(oracle_built, emu_built):
+    """20000 pending partials: the spilled key's 32-bit arena doubles (8192 -> 16384 -> 32768 slots)"""
+    tr = spill_trace(depth=20000, tail=300, seed=6, step=0.004)
+    ref = oracle_rows(DEEP, tr, 2)
+    e = EmuAdapter(DEEP, max_partials=4096)
+    try:
+        got = synth.run(e, tr, 2)
+    finally:
+        e.close()
+    assert len(ref) > 20000 and got == ref
+
+
 def out_of_order(tr, seed, start, jitter=6):
     """the rows from `start` on get their timestamps jittered: per-key decreases inside the batch and across the
     boundary with the rows before"""
