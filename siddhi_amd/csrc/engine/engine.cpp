@@ -491,8 +491,10 @@ bool range_holds(const HostQuery& h, const HostQuery::RangeKey& rk, int qpos, co
 
 // The register sequence kernel (seq3.hip) covers SEQUENCE `every e1=S[f1], e2=S[f2]<m:n>, e3=S[f3]` over one stream
 // (StateInputStreamParser.java:76-408 wiring: e1 the every-start re-armed by its own post processor, e2 a count
-// state with min >= 1 forwarding to e3, e3 the last), without within, timers, @purge, aggregators or range
-// partitions, with FastPred filters and plain-attribute selects whose state events are e1, e2[0], e2[last] or e3.
+// state with min >= 1 forwarding to e3, e3 the last), without timers, @purge, aggregators, range partitions or
+// streams without a partition key, with FastPred filters and plain-attribute selects whose state events are e1,
+// e2[0], e2[last] or e3. `within` is covered: a partial expires as StreamPreStateProcessor.isExpired decides it
+// (|e1.ts - now| > within, :118-129), checked before each event, as the generic NFA does.
 // Fills the spec (operands resolved per processor context) or returns false (the generic NFA runs the query).
 bool seq3_spec_(const HostQuery& h, Seq3Spec& s, int& why);
 bool seq3_spec(const HostQuery& h, Seq3Spec& s) {
@@ -2300,6 +2302,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     q.out_cap = cap;
     ChainArgs a;
     std::memset(&a, 0, sizeof a);
+    a.xcds = g_xcds;
     a.plan = q.d_plan.as<Plan>();
     a.code = q.d_code.as<Instr>();
     a.consts = q.d_consts.as<int64_t>();
@@ -2901,6 +2904,7 @@ int do_flush(sdg_engine* e) {
     e->stats.sched_fires = e->stats.sched_shifted = e->stats.sched_host_keys = e->stats.sched_rerun_keys = 0;
     e->stats.sched_exact_passes = 0;
     e->stats.sorted_view = 0;
+    e->stats.spilled_keys = 0;
     // a flush consumes its batch whether or not it succeeds: a failing query must not make the next flush
     // replay the events onto the queries that already committed them. The batch's positions and its clock are
     // consumed with it: queries that committed before a failing one hold carries, arenas and scheduler state
@@ -3398,6 +3402,9 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             HIPCHECK(hipGetDeviceProperties(&prop, e->device));
             if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
                 throw DeviceError(std::string("device is ") + prop.gcnArchName + ", this build targets gfx950");
+            int xccs = 0;  // the XCD-aware block remaps follow the device's XCD count (partition mode)
+            if (hipDeviceGetAttribute(&xccs, hipDeviceAttributeNumberOfXccs, e->device) != hipSuccess) xccs = 1;
+            g_xcds = std::max(1, xccs);
             HIPCHECK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
             for (auto& ev : e->ev) HIPCHECK(hipEventCreate(&ev));
         }

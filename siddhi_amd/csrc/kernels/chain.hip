@@ -908,10 +908,9 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
     __shared__ unsigned long long bbase[3];
     __shared__ int sb[2];
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    // XCD-aware block order: the hardware deals consecutive block ids round-robin to the 8 XCDs; virtual id v
-    // gives each XCD a contiguous run of segments, so neighbouring segments (which share halo rows) hit one L2
-    const uint32_t G8 = gridDim.x / 8;
-    const uint32_t v = (blockIdx.x & 7u) * G8 + (blockIdx.x >> 3);
+    // XCD-aware block order (kernels.h xcd_block): virtual id v gives each XCD a contiguous run of segments, so
+    // neighbouring segments (which share halo rows) hit one L2
+    const uint32_t v = xcd_block(blockIdx.x, gridDim.x, (uint32_t)a.xcds);
     if (t == 0) sb[0] = -1;
     __syncthreads();
     if (t < a.nb && a.bseg[t] <= v && v < a.bseg[t + 1]) {
@@ -1440,8 +1439,8 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
     __shared__ unsigned long long bbase[3];
     __shared__ int64_t wmin[NW], wmax[NW];
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    const uint32_t G8 = gridDim.x / 8;  // XCD-aware block order: neighbouring blocks (shared halo rows) on one XCD
-    const uint32_t v = (blockIdx.x & 7u) * G8 + (blockIdx.x >> 3);
+    // XCD-aware block order: neighbouring blocks (shared halo rows) on one XCD
+    const uint32_t v = xcd_block(blockIdx.x, gridDim.x, (uint32_t)a.xcds);
     const int64_t lo = (int64_t)v * FU_OWN;
     if (lo >= a.n) return;  // block-uniform: the rounding of the grid
     const int own = (int)min((int64_t)FU_OWN, a.n - lo);
@@ -1903,8 +1902,7 @@ void chain_carry(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
 #define SDG_FU_W8_DEFAULT 1  // r3v: fused 2.52 ms at 8 vs 2.68 ms at 6 waves per SIMD (C2, same box)
 #endif
 int64_t chain_fused_grid(int64_t n, int nb) {
-    const int64_t g = (n + FU_OWN - 1) / FU_OWN + nb;
-    return (g + 7) / 8 * 8;
+    return xcd_round((n + FU_OWN - 1) / FU_OWN + nb);
 }
 
 void chain_fused(const ChainArgs& a, const ChainArgs* d_a, int64_t grid, hipStream_t stream) {
@@ -1933,7 +1931,7 @@ void chain_fused(const ChainArgs& a, const ChainArgs* d_a, int64_t grid, hipStre
 
 void chain_sorted(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
     if (a.n <= 0) return;
-    const int64_t grid = ((a.n + FU_OWN - 1) / FU_OWN + 7) / 8 * 8;  // rounded for the XCD remap
+    const int64_t grid = xcd_round((a.n + FU_OWN - 1) / FU_OWN);  // rounded for the XCD remap
     const dim3 g((unsigned)grid), b(FU_THREADS);
     const bool same = a.sp.scan_col_kind == a.sp.scan_t;
 #define SV_LAUNCH(KK)                                                                    \

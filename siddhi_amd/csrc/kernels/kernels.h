@@ -107,8 +107,20 @@ struct ChainSpec {
 };
 enum ScanMode : int32_t { SCAN_GENERIC = 0, SCAN_TRUE = 1, SCAN_CONST = 2, SCAN_E1 = 3 };
 
+// XCD-aware block order. The hardware deals consecutive workgroup ids round-robin to the device's XCDs (each with
+// its own L2); the kernels that share halo rows or output cache lines between neighbouring blocks remap the block id
+// so that each XCD gets a contiguous run of virtual ids. g_xcds is the device's XCD count
+// (hipDeviceAttributeNumberOfXccs at engine creation: 8 on MI355X in SPX mode, fewer per device under CPX/DPX
+// partitioning); 1 disables the remap. Grids of remapped kernels are rounded up to a multiple of it (xcd_round).
+extern int g_xcds;
+__host__ __device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t grid, uint32_t xcds) {
+    return xcds > 1 ? (bid % xcds) * (grid / xcds) + bid / xcds : bid;
+}
+inline int64_t xcd_round(int64_t g) { return g_xcds > 1 ? (g + g_xcds - 1) / g_xcds * g_xcds : g; }
+
 struct ChainArgs {
     ChainSpec sp;
+    int32_t xcds;                     // XCD count for the block remap (g_xcds at the flush)
     const Plan* plan;                 // device copy
     const Instr* code;
     const int64_t* consts;
@@ -229,7 +241,7 @@ constexpr int FU_ROWS = FU_THREADS * FU_PT;          // 2048 rows in LDS
 constexpr int FU_DQ = SDG_FU_DQ;
 constexpr int FU_HALO = 512;  // ~1.3 s of a bucket at C2 (> T)
 constexpr int FU_OWN = FU_ROWS - FU_HALO;            // candidate rows per block
-// grid size for n rows in nb buckets (a multiple of 8: the XCD remap needs it)
+// grid size for n rows in nb buckets (a multiple of g_xcds: the XCD remap needs it)
 int64_t chain_fused_grid(int64_t n, int nb);
 void chain_fused(const ChainArgs& a, const ChainArgs* d_a, int64_t grid, hipStream_t stream);
 // the rows chain_fused_k handed over (ovf_rows / ovf_count): key-filtered bucket scans in HBM, emitted directly

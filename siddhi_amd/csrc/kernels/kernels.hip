@@ -161,8 +161,8 @@ struct RxPass {
     const int64_t* ts_base;
     uint8_t* lkey_out;        // non-null: u8 keys >> lkey_shift here instead of keys_out
     int lkey_shift;
-    int ntiles;               // tiles; the grid is rounded up to a multiple of 8 (XCD remap)
-    int xcd;                  // 1: XCD-aware tile order
+    int ntiles;               // tiles; the grid is rounded up to a multiple of xcds (XCD remap)
+    int xcds;                 // XCD count of the tile remap (1: tiles in block order)
     int64_t pre_n;            // first pass only: prefix rows [0, pre_n) from pre_keys / pre_src (8-byte slots), the
     const uint32_t* pre_keys; // others from keys_in / src at i - pre_n; a prefix row's orig is 0x80000000 | i
     const void* pre_src[MAX_COLS + 2];
@@ -186,12 +186,10 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
     __shared__ uint8_t sdig[RX_TILE];  // digit of each staged element: its destination is gbase + rank in the run
     __shared__ uint64_t stage[RX_TILE];
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    // XCD-aware tile order: the hardware deals consecutive block ids round-robin to the 8 XCDs; virtual tile v gives
-    // each XCD a contiguous run of tiles. A digit's runs of consecutive tiles are adjacent in the output, so the
-    // cache line where one tile's run ends and the next one's begins is completed in one XCD's L2 instead of being
-    // written back partially by two
-    const uint32_t G8 = gridDim.x / 8;
-    const uint32_t tile = a.xcd ? (blockIdx.x & 7u) * G8 + (blockIdx.x >> 3) : blockIdx.x;
+    // XCD-aware tile order (kernels.h xcd_block): virtual tile v gives each XCD a contiguous run of tiles. A digit's
+    // runs of consecutive tiles are adjacent in the output, so the cache line where one tile's run ends and the next
+    // one's begins is completed in one XCD's L2 instead of being written back partially by two
+    const uint32_t tile = xcd_block(blockIdx.x, gridDim.x, (uint32_t)a.xcds);
     if ((int)tile >= a.ntiles) return;  // block-uniform: the rounding of the grid
     const int64_t base = (int64_t)tile * RX_TILE;
     const int64_t tile_n = min((int64_t)RX_TILE, a.n - base);
@@ -688,8 +686,8 @@ static void launch_rx_hist(int64_t nt, hipStream_t stream, const uint32_t* keys,
 static void launch_rx_scatter(int64_t nt, hipStream_t stream, RxPass rp) {
     static const bool no_xcd = getenv("SDG_RX_NOXCD") != nullptr;  // A/B: tiles in block order
     rp.ntiles = (int)nt;
-    rp.xcd = !no_xcd;
-    const int64_t grid = no_xcd ? nt : (nt + 7) / 8 * 8;
+    rp.xcds = no_xcd ? 1 : g_xcds;
+    const int64_t grid = no_xcd ? nt : xcd_round(nt);
     if (rp.pre_n > 0) {  // (the large tile only: prefix rows exist on the sorted-view path alone)
         if (rx_tile() == RX_TILE_BIG)
             hipLaunchKernelGGL((rx_scatter<RX_TILE_BIG, RX_THREADS_BIG, true>), dim3((unsigned)grid), dim3(RX_THREADS_BIG),
@@ -907,6 +905,8 @@ void nfa_slots_assign(const SlotPool& sp, const uint32_t* seg_start, const uint3
 void nfa_commit_slots(const SlotPool& sp, uint8_t* cur, uint8_t* ran, int64_t slots, hipStream_t st) {
     if (slots > 0) hipLaunchKernelGGL(nfa_commit_slots_k, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, sp, cur, ran, slots);
 }
+
+int g_xcds = 8;
 
 void nfa_commit(uint8_t* cur, uint8_t* ran, int64_t K, hipStream_t stream) {
     if (K <= 0) return;
