@@ -270,6 +270,7 @@ struct QueryRt {
     // sorted view
     DevBuf so_ts, so_qs, so_key, so_orig, so_vrank, so_cols[MAX_COLS], so_nulls[MAX_COLS], seg, kg_counts, kg_gsum;
     DevBuf so_lkey;                                 // fused path: u8 local keys of the bucket view
+    DevBuf sv_tsbase;                               // sorted view: base of its u32 ts offsets (ts_window_base)
     DevBuf bk_plan;                                 // fused path: bstart[257] + bseg[257]
     // carries (double buffered)
     struct Carry {
@@ -902,8 +903,10 @@ void spill_keys(sdg_engine* e, QueryRt& q, const std::vector<uint32_t>& fresh, c
                 HIPCHECK(hipMemcpy(rows.nulls[c].data(), v.nulls[c] + b, (size_t)m, hipMemcpyDeviceToHost));
             }
         }
+        int64_t slack = 4096;
         for (;;) {
             std::unique_ptr<KeyRunT<int32_t>> r(new KeyRunT<int32_t>());
+            r->slack = slack;
             r->key = k;
             r->arena = sp.arena;  // batch-start state (kept until the run succeeds)
             r->ts = rows.ts;
@@ -920,6 +923,10 @@ void spill_keys(sdg_engine* e, QueryRt& q, const std::vector<uint32_t>& fresh, c
                 r->start(&P, q.hq.code.data(), q.hq.consts.data(), sp.L, T, e->seq);
             }
             r->rows_before(INT64_MAX);
+            if (!r->arena_overflow() && r->output_overflow()) {  // one event completed more partials than the
+                slack = (int64_t)r->emitted() + 4096;                // sink's slack: again with room for all of them
+                continue;
+            }
             if (!r->arena_overflow()) {
                 if (r->overflow()) throw DeviceError("spilled key: host run sink overflow");
                 sp.arena.swap(r->arena);
@@ -1605,7 +1612,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     hp.mark("view");
     ev_record(e->ev[0], st);
     const uint32_t* v_segend = nullptr;
-    const uint32_t* v_ts32 = nullptr;  // fused path's slim bucket view (ts offsets, local keys)
+    const uint32_t* v_ts32 = nullptr;  // fused path's slim bucket view / sorted view: ts as u32 offsets from *v_tsbase
+    const int64_t* v_tsbase = d_ts;
     const uint8_t* v_lkey = nullptr;
     int* flags = (int*)q.flags.ensure(32);  // [0] output overflow [1] decreasing ts [2] bounds [3] mono [4] key range
     int bbits = 0;
@@ -1652,6 +1660,18 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             for (int k = 0; k < nc; ++k) a.pre_src[1 + k] = ci.vals.as<int64_t>() + (size_t)k * ci.cap;
         }
         a.no_segments = sorted;
+        // the sorted view moves ts as u32 offsets from ts[0] - 2^31 (a row outside that window sets flags[3]: the
+        // batch reruns on the lane kernels); SDG_SV_WIDE keeps int64 ts (A/B)
+        static const bool sv_wide = getenv("SDG_SV_WIDE") != nullptr;
+        const bool sv32 = sorted && !sv_wide && !ts_by_orig;
+        if (sv32) {
+            int64_t* base = (int64_t*)q.sv_tsbase.ensure(8);
+            ts_window_base(d_ts, base, st);
+            a.ts32_col = 0;  // (ts is payload column 0)
+            a.ts_base = base;
+            a.ts32_flag = flags + 3;
+            v_tsbase = base;
+        }
         keygroup_bind(a, q.kg_counts.ensure(keygroup_workspace(nv, (int32_t)K, a.ncols, a.width)));
         a.keys_sorted = (uint32_t*)q.so_key.ensure(nv * 4);
         a.orig_sorted = (uint32_t*)q.so_orig.ensure(nv * 4);
@@ -1688,6 +1708,10 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         } else {
             HIPCHECK(hipMemsetAsync(flags, 0, 32, st));
             keygroup(a, st, g_no_events ? nullptr : &e->ev[4]);
+            if (a.ts32_col >= 0) {
+                v_ts32 = (const uint32_t*)a.dst[0];
+                v_ts = nullptr;
+            }
         }
         v_key = v_lkey ? nullptr : a.keys_sorted;
         v_seg = a.seg_start;
@@ -2310,7 +2334,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     a.fold = sorted;
     a.ts = v_ts;
     a.ts32 = v_ts32;
-    a.ts_base = v_ts32 ? d_ts : nullptr;
+    a.ts_base = v_ts32 ? v_tsbase : nullptr;
     a.lkey = v_lkey;
     a.qstream = multi_stream ? v_qs : nullptr;
     a.key = partitioned ? v_key : nullptr;

@@ -86,6 +86,9 @@ struct KeyRunT : KeyOut {
     }
     bool overflow() { return c_.ovf() || flags_[0] || flags_[5]; }
     bool arena_overflow() { return c_.ovf(); }
+    bool output_overflow() const { return flags_[0] != 0; }
+    unsigned long long emitted() const { return count; }  // records the run asked for (> the sink on overflow)
+    int64_t slack = 4096;  // free output slots kept before each step (one event can complete many partials)
     int64_t next_row_pos() const { return p_ < (int64_t)ts.size() ? (int64_t)pos[p_] : -1; }
     int64_t purge_last() const { return c_.purge.last; }  // the key's last activity after the replay (@purge)
 
@@ -103,8 +106,8 @@ struct KeyRunT : KeyOut {
     // keep room for a step's worth of outputs and log records (the sinks are plain host vectors)
     void reserve(int64_t min_cap) {
         int64_t cap = (int64_t)o_ts.size();
-        if (cap - (int64_t)count < 4096 || cap < min_cap) {
-            const int64_t nc = std::max<int64_t>({min_cap, 2 * cap, (int64_t)count + 8192});
+        if (cap - (int64_t)count < slack || cap < min_cap) {
+            const int64_t nc = std::max<int64_t>({min_cap, 2 * cap, (int64_t)count + 2 * slack});
             std::vector<int64_t> v((size_t)std::max(n_out_, 1) * nc);
             for (int j = 0; j < n_out_; ++j)
                 for (unsigned long long i = 0; i < count; ++i) v[(size_t)j * nc + i] = o_vals[(size_t)j * cap + i];

@@ -1056,6 +1056,39 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
         // front's ts and the top's value are cached and re-read from LDS only when the front / top changes.
         const bool stack = a.fu_mode == DQ_STACK;
         const int p0 = t * FU_DQ;  // lanes with p0 >= nr (whole waves past FU_ROWS / FU_DQ) have no chunk
+        // the chunk's own rows, read from LDS up front (all reads in flight together). The deque only ever holds
+        // the lane's own positions, so its front's ts and its top's value come from these registers (a select over
+        // FU_DQ values) instead of an LDS round trip after every pop / expiry (SDG_FU_SKIP bit 256: from LDS, A/B)
+        uint32_t cts[FU_DQ];
+        int64_t cx[FU_DQ];
+        uint16_t crow[FU_DQ];
+        T cxv[FU_DQ];
+#pragma unroll
+        for (int i = 0; i < FU_DQ; ++i) {
+            const int q = min(p0 + i, FU_ROWS - 1);
+            cts[i] = s_ts[sw(q)];
+            cx[i] = s_x[sw(q)];
+            crow[i] = s_row[sw(q)];
+            cxv[i] = SAME ? C::get(cx[i]) : C::get(cvt(cx[i], kind, (uint8_t)K));
+        }
+        const bool regs = !(a.fu_skip & 256);
+        auto ts_of = [&](int i) -> uint32_t {  // ts of the lane's own position p0 + i
+            if (!regs) return s_ts[sw(p0 + i)];
+            uint32_t r = cts[0];
+#pragma unroll
+            for (int j = 1; j < FU_DQ; ++j) r = i == j ? cts[j] : r;
+            return r;
+        };
+        auto x_of = [&](int i) -> T {  // converted value of the lane's own position p0 + i
+            if (!regs) {
+                const int64_t yr = s_x[sw(p0 + i)];
+                return SAME ? C::get(yr) : C::get(cvt(yr, kind, (uint8_t)K));
+            }
+            T r = cxv[0];
+#pragma unroll
+            for (int j = 1; j < FU_DQ; ++j) r = i == j ? cxv[j] : r;
+            return r;
+        };
         uint32_t pend = 0, tf = 0;
         T ytop = T(0);
         // one row (ts tq, value x) against the pending partials: expire the prefix, then complete (a suffix / all).
@@ -1065,17 +1098,14 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
             // StreamPreStateProcessor.expireEvents: the expired prefix (oldest first); s_res stays R_NONE
             while (pend && (uint64_t)(tq - tf) > within_u) {
                 pend &= pend - 1;
-                if (pend) tf = s_ts[sw(p0 + __builtin_ctz(pend))];
+                if (pend) tf = ts_of(__builtin_ctz(pend));
             }
             if (stack) {  // x completes the suffix of partials whose e1 value it beats
                 while (pend && (left ? cmp_m(m, x, ytop) : cmp_m(m, ytop, x))) {
                     const int tp = 31 - __builtin_clz(pend);
                     s_res[sw(p0 + tp)] = (uint16_t)q;
                     pend &= ~(1u << tp);
-                    if (pend) {
-                        const int64_t yr = s_x[sw(p0 + 31 - __builtin_clz(pend))];
-                        ytop = SAME ? C::get(yr) : C::get(cvt(yr, kind, (uint8_t)K));
-                    }
+                    if (pend) ytop = x_of(31 - __builtin_clz(pend));
                 }
             } else if (pend && (left ? cmp_m(m, x, kc) : cmp_m(m, kc, x))) {  // complete-all
                 for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = (uint16_t)q;
@@ -1083,17 +1113,6 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
         };
         const int pe = min(p0 + FU_DQ, nr);
         int cur_end = p0 < nr ? (int)lend[s_lk[sw(p0)]] : 0;
-        // the chunk's own rows, read from LDS up front (all reads in flight together)
-        uint32_t cts[FU_DQ];
-        int64_t cx[FU_DQ];
-        uint16_t crow[FU_DQ];
-#pragma unroll
-        for (int i = 0; i < FU_DQ; ++i) {
-            const int q = min(p0 + i, FU_ROWS - 1);
-            cts[i] = s_ts[sw(q)];
-            cx[i] = s_x[sw(q)];
-            crow[i] = s_row[sw(q)];
-        }
         // chunk summaries (stack mode, ordering comparisons): per FU_DQ-position chunk the extreme value that could
         // complete a pending partial -- the max when "x beats y" grows with x, else the min; NaN rows never complete
         // one. A continuation skips a whole chunk of its key when the summary cannot beat its deque's top: pops only
@@ -1107,7 +1126,7 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
             T ext = use_max ? std::numeric_limits<T>::lowest() : std::numeric_limits<T>::max();
 #pragma unroll
             for (int i = 0; i < FU_DQ; ++i) {
-                const T x = SAME ? C::get(cx[i]) : C::get(cvt(cx[i], kind, (uint8_t)K));
+                const T x = cxv[i];
                 if (p0 + i < nr && x == x) ext = use_max ? (x > ext ? x : ext) : (x < ext ? x : ext);
             }
             if (p0 < FU_ROWS) s_cs[t] = ext;
@@ -1119,7 +1138,7 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
             if (q >= pe) break;
             const uint32_t tq = cts[i];
             const int64_t xr = cx[i];
-            const T x = SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K));
+            const T x = cxv[i];
             step(q, tq, x);
             // e1: this lane's own (non-halo) rows start partials, visible from the next row on
             if (crow[i] < own && c0_at(q, xr, x) && (!stack || x == x)) {
@@ -1145,7 +1164,7 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
                         const uint32_t tl = s_ts[sw(q + FU_DQ - 1)];  // the chunk's last (latest) row
                         while (pend && (uint64_t)(tl - tf) > within_u) {
                             pend &= pend - 1;
-                            if (pend) tf = s_ts[sw(p0 + __builtin_ctz(pend))];
+                            if (pend) tf = ts_of(__builtin_ctz(pend));
                         }
                         q += FU_DQ;
                         continue;
@@ -1458,7 +1477,7 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
         const int64_t g = lo + min(row, nr - 1);
         const uint32_t o = a.orig[g];
         rkey[r] = (a.key[g] & SV_KEY) | ((a.fold && (o & SV_CARRIED)) ? SV_CARRIED : 0u);
-        rts[r] = a.ts[g];
+        rts[r] = vts(a, g);
         rx[r] = kind == VK_F64 || kind == VK_I64 ? ((const int64_t*)xcol)[g] : load_col(xcol, kind, g);
         tmn = min(tmn, rts[r]);
         tmx = max(tmx, rts[r]);
@@ -1510,7 +1529,7 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
             pt = (int64_t)s_ts[sw(pos - 1)];
         } else if (lo > 0) {
             pk = a.key[lo - 1] & SV_KEY;
-            pt = a.ts[lo - 1] - tbase;
+            pt = vts(a, lo - 1) - tbase;
         } else {
             continue;
         }
@@ -1543,40 +1562,68 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
         // ---- monotone-deque pass (as chain_fused_k): lane t owns positions [FU_DQ t, FU_DQ (t + 1)) ----------
         const bool stack = a.fu_mode == DQ_STACK;
         const int p0 = t * FU_DQ;
+        // the chunk's rows up front (all LDS reads in flight together); the deque holds only the lane's own
+        // positions, so its front's ts and top's value are register selects (as chain_fused_k)
+        uint32_t cts[FU_DQ], ckey[FU_DQ];
+        int64_t cx[FU_DQ];
+        T cxv[FU_DQ];
+#pragma unroll
+        for (int i = 0; i < FU_DQ; ++i) {
+            const int q = min(p0 + i, FU_ROWS - 1);
+            cts[i] = s_ts[sw(q)];
+            cx[i] = s_x[sw(q)];
+            ckey[i] = s_key[sw(q)];
+            cxv[i] = xval(cx[i]);
+        }
+        auto ts_of = [&](int i) -> uint32_t {
+            uint32_t r = cts[0];
+#pragma unroll
+            for (int j = 1; j < FU_DQ; ++j) r = i == j ? cts[j] : r;
+            return r;
+        };
+        auto x_of = [&](int i) -> T {
+            T r = cxv[0];
+#pragma unroll
+            for (int j = 1; j < FU_DQ; ++j) r = i == j ? cxv[j] : r;
+            return r;
+        };
         uint32_t pend = 0, tf = 0;
         T ytop = T(0);
         auto step = [&](int q, uint32_t tq, T x) {
             while (pend && (uint64_t)(tq - tf) > within_u) {  // expireEvents: the expired prefix
                 pend &= pend - 1;
-                if (pend) tf = s_ts[sw(p0 + __builtin_ctz(pend))];
+                if (pend) tf = ts_of(__builtin_ctz(pend));
             }
             if (stack) {
                 while (pend && (left ? cmp_m(m, x, ytop) : cmp_m(m, ytop, x))) {
                     const int tp = 31 - __builtin_clz(pend);
                     s_res[sw(p0 + tp)] = (uint16_t)q;
                     pend &= ~(1u << tp);
-                    if (pend) ytop = xval(s_x[sw(p0 + 31 - __builtin_clz(pend))]);
+                    if (pend) ytop = x_of(31 - __builtin_clz(pend));
                 }
             } else if (pend && (left ? cmp_m(m, x, kc) : cmp_m(m, kc, x))) {
                 for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = (uint16_t)q;
             }
         };
         const int pe = min(p0 + FU_DQ, own);  // (FU_OWN is a multiple of FU_DQ: a chunk is all own rows or none)
-        uint32_t cur = p0 < own ? (s_key[sw(p0)] & SV_KEY) : 0u;
-        for (int q = p0; q < pe; ++q) {
-            const uint32_t kq = s_key[sw(q)];
+        uint32_t cur = p0 < own ? (ckey[0] & SV_KEY) : 0u;
+#pragma unroll
+        for (int i = 0; i < FU_DQ; ++i) {
+            const int q = p0 + i;
+            if (q >= pe) break;
+            const uint32_t kq = ckey[i];
             if ((kq & SV_KEY) != cur) {  // the previous key's run ended inside the chunk: its partials are carried
                 for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = R_CARRY;
                 cur = kq & SV_KEY;
             }
             if (kq & SV_CARRIED) continue;  // a carried partial: resolved by its forward scan below
-            const uint32_t tq = s_ts[sw(q)];
-            const int64_t xr = s_x[sw(q)];
-            const T x = xval(xr);
+            const uint32_t tq = cts[i];
+            const int64_t xr = cx[i];
+            const T x = cxv[i];
             step(q, tq, x);
             if (c0_at(q, xr, x) && (!stack || x == x)) {  // e1: visible from the next row on
                 if (!pend) tf = tq;
-                pend |= 1u << (q - p0);
+                pend |= 1u << i;
                 ytop = x;
             }
         }
@@ -1773,7 +1820,7 @@ __device__ int64_t sv_wave_scan(const ChainArgs& a, int64_t p, uint32_t kp, int6
         if (q >= a.n || (a.key[q] & SV_KEY) != kp) {
             end = true;  // the key's rows of this batch end: carried
         } else if (!(a.fold && (a.orig[q] & SV_CARRIED))) {
-            if ((uint64_t)(a.ts[q] - ts0) > within_u) stop = true;  // isExpired at this event of the key
+            if ((uint64_t)(vts(a, q) - ts0) > within_u) stop = true;  // isExpired at this event of the key
             else if (always) hit = true;
             else hit = left ? cmp_m(m, C::get(cvt(load_col(a.cols[col], kind, q), kind, (uint8_t)K)), y)
                             : cmp_m(m, y, C::get(cvt(load_col(a.cols[col], kind, q), kind, (uint8_t)K)));
@@ -1812,12 +1859,12 @@ __global__ __launch_bounds__(256, 8) void chain_sovf_k(const ChainArgs* __restri
             }
             int64_t r;
             switch (sp.scan_t) {
-                case VK_I32: r = sv_wave_scan<VK_I32>(a, p, kp, a.ts[p], k, op); break;
-                case VK_I64: r = sv_wave_scan<VK_I64>(a, p, kp, a.ts[p], k, op); break;
-                case VK_F32: r = sv_wave_scan<VK_F32>(a, p, kp, a.ts[p], k, op); break;
-                case VK_F64: r = sv_wave_scan<VK_F64>(a, p, kp, a.ts[p], k, op); break;
-                case VK_BOOL: r = sv_wave_scan<VK_BOOL>(a, p, kp, a.ts[p], k, op); break;
-                default: r = sv_wave_scan<VK_STR>(a, p, kp, a.ts[p], k, op); break;
+                case VK_I32: r = sv_wave_scan<VK_I32>(a, p, kp, vts(a, p), k, op); break;
+                case VK_I64: r = sv_wave_scan<VK_I64>(a, p, kp, vts(a, p), k, op); break;
+                case VK_F32: r = sv_wave_scan<VK_F32>(a, p, kp, vts(a, p), k, op); break;
+                case VK_F64: r = sv_wave_scan<VK_F64>(a, p, kp, vts(a, p), k, op); break;
+                case VK_BOOL: r = sv_wave_scan<VK_BOOL>(a, p, kp, vts(a, p), k, op); break;
+                default: r = sv_wave_scan<VK_STR>(a, p, kp, vts(a, p), k, op); break;
             }
             if (lane == i) mine = r;
         }

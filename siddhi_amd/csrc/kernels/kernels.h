@@ -47,11 +47,13 @@ struct KeyGroupArgs {
     int* key_flag;                    // non-null: set to 1 when some key >= K (the first histogram pass checks)
     const uint32_t* orig_in;          // [n] batch position of each input row (nullptr: the row index itself);
                                       // orig_sorted then holds positions
-    // bucketize only (the fused path's slim bucket view): payload column ts32_col (int64 ts) is written as u32
-    // offsets from *ts_base (the batch's first ts; an offset past 2^32 sets the mono flag), and the keys as u8 local
-    // keys key >> bits into lkey_out instead of keys_sorted (ts32_col < 0 / lkey_out nullptr: off)
+    // payload column ts32_col (int64 ts) is written as u32 offsets from *ts_base (bucketize: the batch's first ts,
+    // an offset past 2^32 sets the mono flag; keygroup: the sorted-view matcher's window base, the first pass
+    // converts and sets *ts32_flag for an offset outside [0, 2^32), the later passes move u32), and (bucketize only)
+    // the keys as u8 local keys key >> bits into lkey_out instead of keys_sorted (ts32_col < 0 / lkey_out nullptr: off)
     int32_t ts32_col = -1;
     const int64_t* ts_base = nullptr;
+    int* ts32_flag = nullptr;
     uint8_t* lkey_out = nullptr;
     // prefix rows (keygroup, the sorted-view matcher's folded carries): rows [0, pre_n) of the input are read from
     // pre_keys / pre_src (8-byte slots per row; a narrower column takes the slot's low bytes), rows [pre_n, n) from
@@ -66,6 +68,8 @@ size_t keygroup_workspace(int64_t n, int32_t K, int32_t ncols, const uint8_t* wi
 void keygroup_bind(KeyGroupArgs& a, void* base);
 // marks (optional, 4 events): recorded before the histograms, after the prefix kernels of pass 1, after
 // the last scatter, after the segment kernel
+// *out = ts[0] - 2^31: the base of the sorted view's u32 ts offsets (rows within +-2^31 ms of the batch's first)
+void ts_window_base(const int64_t* ts, int64_t* out, hipStream_t stream);
 void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks = nullptr);
 
 // ---- bucket grouping (fused chain path): ONE radix pass on the key's low `bits` bits --------------------

@@ -774,6 +774,15 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
         rp.bits = b;
         rp.mono_col = -1;
         rp.ts32_col = -1;
+        if (a.ts32_col >= 0) {  // the first pass converts the int64 ts to u32 offsets, the later ones move u32
+            if (p == 0) {
+                rp.ts32_col = a.ts32_col;
+                rp.ts_base = a.ts_base;
+                rp.mono_flag = a.ts32_flag;
+            } else {
+                rp.width[a.ts32_col] = 4;
+            }
+        }
         if (p == 0 && a.pre_n > 0) {
             rp.pre_n = a.pre_n;
             rp.pre_keys = a.pre_keys;
@@ -907,6 +916,15 @@ void nfa_commit_slots(const SlotPool& sp, uint8_t* cur, uint8_t* ran, int64_t sl
 }
 
 int g_xcds = 8;
+
+namespace {
+__global__ void ts_window_base_k(const int64_t* __restrict__ ts, int64_t* __restrict__ out) {
+    if (threadIdx.x == 0) out[0] = ts[0] - ((int64_t)1 << 31);
+}
+}  // namespace
+void ts_window_base(const int64_t* ts, int64_t* out, hipStream_t stream) {
+    hipLaunchKernelGGL(ts_window_base_k, dim3(1), dim3(64), 0, stream, ts, out);
+}
 
 void nfa_commit(uint8_t* cur, uint8_t* ran, int64_t K, hipStream_t stream) {
     if (K <= 0) return;

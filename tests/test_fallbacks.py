@@ -78,7 +78,7 @@ def test_host_nfa_500_deep_descending_run(batches, oracle_built, emu_built):
     assert L.emu_sched_stat(5) - g0 >= 5  # 16 -> 512 slots at least
 
 
-def spill_trace(depth=6000, tail=600, seed=5, keys=("k0",), step=0.01):
+def spill_trace(depth=6000, tail=600, seed=5, keys=("k0",), step=0.01, noise=True):
     """`depth` slowly descending prices on each key of `keys` (every partial stays pending: more than the device's
     4096 partial matches per key), a lighter key k9 alongside, then a noisy tail that completes them"""
     rng = np.random.default_rng(seed)
@@ -87,11 +87,11 @@ def spill_trace(depth=6000, tail=600, seed=5, keys=("k0",), step=0.01):
         for k in keys:
             out.append(("S", 1000 + i // 8, [i, k, float(100.0 - step * d), int(rng.integers(0, 100))]))
             i += 1
-        if d % 10 == 0:
+        if noise and d % 10 == 0:
             out.append(("S", 1000 + i // 8, [i, "k9", float(np.round(rng.uniform(20, 110), 2)), 1]))
             i += 1
     for _ in range(tail):
-        k = keys[int(rng.integers(0, len(keys)))] if rng.random() < 0.8 else "k9"
+        k = keys[int(rng.integers(0, len(keys)))] if rng.random() < 0.8 or not noise else "k9"
         out.append(("S", 1000 + i // 8, [i, k, float(np.round(rng.uniform(20, 110), 2)), int(rng.integers(0, 100))]))
         i += 1
     return out

@@ -333,8 +333,8 @@ def test_chain_shapes_on_gpu(name, shape, path, oracle_built):
         st = p.rt.stats()
         if not fused:
             assert st.fused == 0 and st.deque == deque
-            # the sorted-view matcher (nan_b2: null prices -> the lane kernels, unless the query reads volume only)
-            nulls_read = shape == "nan_b2" and name != "int_gt_nowithin"
+            # the sorted-view matcher (nan_b2: null prices -> the lane kernels, unless the query does not read price)
+            nulls_read = shape == "nan_b2" and "price" in app
             assert st.sorted_view == (path == "sorted" and name in SORTED_SHAPES and not nulls_read)
         elif name in FUSED_SHAPES and shape != "nan_b2":  # nan_b2: nulls in the scanned column -> radix path
             assert st.fused == 1
