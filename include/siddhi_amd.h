@@ -61,7 +61,9 @@ typedef struct sdg_opts {
     int32_t device;            /* HIP device ordinal (one engine per GPU) */
     int64_t batch_capacity;    /* max events buffered between flushes (0 = default 1<<24) */
     int32_t max_partials;      /* per-key partial-match slots the generic NFA starts with (0 = default 8; the arenas
-                                  double on overflow up to 4096) */
+                                  double on overflow up to 4096; a key past that continues on the host in an arena
+                                  of 32-bit indices -- sdg_stats.spilled_keys --, except in queries with absent
+                                  states, whose flush then fails with SDG_ERR_CAPACITY) */
     int32_t flags;             /* SDG_COMPILE_ONLY: parse + lower only, no device (introspection on hosts
                                   without a GPU; push/flush then fail with SDG_ERR_DEVICE) */
 } sdg_opts;

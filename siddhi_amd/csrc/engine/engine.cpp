@@ -2394,6 +2394,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         a.seg_start = a.seg_end = nullptr;
     }
     if (sorted) {  // chain_sorted_k: deque / forward scans in LDS blocks, the rest of a cut run in chain_sovf_k
+        static const char* skip = getenv("SDG_FU_SKIP");  // (only the A/B bits: 512 = the deque step's loops)
+        a.fu_skip = (skip ? atoi(skip) : 0) & 512;
         a.fu_mode = a.deque_mode;
         a.deque_mode = DQ_OFF;
         a.seg_start = a.seg_end = nullptr;
@@ -3428,7 +3430,11 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
                 throw DeviceError(std::string("device is ") + prop.gcnArchName + ", this build targets gfx950");
             int xccs = 0;  // the XCD-aware block remaps follow the device's XCD count (partition mode)
             if (hipDeviceGetAttribute(&xccs, hipDeviceAttributeNumberOfXccs, e->device) != hipSuccess) xccs = 1;
+            if (const char* x = getenv("SDG_XCDS")) xccs = atoi(x);  // override (A/B)
             g_xcds = std::max(1, xccs);
+            if (getenv("SDG_VERBOSE"))
+                fprintf(stderr, "[sdg] device %d: %s, %d CUs, %d XCDs\n", e->device, prop.gcnArchName,
+                        prop.multiProcessorCount, g_xcds);
             HIPCHECK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
             for (auto& ev : e->ev) HIPCHECK(hipEventCreate(&ev));
         }

@@ -1091,10 +1091,40 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
         };
         uint32_t pend = 0, tf = 0;
         T ytop = T(0);
+        // Branch-free step (default; SDG_FU_SKIP bit 512: the loops below): the pending positions' ts and values are
+        // registers, so a row's effect is two masks over the FU_DQ positions -- `live` (not expired by this row:
+        // the expired ones are a prefix, positions being in time order) and `beat` (completed by it: in stack mode
+        // the pending values are monotone -- every push first popped what it beats --, so the ones a row beats are
+        // exactly the suffix the pop loop would take; in complete-all mode all or none). No data-dependent loop, no
+        // exec-mask juggling per pop.
+        const bool bf = !(a.fu_skip & 512) && (!stack || (m.gt != m.lt && !m.ne));
+        auto live_at = [&](uint32_t tq) -> uint32_t {
+            uint32_t live = 0;
+#pragma unroll
+            for (int i = 0; i < FU_DQ; ++i) live |= (uint32_t)((uint64_t)(tq - cts[i]) <= within_u) << i;
+            return live;
+        };
         // one row (ts tq, value x) against the pending partials: expire the prefix, then complete (a suffix / all).
         // The front's ts (tf) and the top's value (ytop) are cached; pops only ever remove from the top, so tf
         // changes only by expiry or by emptying.
         auto step = [&](int q, uint32_t tq, T x) {
+            if (bf) {
+                uint32_t beat = 0;
+                if (stack) {
+#pragma unroll
+                    for (int i = 0; i < FU_DQ; ++i)
+                        beat |= (uint32_t)(left ? cmp_m(m, x, cxv[i]) : cmp_m(m, cxv[i], x)) << i;
+                } else {
+                    beat = (left ? cmp_m(m, x, kc) : cmp_m(m, kc, x)) ? ~0u : 0u;
+                }
+                pend &= live_at(tq);
+                const uint32_t done = pend & beat;
+                pend &= ~done;
+#pragma unroll
+                for (int i = 0; i < FU_DQ; ++i)
+                    if ((done >> i) & 1u) s_res[sw(p0 + i)] = (uint16_t)q;
+                return;
+            }
             // StreamPreStateProcessor.expireEvents: the expired prefix (oldest first); s_res stays R_NONE
             while (pend && (uint64_t)(tq - tf) > within_u) {
                 pend &= pend - 1;
@@ -1160,11 +1190,16 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
             while (q < cur_end && pend) {
                 if (q + FU_DQ <= cur_end) {  // a whole chunk of this key
                     const T cs = s_cs[q / FU_DQ];
-                    if (!(left ? cmp_m(m, cs, ytop) : cmp_m(m, ytop, cs))) {
+                    const T yt = bf ? x_of(31 - __builtin_clz(pend)) : ytop;
+                    if (!(left ? cmp_m(m, cs, yt) : cmp_m(m, yt, cs))) {
                         const uint32_t tl = s_ts[sw(q + FU_DQ - 1)];  // the chunk's last (latest) row
-                        while (pend && (uint64_t)(tl - tf) > within_u) {
-                            pend &= pend - 1;
-                            if (pend) tf = ts_of(__builtin_ctz(pend));
+                        if (bf) {
+                            pend &= live_at(tl);
+                        } else {
+                            while (pend && (uint64_t)(tl - tf) > within_u) {
+                                pend &= pend - 1;
+                                if (pend) tf = ts_of(__builtin_ctz(pend));
+                            }
                         }
                         q += FU_DQ;
                         continue;
@@ -1589,7 +1624,25 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
         };
         uint32_t pend = 0, tf = 0;
         T ytop = T(0);
+        // branch-free step (as chain_fused_k; SDG_FU_SKIP bit 512: the loops)
+        const bool bf = !(a.fu_skip & 512) && (!stack || (m.gt != m.lt && !m.ne));
         auto step = [&](int q, uint32_t tq, T x) {
+            if (bf) {
+                uint32_t beat = 0, live = 0;
+#pragma unroll
+                for (int i = 0; i < FU_DQ; ++i) {
+                    live |= (uint32_t)((uint64_t)(tq - cts[i]) <= within_u) << i;
+                    if (stack) beat |= (uint32_t)(left ? cmp_m(m, x, cxv[i]) : cmp_m(m, cxv[i], x)) << i;
+                }
+                if (!stack) beat = (left ? cmp_m(m, x, kc) : cmp_m(m, kc, x)) ? ~0u : 0u;
+                pend &= live;
+                const uint32_t done = pend & beat;
+                pend &= ~done;
+#pragma unroll
+                for (int i = 0; i < FU_DQ; ++i)
+                    if ((done >> i) & 1u) s_res[sw(p0 + i)] = (uint16_t)q;
+                return;
+            }
             while (pend && (uint64_t)(tq - tf) > within_u) {  // expireEvents: the expired prefix
                 pend &= pend - 1;
                 if (pend) tf = ts_of(__builtin_ctz(pend));
