@@ -233,13 +233,17 @@ def ordered_gather_leg(rt, step_push, n, dev, dist, rank, world):
     one stable device sort of the concatenated runs by time. Rank 0 checks the merged order."""
     import torch
     from siddhi_amd import shard
-    step_push()
-    rt.flush(deliver=False)
     cap = n + n // 4 + 4096
     t_ts = torch.empty(cap, dtype=torch.int64, device=dev)
     t_seq = torch.empty(cap, dtype=torch.int64, device=dev)
     t_sub = torch.empty(cap, dtype=torch.int64, device=dev)
     t_vals = torch.empty((2, cap), dtype=torch.int64, device=dev)
+    # one untimed export first: the ordering pass sizes its workspaces on first use (device allocations)
+    step_push()
+    rt.flush(deliver=False)
+    rt.export_ordered(0, cap, t_ts.data_ptr(), t_seq.data_ptr(), t_sub.data_ptr(), t_vals.data_ptr())
+    step_push()
+    rt.flush(deliver=False)
     key = ["ts", "rank", "seq", "sub"]
     if dist is not None:
         dist.barrier()

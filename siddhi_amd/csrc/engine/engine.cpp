@@ -248,7 +248,7 @@ struct QueryRt {
     // position (chain path) or an ordinal within the emitting event (generic NFA)
     int64_t emit_base = 0;
     bool sub_is_seq = false;
-    DevBuf ord_ws, g_ts, g_emit, g_vals, g_nulls, g_key;
+    DevBuf ord_ws, g_ts, g_emit, g_vals, g_nulls, g_key, gather_ws;
     // the selector's post pass (aggregators / having): per-key aggregator state, persistent; staging
     DevBuf agg_state, ps_key, ps_vals, ps_nulls, ps_pass, ps_ws;
     int64_t agg_keys = 0;
@@ -2637,9 +2637,16 @@ void drain(sdg_engine* e, QueryRt& q) {
         int64_t* gts = (int64_t*)q.g_ts.ensure((size_t)n * 8);
         int64_t* gem = (int64_t*)q.g_emit.ensure((size_t)n * 8);
         int64_t* gv = (int64_t*)q.g_vals.ensure((size_t)std::max(na, 1) * n * 8);
-        gather_i64((const int64_t*)q.o_ts.p, perm, n, gts, st);
-        gather_i64((const int64_t*)q.o_emit.p, perm, n, gem, st);
-        for (int j = 0; j < na; ++j) gather_i64((const int64_t*)q.o_vals.p + (size_t)j * q.out_cap, perm, n, gv + (size_t)j * n, st);
+        {
+            std::vector<const int64_t*> src{(const int64_t*)q.o_ts.p, (const int64_t*)q.o_emit.p};
+            std::vector<int64_t*> dst{gts, gem};
+            for (int j = 0; j < na; ++j) {
+                src.push_back((const int64_t*)q.o_vals.p + (size_t)j * q.out_cap);
+                dst.push_back(gv + (size_t)j * n);
+            }
+            gather_cols_i64(src.data(), dst.data(), (int)src.size(), perm, n,
+                            q.gather_ws.ensure(gather_cols_workspace(n, std::min((int)src.size(), GATHER_MAX_COLS))), st);
+        }
         if (q.nulls_valid) {
             uint32_t* gn = (uint32_t*)q.g_nulls.ensure((size_t)n * 4);
             gather_u32((const uint32_t*)q.o_nulls.p, perm, n, gn, st);
@@ -3957,11 +3964,14 @@ int export_records(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_t* 
             uint32_t* perm = nullptr;
             order_records((const int64_t*)q.o_emit.p, (const int64_t*)q.o_first.p, n, q.emit_base,
                           q.sub_is_seq ? q.emit_base - (1ll << 40) : 0, q.sub_bits(), work, wb, &perm, st);
-            gather_i64((const int64_t*)q.o_ts.p, perm, n, d_ts, st);
-            gather_i64((const int64_t*)q.o_emit.p, perm, n, d_seq, st);
-            gather_i64((const int64_t*)q.o_first.p, perm, n, d_sub, st);
-            for (int j = 0; j < na; ++j)
-                gather_i64((const int64_t*)q.o_vals.p + (size_t)j * q.out_cap, perm, n, d_vals + (size_t)j * cap, st);
+            std::vector<const int64_t*> src{(const int64_t*)q.o_ts.p, (const int64_t*)q.o_emit.p, (const int64_t*)q.o_first.p};
+            std::vector<int64_t*> dst{d_ts, d_seq, d_sub};
+            for (int j = 0; j < na; ++j) {
+                src.push_back((const int64_t*)q.o_vals.p + (size_t)j * q.out_cap);
+                dst.push_back(d_vals + (size_t)j * cap);
+            }
+            gather_cols_i64(src.data(), dst.data(), (int)src.size(), perm, n,
+                            q.gather_ws.ensure(gather_cols_workspace(n, std::min((int)src.size(), GATHER_MAX_COLS))), st);
             HIPCHECK(hipStreamSynchronize(st));
         } else if (n > 0) {
             HIPCHECK(hipMemcpyAsync(d_ts, q.o_ts.p, n * 8, hipMemcpyDeviceToDevice, st));

@@ -1056,86 +1056,26 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
         // front's ts and the top's value are cached and re-read from LDS only when the front / top changes.
         const bool stack = a.fu_mode == DQ_STACK;
         const int p0 = t * FU_DQ;  // lanes with p0 >= nr (whole waves past FU_ROWS / FU_DQ) have no chunk
-        // the chunk's own rows, read from LDS up front (all reads in flight together). The deque only ever holds
-        // the lane's own positions, so its front's ts and its top's value come from these registers (a select over
-        // FU_DQ values) instead of an LDS round trip after every pop / expiry (SDG_FU_SKIP bit 256: from LDS, A/B)
-        uint32_t cts[FU_DQ];
-        int64_t cx[FU_DQ];
-        uint16_t crow[FU_DQ];
-        T cxv[FU_DQ];
-#pragma unroll
-        for (int i = 0; i < FU_DQ; ++i) {
-            const int q = min(p0 + i, FU_ROWS - 1);
-            cts[i] = s_ts[sw(q)];
-            cx[i] = s_x[sw(q)];
-            crow[i] = s_row[sw(q)];
-            cxv[i] = SAME ? C::get(cx[i]) : C::get(cvt(cx[i], kind, (uint8_t)K));
-        }
-        const bool regs = !(a.fu_skip & 256);
-        auto ts_of = [&](int i) -> uint32_t {  // ts of the lane's own position p0 + i
-            if (!regs) return s_ts[sw(p0 + i)];
-            uint32_t r = cts[0];
-#pragma unroll
-            for (int j = 1; j < FU_DQ; ++j) r = i == j ? cts[j] : r;
-            return r;
-        };
-        auto x_of = [&](int i) -> T {  // converted value of the lane's own position p0 + i
-            if (!regs) {
-                const int64_t yr = s_x[sw(p0 + i)];
-                return SAME ? C::get(yr) : C::get(cvt(yr, kind, (uint8_t)K));
-            }
-            T r = cxv[0];
-#pragma unroll
-            for (int j = 1; j < FU_DQ; ++j) r = i == j ? cxv[j] : r;
-            return r;
-        };
         uint32_t pend = 0, tf = 0;
         T ytop = T(0);
-        // Branch-free step (default; SDG_FU_SKIP bit 512: the loops below): the pending positions' ts and values are
-        // registers, so a row's effect is two masks over the FU_DQ positions -- `live` (not expired by this row:
-        // the expired ones are a prefix, positions being in time order) and `beat` (completed by it: in stack mode
-        // the pending values are monotone -- every push first popped what it beats --, so the ones a row beats are
-        // exactly the suffix the pop loop would take; in complete-all mode all or none). No data-dependent loop, no
-        // exec-mask juggling per pop.
-        const bool bf = !(a.fu_skip & 512) && (!stack || (m.gt != m.lt && !m.ne));
-        auto live_at = [&](uint32_t tq) -> uint32_t {
-            uint32_t live = 0;
-#pragma unroll
-            for (int i = 0; i < FU_DQ; ++i) live |= (uint32_t)((uint64_t)(tq - cts[i]) <= within_u) << i;
-            return live;
-        };
         // one row (ts tq, value x) against the pending partials: expire the prefix, then complete (a suffix / all).
         // The front's ts (tf) and the top's value (ytop) are cached; pops only ever remove from the top, so tf
         // changes only by expiry or by emptying.
         auto step = [&](int q, uint32_t tq, T x) {
-            if (bf) {
-                uint32_t beat = 0;
-                if (stack) {
-#pragma unroll
-                    for (int i = 0; i < FU_DQ; ++i)
-                        beat |= (uint32_t)(left ? cmp_m(m, x, cxv[i]) : cmp_m(m, cxv[i], x)) << i;
-                } else {
-                    beat = (left ? cmp_m(m, x, kc) : cmp_m(m, kc, x)) ? ~0u : 0u;
-                }
-                pend &= live_at(tq);
-                const uint32_t done = pend & beat;
-                pend &= ~done;
-#pragma unroll
-                for (int i = 0; i < FU_DQ; ++i)
-                    if ((done >> i) & 1u) s_res[sw(p0 + i)] = (uint16_t)q;
-                return;
-            }
             // StreamPreStateProcessor.expireEvents: the expired prefix (oldest first); s_res stays R_NONE
             while (pend && (uint64_t)(tq - tf) > within_u) {
                 pend &= pend - 1;
-                if (pend) tf = ts_of(__builtin_ctz(pend));
+                if (pend) tf = s_ts[sw(p0 + __builtin_ctz(pend))];
             }
             if (stack) {  // x completes the suffix of partials whose e1 value it beats
                 while (pend && (left ? cmp_m(m, x, ytop) : cmp_m(m, ytop, x))) {
                     const int tp = 31 - __builtin_clz(pend);
                     s_res[sw(p0 + tp)] = (uint16_t)q;
                     pend &= ~(1u << tp);
-                    if (pend) ytop = x_of(31 - __builtin_clz(pend));
+                    if (pend) {
+                        const int64_t yr = s_x[sw(p0 + 31 - __builtin_clz(pend))];
+                        ytop = SAME ? C::get(yr) : C::get(cvt(yr, kind, (uint8_t)K));
+                    }
                 }
             } else if (pend && (left ? cmp_m(m, x, kc) : cmp_m(m, kc, x))) {  // complete-all
                 for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = (uint16_t)q;
@@ -1143,6 +1083,17 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
         };
         const int pe = min(p0 + FU_DQ, nr);
         int cur_end = p0 < nr ? (int)lend[s_lk[sw(p0)]] : 0;
+        // the chunk's own rows, read from LDS up front (all reads in flight together)
+        uint32_t cts[FU_DQ];
+        int64_t cx[FU_DQ];
+        uint16_t crow[FU_DQ];
+#pragma unroll
+        for (int i = 0; i < FU_DQ; ++i) {
+            const int q = min(p0 + i, FU_ROWS - 1);
+            cts[i] = s_ts[sw(q)];
+            cx[i] = s_x[sw(q)];
+            crow[i] = s_row[sw(q)];
+        }
         // chunk summaries (stack mode, ordering comparisons): per FU_DQ-position chunk the extreme value that could
         // complete a pending partial -- the max when "x beats y" grows with x, else the min; NaN rows never complete
         // one. A continuation skips a whole chunk of its key when the summary cannot beat its deque's top: pops only
@@ -1156,7 +1107,7 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
             T ext = use_max ? std::numeric_limits<T>::lowest() : std::numeric_limits<T>::max();
 #pragma unroll
             for (int i = 0; i < FU_DQ; ++i) {
-                const T x = cxv[i];
+                const T x = SAME ? C::get(cx[i]) : C::get(cvt(cx[i], kind, (uint8_t)K));
                 if (p0 + i < nr && x == x) ext = use_max ? (x > ext ? x : ext) : (x < ext ? x : ext);
             }
             if (p0 < FU_ROWS) s_cs[t] = ext;
@@ -1168,7 +1119,7 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
             if (q >= pe) break;
             const uint32_t tq = cts[i];
             const int64_t xr = cx[i];
-            const T x = cxv[i];
+            const T x = SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K));
             step(q, tq, x);
             // e1: this lane's own (non-halo) rows start partials, visible from the next row on
             if (crow[i] < own && c0_at(q, xr, x) && (!stack || x == x)) {
@@ -1190,16 +1141,11 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
             while (q < cur_end && pend) {
                 if (q + FU_DQ <= cur_end) {  // a whole chunk of this key
                     const T cs = s_cs[q / FU_DQ];
-                    const T yt = bf ? x_of(31 - __builtin_clz(pend)) : ytop;
-                    if (!(left ? cmp_m(m, cs, yt) : cmp_m(m, yt, cs))) {
+                    if (!(left ? cmp_m(m, cs, ytop) : cmp_m(m, ytop, cs))) {
                         const uint32_t tl = s_ts[sw(q + FU_DQ - 1)];  // the chunk's last (latest) row
-                        if (bf) {
-                            pend &= live_at(tl);
-                        } else {
-                            while (pend && (uint64_t)(tl - tf) > within_u) {
-                                pend &= pend - 1;
-                                if (pend) tf = ts_of(__builtin_ctz(pend));
-                            }
+                        while (pend && (uint64_t)(tl - tf) > within_u) {
+                            pend &= pend - 1;
+                            if (pend) tf = s_ts[sw(p0 + __builtin_ctz(pend))];
                         }
                         q += FU_DQ;
                         continue;
@@ -1598,7 +1544,7 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
         const bool stack = a.fu_mode == DQ_STACK;
         const int p0 = t * FU_DQ;
         // the chunk's rows up front (all LDS reads in flight together); the deque holds only the lane's own
-        // positions, so its front's ts and top's value are register selects (as chain_fused_k)
+        // positions, so its front's ts and top's value are register selects
         uint32_t cts[FU_DQ], ckey[FU_DQ];
         int64_t cx[FU_DQ];
         T cxv[FU_DQ];
@@ -1624,7 +1570,12 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
         };
         uint32_t pend = 0, tf = 0;
         T ytop = T(0);
-        // branch-free step (as chain_fused_k; SDG_FU_SKIP bit 512: the loops)
+        // branch-free step (SDG_FU_SKIP bit 512: the loops): the pending positions' ts and values are registers, so a
+        // row's effect is two masks over the FU_DQ positions -- `live` (not expired: the expired ones are a prefix,
+        // positions being in time order) and `beat` (completed: the pending values are monotone -- every push first
+        // popped what it beats --, so the ones a row beats are exactly the suffix the pop loop takes; complete-all
+        // mode: all or none). Measured neutral on C5 (10.63 vs 10.59 ms, r4j); on the fused matcher the register
+        // copies cost more than the LDS round trips they save (2.91 vs 2.42 ms, r4k), so chain_fused_k keeps LDS.
         const bool bf = !(a.fu_skip & 512) && (!stack || (m.gt != m.lt && !m.ne));
         auto step = [&](int q, uint32_t tq, T x) {
             if (bf) {

@@ -417,11 +417,17 @@ void nfa_commit_slots(const SlotPool& sp, uint8_t* cur, uint8_t* ran, int64_t sl
 
 // delivery order of n match records (order.hip): perm = the record indices sorted by (emit - emit_base as u32,
 // sub - sub_bias as a sub_bits-bit key: 48, or 64 when a delivery rank sits in bits 40..62 -- range partitions and
-// broadcast rows); work = order_workspace(n) bytes
+// broadcast rows); both sorts cover only the key range the records use (measured first: one small read-back);
+// work = order_workspace(n) bytes
 size_t order_workspace(int64_t n);
 void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t emit_base, int64_t sub_bias, int sub_bits,
                    void* work, size_t work_bytes, uint32_t** perm_out, hipStream_t stream);
 void gather_i64(const int64_t* src, const uint32_t* perm, int64_t n, int64_t* dst, hipStream_t stream);
+// dst[c][i] = src[c][perm[i]] for ncol int64 columns, through a packed row-major copy (work = gather_cols_workspace)
+constexpr int GATHER_MAX_COLS = 16;
+size_t gather_cols_workspace(int64_t n, int ncol);
+void gather_cols_i64(const int64_t* const* src, int64_t* const* dst, int ncol, const uint32_t* perm, int64_t n,
+                     void* work, hipStream_t stream);
 void gather_u32(const uint32_t* src, const uint32_t* perm, int64_t n, uint32_t* dst, hipStream_t stream);
 void gather_u8(const uint8_t* src, const uint32_t* perm, int64_t n, uint8_t* dst, hipStream_t stream);
 

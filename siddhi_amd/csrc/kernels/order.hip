@@ -5,6 +5,8 @@
 // the matching path) -- by the ordinal, then by the emitting event's position -- and one gather per column, so
 // the host reads the records back already in order.
 #include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -15,13 +17,40 @@
 namespace sdg {
 namespace {
 
+// the key ranges: max of emit - emit_base (u32), min / max of sub - sub_bias (u64); r[0] = max emit, r[1] = min sub,
+// r[2] = max sub (the host sized the sorts by them: the ordinal / e1 position spans far fewer bits than its type)
+__global__ __launch_bounds__(256) void order_range_k(const int64_t* __restrict__ emit, const int64_t* __restrict__ sub,
+                                                     int64_t n, int64_t emit_base, int64_t sub_bias,
+                                                     unsigned long long* __restrict__ r) {
+    unsigned long long emx = 0, smn = ~0ull, smx = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const unsigned long long e = (unsigned long long)(uint32_t)(emit[i] - emit_base);
+        const unsigned long long s = (unsigned long long)(sub[i] - sub_bias);
+        emx = e > emx ? e : emx;
+        smn = s < smn ? s : smn;
+        smx = s > smx ? s : smx;
+    }
+    for (int o = 32; o > 0; o >>= 1) {  // wave reduction, then one atomic per wave
+        const unsigned long long e2 = __shfl_xor(emx, o), n2 = __shfl_xor(smn, o), x2 = __shfl_xor(smx, o);
+        emx = e2 > emx ? e2 : emx;
+        smn = n2 < smn ? n2 : smn;
+        smx = x2 > smx ? x2 : smx;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(&r[0], emx);
+        atomicMin(&r[1], smn);
+        atomicMax(&r[2], smx);
+    }
+}
+
+template <typename SK>
 __global__ __launch_bounds__(256) void order_keys_k(const int64_t* __restrict__ emit, const int64_t* __restrict__ sub,
                                                     int64_t n, int64_t emit_base, int64_t sub_bias, uint32_t* __restrict__ ek,
-                                                    uint64_t* __restrict__ sk, uint32_t* __restrict__ idx) {
+                                                    SK* __restrict__ sk, uint32_t* __restrict__ idx) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     ek[i] = (uint32_t)(emit[i] - emit_base);
-    sk[i] = (uint64_t)(sub[i] - sub_bias);
+    sk[i] = (SK)(sub[i] - sub_bias);
     idx[i] = (uint32_t)i;
 }
 
@@ -30,6 +59,26 @@ __global__ __launch_bounds__(256) void gather_k(const T* __restrict__ src, const
                                                 T* __restrict__ dst) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < n) dst[i] = src[perm[i]];
+}
+
+// packed-record gather: the columns are first written row-major (one record = ncol consecutive int64s, a
+// sequential pass), then each output slot reads its record's bytes in one place instead of ncol random 8-byte
+// reads from ncol columns (a random 8-byte read costs a whole memory transaction)
+struct ColSet {
+    const int64_t* src[GATHER_MAX_COLS];
+    int64_t* dst[GATHER_MAX_COLS];
+};
+__global__ __launch_bounds__(256) void pack_k(ColSet cs, int ncol, int64_t n, int64_t* __restrict__ rec) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    for (int c = 0; c < ncol; ++c) rec[i * ncol + c] = cs.src[c][i];
+}
+__global__ __launch_bounds__(256) void unpack_k(ColSet cs, int ncol, const int64_t* __restrict__ rec,
+                                                const uint32_t* __restrict__ perm, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int64_t* r = rec + (int64_t)perm[i] * ncol;
+    for (int c = 0; c < ncol; ++c) cs.dst[c][i] = r[c];
 }
 
 void temp_sizes(int64_t n, size_t& a, size_t& b) {
@@ -41,13 +90,19 @@ void temp_sizes(int64_t n, size_t& a, size_t& b) {
     rocprim::radix_sort_pairs(nullptr, b, k32, k32, v, v, (size_t)n, 0, 32);
 }
 
+int bits_for(unsigned long long v) {  // bits to hold 0..v
+    int b = 0;
+    while (b < 64 && (v >> b) != 0) ++b;
+    return b;
+}
+
 }  // namespace
 
 size_t order_workspace(int64_t n) {
     size_t a = 0, b = 0;
     temp_sizes(n, a, b);
     const size_t sort_tmp = ((a > b ? a : b) + 255) & ~size_t(255);
-    // keys: sub (2 x 8n) + emit (2 x 4n), index (2 x 4n)
+    // keys: sub (2 x 8n) + emit (2 x 4n), index (2 x 4n), the range (3 x 8)
     return sort_tmp + (size_t)n * (16 + 8 + 8) + 1024;
 }
 
@@ -66,14 +121,67 @@ void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t e
     uint32_t* ek1 = (uint32_t*)p; p += (size_t)n * 4;
     uint32_t* ix0 = (uint32_t*)p; p += (size_t)n * 4;
     uint32_t* ix1 = (uint32_t*)p; p += (size_t)n * 4;
+    unsigned long long* rng = (unsigned long long*)p;
     (void)work_bytes;
     const unsigned grid = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(order_keys_k, dim3(grid), dim3(256), 0, stream, emit, sub, n, emit_base, sub_bias, ek0, sk0, ix0);
-    // by the ordinal, then (stable) by the emitting event
-    rocprim::radix_sort_pairs(tmp, a, sk0, sk1, ix0, ix1, (size_t)n, 0, sub_bits, stream);
-    hipLaunchKernelGGL(gather_k<uint32_t>, dim3(grid), dim3(256), 0, stream, ek0, ix1, n, ek1);
-    rocprim::radix_sort_pairs(tmp, b, ek1, ek0, ix1, ix0, (size_t)n, 0, 32, stream);
+    // the keys' actual ranges (one small read-back): both sorts cover only the bits the flush's records use --
+    // an e1 position / ordinal spans ~30 bits, not the 48 or 64 of its encoding, and then fits a 32-bit key
+    static const bool full = getenv("SDG_ORDER_FULL") != nullptr;  // A/B: the fixed-width sorts
+    int eb = 32, sb = sub_bits;
+    unsigned long long smin = 0;
+    if (!full) {
+        const unsigned long long init[3] = {0ull, ~0ull, 0ull};
+        (void)hipMemcpyAsync(rng, init, sizeof init, hipMemcpyHostToDevice, stream);
+        hipLaunchKernelGGL(order_range_k, dim3((unsigned)std::min<int64_t>(grid, 2048)), dim3(256), 0, stream, emit, sub, n,
+                           emit_base, sub_bias, rng);
+        unsigned long long h[3];
+        (void)hipMemcpyAsync(h, rng, sizeof h, hipMemcpyDeviceToHost, stream);
+        (void)hipStreamSynchronize(stream);
+        eb = std::max(1, bits_for(h[0]));
+        smin = h[1];
+        sb = std::max(1, bits_for(h[2] - h[1]));
+    }
+    uint32_t* perm1 = nullptr;
+    if (!full && sb <= 32) {  // the ordinal as a 32-bit key relative to its minimum
+        uint32_t* s32a = (uint32_t*)sk0;
+        uint32_t* s32b = (uint32_t*)sk1;
+        hipLaunchKernelGGL(order_keys_k<uint32_t>, dim3(grid), dim3(256), 0, stream, emit, sub, n, emit_base,
+                           sub_bias + (int64_t)smin, ek0, s32a, ix0);
+        rocprim::radix_sort_pairs(tmp, b, s32a, s32b, ix0, ix1, (size_t)n, 0, sb, stream);
+    } else {
+        hipLaunchKernelGGL(order_keys_k<uint64_t>, dim3(grid), dim3(256), 0, stream, emit, sub, n, emit_base,
+                           sub_bias + (int64_t)smin, ek0, sk0, ix0);
+        rocprim::radix_sort_pairs(tmp, a, sk0, sk1, ix0, ix1, (size_t)n, 0, full ? sub_bits : sb, stream);
+    }
+    perm1 = ix1;
+    // then (stable) by the emitting event
+    hipLaunchKernelGGL(gather_k<uint32_t>, dim3(grid), dim3(256), 0, stream, ek0, perm1, n, ek1);
+    rocprim::radix_sort_pairs(tmp, b, ek1, ek0, perm1, ix0, (size_t)n, 0, eb, stream);
     *perm_out = ix0;
+}
+
+size_t gather_cols_workspace(int64_t n, int ncol) { return (size_t)std::max<int64_t>(n, 1) * ncol * 8 + 256; }
+
+void gather_cols_i64(const int64_t* const* src, int64_t* const* dst, int ncol, const uint32_t* perm, int64_t n,
+                     void* work, hipStream_t stream) {
+    if (n <= 0 || ncol <= 0) return;
+    static const bool cols = getenv("SDG_GATHER_COLS") != nullptr;  // A/B: one random-read gather per column
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    if (cols || ncol == 1) {
+        for (int c = 0; c < ncol; ++c) hipLaunchKernelGGL(gather_k<int64_t>, dim3(grid), dim3(256), 0, stream, src[c], perm, n, dst[c]);
+        return;
+    }
+    for (int c0 = 0; c0 < ncol; c0 += GATHER_MAX_COLS) {
+        const int nc = std::min(GATHER_MAX_COLS, ncol - c0);
+        ColSet cs{};
+        for (int c = 0; c < nc; ++c) {
+            cs.src[c] = src[c0 + c];
+            cs.dst[c] = dst[c0 + c];
+        }
+        int64_t* rec = (int64_t*)work;
+        hipLaunchKernelGGL(pack_k, dim3(grid), dim3(256), 0, stream, cs, nc, n, rec);
+        hipLaunchKernelGGL(unpack_k, dim3(grid), dim3(256), 0, stream, cs, nc, (const int64_t*)rec, perm, n);
+    }
 }
 
 void gather_i64(const int64_t* src, const uint32_t* perm, int64_t n, int64_t* dst, hipStream_t stream) {

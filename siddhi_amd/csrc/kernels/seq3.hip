@@ -451,9 +451,10 @@ void seq3_run(const Seq3Args& a, const Seq3Args* d_a, hipStream_t stream) {
             code(f2.a) == S3_Y * 8 + x && code(f2.b) == S3_E2L * 8 + x && x < 2)
             fx = x;
     }
-    // waves per SIMD the fixed kernels are compiled for (A/B SDG_S3_W=3: <= 168 VGPRs instead of ~190)
+    // waves per SIMD the fixed kernels are compiled for: 3 (<= 168 VGPRs, no spills) measured 11.03 vs 11.49 ms per
+    // C3 step at 2 (~190 VGPRs; r4j, same box); SDG_S3_W=2 for A/B
     static const char* ws = getenv("SDG_S3_W");
-    const bool w3 = ws && atoi(ws) == 3;
+    const bool w3 = !(ws && atoi(ws) == 2);
 #define S3_FIX(X)                                                                                                  \
     do {                                                                                                           \
         if (w3) hipLaunchKernelGGL((seq3_k<2, 8, true, true, S3_Y * 8 + X, S3_Y * 8 + X, S3_E1 * 8 + X, S3_Y * 8 + X,  \
