@@ -357,7 +357,6 @@ def run_c5(args, rank, world, local, dist):
     # of the emitting event: unique across ranks; shard.merge_runs)
     gcap = args.c5_batch // 2 + (1 << 20)
     g_ts = torch.empty(gcap, dtype=torch.int64, device=dev)
-    g_seq, g_sub = torch.empty_like(g_ts), torch.empty_like(g_ts)
     g_vals = torch.empty((2, gcap), dtype=torch.int64, device=dev)
     last_merged = [None]
 
@@ -365,7 +364,8 @@ def run_c5(args, rank, world, local, dist):
 
     def gather():
         t = time.perf_counter()
-        cnt = rt.export_ordered(0, gcap, g_ts.data_ptr(), g_seq.data_ptr(), g_sub.data_ptr(), g_vals.data_ptr())
+        # (the merge key is (e2id, e1id): the engine's own position columns are not exported)
+        cnt = rt.export_ordered(0, gcap, g_ts.data_ptr(), 0, 0, g_vals.data_ptr())
         recs = {"e2": g_vals[1, :cnt], "e1": g_vals[0, :cnt], "ts": g_ts[:cnt]}
         gph["export"] += time.perf_counter() - t
         if dist is None:
@@ -479,7 +479,7 @@ def run_c5(args, rank, world, local, dist):
         out["gather"]["ordered"] = True
         out["gather"]["records_merged_last_step"] = int(e2.numel())
     last_merged[0] = None
-    del batches, g_ts, g_seq, g_sub, g_vals
+    del batches, g_ts, g_vals
     torch.cuda.empty_cache()
     if rank == 0 and not args.no_cpu:
         out["cpu_baseline"] = c5_cpu_baseline(sh)

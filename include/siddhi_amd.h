@@ -164,7 +164,8 @@ int sdg_discard(sdg_engine* e);
 /* device-side export of query `query`'s records from the last flush (instead of sdg_poll), for a multi-GPU ordered
  * gather: copied device-to-device, unordered, into caller buffers of `cap` records (d_vals: [n_out][cap]); the
  * delivery order is (event_seq, sub) ascending -- event_seq = position of the emitting event, sub = the ordinal
- * within it (chain path: the e1 event's position). *n_out = the record count. Not for queries with absent
+ * within it (chain path: the e1 event's position). *n_out = the record count. A null d_ts / d_seq / d_sub / d_vals
+ * is not exported (a gather keyed on output attributes needs neither position column). Not for queries with absent
  * states (their timer matches are ordered on the host). */
 int sdg_export_device(sdg_engine* e, int query, int64_t cap, int64_t* n_out, int64_t* d_ts, int64_t* d_seq,
                       int64_t* d_sub, int64_t* d_vals);

@@ -2394,8 +2394,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         a.seg_start = a.seg_end = nullptr;
     }
     if (sorted) {  // chain_sorted_k: deque / forward scans in LDS blocks, the rest of a cut run in chain_sovf_k
-        static const char* skip = getenv("SDG_FU_SKIP");  // (only the A/B bits: 512 = the deque step's loops)
-        a.fu_skip = (skip ? atoi(skip) : 0) & 512;
+        static const char* skip = getenv("SDG_FU_SKIP");  // A/B: 512 = the deque step's loops; phase timing (results
+        a.fu_skip = (skip ? atoi(skip) : 0) & (512 | 2 | 8 | 16);  // invalid): 8 staging only, 16 no matching, 2 no emission
         a.fu_mode = a.deque_mode;
         a.deque_mode = DQ_OFF;
         a.seg_start = a.seg_end = nullptr;
@@ -3964,20 +3964,25 @@ int export_records(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_t* 
             uint32_t* perm = nullptr;
             order_records((const int64_t*)q.o_emit.p, (const int64_t*)q.o_first.p, n, q.emit_base,
                           q.sub_is_seq ? q.emit_base - (1ll << 40) : 0, q.sub_bits(), work, wb, &perm, st);
-            std::vector<const int64_t*> src{(const int64_t*)q.o_ts.p, (const int64_t*)q.o_emit.p, (const int64_t*)q.o_first.p};
-            std::vector<int64_t*> dst{d_ts, d_seq, d_sub};
-            for (int j = 0; j < na; ++j) {
-                src.push_back((const int64_t*)q.o_vals.p + (size_t)j * q.out_cap);
-                dst.push_back(d_vals + (size_t)j * cap);
-            }
+            std::vector<const int64_t*> src;  // (a null destination column is not exported)
+            std::vector<int64_t*> dst;
+            auto col = [&](const void* from, int64_t* to) {
+                if (!to) return;
+                src.push_back((const int64_t*)from);
+                dst.push_back(to);
+            };
+            col(q.o_ts.p, d_ts);
+            col(q.o_emit.p, d_seq);
+            col(q.o_first.p, d_sub);
+            for (int j = 0; j < na && d_vals; ++j) col((const int64_t*)q.o_vals.p + (size_t)j * q.out_cap, d_vals + (size_t)j * cap);
             gather_cols_i64(src.data(), dst.data(), (int)src.size(), perm, n,
                             q.gather_ws.ensure(gather_cols_workspace(n, std::min((int)src.size(), GATHER_MAX_COLS))), st);
             HIPCHECK(hipStreamSynchronize(st));
         } else if (n > 0) {
-            HIPCHECK(hipMemcpyAsync(d_ts, q.o_ts.p, n * 8, hipMemcpyDeviceToDevice, st));
-            HIPCHECK(hipMemcpyAsync(d_seq, q.o_emit.p, n * 8, hipMemcpyDeviceToDevice, st));
-            HIPCHECK(hipMemcpyAsync(d_sub, q.o_first.p, n * 8, hipMemcpyDeviceToDevice, st));
-            for (int j = 0; j < na; ++j)
+            if (d_ts) HIPCHECK(hipMemcpyAsync(d_ts, q.o_ts.p, n * 8, hipMemcpyDeviceToDevice, st));
+            if (d_seq) HIPCHECK(hipMemcpyAsync(d_seq, q.o_emit.p, n * 8, hipMemcpyDeviceToDevice, st));
+            if (d_sub) HIPCHECK(hipMemcpyAsync(d_sub, q.o_first.p, n * 8, hipMemcpyDeviceToDevice, st));
+            for (int j = 0; j < na && d_vals; ++j)
                 HIPCHECK(hipMemcpyAsync(d_vals + (size_t)j * cap, (const int64_t*)q.o_vals.p + (size_t)j * q.out_cap, n * 8,
                                         hipMemcpyDeviceToDevice, st));
             HIPCHECK(hipStreamSynchronize(st));

@@ -1497,6 +1497,7 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
     // that row is of the same key; else the key's rows of this batch end there (R_CARRY)
     const uint32_t next_key = lo + nr < a.n ? (a.key[lo + nr] & SV_KEY) : 0xFFFFFFFFu;
     __syncthreads();
+    if (a.fu_skip & 8) return;  // SDG_FU_SKIP phase timing (results invalid): loads + LDS staging only
     // per-key time order (the chain path's precondition): own positions against their predecessor
 #pragma unroll
     for (int r = 0; r < FU_PT; ++r) {
@@ -1539,8 +1540,9 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
     auto off_res = [&](int q, uint32_t k) -> uint16_t {
         return (q < nr || next_key != (k & SV_KEY)) ? R_CARRY : R_OVF;
     };
-    if (a.fu_mode != DQ_OFF) {
-        // ---- monotone-deque pass (as chain_fused_k): lane t owns positions [FU_DQ t, FU_DQ (t + 1)) ----------
+    const bool no_match = (a.fu_skip & 16) != 0;  // phase timing: everything but the matching
+    if (a.fu_mode != DQ_OFF && !no_match) {
+        // ---- monotone-deque pass: lane t owns positions [FU_DQ t, FU_DQ (t + 1)) ------------------------------
         const bool stack = a.fu_mode == DQ_STACK;
         const int p0 = t * FU_DQ;
         // the chunk's rows up front (all LDS reads in flight together); the deque holds only the lane's own
@@ -1641,7 +1643,7 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
     }
     // ---- forward scans: carried partials (and every candidate without a deque mode) -------------------------
 #pragma unroll 1
-    for (int k = 0; k < FU_PT; ++k) {
+    for (int k = 0; k < FU_PT && !no_match; ++k) {
         const int pos = k * FU_THREADS + t;
         if (pos >= own) continue;
         const uint32_t kp = s_key[sw(pos)];
@@ -1706,6 +1708,7 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
     }
     __syncthreads();
     // ---- emit matches (loads of a group of rounds, then its stores: see chain_fused_k) ---------------------
+    if (a.fu_skip & 2) return;  // phase timing: no emission
     constexpr uint32_t NOSLOT = 0xFFFFFFFFu;
     uint32_t slot[FU_PT];
     bool any_co = false;

@@ -24,20 +24,23 @@ __device__ __forceinline__ uint32_t digit_of(uint32_t k, int shift, uint32_t mas
 // per-tile digit histogram: counts[tile * nb + d]
 // kcheck (first pass only): keys >= K (device-resident batches whose ids did not come from this engine) set
 // *kflag; every later kernel masks its key-derived indices, so such a batch fails the flush without a fault
-// prefix rows (keygroup's pre_n): rows [0, pre_n) take their keys from pre_keys, the rest from keys[i - pre_n]
+// prefix rows (keygroup's pre_n, first pass): virtual rows [0, hole) are not rows (they align the batch rows: the
+// batch starts at the 64-row boundary hole + pre_n), rows [hole, hole + pre_n) take their keys from pre_keys, the rest
+// from keys[i - hole - pre_n]; n counts the hole
 template <int RX_TILE, int RX_THREADS>
 __global__ __launch_bounds__(RX_THREADS) void rx_hist(const uint32_t* __restrict__ keys, int64_t n, int shift,
                                                       uint32_t mask, int nb, uint32_t* __restrict__ counts,
                                                       uint32_t kcheck, int* __restrict__ kflag,
-                                                      const uint32_t* __restrict__ pre_keys, int64_t pre_n) {
+                                                      const uint32_t* __restrict__ pre_keys, int64_t pre_n, int64_t hole) {
     __shared__ uint32_t h[1 << RX_MAXBITS];
     for (int d = threadIdx.x; d < nb; d += RX_THREADS) h[d] = 0;
     __syncthreads();
     int64_t base = (int64_t)blockIdx.x * RX_TILE;
-    if (base + RX_TILE <= n && base >= pre_n && (((uintptr_t)(keys + base - pre_n)) & 15) == 0) {
+    const int64_t pre_end = hole + pre_n;
+    if (base + RX_TILE <= n && base >= pre_end && (((uintptr_t)(keys + base - pre_end)) & 15) == 0) {
         // full, 16-B aligned tile: 4 keys per load, every load of the thread in flight before the atomics
         constexpr int V = RX_TILE / RX_THREADS / 4;
-        const uint4* kv = reinterpret_cast<const uint4*>(keys + base - pre_n);
+        const uint4* kv = reinterpret_cast<const uint4*>(keys + base - pre_end);
         uint4 x[V];
 #pragma unroll
         for (int r = 0; r < V; ++r) x[r] = kv[r * RX_THREADS + threadIdx.x];
@@ -53,8 +56,8 @@ __global__ __launch_bounds__(RX_THREADS) void rx_hist(const uint32_t* __restrict
 #pragma unroll 4
         for (int r = 0; r < RX_TILE / RX_THREADS; ++r) {
             int64_t i = base + r * RX_THREADS + threadIdx.x;
-            if (i < n) {
-                const uint32_t k = i < pre_n ? pre_keys[i] : keys[i - pre_n];
+            if (i < n && i >= hole) {
+                const uint32_t k = i < pre_end ? pre_keys[i - hole] : keys[i - pre_end];
                 if (kcheck && k >= kcheck) *kflag = 1;
                 atomicAdd(&h[digit_of(k, shift, mask)], 1u);
             }
@@ -163,8 +166,10 @@ struct RxPass {
     int lkey_shift;
     int ntiles;               // tiles; the grid is rounded up to a multiple of xcds (XCD remap)
     int xcds;                 // XCD count of the tile remap (1: tiles in block order)
-    int64_t pre_n;            // first pass only: prefix rows [0, pre_n) from pre_keys / pre_src (8-byte slots), the
-    const uint32_t* pre_keys; // others from keys_in / src at i - pre_n; a prefix row's orig is 0x80000000 | i
+    int64_t pre_n;            // first pass only: virtual rows [0, hole) are not rows (n counts them; the batch rows
+    int64_t hole;             // start 64-row aligned at hole + pre_n), prefix rows [hole, hole + pre_n) come from
+    const uint32_t* pre_keys; // pre_keys / pre_src (8-byte slots), the others from keys_in / src at i - hole - pre_n;
+                              // a prefix row's orig is 0x80000000 | its index
     const void* pre_src[MAX_COLS + 2];
 };
 
@@ -193,6 +198,9 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
     if ((int)tile >= a.ntiles) return;  // block-uniform: the rounding of the grid
     const int64_t base = (int64_t)tile * RX_TILE;
     const int64_t tile_n = min((int64_t)RX_TILE, a.n - base);
+    const int64_t hole = PRE ? a.hole : 0;
+    const int64_t pre_end = PRE ? a.hole + a.pre_n : 0;
+    const int64_t tile_v = tile_n - (base < hole ? hole - base : 0);  // the tile's rows (its staged elements)
     const int64_t wbase = base + w * (R * 64);
     for (int d = t; d < a.nb; d += RX_THREADS) {
         gbase[d] = a.offsets[(int64_t)tile * a.nb + d];
@@ -207,12 +215,12 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int64_t i = wbase + r * 64 + lane;
-        kreg[r] = i < a.n ? (PRE && i < a.pre_n ? a.pre_keys[i] : a.keys_in[i - (PRE ? a.pre_n : 0)]) : 0u;
+        kreg[r] = i < a.n && i >= hole ? (PRE && i < pre_end ? a.pre_keys[i - hole] : a.keys_in[i - pre_end]) : 0u;
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int64_t i = wbase + r * 64 + lane;
-        const bool valid = i < a.n;
+        const bool valid = i < a.n && i >= hole;
         const uint32_t d = valid ? digit_of(kreg[r], a.shift, a.mask) : 0u;
         uint64_t peers = __ballot(valid);
         for (int bit = 0; bit < a.bits; ++bit) {
@@ -258,7 +266,7 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
         const uint32_t wr = wc[w][dig[r]] + rank[r];  // rank among the tile's elements of this digit
         const uint32_t p = tstart[dig[r]] + wr;
         sp2[r / 2] = (r & 1) ? (sp2[r / 2] | (p << 16)) : p;
-        if (i < a.n) sdig[p] = dig[r];
+        if (i < a.n && i >= hole) sdig[p] = dig[r];
     }
     auto sp_of = [&](int r) -> uint32_t { return (sp2[r / 2] >> ((r & 1) * 16)) & 0xFFFFu; };
     // keys | original rows as one word, then every payload column. Software-pipelined: column c + 1 is loaded
@@ -271,10 +279,10 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
         for (int r = 0; r < R; ++r) {
             const int64_t i = wbase + r * 64 + lane;
             uint64_t x = 0;
-            if (PRE && i < a.pre_n) {
-                x = ((const uint64_t*)a.pre_src[c])[i];  // an 8-byte slot: the store keeps the column's low bytes
-            } else if (i < a.n) {
-                const int64_t j = i - (PRE ? a.pre_n : 0);
+            if (PRE && i < pre_end) {
+                if (i >= hole) x = ((const uint64_t*)a.pre_src[c])[i - hole];  // an 8-byte slot: the store keeps the
+            } else if (i < a.n) {                                               // column's low bytes
+                const int64_t j = i - pre_end;
                 if (wd == 8) x = ((const uint64_t*)src)[j];
                 else if (wd == 4) x = ((const uint32_t*)src)[j];
                 else x = ((const uint8_t*)src)[j];
@@ -287,16 +295,16 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
     for (int r = 0; r < R; ++r) {
         const int64_t i = wbase + r * 64 + lane;
         uint32_t o;
-        if (PRE && i < a.pre_n) o = 0x80000000u | (uint32_t)i;
-        else if (a.orig_in) o = i < a.n ? a.orig_in[i - (PRE ? a.pre_n : 0)] : 0u;
-        else o = (uint32_t)(i - (PRE ? a.pre_n : 0));
+        if (PRE && i < pre_end) o = 0x80000000u | (uint32_t)(i - hole);
+        else if (a.orig_in) o = i < a.n ? a.orig_in[i - pre_end] : 0u;
+        else o = (uint32_t)(i - pre_end);
         cur[r] = (uint64_t)kreg[r] | ((uint64_t)o << 32);
     }
     for (int c = -1; c < a.ncols; ++c) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int64_t i = wbase + r * 64 + lane;
-            if (i < a.n) stage[sp_of(r)] = cur[r];
+            if (i < a.n && i >= hole) stage[sp_of(r)] = cur[r];
         }
         if (a.mono_col >= 0 && c == a.mono_col) {  // arrival-order timestamps: compare with row i - 1
             const uint64_t* src = (const uint64_t*)a.src[c];
@@ -317,7 +325,7 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int j = r * RX_THREADS + t;
-            if (j < tile_n) {
+            if (j < tile_v) {
                 const uint32_t dj = sdig[j];
                 const uint32_t o = gbase[dj] + (uint32_t)j - tstart[dj];
                 const uint64_t v = stage[j];
@@ -675,13 +683,13 @@ static int rx_tile() {
 static int64_t rx_ntiles(int64_t n, int tile = RX_TILE) { return n <= 0 ? 1 : (n + tile - 1) / tile; }
 static void launch_rx_hist(int64_t nt, hipStream_t stream, const uint32_t* keys, int64_t n, int shift, uint32_t mask,
                            int nb, uint32_t* counts, uint32_t kcheck, int* kflag, const uint32_t* pre_keys = nullptr,
-                           int64_t pre_n = 0) {
+                           int64_t pre_n = 0, int64_t hole = 0) {
     if (rx_tile() == RX_TILE_BIG)
         hipLaunchKernelGGL((rx_hist<RX_TILE_BIG, RX_THREADS_BIG>), dim3((unsigned)nt), dim3(RX_THREADS_BIG), 0, stream,
-                           keys, n, shift, mask, nb, counts, kcheck, kflag, pre_keys, pre_n);
+                           keys, n, shift, mask, nb, counts, kcheck, kflag, pre_keys, pre_n, hole);
     else
         hipLaunchKernelGGL((rx_hist<RX_TILE, RX_THREADS>), dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, keys, n,
-                           shift, mask, nb, counts, kcheck, kflag, pre_keys, pre_n);
+                           shift, mask, nb, counts, kcheck, kflag, pre_keys, pre_n, hole);
 }
 static void launch_rx_scatter(int64_t nt, hipStream_t stream, RxPass rp) {
     static const bool no_xcd = getenv("SDG_RX_NOXCD") != nullptr;  // A/B: tiles in block order
@@ -703,7 +711,7 @@ static void launch_rx_scatter(int64_t nt, hipStream_t stream, RxPass rp) {
 }
 
 size_t keygroup_workspace(int64_t n, int32_t K, int32_t ncols, const uint8_t* widths) {
-    int64_t nt = rx_ntiles(n);
+    int64_t nt = rx_ntiles(n + 64);  // (+ the first pass's alignment hole)
     int64_t ng = (nt + KG_GROUP - 1) / KG_GROUP;
     size_t b = (size_t)nt * 256 * 4 + (size_t)ng * 256 * 4 + 257 * 4 + 4 * (size_t)n * 4;
     for (int c = 0; c < ncols; ++c) b += 2 * (size_t)n * widths[c] + 256;
@@ -717,7 +725,7 @@ void keygroup_bind(KeyGroupArgs& a, void* base) {
         p += (bytes + 255) & ~size_t(255);
         return (void*)r;
     };
-    int64_t nt = rx_ntiles(a.n);
+    int64_t nt = rx_ntiles(a.n + 64);
     int64_t ng = (nt + KG_GROUP - 1) / KG_GROUP;
     a.counts = (uint32_t*)take((size_t)nt * 256 * 4);
     a.gsum = (uint32_t*)take((size_t)ng * 256 * 4);
@@ -736,8 +744,9 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
     if (kbits == 0) kbits = 1;
     int npass = (kbits + RX_MAXBITS - 1) / RX_MAXBITS;
     int bits = (kbits + npass - 1) / npass;
-    int64_t nt = rx_ntiles(a.n, rx_tile());
-    int ng = (int)((nt + KG_GROUP - 1) / KG_GROUP);
+    // the first pass reads the prefix rows (the sorted view's carried partials) ahead of the batch; a hole of < 64
+    // virtual rows in front of them puts the batch rows at a 64-row boundary, so the batch's loads stay aligned
+    const int64_t hole = a.pre_n > 0 ? (64 - a.pre_n % 64) % 64 : 0;
     if (marks) (void)hipEventRecord(marks[0], stream);
     for (int p = 0; p < npass; ++p) {
         int shift = p * bits;
@@ -746,8 +755,11 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
         uint32_t mask = (uint32_t)nb - 1;
         const uint32_t* kin = p == 0 ? a.keys : a.tmp_keys[(p - 1) & 1];
         bool last = p == npass - 1;
-        launch_rx_hist(nt, stream, kin, a.n, shift, mask, nb, a.counts, p == 0 && a.key_flag ? (uint32_t)a.K : 0u,
-                       a.key_flag, p == 0 ? a.pre_keys : nullptr, p == 0 ? a.pre_n : 0);
+        const int64_t np = p == 0 ? a.n + hole : a.n;  // rows of this pass (virtual: with the hole)
+        const int64_t nt = rx_ntiles(np, rx_tile());
+        const int ng = (int)((nt + KG_GROUP - 1) / KG_GROUP);
+        launch_rx_hist(nt, stream, kin, np, shift, mask, nb, a.counts, p == 0 && a.key_flag ? (uint32_t)a.K : 0u,
+                       a.key_flag, p == 0 ? a.pre_keys : nullptr, p == 0 ? a.pre_n : 0, p == 0 ? hole : 0);
         int64_t gk = (int64_t)ng * nb;
         hipLaunchKernelGGL(rx_p1, dim3((unsigned)((gk + 255) / 256)), dim3(256), 0, stream, a.counts, (int)nt, nb, a.gsum);
         hipLaunchKernelGGL(rx_p2, dim3(1), dim3(256), 0, stream, a.gsum, ng, nb, a.tot);
@@ -767,7 +779,7 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
             rp.width[c] = a.width[c];
         }
         rp.offsets = a.counts;
-        rp.n = a.n;
+        rp.n = np;
         rp.shift = shift;
         rp.mask = mask;
         rp.nb = nb;
@@ -785,6 +797,7 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
         }
         if (p == 0 && a.pre_n > 0) {
             rp.pre_n = a.pre_n;
+            rp.hole = hole;
             rp.pre_keys = a.pre_keys;
             for (int c = 0; c < a.ncols; ++c) rp.pre_src[c] = a.pre_src[c];
         }
