@@ -1423,6 +1423,14 @@ __device__ __forceinline__ int64_t sv_seq(const ChainArgs& a, uint32_t o) {
     return (a.fold && (o & SV_CARRIED)) ? a.cin_seq[o & SV_KEY] : a.seq_base + (int64_t)o;
 }
 
+// group summaries of the sorted-view deque (stack mode, ordering comparisons): per SV_GROUP positions the extreme
+// value that could complete a pending partial -- the max when "x beats y" grows with x, else the min; carried rows
+// (not events) and NaN rows never complete one. A continuation skips a whole group of its key when the summary cannot
+// beat its deque's top (pops only ever take the top, so the group changes the deque by expiry alone, which the
+// group's last -- latest -- row applies). C5's keys keep partials for ~half a batch: continuations run long there.
+constexpr int SV_GROUP = 8;
+static_assert(SV_GROUP == 2 * FU_DQ, "a group summary combines two lanes' chunks");
+
 template <int K, bool SAME>
 __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs* __restrict__ pa) {
     using C = KT<K>;
@@ -1438,6 +1446,7 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
     __shared__ uint32_t wcnt[3][FU_PT][NW];
     __shared__ unsigned long long bbase[3];
     __shared__ int64_t wmin[NW], wmax[NW];
+    __shared__ int64_t s_gs[FU_ROWS / SV_GROUP];  // per SV_GROUP positions: the value that could complete a partial
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     // XCD-aware block order: neighbouring blocks (shared halo rows) on one XCD
     const uint32_t v = xcd_block(blockIdx.x, gridDim.x, (uint32_t)a.xcds);
@@ -1611,6 +1620,21 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
                 for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = (uint16_t)q;
             }
         };
+        const bool mono = bf && stack && (m.gt != m.lt) && !m.ne && !(a.fu_skip & 128);
+        const bool use_max = left == m.gt;
+        T* s_gsum = reinterpret_cast<T*>(s_gs);
+        if (mono) {  // (every lane: the pair combine is a cross-lane shuffle)
+            T ext = use_max ? std::numeric_limits<T>::lowest() : std::numeric_limits<T>::max();
+#pragma unroll
+            for (int i = 0; i < FU_DQ; ++i) {
+                const T x = cxv[i];
+                if (p0 + i < nr && !(ckey[i] & SV_CARRIED) && x == x) ext = use_max ? (x > ext ? x : ext) : (x < ext ? x : ext);
+            }
+            const T o = __shfl_xor(ext, 1);
+            ext = use_max ? (o > ext ? o : ext) : (o < ext ? o : ext);
+            if (!(t & 1)) s_gsum[t >> 1] = ext;
+        }
+        __syncthreads();
         const int pe = min(p0 + FU_DQ, own);  // (FU_OWN is a multiple of FU_DQ: a chunk is all own rows or none)
         uint32_t cur = p0 < own ? (ckey[0] & SV_KEY) : 0u;
 #pragma unroll
@@ -1633,9 +1657,28 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
                 ytop = x;
             }
         }
-        // continuation over the key's following positions until the deque drains
+        // continuation over the key's following positions until the deque drains (whole groups that cannot complete
+        // the deque's top are skipped, their last row's ts applied)
         int q = pe;
-        for (; pend && q < nr && (s_key[sw(q)] & SV_KEY) == cur; ++q) step(q, s_ts[sw(q)], xval(s_x[sw(q)]));
+        while (pend && q < nr) {
+            if (mono && (q & (SV_GROUP - 1)) == 0 && q + SV_GROUP <= nr &&
+                (s_key[sw(q + SV_GROUP - 1)] & SV_KEY) == cur && (s_key[sw(q)] & SV_KEY) == cur) {
+                const T cs = s_gsum[q / SV_GROUP];
+                const T yt = x_of(31 - __builtin_clz(pend));
+                if (!(left ? cmp_m(m, cs, yt) : cmp_m(m, yt, cs))) {
+                    const uint32_t tl = s_ts[sw(q + SV_GROUP - 1)];
+                    uint32_t live = 0;
+#pragma unroll
+                    for (int i = 0; i < FU_DQ; ++i) live |= (uint32_t)((uint64_t)(tl - cts[i]) <= within_u) << i;
+                    pend &= live;
+                    q += SV_GROUP;
+                    continue;
+                }
+            }
+            if ((s_key[sw(q)] & SV_KEY) != cur) break;
+            step(q, s_ts[sw(q)], xval(s_x[sw(q)]));
+            ++q;
+        }
         if (pend) {
             const uint16_t rr = off_res(q, cur);
             for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = rr;
