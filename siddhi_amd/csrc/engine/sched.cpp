@@ -122,19 +122,14 @@ void SchedSim::qpop(KS& k) {
 
 void SchedSim::due_add(SchedState& S, uint32_t key, KS& k) {
     const DueE e{okey(S, k, key), ++k.ver};
-    std::vector<DueE>& h = S.due[qfront(k)];
-    h.push_back(e);
-    std::push_heap(h.begin(), h.end(), std::greater<DueE>());
+    S.due[qfront(k)].push(e);
 }
 
 bool SchedSim::due_front(SchedState& S, int64_t& t, OKey& k) {
     while (!S.due.empty()) {
         auto it = S.due.begin();
-        std::vector<DueE>& h = it->second;
-        while (!h.empty() && stale(S, h.front())) {
-            std::pop_heap(h.begin(), h.end(), std::greater<DueE>());
-            h.pop_back();
-        }
+        DueHeap& h = it->second;
+        while (!h.empty() && stale(S, h.front())) h.pop();
         if (h.empty()) {
             S.due.erase(it);
             continue;
@@ -161,10 +156,10 @@ void SchedSim::resize(SchedState& S) {  // HashMap.resize(): 16 / 12, then doubl
         if (!k.in_map) continue;
         S.bin[(uint32_t)k.hash & (S.cap - 1)]++;
         if (k.n) {  // re-keyed by the new buckets (heaps rebuilt below)
-            S.due[qfront(k)].push_back(DueE{okey(S, k, (uint32_t)key), ++k.ver});
+            S.due[qfront(k)].append(DueE{okey(S, k, (uint32_t)key), ++k.ver});
         }
     }
-    for (auto& kv : S.due) std::make_heap(kv.second.begin(), kv.second.end(), std::greater<DueE>());
+    for (auto& kv : S.due) kv.second.make_heap();
 }
 
 void SchedSim::notify(int sch, uint32_t key, int64_t t) {
@@ -525,11 +520,8 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
                     SchedState& S = work_.sc[s];
                     W.clear();
                     for (auto it = S.due.begin(); it != S.due.end() && it->first <= clock;) {
-                        std::vector<DueE>& h = it->second;
-                        while (!h.empty() && stale(S, h.front())) {
-                            std::pop_heap(h.begin(), h.end(), std::greater<DueE>());
-                            h.pop_back();
-                        }
+                        DueHeap& h = it->second;
+                        while (!h.empty() && stale(S, h.front())) h.pop();
                         if (h.empty()) {
                             it = S.due.erase(it);
                             continue;
@@ -754,7 +746,7 @@ void SchedSim::save(std::vector<uint8_t>& o) const {
         put<uint64_t>(o, S.due.size());
         for (const auto& kv : S.due) {
             put<int64_t>(o, kv.first);
-            put_vec(o, kv.second);
+            put_vec(o, std::vector<DueE>(kv.second.data(), kv.second.data() + kv.second.n));
         }
         put<uint64_t>(o, S.cap);
         put<uint64_t>(o, S.threshold);
@@ -780,7 +772,10 @@ const uint8_t* SchedSim::load(const uint8_t* p, const uint8_t* end) {
         const uint64_t nd = get<uint64_t>(p, end);
         for (uint64_t i = 0; i < nd; ++i) {
             const int64_t t = get<int64_t>(p, end);
-            get_vec(p, end, S.due[t]);
+            std::vector<DueE> v;
+            get_vec(p, end, v);
+            DueHeap& h = S.due[t];
+            for (const DueE& e : v) h.append(e);  // (saved in heap order: the layout is a heap already)
         }
         S.cap = get<uint64_t>(p, end);
         S.threshold = get<uint64_t>(p, end);
