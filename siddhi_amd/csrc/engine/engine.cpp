@@ -2630,13 +2630,15 @@ void drain(sdg_engine* e, QueryRt& q) {
     const bool dev_order = !q.last_timers && n > 1 && hruns.empty();
     if (dev_order) {
         const size_t wb = order_workspace(n);
-        void* work = q.ord_ws.ensure(wb);
+        void* work = q.ord_ws.ensure(wb + wb / 4);  // (slack: a slightly larger flush must not reallocate -- a
+                                                     // hipFree + hipMalloc of GBs costs more than the ordering)
         uint32_t* perm = nullptr;
         order_records((const int64_t*)q.o_emit.p, (const int64_t*)q.o_first.p, n, q.emit_base,
                       q.sub_is_seq ? q.emit_base - (1ll << 40) : 0, q.sub_bits(), work, wb, &perm, st);
-        int64_t* gts = (int64_t*)q.g_ts.ensure((size_t)n * 8);
-        int64_t* gem = (int64_t*)q.g_emit.ensure((size_t)n * 8);
-        int64_t* gv = (int64_t*)q.g_vals.ensure((size_t)std::max(na, 1) * n * 8);
+        const size_t ns = (size_t)(n + n / 4);  // (slack, as the workspaces)
+        int64_t* gts = (int64_t*)q.g_ts.ensure(ns * 8);
+        int64_t* gem = (int64_t*)q.g_emit.ensure(ns * 8);
+        int64_t* gv = (int64_t*)q.g_vals.ensure((size_t)std::max(na, 1) * ns * 8);
         {
             std::vector<const int64_t*> src{(const int64_t*)q.o_ts.p, (const int64_t*)q.o_emit.p};
             std::vector<int64_t*> dst{gts, gem};
@@ -2645,7 +2647,7 @@ void drain(sdg_engine* e, QueryRt& q) {
                 dst.push_back(gv + (size_t)j * n);
             }
             gather_cols_i64(src.data(), dst.data(), (int)src.size(), perm, n,
-                            q.gather_ws.ensure(gather_cols_workspace(n, std::min((int)src.size(), GATHER_MAX_COLS))), st);
+                            q.gather_ws.ensure(gather_cols_workspace(n + n / 4, std::min((int)src.size(), GATHER_MAX_COLS))), st);
         }
         if (q.nulls_valid) {
             uint32_t* gn = (uint32_t*)q.g_nulls.ensure((size_t)n * 4);
@@ -3960,7 +3962,7 @@ int export_records(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_t* 
         const int na = q.hq.plan.n_user_out;
         if (n > 0 && ordered) {  // the delivery-order pass of drain(), gathering straight into the caller's buffers
             const size_t wb = order_workspace(n);
-            void* work = q.ord_ws.ensure(wb);
+            void* work = q.ord_ws.ensure(wb + wb / 4);
             uint32_t* perm = nullptr;
             order_records((const int64_t*)q.o_emit.p, (const int64_t*)q.o_first.p, n, q.emit_base,
                           q.sub_is_seq ? q.emit_base - (1ll << 40) : 0, q.sub_bits(), work, wb, &perm, st);
@@ -3976,7 +3978,7 @@ int export_records(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_t* 
             col(q.o_first.p, d_sub);
             for (int j = 0; j < na && d_vals; ++j) col((const int64_t*)q.o_vals.p + (size_t)j * q.out_cap, d_vals + (size_t)j * cap);
             gather_cols_i64(src.data(), dst.data(), (int)src.size(), perm, n,
-                            q.gather_ws.ensure(gather_cols_workspace(n, std::min((int)src.size(), GATHER_MAX_COLS))), st);
+                            q.gather_ws.ensure(gather_cols_workspace(n + n / 4, std::min((int)src.size(), GATHER_MAX_COLS))), st);
             HIPCHECK(hipStreamSynchronize(st));
         } else if (n > 0) {
             if (d_ts) HIPCHECK(hipMemcpyAsync(d_ts, q.o_ts.p, n * 8, hipMemcpyDeviceToDevice, st));
