@@ -238,6 +238,7 @@ def ordered_gather_leg(rt, step_push, n, dev, dist, rank, world):
     t_seq = torch.empty(cap, dtype=torch.int64, device=dev)
     t_sub = torch.empty(cap, dtype=torch.int64, device=dev)
     t_vals = torch.empty((2, cap), dtype=torch.int64, device=dev)
+    t_rank = torch.full((cap,), rank, dtype=torch.int64, device=dev)  # the merge key's rank column
     # one untimed export first: the ordering pass sizes its workspaces on first use (device allocations)
     step_push()
     rt.flush(deliver=False)
@@ -251,7 +252,7 @@ def ordered_gather_leg(rt, step_push, n, dev, dist, rank, world):
     t0 = time.perf_counter()
     cnt = rt.export_ordered(0, cap, t_ts.data_ptr(), t_seq.data_ptr(), t_sub.data_ptr(), t_vals.data_ptr())
     recs = {"ts": t_ts[:cnt], "seq": t_seq[:cnt], "sub": t_sub[:cnt],
-            "rank": torch.full((cnt,), rank, dtype=torch.int64, device=dev), "vals": t_vals[:, :cnt]}
+            "rank": t_rank[:cnt], "vals": t_vals[:, :cnt]}
     gph = {"export": time.perf_counter() - t0, "transfer": 0.0, "merge": 0.0}
     if dist is None:
         merged = recs

@@ -122,14 +122,19 @@ void SchedSim::qpop(KS& k) {
 
 void SchedSim::due_add(SchedState& S, uint32_t key, KS& k) {
     const DueE e{okey(S, k, key), ++k.ver};
-    S.due[qfront(k)].push(e);
+    std::vector<DueE>& h = S.due[qfront(k)];
+    h.push_back(e);
+    std::push_heap(h.begin(), h.end(), std::greater<DueE>());
 }
 
 bool SchedSim::due_front(SchedState& S, int64_t& t, OKey& k) {
     while (!S.due.empty()) {
         auto it = S.due.begin();
-        DueHeap& h = it->second;
-        while (!h.empty() && stale(S, h.front())) h.pop();
+        std::vector<DueE>& h = it->second;
+        while (!h.empty() && stale(S, h.front())) {
+            std::pop_heap(h.begin(), h.end(), std::greater<DueE>());
+            h.pop_back();
+        }
         if (h.empty()) {
             S.due.erase(it);
             continue;
@@ -156,10 +161,10 @@ void SchedSim::resize(SchedState& S) {  // HashMap.resize(): 16 / 12, then doubl
         if (!k.in_map) continue;
         S.bin[(uint32_t)k.hash & (S.cap - 1)]++;
         if (k.n) {  // re-keyed by the new buckets (heaps rebuilt below)
-            S.due[qfront(k)].append(DueE{okey(S, k, (uint32_t)key), ++k.ver});
+            S.due[qfront(k)].push_back(DueE{okey(S, k, (uint32_t)key), ++k.ver});
         }
     }
-    for (auto& kv : S.due) kv.second.make_heap();
+    for (auto& kv : S.due) std::make_heap(kv.second.begin(), kv.second.end(), std::greater<DueE>());
 }
 
 void SchedSim::notify(int sch, uint32_t key, int64_t t) {
@@ -520,8 +525,11 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
                     SchedState& S = work_.sc[s];
                     W.clear();
                     for (auto it = S.due.begin(); it != S.due.end() && it->first <= clock;) {
-                        DueHeap& h = it->second;
-                        while (!h.empty() && stale(S, h.front())) h.pop();
+                        std::vector<DueE>& h = it->second;
+                        while (!h.empty() && stale(S, h.front())) {
+                            std::pop_heap(h.begin(), h.end(), std::greater<DueE>());
+                            h.pop_back();
+                        }
                         if (h.empty()) {
                             it = S.due.erase(it);
                             continue;
@@ -746,7 +754,7 @@ void SchedSim::save(std::vector<uint8_t>& o) const {
         put<uint64_t>(o, S.due.size());
         for (const auto& kv : S.due) {
             put<int64_t>(o, kv.first);
-            put_vec(o, std::vector<DueE>(kv.second.data(), kv.second.data() + kv.second.n));
+            put_vec(o, kv.second);
         }
         put<uint64_t>(o, S.cap);
         put<uint64_t>(o, S.threshold);
@@ -772,10 +780,7 @@ const uint8_t* SchedSim::load(const uint8_t* p, const uint8_t* end) {
         const uint64_t nd = get<uint64_t>(p, end);
         for (uint64_t i = 0; i < nd; ++i) {
             const int64_t t = get<int64_t>(p, end);
-            std::vector<DueE> v;
-            get_vec(p, end, v);
-            DueHeap& h = S.due[t];
-            for (const DueE& e : v) h.append(e);  // (saved in heap order: the layout is a heap already)
+            get_vec(p, end, S.due[t]);
         }
         S.cap = get<uint64_t>(p, end);
         S.threshold = get<uint64_t>(p, end);

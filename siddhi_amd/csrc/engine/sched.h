@@ -216,81 +216,9 @@ class SchedSim {
         uint32_t ver;
         bool operator>(const DueE& o) const { return o.k < k; }
     };
-    // the states whose queue head is one time: a min-heap (lazy deletion) with two entries inline -- most due times
-    // hold one or two states, so the common case allocates nothing
-    struct DueHeap {
-        DueE in[2];
-        uint32_t n = 0;
-        std::vector<DueE> big;  // all entries once more than two were ever held
-        DueE* data() { return big.empty() ? in : big.data(); }
-        const DueE* data() const { return big.empty() ? in : big.data(); }
-        bool empty() const { return n == 0; }
-        const DueE& front() const { return data()[0]; }
-        void push(const DueE& e) {
-            if (big.empty() && n < 2) {
-                in[n++] = e;
-            } else {
-                if (big.empty()) big.assign(in, in + n);
-                big.push_back(e);
-                ++n;
-            }
-            std::push_heap(data(), data() + n, std::greater<DueE>());
-        }
-        void append(const DueE& e) {  // unordered (make_heap afterwards)
-            if (big.empty() && n < 2) {
-                in[n++] = e;
-            } else {
-                if (big.empty()) big.assign(in, in + n);
-                big.push_back(e);
-                ++n;
-            }
-        }
-        void make_heap() { std::make_heap(data(), data() + n, std::greater<DueE>()); }
-        void pop() {
-            std::pop_heap(data(), data() + n, std::greater<DueE>());
-            --n;
-            if (!big.empty()) big.pop_back();
-        }
-    };
-    // std::map nodes from a per-thread free list (a due time's node is created and erased once per time: the
-    // allocator was a third of the scheduler simulation's cost at 10^6 keys)
-    template <class T>
-    struct PoolAlloc {
-        using value_type = T;
-        PoolAlloc() = default;
-        template <class U>
-        PoolAlloc(const PoolAlloc<U>&) noexcept {}
-        static std::vector<void*>& freelist() {
-            static thread_local std::vector<void*> f;
-            return f;
-        }
-        T* allocate(size_t n) {
-            if (n == 1) {
-                std::vector<void*>& f = freelist();
-                if (!f.empty()) {
-                    void* p = f.back();
-                    f.pop_back();
-                    return (T*)p;
-                }
-            }
-            return (T*)::operator new(n * sizeof(T));
-        }
-        void deallocate(T* p, size_t n) noexcept {
-            if (n == 1 && freelist().size() < (1u << 20)) {
-                freelist().push_back(p);
-                return;
-            }
-            ::operator delete(p);
-        }
-        template <class U>
-        bool operator==(const PoolAlloc<U>&) const noexcept { return true; }
-        template <class U>
-        bool operator!=(const PoolAlloc<U>&) const noexcept { return false; }
-    };
-    using DueMap = std::map<int64_t, DueHeap, std::less<int64_t>, PoolAlloc<std::pair<const int64_t, DueHeap>>>;
     struct SchedState {
         std::vector<KS> ks;                                 // [dense key id]
-        DueMap due;                                         // head time -> min-heap of states (lazy deletion)
+        std::map<int64_t, std::vector<DueE>> due;           // head time -> min-heap of states (lazy deletion)
         uint64_t cap = 0, threshold = 0, size = 0, stamp = 0;
         size_t kend = 0;                                    // keys [0, kend) have ever entered the map (resize scans them)
         std::vector<uint32_t> bin;                          // keys per bucket (treeifyBin on a small table resizes)
