@@ -54,6 +54,36 @@ __global__ __launch_bounds__(256) void order_keys_k(const int64_t* __restrict__ 
     idx[i] = (uint32_t)i;
 }
 
+// after the sort by the emitting event: each run of records with one emitting event, in ordinal order. A run is
+// short (the partials one event completes / the records one event emits); its first record's thread insertion-sorts
+// the run's record indices by sub. A run longer than RUN_MAX is left to the two-sort ordering (*long_run set).
+constexpr int RUN_MAX = 256;
+__global__ __launch_bounds__(256) void order_runs_k(const uint32_t* __restrict__ ek, uint32_t* __restrict__ perm,
+                                                    const int64_t* __restrict__ sub, int64_t n, int* __restrict__ long_run) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t e = ek[i];
+    if (i > 0 && ek[i - 1] == e) return;  // not the first record of its run
+    int64_t j = i + 1;
+    while (j < n && ek[j] == e && j - i <= RUN_MAX) ++j;
+    const int64_t len = j - i;
+    if (len < 2) return;
+    if (len > RUN_MAX) {
+        atomicOr(long_run, 1);
+        return;
+    }
+    for (int64_t x = i + 1; x < j; ++x) {  // insertion sort by sub (the run's records are few)
+        const uint32_t v = perm[x];
+        const int64_t kv = sub[v];
+        int64_t y = x - 1;
+        while (y >= i && sub[perm[y]] > kv) {
+            perm[y + 1] = perm[y];
+            --y;
+        }
+        perm[y + 1] = v;
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void gather_k(const T* __restrict__ src, const uint32_t* __restrict__ perm, int64_t n,
                                                 T* __restrict__ dst) {
@@ -140,6 +170,25 @@ void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t e
         eb = std::max(1, bits_for(h[0]));
         smin = h[1];
         sb = std::max(1, bits_for(h[2] - h[1]));
+    }
+    // one sort by the emitting event, then each run of one event's records put in ordinal order (order_runs_k);
+    // runs longer than RUN_MAX (an event that completed hundreds of partials) take the two-sort ordering below
+    static const bool two = getenv("SDG_ORDER_TWO") != nullptr;  // A/B: always the two sorts
+    if (!full && !two) {
+        uint32_t* s32a = (uint32_t*)sk0;
+        hipLaunchKernelGGL(order_keys_k<uint32_t>, dim3(grid), dim3(256), 0, stream, emit, sub, n, emit_base,
+                           sub_bias + (int64_t)smin, ek0, s32a, ix0);  // (only ek0 / ix0 are used here)
+        rocprim::radix_sort_pairs(tmp, b, ek0, ek1, ix0, ix1, (size_t)n, 0, eb, stream);
+        int* flag = (int*)(rng + 3);
+        (void)hipMemsetAsync(flag, 0, 4, stream);
+        hipLaunchKernelGGL(order_runs_k, dim3(grid), dim3(256), 0, stream, ek1, ix1, sub, n, flag);
+        int hf = 0;
+        (void)hipMemcpyAsync(&hf, flag, 4, hipMemcpyDeviceToHost, stream);
+        (void)hipStreamSynchronize(stream);
+        if (!hf) {
+            *perm_out = ix1;
+            return;
+        }
     }
     uint32_t* perm1 = nullptr;
     if (!full && sb <= 32) {  // the ordinal as a 32-bit key relative to its minimum
