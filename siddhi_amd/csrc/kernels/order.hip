@@ -1,9 +1,11 @@
 // Delivery order of a flush's match records on the device: records come out of the matchers in arbitrary order
 // (wave-aggregated appends), and the reference delivers them by emitting event, then by the partial's place in
 // the pending list (StateMultiProcessStreamReceiver.processAndClear :47-68, QuerySelector.processNoGroupBy
-// :161-205). Two stable LSD radix sorts of a record index (rocPRIM: a library sort for a bookkeeping pass, not
-// the matching path) -- by the ordinal, then by the emitting event's position -- and one gather per column, so
-// the host reads the records back already in order.
+// :161-205). One LSD radix sort of a record index by the emitting event's position (rocPRIM: a library sort for a
+// bookkeeping pass, not the matching path) over the bits the flush's records use, then each run of one event's
+// records (short: the partials one event completed) insertion-sorted by its ordinal; a run over RUN_MAX records
+// falls back to two sorts (by the ordinal, then stably by the event). The columns follow through one packed
+// gather, so the host / the gather reads the records already in order.
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdlib>
