@@ -247,6 +247,7 @@ struct QueryRt {
     // delivery order on the device (order.hip): the flush's first position, and whether `sub` holds the e1 event's
     // position (chain path) or an ordinal within the emitting event (generic NFA)
     int64_t emit_base = 0;
+    int64_t emit_span = 0;  // positions of that flush (emit - emit_base < emit_span)
     bool sub_is_seq = false;
     DevBuf ord_ws, g_ts, g_emit, g_vals, g_nulls, g_key, gather_ws;
     // the selector's post pass (aggregators / having): per-key aggregator state, persistent; staging
@@ -348,6 +349,7 @@ struct sdg_engine {
     int32_t max_partials = 8;  // starting slots per key (arenas double on overflow): small arenas stage in LDS
     int64_t pending_n = 0;
     int64_t seq = 0;             // batch positions flushed so far (sequence number of the next batch's position 0)
+    int64_t flush_G = 0;         // positions of the flush being run (its records' emitting events are < seq + flush_G)
     int64_t clock = 0;           // currentTime(): playback = max event ts seen; live = the modelled wall clock
     bool any_sched = false;      // some query has absent states (the batch clock is built)
     bool any_purge = false;      // some query's partition purges idle keys (the batch clock is built)
@@ -1808,6 +1810,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         q.runs.clear();
         q.last_seq_base = e->seq;
         q.emit_base = e->seq;
+        q.emit_span = e->flush_G;
         q.sub_is_seq = false;
         float ms_kg = 0, ms_m = 0, t;
         ev_elapsed(&ms_kg, e->ev[0], e->ev[1]);
@@ -2104,6 +2107,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         q.runs.clear();
         q.last_seq_base = e->seq;
         q.emit_base = e->seq;
+        q.emit_span = e->flush_G;
         q.sub_is_seq = false;
         q.spill_runs.clear();
         if (can_spill && (!spill_new.empty() || !q.spill.empty())) {
@@ -2576,6 +2580,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     e->stats.path = 0;
     q.last_timers = false;
     q.emit_base = e->seq;
+    q.emit_span = e->flush_G;
     q.sub_is_seq = true;
     hp.mark("post_sync");
     return true;
@@ -2633,7 +2638,7 @@ void drain(sdg_engine* e, QueryRt& q) {
         void* work = q.ord_ws.ensure(wb + wb / 4);  // (slack: a slightly larger flush must not reallocate -- a
                                                      // hipFree + hipMalloc of GBs costs more than the ordering)
         uint32_t* perm = nullptr;
-        order_records((const int64_t*)q.o_emit.p, (const int64_t*)q.o_first.p, n, q.emit_base,
+        order_records((const int64_t*)q.o_emit.p, (const int64_t*)q.o_first.p, n, q.emit_base, q.emit_span,
                       q.sub_is_seq ? q.emit_base - (1ll << 40) : 0, q.sub_bits(), work, wb, &perm, st);
         const size_t ns = (size_t)(n + n / 4);  // (slack, as the workspaces)
         int64_t* gts = (int64_t*)q.g_ts.ensure(ns * 8);
@@ -2964,6 +2969,7 @@ int do_flush(sdg_engine* e) {
     int64_t G = 0;
     for (auto& c : e->pending) G += c.n;
     consume.G = G;
+    e->flush_G = G;
     if (G >= (int64_t)0xFFFFFFF0) throw CompileError(SDG_ERR_CAPACITY, "a flush holds more than 2^32 - 16 events");
     if (e->any_sched || e->any_purge) {
         build_clock(e, G);
@@ -3964,7 +3970,7 @@ int export_records(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_t* 
             const size_t wb = order_workspace(n);
             void* work = q.ord_ws.ensure(wb + wb / 4);
             uint32_t* perm = nullptr;
-            order_records((const int64_t*)q.o_emit.p, (const int64_t*)q.o_first.p, n, q.emit_base,
+            order_records((const int64_t*)q.o_emit.p, (const int64_t*)q.o_first.p, n, q.emit_base, q.emit_span,
                           q.sub_is_seq ? q.emit_base - (1ll << 40) : 0, q.sub_bits(), work, wb, &perm, st);
             std::vector<const int64_t*> src;  // (a null destination column is not exported)
             std::vector<int64_t*> dst;

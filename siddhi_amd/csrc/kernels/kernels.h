@@ -233,7 +233,10 @@ void chain_sovf(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
 // (the same scan over the bucket in HBM, key-filtered); one that reaches the bucket end is carried.
 // Preconditions (host): partitioned, one stream, two states, `within`, typed e2 scan without nulls, FastPred
 // e1 filter, plain-attribute selects, K <= 2^16, batch timestamps non-decreasing (checked by bucketize).
-constexpr int FU_THREADS = 512;
+#ifndef SDG_FU_THREADS
+#define SDG_FU_THREADS 512  // (A/B builds: 1024 -> 4096 staged rows per block, 2 blocks of ~78 KB LDS per CU)
+#endif
+constexpr int FU_THREADS = SDG_FU_THREADS;
 constexpr int FU_PT = 4;                             // staged rows per lane (= the deque chunk)
 constexpr int FU_ROWS = FU_THREADS * FU_PT;          // 2048 rows in LDS
 #ifndef SDG_FU_DQ
@@ -420,7 +423,9 @@ void nfa_commit_slots(const SlotPool& sp, uint8_t* cur, uint8_t* ran, int64_t sl
 // broadcast rows); both sorts cover only the key range the records use (measured first: one small read-back);
 // work = order_workspace(n) bytes
 size_t order_workspace(int64_t n);
-void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t emit_base, int64_t sub_bias, int sub_bits,
+// emit_span: the flush's positions (emit - emit_base < emit_span; 0: unknown, measured)
+void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t emit_base, int64_t emit_span,
+                   int64_t sub_bias, int sub_bits,
                    void* work, size_t work_bytes, uint32_t** perm_out, hipStream_t stream);
 void gather_i64(const int64_t* src, const uint32_t* perm, int64_t n, int64_t* dst, hipStream_t stream);
 // dst[c][i] = src[c][perm[i]] for ncol int64 columns, through a packed row-major copy (work = gather_cols_workspace)

@@ -45,6 +45,14 @@ __global__ __launch_bounds__(256) void order_range_k(const int64_t* __restrict__
     }
 }
 
+__global__ __launch_bounds__(256) void order_emit_keys_k(const int64_t* __restrict__ emit, int64_t n, int64_t emit_base,
+                                                         uint32_t* __restrict__ ek, uint32_t* __restrict__ idx) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    ek[i] = (uint32_t)(emit[i] - emit_base);
+    idx[i] = (uint32_t)i;
+}
+
 template <typename SK>
 __global__ __launch_bounds__(256) void order_keys_k(const int64_t* __restrict__ emit, const int64_t* __restrict__ sub,
                                                     int64_t n, int64_t emit_base, int64_t sub_bias, uint32_t* __restrict__ ek,
@@ -138,8 +146,8 @@ size_t order_workspace(int64_t n) {
     return sort_tmp + (size_t)n * (16 + 8 + 8) + 1024;
 }
 
-void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t emit_base, int64_t sub_bias, int sub_bits,
-                   void* work, size_t work_bytes, uint32_t** perm_out, hipStream_t stream) {
+void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t emit_base, int64_t emit_span,
+                   int64_t sub_bias, int sub_bits, void* work, size_t work_bytes, uint32_t** perm_out, hipStream_t stream) {
     if (n <= 0) return;
     size_t a = 0, b = 0;
     temp_sizes(n, a, b);
@@ -159,27 +167,15 @@ void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t e
     // the keys' actual ranges (one small read-back): both sorts cover only the bits the flush's records use --
     // an e1 position / ordinal spans ~30 bits, not the 48 or 64 of its encoding, and then fits a 32-bit key
     static const bool full = getenv("SDG_ORDER_FULL") != nullptr;  // A/B: the fixed-width sorts
+    static const bool two = getenv("SDG_ORDER_TWO") != nullptr;    // A/B: always the two sorts
     int eb = 32, sb = sub_bits;
     unsigned long long smin = 0;
-    if (!full) {
-        const unsigned long long init[3] = {0ull, ~0ull, 0ull};
-        (void)hipMemcpyAsync(rng, init, sizeof init, hipMemcpyHostToDevice, stream);
-        hipLaunchKernelGGL(order_range_k, dim3((unsigned)std::min<int64_t>(grid, 2048)), dim3(256), 0, stream, emit, sub, n,
-                           emit_base, sub_bias, rng);
-        unsigned long long h[3];
-        (void)hipMemcpyAsync(h, rng, sizeof h, hipMemcpyDeviceToHost, stream);
-        (void)hipStreamSynchronize(stream);
-        eb = std::max(1, bits_for(h[0]));
-        smin = h[1];
-        sb = std::max(1, bits_for(h[2] - h[1]));
-    }
     // one sort by the emitting event, then each run of one event's records put in ordinal order (order_runs_k);
-    // runs longer than RUN_MAX (an event that completed hundreds of partials) take the two-sort ordering below
-    static const bool two = getenv("SDG_ORDER_TWO") != nullptr;  // A/B: always the two sorts
-    if (!full && !two) {
-        uint32_t* s32a = (uint32_t*)sk0;
-        hipLaunchKernelGGL(order_keys_k<uint32_t>, dim3(grid), dim3(256), 0, stream, emit, sub, n, emit_base,
-                           sub_bias + (int64_t)smin, ek0, s32a, ix0);  // (only ek0 / ix0 are used here)
+    // runs longer than RUN_MAX (an event that completed hundreds of partials) take the two-sort ordering below.
+    // The emitting events lie in the flush's positions, so that sort needs no range pass
+    if (!full && !two && emit_span > 0) {
+        eb = std::max(1, bits_for((unsigned long long)(emit_span - 1)));
+        hipLaunchKernelGGL(order_emit_keys_k, dim3(grid), dim3(256), 0, stream, emit, n, emit_base, ek0, ix0);
         rocprim::radix_sort_pairs(tmp, b, ek0, ek1, ix0, ix1, (size_t)n, 0, eb, stream);
         int* flag = (int*)(rng + 3);
         (void)hipMemsetAsync(flag, 0, 4, stream);
@@ -191,6 +187,18 @@ void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t e
             *perm_out = ix1;
             return;
         }
+    }
+    if (!full) {
+        const unsigned long long init[3] = {0ull, ~0ull, 0ull};
+        (void)hipMemcpyAsync(rng, init, sizeof init, hipMemcpyHostToDevice, stream);
+        hipLaunchKernelGGL(order_range_k, dim3((unsigned)std::min<int64_t>(grid, 2048)), dim3(256), 0, stream, emit, sub, n,
+                           emit_base, sub_bias, rng);
+        unsigned long long h[3];
+        (void)hipMemcpyAsync(h, rng, sizeof h, hipMemcpyDeviceToHost, stream);
+        (void)hipStreamSynchronize(stream);
+        eb = std::max(1, bits_for(h[0]));
+        smin = h[1];
+        sb = std::max(1, bits_for(h[2] - h[1]));
     }
     uint32_t* perm1 = nullptr;
     if (!full && sb <= 32) {  // the ordinal as a 32-bit key relative to its minimum
