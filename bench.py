@@ -650,7 +650,7 @@ def main():
     d_ts0 = torch.from_numpy(cols["ts"]).to(dev)
     span = int(cols["ts"][-1] - cols["ts"][0]) + 1
     nsteps = args.warmup + args.steps
-    ts_steps = [d_ts0 + s * span for s in range(nsteps + 1)]  # consecutive batches of one stream (+1: gather leg)
+    ts_steps = [d_ts0 + s * span for s in range(nsteps + 2)]  # consecutive batches of one stream (+2: gather leg)
     torch.cuda.synchronize()
 
     def step(s):
@@ -755,10 +755,14 @@ def main():
         out["cpu_baseline"] = None
     if not args.no_gather:
         log("ordered result gather (one more batch, outside the timed region)")
-        out["ordered_gather"] = ordered_gather_leg(rt, step_push=lambda: rt.push_device(
-            "StockStream", n, ts_steps[nsteps].data_ptr(), [d_id.data_ptr(), d_sym.data_ptr(), d_price.data_ptr(),
-                                                            d_vol.data_ptr()]), n=n, dev=dev, dist=dist, rank=rank,
-            world=world)
+        nxt = [nsteps]  # the leg's two batches (a warm-up export, then the timed one) continue the stream's time
+
+        def leg_push():
+            rt.push_device("StockStream", n, ts_steps[nxt[0]].data_ptr(),
+                           [d_id.data_ptr(), d_sym.data_ptr(), d_price.data_ptr(), d_vol.data_ptr()])
+            nxt[0] += 1
+        out["ordered_gather"] = ordered_gather_leg(rt, step_push=leg_push, n=n, dev=dev, dist=dist, rank=rank,
+                                                   world=world)
     rt.shutdown()
     if args.e2e_steps > 0 and world == 1:
         log("end-to-end (host push -> poll), %d step(s)" % args.e2e_steps)
