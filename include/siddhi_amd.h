@@ -21,6 +21,7 @@
  *                            core/stream/output/StreamCallback.java:93-129), columnar
  *   sdg_snapshot /       <- SiddhiAppRuntime.snapshot() / restore(byte[]), persist() / restoreRevision()
  *   sdg_restore             (core/SiddhiAppRuntimeImpl.java:677-737)
+ *   sdg_snapshot_states  <- the StreamPreState maps SnapshotService collects (StreamPreStateProcessor.java:450-469)
  *   sdg_destroy          <- SiddhiAppRuntime.shutdown()
  *
  * Conventions (mirroring the reference): compile errors are returned as status codes with a thread-local
@@ -180,6 +181,11 @@ int sdg_export_ordered(sdg_engine* e, int query, int64_t cap, int64_t* n_out, in
  * from the same app text (else SDG_ERR_ARG, CannotRestoreSiddhiAppStateException) and nothing pending. */
 int sdg_snapshot(sdg_engine* e, const uint8_t** data, int64_t* len);
 int sdg_restore(sdg_engine* e, const uint8_t* data, int64_t len);
+/* a snapshot of this app decoded into the reference's state maps: per query, per partition key, per processor the
+ * StreamPreState.snapshot() map (core/query/input/stream/state/StreamPreStateProcessor.java:450-459, + the Count /
+ * Absent / AbsentLogical fields), as JSON (layout in DESIGN.md "Snapshot state maps"). Needs no device: the blob
+ * holds the arenas. The text stays valid until the next call / sdg_destroy. */
+int sdg_snapshot_states(sdg_engine* e, const uint8_t* data, int64_t len, const char** json, int64_t* json_len);
 
 /* introspection for measurement: device time of the last flush per kernel family, algorithmic bytes,
  * match count, and which kernel path each query took (0 = chain, 1 = generic). */

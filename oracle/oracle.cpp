@@ -2949,6 +2949,155 @@ extern "C" const char* orc_string(orc_engine* e, uint32_t id) {
     return e->rt.eng.strings.strs[id].c_str();
 }
 
+// ---- state dump: every StateHolder's snapshot() map of the pattern processors -------------------------------
+// StreamPreState.snapshot() (StreamPreStateProcessor.java:450-459) + CountStreamPreState (CountPreStateProcessor
+// .java:206-212), AbsentStreamPreState (AbsentStreamPreStateProcessor.java:328-334), LogicalStreamPreState of an
+// absent side (AbsentLogicalPreStateProcessor.java:407-413), as JSON:
+//   {"queries":[{"name":..,"states":{"<partition key>":{"<stateId>":{"FirstEvent":..,"PendingStateEventList":[SE..],
+//     "NewAndEveryStateEventList":[SE..],"Initialized":..,"Started":.., +subclass fields}}}}]}
+//   SE = {"ts":..,"type":..,"events":[null | [{"ts":..,"data":[v..]} ..] per position]}
+// States a holder would destroy on return (canDestroy) are left out, as are keys left with none: the dump shows
+// what a snapshot taken between two events holds. Values: integers, reals as "%.17g" of the double (strings
+// "NaN" / "Infinity" / "-Infinity"), booleans, strings; null.
+static void dump_str(std::string& o, const std::string& s) {
+    o += '"';
+    for (unsigned char c : s) {
+        if (c == '"' || c == '\\') {
+            o += '\\';
+            o += (char)c;
+        } else if (c < 0x20) {
+            char b[8];
+            std::snprintf(b, sizeof b, "\\u%04x", c);
+            o += b;
+        } else {
+            o += (char)c;
+        }
+    }
+    o += '"';
+}
+static void dump_real(std::string& o, double x) {
+    if (x != x) { o += "\"NaN\""; return; }
+    if (std::isinf(x)) { o += x > 0 ? "\"Infinity\"" : "\"-Infinity\""; return; }
+    char b[40];
+    std::snprintf(b, sizeof b, "%.17g", x);
+    o += b;
+}
+static void dump_val(std::string& o, const Val& v, const Interner& S) {
+    if (v.null) { o += "null"; return; }
+    switch ((Type)v.t) {
+        case Type::INT: o += std::to_string(v.i()); break;
+        case Type::LONG: o += std::to_string(v.l()); break;
+        case Type::FLOAT: dump_real(o, (double)v.f()); break;
+        case Type::DOUBLE: dump_real(o, v.d()); break;
+        case Type::BOOL: o += v.b() ? "true" : "false"; break;
+        default: dump_str(o, v.raw >= 0 && (size_t)v.raw < S.strs.size() ? S.strs[(size_t)v.raw] : std::string()); break;
+    }
+}
+static void dump_se(std::string& o, const StateEvent* s, const Interner& S) {
+    if (!s) { o += "null"; return; }
+    o += "{\"ts\":" + std::to_string(s->ts) + ",\"type\":" + std::to_string((int)s->type) + ",\"events\":[";
+    for (size_t p = 0; p < s->se.size(); ++p) {
+        if (p) o += ',';
+        const StreamEvent* e = s->se[p].get();
+        if (!e) { o += "null"; continue; }
+        o += '[';
+        for (bool first = true; e; e = e->next.get(), first = false) {
+            if (!first) o += ',';
+            o += "{\"ts\":" + std::to_string(e->ts) + ",\"data\":[";
+            for (size_t j = 0; j < e->data.size(); ++j) {
+                if (j) o += ',';
+                dump_val(o, e->data[j], S);
+            }
+            o += "]}";
+        }
+        o += ']';
+    }
+    o += "]}";
+}
+static void dump_list(std::string& o, const std::list<StEv>& l, const Interner& S) {
+    o += '[';
+    bool first = true;
+    for (const StEv& s : l) {
+        if (!first) o += ',';
+        first = false;
+        dump_se(o, s.get(), S);
+    }
+    o += ']';
+}
+static void dump_state(std::string& o, const PreProc* p, const PreState& s, const Interner& S) {
+    o += "{\"FirstEvent\":";
+    dump_se(o, s.cur.first.get(), S);
+    o += ",\"PendingStateEventList\":";
+    dump_list(o, s.pending, S);
+    o += ",\"NewAndEveryStateEventList\":";
+    dump_list(o, s.newAndEvery, S);
+    o += std::string(",\"Initialized\":") + (s.initialized ? "true" : "false");
+    o += std::string(",\"Started\":") + (s.started ? "true" : "false");
+    if (p->kind == PreKind::COUNT) {
+        o += std::string(",\"SuccessCondition\":") + (s.successCondition ? "true" : "false");
+        o += std::string(",\"StartStateReset\":") + (s.startStateReset ? "true" : "false");
+    } else if (dynamic_cast<const AbsentLogicalPre*>(p)) {
+        o += std::string(",\"IsActive\":") + (s.active ? "true" : "false");
+        o += ",\"LastArrivalTime\":" + std::to_string(s.lastArrivalTime);
+    } else if (p->kind == PreKind::ABSENT) {
+        o += std::string(",\"IsActive\":") + (s.active ? "true" : "false");
+        o += ",\"LastScheduledTime\":" + std::to_string(s.lastScheduledTime);
+    }
+    o += '}';
+}
+
+static thread_local std::string g_dump;
+
+extern "C" const char* orc_state_dump(orc_engine* e) {
+    try {
+        const Interner& S = e->rt.eng.strings;
+        std::string& o = g_dump;
+        o = "{\"queries\":[";
+        for (size_t qi = 0; qi < e->rt.queries.size(); ++qi) {
+            const QueryRt& q = *e->rt.queries[qi];
+            if (qi) o += ',';
+            o += "{\"name\":";
+            dump_str(o, q.name);
+            o += ",\"states\":{";
+            std::vector<const PreProc*> pres(q.allPre.begin(), q.allPre.end());
+            std::sort(pres.begin(), pres.end(), [](const PreProc* a, const PreProc* b) { return a->stateId < b->stateId; });
+            // key -> (stateId -> state)
+            std::map<std::string, std::vector<std::pair<int, const PreState*>>> keys;
+            for (const PreProc* p : pres) {
+                const PreStateHolder& h = p->holder;
+                if (!h.partitioned) {
+                    if (h.single && !h.single->canDestroy()) keys[""].push_back({p->stateId, h.single.get()});
+                } else {
+                    for (const auto& kv : h.map)
+                        if (kv.second && !kv.second->canDestroy()) keys[kv.first].push_back({p->stateId, kv.second.get()});
+                }
+            }
+            bool fk = true;
+            for (const auto& kv : keys) {
+                if (!fk) o += ',';
+                fk = false;
+                dump_str(o, kv.first);
+                o += ":{";
+                for (size_t i = 0; i < kv.second.size(); ++i) {
+                    if (i) o += ',';
+                    o += '"' + std::to_string(kv.second[i].first) + "\":";
+                    const PreProc* p = nullptr;
+                    for (const PreProc* x : pres)
+                        if (x->stateId == kv.second[i].first) p = x;
+                    dump_state(o, p, *kv.second[i].second, S);
+                }
+                o += '}';
+            }
+            o += "}}";
+        }
+        o += "]}";
+        return o.c_str();
+    } catch (const std::exception& ex) {
+        g_err = ex.what();
+        return nullptr;
+    }
+}
+
 static void live_fire_until(orc_engine* e, int64_t t) {
     Engine& g = e->rt.eng;
     while (true) {

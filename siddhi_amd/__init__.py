@@ -145,6 +145,7 @@ def load_library():
                                 ctypes.POINTER(ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)))]
     L.sdg_snapshot.argtypes = [P, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(I64)]
     L.sdg_restore.argtypes = [P, ctypes.c_char_p, I64]
+    L.sdg_snapshot_states.argtypes = [P, ctypes.c_char_p, I64, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(I64)]
     L.sdg_export_device.argtypes = [P, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), P, P, P, P]
     L.sdg_export_ordered.argtypes = [P, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), P, P, P, P]
     L.sdg_query_key_attr.argtypes = [P, I32, I32]
@@ -438,6 +439,18 @@ class SiddhiAppRuntime:
             _check(self._L.sdg_restore(self._h, bytes(snapshot), len(snapshot)))
         except (SiddhiAppCreationException, ValueError) as ex:
             raise CannotRestoreSiddhiAppStateException(str(ex))
+
+    def snapshot_states(self, snapshot=None):
+        """a snapshot (default: a new one) decoded into the reference's state maps: {query: {"form": ..,
+        "states": {partition key: {stateId: StreamPreState.snapshot() map}}}} (StreamPreStateProcessor.java:450-459;
+        layout: DESIGN.md "Snapshot state maps")"""
+        import json
+        blob = self.snapshot() if snapshot is None else bytes(snapshot)
+        out = ctypes.c_char_p()
+        n = ctypes.c_int64()
+        _check(self._L.sdg_snapshot_states(self._h, blob, len(blob), ctypes.byref(out), ctypes.byref(n)))
+        doc = json.loads(ctypes.string_at(out, n.value).decode())
+        return {q["name"]: {"form": q["form"], "states": q["states"]} for q in doc["queries"]}
 
     def persist(self):
         """snapshot into the manager's persistence store; returns the revision"""

@@ -368,6 +368,7 @@ struct sdg_engine {
     bool no_sorted = false;      // SDG_NO_SORTED: the radix chain path keeps the lane deque kernels
     uint64_t app_hash = 0;       // FNV-1a of the app text: a snapshot restores only into the app it came from
     std::vector<uint8_t> snap;   // the last sdg_snapshot's bytes (valid until the next snapshot / destroy)
+    std::string states_json;     // the last sdg_snapshot_states text
     std::vector<Stage> stage;    // per stream: host pushes staged in HBM (see stage_push)
     std::vector<char> stage_ok;  // per stream: every query of the stream takes device-resident batches
     std::vector<char> host_pending;  // per stream: the pending batch holds host rows of it (no staging until flush)
@@ -3163,51 +3164,59 @@ void snapshot(sdg_engine* e, std::vector<uint8_t>& out) {
 // restore in two phases, like the reference (which deserialises the whole snapshot before touching a state): the
 // blob is parsed and validated completely first (device payloads stay as views into it), then applied. A truncated
 // or corrupt blob throws before any engine state changed.
-void restore(sdg_engine* e, const uint8_t* data, size_t len) {
+struct SnapView {
+    const uint8_t* p = nullptr;
+    size_t n = 0;
+};
+struct SnapStage {
+    int32_t chain = 0;
+    bool replay = false, nullable = false;
+    int64_t cn = 0;
+    SnapView ckey, cts, cseq, cnulls;
+    std::vector<SnapView> cvals;
+    std::vector<int64_t> ik;
+    std::vector<uint32_t> iv;
+    uint64_t in = 0;
+    std::vector<std::string> keystr;
+    std::vector<int32_t> key_hash;
+    PartitionKeyOrder korder;
+    nfa::Layout L{};
+    int64_t arena_keys = 0;
+    SnapView arena, arena2, cur_bits, last_seen, agg;
+    bool reclaim = false;
+    int64_t map_keys = 0;
+    SnapView slot_of, idle_rec, slot_key, free_slots, pool_ctr;
+    int64_t purge_first = INT64_MIN, agg_keys = 0;
+    int64_t s3_kcap = 0;
+    SnapView s3_hdr, s3_pn, s3_qn, s3_vals, s3_ts;
+    SchedSim sim;
+    std::map<uint32_t, QueryRt::Spilled> spill;
+};
+struct SnapParsed {
+    int64_t seq = 0, clock = 0;
+    Interner strings;
+    std::vector<SnapStage> stg;  // per query (device payloads are views into the blob)
+};
+
+void parse_snapshot(sdg_engine* e, const uint8_t* data, size_t len, SnapParsed& out) {
     SnapR r{data, data + len};
     if (r.get<uint64_t>() != SNAP_MAGIC) throw CompileError(SDG_ERR_ARG, "not an engine snapshot");
     if (r.get<uint64_t>() != e->app_hash)
         throw CompileError(SDG_ERR_ARG, "the snapshot was taken from a different Siddhi app");  // CannotRestoreSiddhiAppStateException
-    struct View {
-        const uint8_t* p = nullptr;
-        size_t n = 0;
-    };
+    using View = SnapView;
     auto view = [&]() {
         View v;
         v.p = r.bytes(&v.n);
         return v;
     };
-    struct Stage {
-        int32_t chain = 0;
-        bool replay = false, nullable = false;
-        int64_t cn = 0;
-        View ckey, cts, cseq, cnulls;
-        std::vector<View> cvals;
-        std::vector<int64_t> ik;
-        std::vector<uint32_t> iv;
-        uint64_t in = 0;
-        std::vector<std::string> keystr;
-        std::vector<int32_t> key_hash;
-        PartitionKeyOrder korder;
-        nfa::Layout L{};
-        int64_t arena_keys = 0;
-        View arena, arena2, cur_bits, last_seen, agg;
-        bool reclaim = false;
-        int64_t map_keys = 0;
-        View slot_of, idle_rec, slot_key, free_slots, pool_ctr;
-        int64_t purge_first = INT64_MIN, agg_keys = 0;
-        int64_t s3_kcap = 0;
-        View s3_hdr, s3_pn, s3_qn, s3_vals, s3_ts;
-        SchedSim sim;
-        std::map<uint32_t, QueryRt::Spilled> spill;
-    };
-    const int64_t seq = r.get<int64_t>();
-    const int64_t clock = r.get<int64_t>();
-    Interner strings;
+    using Stage = SnapStage;
+    out.seq = r.get<int64_t>();
+    out.clock = r.get<int64_t>();
     const uint64_t ns = r.get<uint64_t>();
-    for (uint64_t i = 0; i < ns; ++i) strings.get(r.str());
+    for (uint64_t i = 0; i < ns; ++i) out.strings.get(r.str());
     if (r.get<uint32_t>() != e->qs.size()) throw CompileError(SDG_ERR_ARG, "snapshot query count differs");
-    std::vector<Stage> stg(e->qs.size());
+    std::vector<Stage>& stg = out.stg;
+    stg.resize(e->qs.size());
     for (size_t qi = 0; qi < e->qs.size(); ++qi) {
         const Plan& P = e->qs[qi]->hq.plan;
         Stage& g = stg[qi];
@@ -3300,9 +3309,16 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
         r.p = g.sim.load(r.p, r.end);
     }
     if (r.p != r.end) throw CompileError(SDG_ERR_ARG, "snapshot has trailing bytes");
+}
+
+void restore(sdg_engine* e, const uint8_t* data, size_t len) {
+    SnapParsed parsed;
+    parse_snapshot(e, data, len, parsed);
+    std::vector<SnapStage>& stg = parsed.stg;
+    using Stage = SnapStage;
     // ---- apply ------------------------------------------------------------------------------------------
     hipStream_t st = e->stream;
-    auto up = [&](DevBuf& d, const View& v) {
+    auto up = [&](DevBuf& d, const SnapView& v) {
         void* x = d.ensure(v.n);
         if (v.n) HIPCHECK(hipMemcpyAsync(x, v.p, v.n, hipMemcpyHostToDevice, st));
     };
@@ -3382,9 +3398,290 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
         q.sim = std::move(g.sim);
         HIPCHECK(hipStreamSynchronize(st));  // the views point into the caller's blob
     }
-    e->seq = seq;
-    e->clock = clock;
-    e->strings = std::move(strings);
+    e->seq = parsed.seq;
+    e->clock = parsed.clock;
+    e->strings = std::move(parsed.strings);
+}
+
+// ---- snapshot -> the reference's state maps ------------------------------------------------------------------
+// A snapshot blob decoded into what SnapshotService would collect from the pattern processors of the same app:
+// per query, per partition key, per processor (stateId) the StreamPreState.snapshot() map
+// (StreamPreStateProcessor.java:450-459: FirstEvent, PendingStateEventList, NewAndEveryStateEventList,
+// Initialized, Started) plus the subclass fields (CountPreStateProcessor.java:206-212, AbsentStreamPreStateProcessor
+// .java:328-334, AbsentLogicalPreStateProcessor.java:407-413). JSON, in the layout of the oracle's orc_state_dump:
+//   {"queries":[{"name":..,"form":..,"states":{"<key>":{"<stateId>":{..map..}}}}]}
+//   StateEvent = {"ts":..,"type":..,"events":[null | [{"ts":..,"data":{"<attribute index>":v}} ..] per position]}
+// A StreamEvent holds the attributes the query reads (the arena keeps no others). States a holder would destroy
+// (canDestroy) and keys left with none are omitted. "form" says how exact the map is:
+//   "arena"     the generic NFA's arenas ARE these maps (nfa.h PState = StreamPreState, SE = StateEvent, the
+//               Node chain = the StreamEvent chain of a position): exact;
+//   "chain"     the fused path keeps only the pending partials (e1 events, in arrival order): the map is given as
+//               the next event's updateState() sees it -- NewAndEvery merged into Pending, the start state's seed
+//               with timestamp -1 -- and only for the keys holding partials (a key whose only state is the seed
+//               equals a fresh key);
+//   "registers" the sequence register kernel (seq3.hip): not decoded (SDG_NO_SEQ3 runs the query on the arenas).
+struct StateJson {
+    std::string o;
+    void str(const std::string& s) {
+        o += '"';
+        for (unsigned char c : s) {
+            if (c == '"' || c == '\\') {
+                o += '\\';
+                o += (char)c;
+            } else if (c < 0x20) {
+                char b[8];
+                std::snprintf(b, sizeof b, "\\u%04x", c);
+                o += b;
+            } else {
+                o += (char)c;
+            }
+        }
+        o += '"';
+    }
+    void real(double x) {
+        if (x != x) { o += "\"NaN\""; return; }
+        if (std::isinf(x)) { o += x > 0 ? "\"Infinity\"" : "\"-Infinity\""; return; }
+        char b[40];
+        std::snprintf(b, sizeof b, "%.17g", x);
+        o += b;
+    }
+    void val(uint8_t kind, int64_t v, bool null, const Interner& S) {
+        if (null) { o += "null"; return; }
+        switch (kind) {
+            case VK_I32: o += std::to_string((int32_t)v); break;
+            case VK_I64: o += std::to_string(v); break;
+            case VK_F32: {
+                const uint32_t u = (uint32_t)v;
+                float f;
+                std::memcpy(&f, &u, 4);
+                real((double)f);
+                break;
+            }
+            case VK_F64: {
+                double d;
+                std::memcpy(&d, &v, 8);
+                real(d);
+                break;
+            }
+            case VK_BOOL: o += v ? "true" : "false"; break;
+            default: {
+                const uint32_t id = (uint32_t)v;
+                str(id < S.strs.size() ? S.strs[id] : std::string());
+            }
+        }
+    }
+    void flag(const char* name, bool b) { o += std::string(",\"") + name + "\":" + (b ? "true" : "false"); }
+};
+
+// one stream event of position p: the query's columns of that position's stream, by attribute index
+void state_event_data(StateJson& J, const HostQuery& h, int p, const int64_t* vals, uint32_t nullmask,
+                      const Interner& S) {
+    const Plan& P = h.plan;
+    const int qp = h.stream_pos(P.st[p].stream);
+    J.o += "{";
+    bool first = true;
+    for (int c = 0; c < P.n_cols; ++c) {
+        const int ai = qp >= 0 && qp < (int)h.col_attr.size() && c < (int)h.col_attr[qp].size() ? h.col_attr[qp][c] : -1;
+        if (ai < 0) continue;
+        if (!first) J.o += ',';
+        first = false;
+        J.o += '"' + std::to_string(ai) + "\":";
+        J.val(P.col_kind[c], vals[c], (nullmask >> c) & 1u, S);
+    }
+    J.o += "}";
+}
+
+template <class IX>
+void state_maps_of_key(StateJson& J, const HostQuery& h, const nfa::Layout& L, uint8_t* base, const Interner& S) {
+    const Plan& P = h.plan;
+    nfa::CtxT<true, IX> c;
+    c.P = &P;
+    c.L = L;
+    c.base = base;
+    auto se_json = [&](IX s) {
+        const auto& e = c.se(s);
+        J.o += "{\"ts\":" + std::to_string(e.ts) + ",\"type\":" + std::to_string((int)e.type) + ",\"events\":[";
+        const IX* sl = c.slots(s);
+        for (int p = 0; p < L.n_states; ++p) {
+            if (p) J.o += ',';
+            if (sl[p] == (IX)nfa::NIL) {
+                J.o += "null";
+                continue;
+            }
+            J.o += '[';
+            int guard = 0;
+            for (IX n = sl[p]; n != (IX)nfa::NIL; n = c.nd(n).next) {
+                if (guard++ > L.nn) throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (event chain)");
+                if (guard > 1) J.o += ',';
+                const IX r = c.nd(n).rec;
+                J.o += "{\"ts\":" + std::to_string(c.rc(r).ts) + ",\"data\":";
+                state_event_data(J, h, p, c.vals(r), c.rc(r).nullmask, S);
+                J.o += '}';
+            }
+            J.o += ']';
+        }
+        J.o += "]}";
+    };
+    bool first = true;
+    for (int p = 0; p < L.n_states; ++p) {
+        const auto& st = c.ps(p);
+        if (st.pn == 0 && st.nw == 0 && !st.initialized && st.last_arrival == 0) continue;  // canDestroy
+        if (!first) J.o += ',';
+        first = false;
+        J.o += '"' + std::to_string(p) + "\":{\"FirstEvent\":null,\"PendingStateEventList\":[";
+        for (int j = 0; j < st.pn; ++j) {
+            if (j) J.o += ',';
+            se_json(c.pend(p)[j]);
+        }
+        J.o += "],\"NewAndEveryStateEventList\":[";
+        for (int j = 0; j < st.nw; ++j) {
+            if (j) J.o += ',';
+            se_json(c.newe(p)[j]);
+        }
+        J.o += ']';
+        const StateRow& row = P.st[p];
+        J.flag("Initialized", st.initialized);
+        // partitionCreated() sets `started` on every startup processor, but a non-start one's state is empty then
+        // and its holder destroys it on return (canDestroy), so the reference never holds started == true there;
+        // the arena keeps the bit (nothing reads it again)
+        J.flag("Started", st.started && row.is_start);
+        if (row.kind == PK_COUNT) {
+            J.flag("SuccessCondition", st.success);
+            J.flag("StartStateReset", st.start_reset);
+        } else if (row.kind == PK_LOGICAL && row.absent) {
+            J.flag("IsActive", st.active);
+            J.o += ",\"LastArrivalTime\":" + std::to_string(st.last_arrival);
+        } else if (row.kind == PK_ABSENT) {
+            J.flag("IsActive", st.active);
+            J.o += ",\"LastScheduledTime\":" + std::to_string(st.last_sched);
+        }
+        J.o += '}';
+    }
+}
+
+void snapshot_states(sdg_engine* e, const SnapParsed& sp, std::string& out) {
+    StateJson J;
+    const Interner& S = sp.strings;
+    J.o = "{\"queries\":[";
+    for (size_t qi = 0; qi < e->qs.size(); ++qi) {
+        const QueryRt& q = *e->qs[qi];
+        const HostQuery& h = q.hq;
+        const Plan& P = h.plan;
+        const SnapStage& g = sp.stg[qi];
+        if (qi) J.o += ',';
+        J.o += "{\"name\":";
+        J.str(h.name);
+        const char* form = q.seq3 ? "registers" : (g.chain || g.cn > 0) ? "chain" : "arena";
+        J.o += std::string(",\"form\":\"") + form + "\",\"states\":{";
+        // key ids: the string table's ids for string partition values, else the query's own dictionary
+        const int64_t K = !P.partitioned ? 1 : q.string_keys ? (int64_t)S.strs.size() : (int64_t)g.keystr.size();
+        auto key_name = [&](int64_t k) {
+            return !P.partitioned ? std::string() : q.string_keys ? S.strs[(size_t)k] : g.keystr[(size_t)k];
+        };
+        // per key JSON of its processors (keys sorted by name: the maps are unordered)
+        std::map<std::string, std::string> keys;
+        if (!q.seq3 && (g.chain || g.cn > 0)) {
+            // carried partials per key, arrival order
+            std::vector<std::vector<int64_t>> per(K);
+            const int nc = std::max(P.n_cols, 1);
+            for (int64_t i = 0; i < g.cn; ++i) {
+                uint32_t k;
+                std::memcpy(&k, g.ckey.p + i * 4, 4);
+                if (!P.partitioned) k = 0;
+                if ((int64_t)k >= K) throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (carried partial key)");
+                per[k].push_back(i);
+            }
+            auto rd = [](const SnapView& v, int64_t i) {
+                int64_t x;
+                std::memcpy(&x, v.p + i * 8, 8);
+                return x;
+            };
+            for (int64_t k = 0; k < K; ++k) {
+                // (a key without carried partials holds only the start state's seed, as a fresh key would: the
+                // fused path keeps no record of it, so it is left out -- see "chain" above)
+                if (per[k].empty()) continue;
+                std::sort(per[k].begin(), per[k].end(), [&](int64_t a, int64_t b) { return rd(g.cseq, a) < rd(g.cseq, b); });
+                StateJson kj;
+                kj.o = "\"0\":{\"FirstEvent\":null,\"PendingStateEventList\":[],\"NewAndEveryStateEventList\":[{\"ts\":-1,"
+                       "\"type\":0,\"events\":[";
+                for (int p = 0; p < P.n_states; ++p) kj.o += p ? ",null" : "null";
+                kj.o += "]}],\"Initialized\":true,\"Started\":false}";
+                if (!per[k].empty()) {
+                    kj.o += ",\"1\":{\"FirstEvent\":null,\"PendingStateEventList\":[";
+                    std::vector<int64_t> vals(nc);
+                    for (size_t j = 0; j < per[k].size(); ++j) {
+                        const int64_t i = per[k][j];
+                        const int64_t ts = rd(g.cts, i);
+                        for (int cidx = 0; cidx < nc; ++cidx) vals[cidx] = rd(g.cvals[cidx], i);
+                        uint32_t nm;
+                        std::memcpy(&nm, g.cnulls.p + i * 4, 4);
+                        if (j) kj.o += ',';
+                        kj.o += "{\"ts\":" + std::to_string(ts) + ",\"type\":0,\"events\":[[{\"ts\":" + std::to_string(ts) +
+                                ",\"data\":";
+                        state_event_data(kj, h, 0, vals.data(), nm, S);
+                        kj.o += "}]";
+                        for (int p = 1; p < P.n_states; ++p) kj.o += ",null";
+                        kj.o += "]}";
+                    }
+                    kj.o += "],\"NewAndEveryStateEventList\":[],\"Initialized\":false,\"Started\":false}";
+                }
+                keys[key_name(k)] = std::move(kj.o);
+            }
+        } else if (!q.seq3) {
+            const nfa::Layout& L = g.L;
+            std::vector<uint8_t> scratch;
+            const int ib = nfa::idle_bytes(P.n_states);
+            auto slot_of = [&](int64_t k) {
+                int32_t so;
+                std::memcpy(&so, g.slot_of.p + k * 4, 4);
+                return so;
+            };
+            for (int64_t k = 0; k < K; ++k) {
+                StateJson kj;
+                auto sit = g.spill.find((uint32_t)k);
+                if (sit != g.spill.end()) {  // spilled: its host arena (32-bit indices)
+                    scratch.assign(sit->second.arena.begin(), sit->second.arena.end());
+                    state_maps_of_key<int32_t>(kj, h, sit->second.L, scratch.data(), S);
+                } else {
+                    int64_t s = k;
+                    bool idle = false;
+                    if (g.reclaim) {
+                        if (k >= g.map_keys) continue;
+                        const int32_t so = slot_of(k);
+                        if (so == -1 || so == -3) continue;
+                        if (so == -2) idle = true;
+                        else s = so;
+                    }
+                    if (!idle && s >= g.arena_keys) continue;
+                    scratch.assign((size_t)L.bytes, 0);
+                    if (idle) {
+                        nfa::CtxT<true> c;
+                        c.P = &P;
+                        c.L = L;
+                        c.base = scratch.data();
+                        nfa::from_idle(c, g.idle_rec.p + k * ib);
+                    } else {
+                        const uint8_t cur = g.cur_bits.p[s];
+                        std::memcpy(scratch.data(), (cur ? g.arena2.p : g.arena.p) + s * L.bytes, (size_t)L.bytes);
+                    }
+                    const nfa::KHead& kh = *(const nfa::KHead*)scratch.data();
+                    if (!(kh.flags & 2)) continue;  // never initialised
+                    state_maps_of_key<int16_t>(kj, h, L, scratch.data(), S);
+                }
+                if (!kj.o.empty()) keys[key_name(k)] = std::move(kj.o);
+            }
+        }
+        bool first = true;
+        for (auto& kv : keys) {
+            if (!first) J.o += ',';
+            first = false;
+            J.str(kv.first);
+            J.o += ":{" + kv.second + '}';
+        }
+        J.o += "}}";
+    }
+    J.o += "]}";
+    out.swap(J.o);
 }
 
 template <class F>
@@ -3542,6 +3839,18 @@ int sdg_restore(sdg_engine* e, const uint8_t* data, int64_t len) {
         if (!e->pending.empty()) throw CompileError(SDG_ERR_ARG, "events are pending: flush before restoring");
         HIPCHECK(hipSetDevice(e->device));
         restore(e, data, (size_t)len);
+        return (int)SDG_OK;
+    });
+}
+
+int sdg_snapshot_states(sdg_engine* e, const uint8_t* data, int64_t len, const char** json, int64_t* json_len) {
+    if (!e || !data || len < 0 || !json || !json_len) return fail(SDG_ERR_ARG, "bad snapshot_states arguments");
+    return guarded([&]() {
+        SnapParsed parsed;
+        parse_snapshot(e, data, (size_t)len, parsed);
+        snapshot_states(e, parsed, e->states_json);
+        *json = e->states_json.c_str();
+        *json_len = (int64_t)e->states_json.size();
         return (int)SDG_OK;
     });
 }

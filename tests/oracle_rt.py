@@ -52,6 +52,8 @@ def lib():
         L.orc_export_query_outputs.restype = I64
         L.orc_export_query_outputs.argtypes = [P, I64, I32, P, P, P]
         L.orc_last_error.restype = ctypes.c_char_p
+        L.orc_state_dump.restype = ctypes.c_char_p
+        L.orc_state_dump.argtypes = [P]
         _lib = L
     return _lib
 
@@ -165,6 +167,14 @@ class Oracle:
         if t == STRING:
             return ("s", self.L.orc_string(self.h, slot).decode())
         return ("?", slot)
+
+    def state_dump(self):
+        """every pattern processor's StreamPreState.snapshot() map per partition key (orc_state_dump)"""
+        import json
+        r = self.L.orc_state_dump(self.h)
+        if r is None:
+            raise OracleError(self.L.orc_last_error().decode())
+        return json.loads(r.decode())
 
     def query_arrays(self, nv):
         """query-callback rows as numpy arrays (ts[n], vals[n][nv] slots, nulls[n][nv]) in delivery order"""
