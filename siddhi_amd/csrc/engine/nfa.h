@@ -498,6 +498,18 @@ struct CtxT {
     // (PartitionStateHolder.returnState): its lastScheduledTime restarts from 0. Only that field of a destroyed
     // state is ever read again (start states are initialised, so never destroyed), so it is the one reset here,
     // at the end of each event / fire (every getState/returnState scope of the reference has ended by then)
+    // Any other state its holder would destroy (canDestroy: both lists empty, not initialised, no lastArrivalTime)
+    // restarts from its defaults too. Its flags are rewritten before they are read (SuccessCondition), read only
+    // by updateState of start states, which are initialised (StartStateReset), or set once per key
+    // (partitionCreated: Started), so this changes no result -- it keeps snapshots (sdg_snapshot_states) equal to
+    // the reference's maps. Run at the end of each event.
+    SDG_HD void destroyed_gc() {
+        for (int p = 0; p < L.n_states; ++p) {
+            PState& s = ps(p);
+            if (s.pn || s.nw || s.initialized || s.last_arrival) continue;
+            s.success = s.start_reset = s.started = 0;
+        }
+    }
     SDG_HD void absent_gc() {
         if (!TM) return;
         for (int i = 0; i < P->n_sched; ++i) {
@@ -1481,6 +1493,7 @@ SDG_HD bool key_row(CtxT<TM, IX>& c, const KeyEvents& ev, int64_t p, bool& need_
     c.cur_sub = ev.vrank ? (int64_t)ev.vrank[p] << 40 : 0;
     c.on_event(ev.qstream ? ev.qstream[p] : 0, r, ts);
     if (TM && P->n_sched) c.absent_gc();
+    c.destroyed_gc();
     return !c.ovf();
 }
 template <bool TM, class IX>

@@ -10,39 +10,9 @@ import pytest
 import synth
 from oracle_rt import Oracle
 from product_rt import ProductAdapter
+from state_maps_util import check_maps, merge_lists as _merge_lists
 
 pytestmark = pytest.mark.gpu
-
-
-def _project(o, e):
-    """oracle events carry every attribute of their stream; keep those the engine's event names"""
-    if isinstance(o, dict) and isinstance(e, dict):
-        if isinstance(o.get("data"), list) and isinstance(e.get("data"), dict):
-            d = o["data"]
-            return {"ts": o["ts"], "data": {k: d[int(k)] if int(k) < len(d) else "<missing>" for k in e["data"]}}
-        return {k: (_project(v, e[k]) if k in e else v) for k, v in o.items()}
-    if isinstance(o, list) and isinstance(e, list) and len(o) == len(e):
-        return [_project(a, b) for a, b in zip(o, e)]
-    return o
-
-
-def _merge_lists(states):
-    """what the next event's updateState() sees: NewAndEvery appended to Pending; the start state's seed (no
-    bound event) without its timestamp; keys whose only state is that seed (equal to a fresh key) left out"""
-    out = {}
-    for key, procs in states.items():
-        ms = {}
-        for sid, m in procs.items():
-            m = dict(m)
-            lst = m["PendingStateEventList"] + m["NewAndEveryStateEventList"]
-            m["PendingStateEventList"] = [dict(s, ts=-1) if all(x is None for x in s["events"]) else s for s in lst]
-            m["NewAndEveryStateEventList"] = []
-            ms[sid] = m
-        seed_only = list(ms) == ["0"] and all(all(x is None for x in s["events"])
-                                              for s in ms["0"]["PendingStateEventList"])
-        if not seed_only:
-            out[key] = ms
-    return out
 
 
 def _compare(app, tr, cut_batches, total_batches=None, force_generic=True, expect_form="arena", **kw):
@@ -56,22 +26,7 @@ def _compare(app, tr, cut_batches, total_batches=None, force_generic=True, expec
     finally:
         p.close()
         o.close()
-    assert set(got) == set(ref)
-    n = 0
-    for name, g in got.items():
-        assert g["form"] == expect_form, name
-        r = ref[name]
-        for procs in r.values():
-            for m in procs.values():
-                assert m["FirstEvent"] is None  # between events the processing chunk is empty
-        if g["form"] == "chain":
-            r, gs = _merge_lists(r), _merge_lists(g["states"])
-        else:
-            gs = g["states"]
-        assert _project(r, gs) == gs, name
-        n += sum(len(m["PendingStateEventList"]) + len(m["NewAndEveryStateEventList"])
-                 for procs in gs.values() for m in procs.values())
-    return n
+    return check_maps(ref, got, expect_form)
 
 
 GENERIC = ["c3_sequence", "three_state_within", "non_every", "every_group", "count_pattern", "count_zero_min",
@@ -148,3 +103,22 @@ def test_restored_engine_decodes_the_same_maps():
     finally:
         q.close()
     assert first == again and first["q"]["states"]
+
+
+def test_spilled_key_state_maps():
+    """a key past the device arena's 4096 partials lives in a host arena with 32-bit indices: decoded the same"""
+    from test_fallbacks import DEEP, spill_trace
+    tr = spill_trace(depth=4600, keys=("k0",), seed=8)
+    tr = tr[:int(len(tr) * 0.9)]  # inside the tail: thousands of partials still pending
+    o = Oracle(DEEP)
+    p = ProductAdapter(DEEP, force_generic=True, max_partials=4096)
+    try:
+        synth.run(o, tr, 1)
+        synth.run(p, tr, 1)
+        assert sum(s.spilled_keys for s in p.stats) == 1
+        ref = {q["name"]: q["states"] for q in o.state_dump()["queries"]}
+        got = p.rt.snapshot_states()
+    finally:
+        p.close()
+        o.close()
+    assert check_maps(ref, got, "arena") > 4000

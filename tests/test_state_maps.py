@@ -1,11 +1,18 @@
-"""Snapshot state maps, CPU side: the oracle's StreamPreState dump (orc_state_dump) pinned on a hand-checked history,
-and the engine's decoder (sdg_snapshot_states) refusing what is not a snapshot of its app. The engine-vs-oracle
+"""Snapshot state maps, CPU side: the oracle's StreamPreState dump (orc_state_dump) pinned on a hand-checked history;
+the engine's decoder (sdg_snapshot_states) refusing what is not a snapshot of its app; and snapshots the GPU engine
+wrote (tests/golden/state_maps/) decoded here without a device, equal to the oracle's maps. The live engine-vs-oracle
 comparison runs on the GPU (test_gpu_state_maps.py)."""
+import os
+
 import pytest
 
 import siddhi_amd as sa
+import state_fixture_cases
 import synth
 from oracle_rt import Oracle
+from state_maps_util import check_maps
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "state_maps")
 
 CHAIN = synth.part_s("@info(name='q') from every e1=S[price>20] -> e2=S[price>e1.price] "
                      "select e1.id as a, e2.id as b insert into O;")
@@ -69,3 +76,20 @@ def test_engine_decoder_refuses_foreign_bytes():
         rt.snapshot_states(b"\0" * 64)
     with pytest.raises(Exception, match="truncated|not an engine snapshot"):
         rt.snapshot_states(b"")
+
+
+@pytest.mark.parametrize("name", sorted(state_fixture_cases.CASES))
+def test_committed_snapshot_decodes_to_the_oracle_maps(name, oracle_built):
+    """snapshots the GPU engine wrote (scripts/make_state_fixtures.py), decoded here by a compile-only engine of
+    the same app -- no device -- equal the oracle's maps after the same seeded history"""
+    app, tr, batches, generic = state_fixture_cases.CASES[name]
+    with open(os.path.join(GOLD, name + ".snap"), "rb") as f:
+        blob = f.read()
+    got = sa.SiddhiAppRuntime(app, compile_only=True, force_generic=generic).snapshot_states(blob)
+    o = Oracle(app)
+    try:
+        state_fixture_cases.feed(o, tr, batches)
+        ref = {q["name"]: q["states"] for q in o.state_dump()["queries"]}
+    finally:
+        o.close()
+    assert check_maps(ref, got, "arena" if generic else "chain") > 0
