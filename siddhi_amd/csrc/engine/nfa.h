@@ -248,7 +248,6 @@ struct CtxT {
     int64_t clk_hi;          // during a fire: the largest clock that gives the same result (see LOG_FIRE_END)
     int64_t pos;             // batch position being processed (-1: before position 0)
     int32_t fsched;          // scheduler whose fire is running (-1: event processing)
-    int32_t held = -1;       // processor whose processAndReturn loop holds its state (-1: none)
 
     // ---- arena access ------------------------------------------------------------------------------------
     SDG_HD KHead& head() { return *(KHead*)base; }
@@ -786,11 +785,7 @@ struct CtxT {
         IX e = slots(s)[p];
         int n = 1;
         while (nd(e).next != NIL) { ++n; e = nd(e).next; }
-        // CountPreStateProcessor.successCondition() takes the state from its holder: outside the processor's own
-        // processAndReturn loop (which holds it) a state its holder may destroy (canDestroy) is dropped on return,
-        // flag included. (The flag is rewritten before every read, so this only keeps snapshots exact.)
-        const PState& cs = ps(p);
-        if (held == p || cs.pn || cs.nw || cs.initialized || cs.last_arrival) ps(p).success = 1;
+        ps(p).success = 1;
         se(s).ts = rc(nd(e).rec).ts;
         if (n >= r.min_count) {
             if (r.seq) {
@@ -926,8 +921,6 @@ struct CtxT {
         const int last = r.last;
         IX* ret = (IX*)(base + L.off_ret);
         int nret = 0;
-        const int held0 = held;
-        held = p;
         for (int j = 0; j < st.pn;) {
             if (ovf()) return;
             IX s = pd[j];
@@ -985,7 +978,9 @@ struct CtxT {
             }
             if (!erased) ++j;
         }
-        held = held0;
+        // processAndReturn's getState / returnState scope ends here: a state its holder can destroy now is dropped
+        // (PartitionStateHolder.returnState), its flags with it -- a later addState in this event starts afresh
+        if (!st.pn && !st.nw && !st.initialized && !st.last_arrival) st.success = st.start_reset = st.started = 0;
         if (selector)
             for (int i = 0; i < nret; ++i) emit(ret[i]);
     }
@@ -1432,7 +1427,6 @@ SDG_HD bool key_begin(CtxT<TM, IX>& c, const KeyEvents& ev) {  // returns need_i
     const Plan* P = c.P;
     c.seq_base = ev.seq_base;
     c.fsched = -1;
-    c.held = -1;
     c.fi = 0;
     c.pos = -1;
     c.clock = c.T.clock0;
