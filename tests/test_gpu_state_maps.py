@@ -109,7 +109,7 @@ def test_spilled_key_state_maps():
     """a key past the device arena's 4096 partials lives in a host arena with 32-bit indices: decoded the same"""
     from test_fallbacks import DEEP, spill_trace
     tr = spill_trace(depth=4600, keys=("k0",), seed=8)
-    tr = tr[:int(len(tr) * 0.9)]  # inside the tail: thousands of partials still pending
+    tr = tr[:int(len(tr) * 0.85)]  # k0 holds 4374 pending partials here (past the 4096 of the device arena)
     o = Oracle(DEEP)
     p = ProductAdapter(DEEP, force_generic=True, max_partials=4096)
     try:
