@@ -1,7 +1,13 @@
 /* siddhi_amd — MI355X engine for Siddhi's pattern/sequence NFA path: the drop-in C-ABI.
  *
- * Everything behind this header runs on the GPU (gfx950 HIP kernels); there is no CPU fallback. The ABI is
- * what a JNI / Panama FFM binding of the reference's API would call (INTEGRATION.md shows the bindings):
+ * The pattern path behind this header runs on the GPU (gfx950 HIP kernels); there is no CPU fallback for a query or a
+ * flush (no device => sdg_compile fails with SDG_ERR_DEVICE). Two bounded cases run parts of a flush on the host with
+ * the engine's own NFA code (never the test oracle), and sdg_stats.host_rows counts the rows they processed:
+ *   - a partition key that outgrows the device arena's 4096 partial matches spills to a host arena and its rows run
+ *     there from then on (sdg_stats.spilled_keys);
+ *   - absent-state (timer) queries: a key whose results the scheduler's cross-key timer collapse reorders beyond what
+ *     a device rerun reproduces is replayed on the host (sdg_stats.sched_host_keys).
+ * The ABI is what a JNI / Panama FFM binding of the reference's API would call (INTEGRATION.md shows the bindings):
  *
  *   sdg_compile          <- SiddhiManager.createSiddhiAppRuntime(String)
  *                           (modules/siddhi-core/src/main/java/io/siddhi/core/SiddhiManager.java:93-96)
@@ -227,6 +233,8 @@ typedef struct sdg_stats {
                                   the key sort), 0 otherwise */
     int32_t spilled_keys;      /* generic NFA: partition keys the last flush moved to the host because they outgrew
                                   the device arena's 4096 partial matches (they run there from then on) */
+    int64_t host_rows;         /* rows of the last flush processed on the host (the engine's NFA code, not the test
+                                  oracle): spilled keys' rows plus the scheduler's host replays (sched_host_keys) */
 } sdg_stats;
 int sdg_last_stats(sdg_engine* e, sdg_stats* out);
 

@@ -87,7 +87,8 @@ class Stats(ctypes.Structure):
                 ("ms_nfa_kernel", ctypes.c_double), ("ms_sched_host", ctypes.c_double),
                 ("arena_growths", ctypes.c_int64), ("carry_in", ctypes.c_int64), ("carry_out", ctypes.c_int64),
                 ("arena_slots", ctypes.c_int64), ("sched_exact_passes", ctypes.c_int64),
-                ("sorted_view", ctypes.c_int32), ("spilled_keys", ctypes.c_int32)]
+                ("sorted_view", ctypes.c_int32), ("spilled_keys", ctypes.c_int32),
+                ("host_rows", ctypes.c_int64)]
 
 
 _lib = None

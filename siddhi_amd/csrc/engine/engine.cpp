@@ -934,6 +934,7 @@ void spill_keys(sdg_engine* e, QueryRt& q, const std::vector<uint32_t>& fresh, c
                 if (r->overflow()) throw DeviceError("spilled key: host run sink overflow");
                 sp.arena.swap(r->arena);
                 if (P.purge) sp.purge_last = r->purge_last();
+                e->stats.host_rows += m;
                 q.spill_runs.push_back(std::move(r));
                 break;
             }
@@ -2272,6 +2273,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 if (r->overflow())
                     throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': a partition key exceeded max_partials "
                                                          "(host replay of a key the scheduler reordered)");
+                e->stats.host_rows += (int64_t)r->ts.size();
                 uint8_t cur = 0;  // its state goes where the device run's went (nfa_commit makes it current)
                 HIPCHECK(hipMemcpy(&cur, q.cur_bits.as<uint8_t>() + r->key, 1, hipMemcpyDeviceToHost));
                 uint8_t* work = (cur ? q.arena.as<uint8_t>() : q.arena2.as<uint8_t>()) + (int64_t)r->key * q.L.bytes;
@@ -2390,6 +2392,10 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         static const bool no_cskip = getenv("SDG_FU_NOSKIP") != nullptr;  // A/B: chunk-summary skipping in the deque
         if (no_cskip) a.fu_skip |= 128;
         a.fu_mode = getenv("SDG_FU_NODEQUE") ? DQ_OFF : a.deque_mode;
+        // A/B: the round-4 match passes (chunked deque; SDG_FU_NODEQUE: fixed per-lane forward scans) instead of
+        // the wave work queue
+        static const bool old_match = getenv("SDG_FU_DEQUE") != nullptr || getenv("SDG_FU_NODEQUE") != nullptr;
+        if (old_match) a.fu_skip |= 256;
         a.deque_mode = DQ_OFF;
         a.bstart = b_start;
         a.bseg = b_seg;
@@ -2946,6 +2952,7 @@ int do_flush(sdg_engine* e) {
     e->stats.sched_exact_passes = 0;
     e->stats.sorted_view = 0;
     e->stats.spilled_keys = 0;
+    e->stats.host_rows = 0;
     // a flush consumes its batch whether or not it succeeds: a failing query must not make the next flush
     // replay the events onto the queries that already committed them. The batch's positions and its clock are
     // consumed with it: queries that committed before a failing one hold carries, arenas and scheduler state

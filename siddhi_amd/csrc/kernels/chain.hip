@@ -1047,6 +1047,91 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
     };
     if (a.fu_skip & 16) {
         // phase timing: no matching
+    } else if (!(a.fu_skip & 256)) {
+        // ---- wave work queue (round 5): each candidate's result is independent of every other partial's (DESIGN.md
+        // 4: a partial completes at the first later row of its key that passes c1 while it is alive), so it is a
+        // forward scan over its key's run in LDS. Scan lengths are uneven (a high e1 price waits for expiry, ~a window
+        // of its key's rows; most resolve within a few rows), so instead of a fixed candidate per lane (the wave
+        // waiting for its slowest lane every round) or a deque per lane (rows revisited by several lanes), a lane
+        // that resolves its candidate takes the wave's next one from a list: every lane stays busy and each
+        // iteration advances 64 scans by WQ_U rows.
+        constexpr int WQ_U = 2;
+        uint16_t* const cand = &wc[w][0];  // the wave's candidate positions in position order (wc is free now)
+        int ncand = 0;
+#pragma unroll
+        for (int r = 0; r < FU_PT; ++r) {
+            const int pos = w * WROWS + r * 64 + lane;
+            bool c = false;
+            if (pos < nr && s_row[sw(pos)] < own) {
+                const int64_t xr = s_x[sw(pos)];
+                c = c0_at(pos, xr, SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K)));
+            }
+            const uint64_t bm = __ballot(c);
+            if (c) cand[ncand + __popcll(bm & lt)] = (uint16_t)pos;
+            ncand += __popcll(bm);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        int p = -1, q = 0, end = 0, head = 0;
+        uint32_t t0 = 0;
+        T y = kc;
+        bool live = true;  // the e1 operand is not null (a null operand compares false on every row)
+#pragma unroll 1
+        for (;;) {
+            const uint64_t need = __ballot(p < 0);
+            if (need) {  // wave-uniform
+                const int idx = head + __popcll(need & lt);
+                head += __popcll(need);
+                if (p < 0 && idx < ncand) {
+                    p = cand[idx];
+                    t0 = s_ts[sw(p)];
+                    const int64_t xr = s_x[sw(p)];
+                    end = (int)lend[s_lk[sw(p)]];
+                    if (!FU_OK(end <= nr && end > p, 4)) end = p + 1;
+                    q = p + 1;
+                    live = true;
+                    if (stream_e1) {
+                        if (e1_is_x) {
+                            y = SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K));
+                        } else {
+                            const int64_t g = lo + s_row[sw(p)];
+                            live = !(a.nulls[sp.e1_col] && a.nulls[sp.e1_col][g]);
+                            y = C::get(cvt(load_col(a.cols[sp.e1_col], sp.e1_col_kind, g), sp.e1_col_kind, (uint8_t)K));
+                        }
+                    }
+                }
+                if (__ballot(p >= 0) == 0) break;
+            }
+            if (p >= 0) {
+                uint32_t tq[WQ_U];
+                T xq[WQ_U];
+#pragma unroll
+                for (int u = 0; u < WQ_U; ++u) {
+                    const int qq = min(q + u, FU_ROWS - 1);
+                    tq[u] = s_ts[sw(qq)];
+                    const int64_t xr = s_x[sw(qq)];
+                    xq[u] = SAME ? C::get(xr) : C::get(cvt(xr, kind, (uint8_t)K));
+                }
+                int r = -1;  // -1 pending, else the s_res value
+#pragma unroll
+                for (int u = 0; u < WQ_U; ++u) {
+                    if (r >= 0) break;
+                    if (q + u >= end) {  // the key's staged rows ended with the partial pending
+                        r = (!to_end && (uint64_t)(tl_off - t0) > within_u) ? R_NONE : ran_off;
+                    } else if ((uint64_t)(tq[u] - t0) > within_u) {  // isExpired before the row is processed
+                        r = R_NONE;
+                    } else if (live && (left ? cmp_m(m, xq[u], y) : cmp_m(m, y, xq[u]))) {
+                        r = q + u;
+                    }
+                }
+                if (r >= 0) {
+                    s_res[sw(p)] = (uint16_t)r;
+                    p = -1;
+                } else {
+                    q += WQ_U;
+                }
+            }
+        }
     } else if (a.fu_mode != DQ_OFF) {
         // ---- monotone-deque pass (chain_deque_k), one lane per FU_DQ consecutive positions: the lane
         // pushes partials from its own positions only and keeps popping over the following positions of the key

@@ -1,0 +1,138 @@
+"""Every BASELINE.json config at its full size, row for row against the oracle's output made in the build container.
+
+tests/golden/make_config_fixtures.py ran the oracle on each config's synthetic input (siddhi_amd/workloads.py) and
+committed the row count and a SHA-256 digest of the rows in delivery order (tests/golden/configs/*.json). Here the
+product runs the same input on the GPU and its rows must hash to the same digest -- no oracle run on the GPU box.
+
+C1  10^6 ticks, unpartitioned, one flush (random and adversarial prices)
+C2  the bench's step: 10^8 device-resident events over 10^4 keys, one flush on the fused bucket matcher
+C3  10^6 long keys x 100 events in one flush (register sequence kernel), `<1:5>` and the literal `<2:5>`
+C4  10^6 keys x 20 events, 4 interleaved streams, then advance_time(T_end + 5000): the default flush path, which at
+    this size runs the scheduler's exact pass and replays keys on the host; also 10^5 keys through
+    both forced scheduler branches (SDG_SCHED_EXACT / SDG_SCHED_HOST)
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import siddhi_amd as sa
+from siddhi_amd import workloads as w
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+from make_config_fixtures import digest_rows, load_fixture  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def check(name, ts, vals, nulls, nv):
+    """vals / nulls as returned by poll_arrays: [nv][m]"""
+    fx = load_fixture(name)
+    vals = np.asarray(vals).reshape(nv, -1).T
+    nulls = np.asarray(nulls).reshape(nv, -1).T
+    m = len(ts)
+    head = [[int(ts[i]), [int(x) for x in vals[i]], [int(x) for x in nulls[i]]] for i in range(min(m, 8))]
+    assert m == fx["rows"], (name, m, fx["rows"], head[:2], fx["head"][:2])
+    assert head == fx["head"], (name, head, fx["head"])
+    assert digest_rows(ts, vals, nulls) == fx["sha256"], name
+
+
+@pytest.mark.parametrize("adversarial", [False, True])
+def test_c1_full_config(adversarial):
+    n = 1_000_000
+    c = w.c1_columns(n, adversarial=adversarial)
+    rt = sa.SiddhiAppRuntime(w.C1_APP, batch_capacity=n + 1)
+    try:
+        sym = np.full(n, rt.intern("IBM"), dtype=np.uint32)
+        rt.getInputHandler("StockStream").send_columns(c["ts"], [c["id"], sym, c["price"], c["volume"]])
+        rt.flush(deliver=False)
+        ts, vals, nulls, _ = rt.poll_arrays(0)
+    finally:
+        rt.shutdown()
+    check("c1_adv" if adversarial else "c1", ts, vals, nulls, 2)
+
+
+def test_c2_full_step():
+    """C2's bench step: 10^8 device-resident events over 10^4 string keys in one flush on the fused matcher"""
+    import torch
+    n, keys = 100_000_000, 10_000
+    cols = w.c2_columns(n, keys=keys)
+    syms = w.symbols(keys)
+    rt = sa.SiddhiAppRuntime(w.C2_APP)
+    try:
+        sym_ids = np.array([rt.intern(s) for s in syms], dtype=np.uint32)
+        dev = [torch.from_numpy(np.ascontiguousarray(v)).cuda() for v in
+               (cols["ts"], cols["id"], sym_ids[cols["key"]].astype(np.int32), cols["price"], cols["volume"])]
+        del cols
+        rt.push_device("StockStream", n, dev[0].data_ptr(), [d.data_ptr() for d in dev[1:]])
+        rt.flush(deliver=False)
+        assert rt.stats().fused == 1
+        ts, vals, nulls, _ = rt.poll_arrays(0)
+        del dev
+    finally:
+        rt.shutdown()
+    check("c2", ts, vals, nulls, 2)
+
+
+@pytest.mark.parametrize("query", ["<1:5>", "<2:5>"])
+def test_c3_full_config(query):
+    c = w.c3_columns(1_000_000)
+    app = w.C3_APP.replace("<2:5>", query)
+    rt = sa.SiddhiAppRuntime(app, batch_capacity=len(c["ts"]) + 1)  # one flush (no auto-flush)
+    try:
+        assert rt.query_paths() == [2]
+        rt.getInputHandler("S").send_columns(c["ts"], [c["id"], c["key"], c["price"], c["volume"]])
+        rt.flush(deliver=False)
+        ts, vals, nulls, _ = rt.poll_arrays(0)
+    finally:
+        rt.shutdown()
+    check("c3_15" if query == "<1:5>" else "c3_25", ts, vals, nulls, 4)
+
+
+def run_c4(keys, **kw):
+    """bench_configs.run_c4's sequence: one mixed push of the whole trace, flush, advance_time(T_end + 5000), flush"""
+    c = w.c4_columns(keys, per_tick=keys // 100)
+    n = len(c["ts"])
+    end = int(c["ts"][-1]) + 5000
+    rt = sa.SiddhiAppRuntime(w.C4_APP, batch_capacity=n + 1, **kw)
+    try:
+        idx = np.array([rt._L.sdg_stream_index(rt._h, s.encode()) for s in w.C4_STREAMS], dtype=np.int32)
+        rt.push_mixed(idx[c["stream"]], c["ts"], [c["id"], c["key"], c["v"]])
+        rt.flush(deliver=False)
+        s1 = rt.stats()
+        rt.advance_time(end)
+        rt.flush(deliver=False)
+        s2 = rt.stats()
+        ts, vals, nulls, _ = rt.poll_arrays(0)
+    finally:
+        rt.shutdown()
+    return ts, vals, nulls, (s1, s2)
+
+
+def test_c4_full_config_default_path():
+    ts, vals, nulls, st = run_c4(1_000_000)
+    print("C4 1e6 keys: rerun %d, exact passes %d, host replays %d, host rows %d"
+          % (sum(s.sched_rerun_keys for s in st), sum(s.sched_exact_passes for s in st),
+             sum(s.sched_host_keys for s in st), sum(s.host_rows for s in st)))
+    assert sum(s.sched_shifted for s in st) > 0 and sum(s.sched_rerun_keys for s in st) > 0
+    check("c4_1e6", ts, vals, nulls, 3)
+
+
+@pytest.mark.parametrize("mode", ["batches3", "exact", "host"])
+def test_c4_1e5_scheduler_branches(mode):
+    """10^5 keys: the default path over 3 batches + the final advance (test_gpu_parity.product_c4), and one flush
+    through each forced scheduler branch"""
+    if mode == "batches3":
+        from test_gpu_parity import product_c4
+        c = w.c4_columns(100_000, per_tick=1000)
+        ts, vals, nulls, st = product_c4(c, int(c["ts"][-1]) + 5000)
+        assert sum(s.sched_shifted for s in st) > 0 and sum(s.sched_rerun_keys for s in st) > 0
+        check("c4_1e5", ts, vals, nulls, 3)
+        return
+    kw = {"sched_exact": True} if mode == "exact" else {"sched_host": True}
+    ts, vals, nulls, st = run_c4(100_000, **kw)
+    assert sum(s.sched_exact_passes for s in st) > 0
+    if mode == "host":
+        assert sum(s.sched_host_keys for s in st) > 100 and sum(s.sched_rerun_keys for s in st) == 0
+    check("c4_1e5", ts, vals, nulls, 3)
