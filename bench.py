@@ -582,6 +582,7 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=2, help="end-to-end (host push -> poll) steps, 0 = skip")
     ap.add_argument("--no-gather", action="store_true", help="skip the ordered result gather leg")
+    ap.add_argument("--no-ordered", action="store_true", help="skip the timed flush + delivery-order export steps")
     ap.add_argument("--config", choices=["c2", "c5"], default="c2",
                     help="c2 (default, the metric's 1-GPU config) or c5 (10^10 events / 10^8 keys, key-hash sharded)")
     ap.add_argument("--c5-events", type=int, default=10 ** 10, help="C5: events of the whole stream")
@@ -650,7 +651,8 @@ def main():
     d_ts0 = torch.from_numpy(cols["ts"]).to(dev)
     span = int(cols["ts"][-1] - cols["ts"][0]) + 1
     nsteps = args.warmup + args.steps
-    ts_steps = [d_ts0 + s * span for s in range(nsteps + 2)]  # consecutive batches of one stream (+2: gather leg)
+    ts_steps = [d_ts0 + s * span for s in range(nsteps + 2)]  # consecutive batches of one stream (+2: gather leg;
+                                                              # the ordered steps follow them)
     torch.cuda.synchronize()
 
     def step(s):
@@ -736,6 +738,49 @@ def main():
                      "step_frac": step_bytes / (ms_per_step / 1000.0) / 1e9 / HBM_PEAK_GBS,
                      "kernel_ms": per_kernel},
     }
+    if not args.no_ordered:
+        # the same steps with the reference's observable order inside the timed region: flush, then the flush's
+        # records exported in delivery order (sdg_export_ordered: ts, emitting position, e1id, e2id into device buffers)
+        log("timed ordered steps (%d): flush + delivery-order export" % K)
+        cap = n + n // 4 + 4096
+        o_ts = torch.empty(cap, dtype=torch.int64, device=dev)
+        o_seq = torch.empty(cap, dtype=torch.int64, device=dev)
+        o_vals = torch.empty((2, cap), dtype=torch.int64, device=dev)
+        ots = [d_ts0 + (nsteps + 2 + s) * span for s in range(K + 1)]  # (the stream's time continues)
+
+        def ostep(s):
+            rt.push_device("StockStream", n, ots[s].data_ptr(),
+                           [d_id.data_ptr(), d_sym.data_ptr(), d_price.data_ptr(), d_vol.data_ptr()])
+            rt.flush(deliver=False)
+            return rt.export_ordered(0, cap, o_ts.data_ptr(), o_seq.data_ptr(), 0, o_vals.data_ptr())
+        ostep(0)  # (warm-up: the ordering pass sizes its workspaces on first use)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        orecs = 0
+        for s in range(1, K + 1):
+            orecs += ostep(s)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        oel = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([oel], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            oel = float(t.item())
+        if orecs > 1:  # the last step's export is in delivery order: (emitting position, e1 position) increasing
+            m = orecs // K
+            seq, e1 = o_seq[:m], o_vals[0, :m]
+            okd = bool(((seq[1:] > seq[:-1]) | ((seq[1:] == seq[:-1]) & (e1[1:] > e1[:-1]))).all().item())
+            if not okd:
+                raise RuntimeError("ordered steps: the export is not in delivery order")
+        out["value_ordered"] = n * world * K / oel
+        out["ordered"] = {"ms_per_step": oel * 1000.0 / K, "records_per_step": orecs / K,
+                          "ms_export_per_step": oel * 1000.0 / K - ms_per_step,
+                          "path": "flush + sdg_export_ordered (device radix sort by emitting position, run ranks by "
+                                  "e1 position, one row gather) per step, inside the timed region",
+                          "step_frac": step_bytes / (oel / K) / 1e9 / HBM_PEAK_GBS}
     if rank == 0 and not args.no_cpu:  # (at N > 1: rank 0's shard, a third of the sample, after the timed region)
         cs = min(args.cpu_sample if world == 1 else args.cpu_sample // 3, n)
         log("cpu baseline (oracle, 1 thread, %d events)" % cs)

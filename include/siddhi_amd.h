@@ -120,6 +120,9 @@ int sdg_query_flags(sdg_engine* e, int query);
  * value partition, -2 range partitions, -3 no key (broadcast), -1 the query does not read the stream or is not
  * partitioned. A multi-GPU router shards the stream's events by the hash of that attribute's toString. */
 int sdg_query_key_attr(sdg_engine* e, int query, int stream);
+/* 1 when the query reads the stream (one of its pattern states is on it), else 0: a multi-GPU router sends a stream
+ * that an unpartitioned query reads whole to one GPU */
+int sdg_query_reads(sdg_engine* e, int query, int stream);
 const char* sdg_query_name(sdg_engine* e, int query);
 const char* sdg_query_target(sdg_engine* e, int query);
 int sdg_query_output_schema(sdg_engine* e, int query, int32_t* n_attrs, const int32_t** types,

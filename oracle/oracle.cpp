@@ -1380,6 +1380,11 @@ struct SchedState {
     bool has_key = false;
     int activeUseCount = 0;
     int64_t seq = 0;  // creation order (live-mode tie break)
+    // due index (not reference state, Scheduler::heads): the state's HashMap iteration position = (bucket of its
+    // spread hash, newest-inserted first within a bucket -- computeIfAbsent links a new key at the bin's head and
+    // resize keeps relative order), with the bucket it was indexed under
+    int32_t hash = 0;
+    uint64_t stamp = 0, ibucket = 0;
     bool canDestroy() const { return queue.empty(); }
 };
 using SSP = std::shared_ptr<SchedState>;
@@ -1390,21 +1395,62 @@ struct Scheduler {
     bool partitioned = false;
     SSP single;
     JHashMap<SSP> map;
-    // heads of the non-empty queues (not reference state: lets onTimeChange skip the full map walk, which finds
-    // nothing due, when the earliest head is later than the clock)
-    std::multiset<int64_t> heads;
+    // Due index over the non-empty queues, ordered (head time, map iteration position) -- not reference state. The
+    // reference's onTimeChange walks every state of the map per clock advance and keeps, per distinct head time <=
+    // now, the first state in iteration order (TreeMultimap with compareTo() == 0); the walk is O(map) per advance,
+    // and with the collapse draining one state per due time per advance that was O(keys x events) (C4 at 10^6 keys:
+    // hours). The first index entry of each time <= now is the state that walk keeps. ORACLE_SCHED_WALK=1 runs the
+    // walk itself (the A/B that pins this index: tests/test_oracle_sched_index.py).
+    struct DueKey {
+        int64_t t;
+        uint64_t bucket, nstamp;
+        SchedState* s;
+        bool operator<(const DueKey& o) const {
+            if (t != o.t) return t < o.t;
+            if (bucket != o.bucket) return bucket < o.bucket;
+            if (nstamp != o.nstamp) return nstamp < o.nstamp;
+            return s < o.s;
+        }
+    };
+    std::set<DueKey> heads;
+    size_t idx_cap = 0;  // map.table.size() the index's buckets were computed for
+    uint64_t stamps = 0;
+    uint64_t bucket_of(const SchedState* st) const {
+        return partitioned && !map.table.empty() ? (uint64_t)((map.table.size() - 1) & (uint32_t)st->hash) : 0;
+    }
+    void idx_sync() {  // a resize moved the states' buckets: re-key the index
+        if (map.table.size() == idx_cap) return;
+        idx_cap = map.table.size();
+        std::vector<SchedState*> all;
+        for (const DueKey& d : heads) all.push_back(d.s);
+        heads.clear();
+        for (SchedState* st : all) {
+            st->ibucket = bucket_of(st);
+            heads.insert(DueKey{st->queue.front(), st->ibucket, ~st->stamp, st});
+        }
+    }
+    void idx_add(SchedState* st) {
+        idx_sync();
+        st->ibucket = bucket_of(st);
+        heads.insert(DueKey{st->queue.front(), st->ibucket, ~st->stamp, st});
+    }
+    void idx_del(SchedState* st) {
+        idx_sync();
+        heads.erase(DueKey{st->queue.front(), st->ibucket, ~st->stamp, st});
+    }
     SSP getState();
     void returnState(const SSP& s);
     void notifyAt(int64_t t) {
         SSP s = getState();
-        if (s->queue.empty()) heads.insert(t);
+        const bool was_empty = s->queue.empty();
         s->queue.push_back(t);
+        if (was_empty) idx_add(s.get());
         returnState(s);
     }
     void popHead(const SSP& s) {
-        heads.erase(heads.find(s->queue.front()));
+        idx_del(s.get());
         s->queue.pop_front();
-        if (!s->queue.empty()) heads.insert(s->queue.front());
+        if (!s->queue.empty()) idx_add(s.get());
     }
     void sendTimerEvents(const SSP& s);
     void purgeKey(const std::string& k) {  // partition purge: the key's SchedulerState is destroyed
@@ -1413,7 +1459,7 @@ struct Scheduler {
             if (kk == k) found = st;
         });
         if (!found) return;
-        if (!found->queue.empty()) heads.erase(heads.find(found->queue.front()));
+        if (!found->queue.empty()) idx_del(found.get());
         map.remove(k);
     }
     void onTimeChange(int64_t now);  // playback TimeChangeListener
@@ -1445,6 +1491,8 @@ SSP Scheduler::getState() {
         s->key = key;
         s->has_key = true;
         s->seq = e->schedSeq++;
+        s->hash = JHashMap<SSP>::spread(key);
+        s->stamp = ++stamps;  // insertion order into the map (computeIfAbsent links it at its bin's head)
         return s;
     });
     p->activeUseCount++;
@@ -2101,7 +2149,34 @@ void Scheduler::onTimeChange(int64_t now) {
         }
         return;
     }
-    if (heads.empty() || *heads.begin() > now) return;  // nothing due: the walk below would fire nothing
+    if (heads.empty() || heads.begin()->t > now) return;  // nothing due: the walk below would fire nothing
+    static const bool walk = std::getenv("ORACLE_SCHED_WALK") != nullptr;
+    if (!walk) {
+        // the walk's TreeMultimap holds, per distinct head time <= now, the first state in iteration order: the
+        // first index entry of that time. Only those states are used (activeUseCount) and can drain, so they are
+        // the only ones returnAllStates can destroy
+        idx_sync();
+        std::vector<SSP> chosen;
+        for (auto it = heads.begin(); it != heads.end() && it->t <= now;) {
+            const JHashMap<SSP>::Node* nd = map.find(it->s->key);
+            if (!nd) throw OracleError("scheduler due index: a state missing from the map");
+            chosen.push_back(nd->val);
+            it = heads.lower_bound(DueKey{it->t + 1, 0, 0, nullptr});
+        }
+        for (auto& st : chosen) st->activeUseCount++;
+        for (auto& st : chosen) {
+            Ctx saved = eng->ctx;
+            eng->ctx.has_key = true;
+            eng->ctx.key = st->key;
+            sendTimerEvents(st);
+            eng->ctx = saved;
+        }
+        for (auto& st : chosen) {
+            st->activeUseCount--;
+            if (st->activeUseCount == 0 && st->canDestroy()) map.remove(st->key);
+        }
+        return;
+    }
     // getAllStates (activeUseCount++ on all), TreeMultimap<Long, SchedulerState> with compareTo()==0
     std::vector<SSP> all;
     map.for_each([&](const std::string&, SSP& s) { all.push_back(s); });

@@ -150,6 +150,7 @@ def load_library():
     L.sdg_export_device.argtypes = [P, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), P, P, P, P]
     L.sdg_export_ordered.argtypes = [P, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), P, P, P, P]
     L.sdg_query_key_attr.argtypes = [P, I32, I32]
+    L.sdg_query_reads.argtypes = [P, I32, I32]
     L.sdg_last_stats.argtypes = [P, ctypes.POINTER(Stats)]
     _lib = L
     return L
@@ -305,6 +306,10 @@ class SiddhiAppRuntime:
         """how query q keys stream_id: attribute index of its value partition, -2 ranges, -3 no key (broadcast), -1
         not read / not partitioned (sdg_query_key_attr)"""
         return self._L.sdg_query_key_attr(self._h, q, self._L.sdg_stream_index(self._h, stream_id.encode()))
+
+    def query_reads(self, q, stream_id):
+        """whether query q reads stream_id (sdg_query_reads)"""
+        return bool(self._L.sdg_query_reads(self._h, q, self._L.sdg_stream_index(self._h, stream_id.encode())))
 
     def query_paths(self):
         """device path per query: 0 chain kernel, 1 generic keyed NFA, 2 register sequence kernel (seq3)"""

@@ -1365,6 +1365,10 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             const std::vector<uint32_t>& o = q.korder.order();
             if (o.size() >= ((size_t)1 << 23))
                 throw CompileError(SDG_ERR_CAPACITY, "a broadcast to more than 2^23 partition keys");
+            if (q.korder.tree_bins())  // the JDK's tree-bin iteration order is not modelled (keyorder.h)
+                throw CompileError(SDG_ERR_UNSUPPORTED, "query '" + q.hq.name + "': the partition's key set has a "
+                                                        "hash bin the JDK would turn into a tree bin; its broadcast "
+                                                        "order is not modelled");
             return o;
         };
         ts.reserve(n);
@@ -3078,7 +3082,10 @@ struct SnapR {
         if (n) HIPCHECK(hipStreamSynchronize(st));
     }
 };
-constexpr uint64_t SNAP_MAGIC = 0x31504e5347445353ull;  // "SSDGSNP1"
+// "SSDGSNP2": format 2 (round 4 on: spilled-key host arenas and the broadcast PartitionKeyOrder per query). Blobs of
+// format 1 (earlier builds) are rejected with a version error instead of being misread
+constexpr uint64_t SNAP_MAGIC = 0x32504e5347445353ull;      // "SSDGSNP2"
+constexpr uint64_t SNAP_MAGIC_V1 = 0x31504e5347445353ull;   // "SSDGSNP1"
 }  // namespace
 void sdg::PartitionKeyOrder::throw_corrupt() { throw CompileError(SDG_ERR_ARG, "snapshot is corrupt (partition keys)"); }
 namespace {
@@ -3207,7 +3214,11 @@ struct SnapParsed {
 
 void parse_snapshot(sdg_engine* e, const uint8_t* data, size_t len, SnapParsed& out) {
     SnapR r{data, data + len};
-    if (r.get<uint64_t>() != SNAP_MAGIC) throw CompileError(SDG_ERR_ARG, "not an engine snapshot");
+    const uint64_t magic = r.get<uint64_t>();
+    if (magic == SNAP_MAGIC_V1)
+        throw CompileError(SDG_ERR_ARG, "snapshot format 1 (written by an earlier engine build) cannot be restored by "
+                                        "this build (format 2)");
+    if (magic != SNAP_MAGIC) throw CompileError(SDG_ERR_ARG, "not an engine snapshot");
     if (r.get<uint64_t>() != e->app_hash)
         throw CompileError(SDG_ERR_ARG, "the snapshot was taken from a different Siddhi app");  // CannotRestoreSiddhiAppStateException
     using View = SnapView;
@@ -3885,6 +3896,10 @@ int sdg_query_key_attr(sdg_engine* e, int q, int stream) {
     if (qp < 0 || !h.plan.partitioned) return -1;
     return h.key_attr[qp];
 }
+int sdg_query_reads(sdg_engine* e, int q, int stream) {
+    if (!e || q < 0 || q >= (int)e->qs.size()) return 0;
+    return e->qs[q]->hq.stream_pos(stream) >= 0 ? 1 : 0;
+}
 int sdg_query_path(sdg_engine* e, int q) {
     if (!e || q < 0 || q >= (int)e->qs.size()) return -1;
     return e->qs[q]->hq.plan.chain ? 0 : e->qs[q]->seq3 ? 2 : 1;
@@ -4062,6 +4077,19 @@ int push_host(sdg_engine* e, int stream, int64_t n, const int64_t* ts, const voi
     if (!e || stream < 0 || stream >= (int)e->stream_types.size() || n < 0 || (n > 0 && !ts))
         return fail(SDG_ERR_ARG, "bad push arguments");
     return guarded([&]() {
+        if (event_array && n > 1) {
+            // PartitionStreamReceiver.receive(Event[]) (:176-188) of a stream with no partition key hands the WHOLE
+            // chunk to each key in turn (key-major delivery); the engine's broadcast rows are event-major (one event
+            // to every key, then the next), so a multi-event array on such a stream is refused, not reordered
+            for (auto& qp : e->qs) {
+                const int qpos = qp->hq.stream_pos(stream);
+                if (qp->broadcast && qpos >= 0 && qp->hq.key_attr[qpos] == -3)
+                    throw CompileError(SDG_ERR_UNSUPPORTED, "send(Event[]) of more than one event to stream '" +
+                                                                e->app.streams[stream].id + "', which has no partition "
+                                                                "key in partition query '" + qp->hq.name +
+                                                                "' (key-major delivery of the chunk is not supported)");
+            }
+        }
         if (event_array && n > 0 && e->app.playback) {  // InputHandler.send(Event[]) :85-95: the clock first
             PushChunk a;                                  // moves to the last event's timestamp
             a.stream = -1;

@@ -11,8 +11,9 @@
 //     presizes (doubling until tableSizeFor(3n + 1) <= 0.75 n') instead of building a tree bin;
 //   * the copy: a HashMap of tableSizeFor(max((int)(size / .75f) + 1, 16)) bins filled in the map's order (tail
 //     appends, order-kept doubling when a bin of a table < 64 reaches 9 keys), iterated bin by bin.
-// Tree bins (a bin of >= 9 keys in a table >= 64, impossible at these load factors short of engineered hash
-// collisions) are not modelled. Keys are the engine's dense key ids; h is the Java String.hashCode of the key's
+// Tree bins (a put that walks >= 8 nodes of a map bin on a table >= 64, or a set bin reaching 9 keys at capacity
+// >= 64: rare at these load factors short of colliding hashes) are not modelled: they are detected (tree_bins())
+// and the engine refuses the broadcast, as the oracle does, instead of delivering a possibly wrong order. Keys are the engine's dense key ids; h is the Java String.hashCode of the key's
 // toString after HashMap.hash spreading (java_spread_hash).
 #pragma once
 #include <stdint.h>
@@ -36,6 +37,13 @@ class PartitionKeyOrder {
                     while (p < b.size() && b[p].k != k) ++p;
                     if (p + 1 >= 8) presize();
                 }
+            } else {  // putVal's binCount >= TREEIFY_THRESHOLD on a table >= 64: treeifyBin builds a tree bin
+                const std::vector<E>& b = bins_[(uint32_t)h & (bins_.size() - 1)];
+                if (b.size() >= 8) {
+                    size_t p = 0;
+                    while (p < b.size() && b[p].k != k) ++p;
+                    if (p + 1 >= 8) tree_ = true;
+                }
             }
             return;
         }
@@ -48,11 +56,16 @@ class PartitionKeyOrder {
         std::vector<E>& b = bins_[(uint32_t)h & (bins_.size() - 1)];
         const size_t before = b.size();
         b.push_back(E{k, h});
-        if (before >= 8 && bins_.size() < 64) presize();
+        if (before >= 8) {
+            if (bins_.size() < 64) presize();
+            else tree_ = true;
+        }
         if (++count_ >= size_ctl_) grow();
         dirty_ = true;
     }
     int64_t size() const { return count_; }
+    // a tree bin was (or would be) built in the map or its HashSet copy: order() is not the JDK's order then
+    bool tree_bins() const { return tree_; }
     // the keys in getPartitionKeys() order (valid until the next add)
     const std::vector<uint32_t>& order() {
         if (!dirty_) return order_;
@@ -64,14 +77,22 @@ class PartitionKeyOrder {
                 order_.push_back(x.k);
                 hs.push_back(x.h);
             }
-        // the HashSet's capacity, after the order-keeping doublings of small tables
+        // the HashSet's capacity: HashMap(c) then add() in the map's order; an add that makes a bin 9 long calls
+        // treeifyBin, which on a table < 64 doubles it ONCE (order-keeping split) and on a larger one builds a tree
+        // bin. The next add into a bin still >= 9 long triggers again.
         int64_t cap = pow2_at_least(std::max<int64_t>((int64_t)((float)count_ / 0.75f) + 1, 16));
-        for (bool again = true; again && cap < 64;) {
-            again = false;
+        {
             std::vector<uint32_t> cnt((size_t)cap, 0);
-            for (int32_t h : hs)
-                if (++cnt[(uint32_t)h & (cap - 1)] == 9) { again = true; break; }
-            if (again) cap *= 2;
+            for (size_t i = 0; i < hs.size(); ++i) {
+                if (++cnt[(uint32_t)hs[i] & (cap - 1)] < 9) continue;
+                if (cap >= 64) {
+                    tree_ = true;
+                    continue;
+                }
+                cap *= 2;
+                cnt.assign((size_t)cap, 0);
+                for (size_t j = 0; j <= i; ++j) ++cnt[(uint32_t)hs[j] & (cap - 1)];
+            }
         }
         if (cap != (int64_t)bins_.size()) {  // bins of the map are not the set's bins: stable regroup
             std::vector<uint32_t> idx(order_.size());
@@ -112,6 +133,7 @@ class PartitionKeyOrder {
                 x.k = r.template get<uint32_t>();
                 x.h = r.template get<int32_t>();
                 b.push_back(x);
+                if (nb >= 64 && b.size() >= 9) tree_ = true;  // the 9th put walked 8 nodes: a tree bin
                 if (x.k >= live_.size()) live_.resize((size_t)x.k + 1, 0);
                 live_[x.k] = 1;
                 ++count_;
@@ -130,6 +152,7 @@ class PartitionKeyOrder {
     int64_t count_ = 0, size_ctl_ = 0;
     std::vector<uint32_t> order_;
     bool dirty_ = true;
+    bool tree_ = false;
     static int64_t pow2_at_least(int64_t c) {
         int64_t n = 1;
         while (n < c) n <<= 1;

@@ -885,6 +885,9 @@ constexpr uint16_t R_NONE = 0xFFFF, R_CARRY = 0xFFFE, R_OVF = 0xFFFD;
 static_assert((FU_DQ & (FU_DQ - 1)) == 0, "sw() swizzles at the deque chunk size");
 __device__ __forceinline__ int sw(int p) { return p ^ ((p / FU_DQ) & (FU_DQ - 1)); }
 static_assert(FU_ROWS < 65536, "chain_fused_k: u16 rows / run offsets");
+#ifndef SDG_WQ_U
+#define SDG_WQ_U 2  // rows each lane of the work queue tests per iteration
+#endif
 
 // SAME: the scanned column's kind is the comparison kind (no conversion in the scan loop). W: minimum waves per SIMD
 // the allocator must allow -- 8 = four 512-thread blocks per CU (LDS 4 x 40 KB fits); at 6 it used 104 SGPRs, which
@@ -1055,7 +1058,7 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
         // waiting for its slowest lane every round) or a deque per lane (rows revisited by several lanes), a lane
         // that resolves its candidate takes the wave's next one from a list: every lane stays busy and each
         // iteration advances 64 scans by WQ_U rows.
-        constexpr int WQ_U = 2;
+        constexpr int WQ_U = SDG_WQ_U;
         uint16_t* const cand = &wc[w][0];  // the wave's candidate positions in position order (wc is free now)
         int ncand = 0;
 #pragma unroll
@@ -1309,17 +1312,27 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
     }
     FU_TRACE(5);
     __syncthreads();
-    if (t < 3) {
-        uint32_t run = 0;
-        for (int k = 0; k < FU_PT; ++k)
-            for (int x = 0; x < NW; ++x) {
-                const uint32_t c = wcnt[t][k][x];
-                wcnt[t][k][x] = run;
-                run += c;
-            }
-        unsigned long long* ctr = t == 0 ? a.out_count : t == 1 ? a.carry_count : a.ovf_count;
-        if (a.fu_skip & 32) bbase[t] = t == 0 ? (unsigned long long)v * FU_OWN : 0ull;  // phase timing only
-        else bbase[t] = run ? atomicAdd(ctr, (unsigned long long)run) : 0ull;
+    // per counter (matches / carries / overflow rows): exclusive prefix over (round, wave) -- one wave per counter,
+    // a lane per count (a shuffle scan; one thread walking the FU_PT x NW counts was a chain of dependent LDS round
+    // trips), then the block's reservation
+    static_assert(FU_PT * NW <= 64, "chain_fused_k: one wave scans a counter's (round, wave) counts");
+    if (w < 3) {
+        const int ci = w;
+        const bool on = lane < FU_PT * NW;
+        const uint32_t c = on ? wcnt[ci][lane / NW][lane % NW] : 0u;
+        uint32_t inc = c;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(inc, off);
+            if (lane >= off) inc += y;
+        }
+        if (on) wcnt[ci][lane / NW][lane % NW] = inc - c;
+        const uint32_t run = __shfl(inc, 63);
+        if (lane == 0) {
+            unsigned long long* ctr = ci == 0 ? a.out_count : ci == 1 ? a.carry_count : a.ovf_count;
+            if (a.fu_skip & 32) bbase[ci] = ci == 0 ? (unsigned long long)v * FU_OWN : 0ull;  // phase timing only
+            else bbase[ci] = run ? atomicAdd(ctr, (unsigned long long)run) : 0ull;
+        }
     }
     __syncthreads();
     // ---- emit matches: slots and rows of every round first (LDS only), then every load of every round, then

@@ -121,6 +121,56 @@ __global__ __launch_bounds__(256) void unpack_k(ColSet cs, int ncol, const int64
     for (int c = 0; c < ncol; ++c) cs.dst[c][i] = r[c];
 }
 
+// the same result as order_runs_k, written to a second index array: each record finds its run of equal emitting
+// events around it (a few coalesced reads of the sorted keys), counts the run's records that precede it by
+// (sub, sorted index) and writes its index at run start + that rank. No thread walks a whole run serially, and no
+// record moves twice (order_runs_k insertion-sorted each run in place, one thread per run: 0.62 ms per 40M records)
+__global__ __launch_bounds__(256) void order_runs_rank_k(const uint32_t* __restrict__ ek, const uint32_t* __restrict__ ix,
+                                                         const int64_t* __restrict__ sub, int64_t n,
+                                                         uint32_t* __restrict__ perm, int* __restrict__ long_run) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t e = ek[i];
+    int64_t s = i, t = i + 1;
+    while (s > 0 && i - s <= RUN_MAX && ek[s - 1] == e) --s;
+    while (t < n && t - s <= RUN_MAX && ek[t] == e) ++t;
+    if (t - s > RUN_MAX) {  // (left to the two-sort ordering)
+        atomicOr(long_run, 1);
+        return;
+    }
+    const uint32_t me = ix[i];
+    if (t - s == 1) {
+        perm[i] = me;
+        return;
+    }
+    const int64_t my = sub[me];
+    int64_t rank = 0;
+    for (int64_t j = s; j < t; ++j) {
+        if (j == i) continue;
+        const int64_t o = sub[ix[j]];
+        rank += o < my || (o == my && j < i);  // stable: equal subs keep the sorted (emission) order
+    }
+    perm[s + rank] = me;
+}
+
+// every column of a record through one index read: dst[c][i] = src[c][perm[i]]. Blocks are mapped XCD-contiguous
+// (kernels.h xcd_block): consecutive output records come from a few hundred emission streams (the matcher's blocks),
+// each read forward, so one XCD's slice of the output keeps those streams' lines in its own L2
+__global__ __launch_bounds__(256) void gather_rows_k(ColSet cs, int ncol, const uint32_t* __restrict__ perm, int64_t n,
+                                                     uint32_t xcds) {
+    const uint32_t v = xcd_block(blockIdx.x, gridDim.x, xcds);
+    const int64_t i = (int64_t)v * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t p = perm[i];
+    int64_t x[GATHER_MAX_COLS];
+#pragma unroll
+    for (int c = 0; c < GATHER_MAX_COLS; ++c)
+        if (c < ncol) x[c] = cs.src[c][p];
+#pragma unroll
+    for (int c = 0; c < GATHER_MAX_COLS; ++c)
+        if (c < ncol) cs.dst[c][i] = x[c];
+}
+
 void temp_sizes(int64_t n, size_t& a, size_t& b) {
     uint64_t* k64 = nullptr;
     uint32_t* k32 = nullptr;
@@ -179,12 +229,14 @@ void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t e
         rocprim::radix_sort_pairs(tmp, b, ek0, ek1, ix0, ix1, (size_t)n, 0, eb, stream);
         int* flag = (int*)(rng + 3);
         (void)hipMemsetAsync(flag, 0, 4, stream);
-        hipLaunchKernelGGL(order_runs_k, dim3(grid), dim3(256), 0, stream, ek1, ix1, sub, n, flag);
+        static const bool serial_runs = getenv("SDG_ORDER_SERIAL_RUNS") != nullptr;  // A/B: order_runs_k
+        if (serial_runs) hipLaunchKernelGGL(order_runs_k, dim3(grid), dim3(256), 0, stream, ek1, ix1, sub, n, flag);
+        else hipLaunchKernelGGL(order_runs_rank_k, dim3(grid), dim3(256), 0, stream, ek1, ix1, sub, n, ix0, flag);
         int hf = 0;
         (void)hipMemcpyAsync(&hf, flag, 4, hipMemcpyDeviceToHost, stream);
         (void)hipStreamSynchronize(stream);
         if (!hf) {
-            *perm_out = ix1;
+            *perm_out = serial_runs ? ix1 : ix0;
             return;
         }
     }
@@ -225,7 +277,21 @@ void gather_cols_i64(const int64_t* const* src, int64_t* const* dst, int ncol, c
                      void* work, hipStream_t stream) {
     if (n <= 0 || ncol <= 0) return;
     static const bool cols = getenv("SDG_GATHER_COLS") != nullptr;  // A/B: one random-read gather per column
+    static const bool packed = getenv("SDG_GATHER_PACKED") != nullptr;  // A/B: pack_k + unpack_k (round 4)
     const unsigned grid = (unsigned)((n + 255) / 256);
+    if (!cols && !packed) {  // one pass, every column of a record per thread, XCD-contiguous output slices
+        const unsigned g8 = (unsigned)xcd_round(grid);
+        for (int c0 = 0; c0 < ncol; c0 += GATHER_MAX_COLS) {
+            const int nc = std::min(GATHER_MAX_COLS, ncol - c0);
+            ColSet cs{};
+            for (int c = 0; c < nc; ++c) {
+                cs.src[c] = src[c0 + c];
+                cs.dst[c] = dst[c0 + c];
+            }
+            hipLaunchKernelGGL(gather_rows_k, dim3(g8), dim3(256), 0, stream, cs, nc, perm, n, (uint32_t)g_xcds);
+        }
+        return;
+    }
     if (cols || ncol == 1) {
         for (int c = 0; c < ncol; ++c) hipLaunchKernelGGL(gather_k<int64_t>, dim3(grid), dim3(256), 0, stream, src[c], perm, n, dst[c]);
         return;

@@ -28,26 +28,24 @@ def owner(key, world):
 def route(keys, world, cache=None):
     """rank of each event, for an array/list of partition key values (PartitionStreamReceiver.receive(Event[])
     :176-216 routes a batch key by key; here the batch is split by owner at once): each distinct key's toString is
-    hashed once (np.unique + a per-router cache), then the ranks are gathered back to the rows"""
+    hashed once (np.unique + a per-router cache keyed by that string), then the ranks are gathered back to the rows.
+    The distinct keys are hashed as the numpy scalars of the column (str(np.float32(0.1)) == '0.1', as a per-row
+    send() of the same float32 value hashes it), never as Python floats widened from another width."""
     if world == 1:
         return np.zeros(len(keys), dtype=np.int32)
     cache = {} if cache is None else cache
+
+    def rank_of(k):
+        sk = str(k)
+        r = cache.get(sk)
+        if r is None:
+            r = cache[sk] = key_hash(sk) % world
+        return r
     arr = np.asarray(keys)
     if arr.dtype == object or arr.ndim != 1:
-        out = np.empty(len(keys), dtype=np.int32)
-        for i, k in enumerate(keys):
-            r = cache.get(k)
-            if r is None:
-                r = cache[k] = owner(k, world)
-            out[i] = r
-        return out
+        return np.fromiter((rank_of(k) for k in keys), dtype=np.int32, count=len(keys))
     uniq, inv = np.unique(arr, return_inverse=True)
-    ranks = np.empty(len(uniq), dtype=np.int32)
-    for j, k in enumerate(uniq.tolist()):
-        r = cache.get(k)
-        if r is None:
-            r = cache[k] = owner(k, world)
-        ranks[j] = r
+    ranks = np.fromiter((rank_of(k) for k in uniq), dtype=np.int32, count=len(uniq))
     return ranks[inv]
 
 
@@ -162,7 +160,8 @@ Q_PARTITIONED, Q_TIMERS, Q_BROADCAST = 1, 2, 4
 class ShardedAppRuntime:
     """One rank's share of a Siddhi app on an N-GPU node: partitioned queries are key-hash sharded
     (rank r processes the events whose partition key hashes to r, `owner`), unpartitioned queries run as replicas
-    on rank 0. Each stream is routed by the partition attribute the ENGINE compiled for it (sdg_query_key_attr), so
+    on rank 0 (the streams only they read go to rank 0 whole; a stream read by both kinds makes the whole app run on
+    rank 0, with a RuntimeWarning). Each stream is routed by the partition attribute the ENGINE compiled for it (sdg_query_key_attr), so
     the router and the queries cannot disagree; a stream keyed by different attributes in different partitions
     cannot be routed by one key and is refused. Also refused at N > 1, with OperationNotSupportedException:
       * absent states: the reference's Scheduler collapses the due timers of ALL partition keys into one
@@ -193,11 +192,23 @@ class ShardedAppRuntime:
             if bcast:
                 refuse("queries %s read a stream without a partition key: its events reach every key in one global "
                        "key order (PartitionStreamReceiver.java:274-283); run the app on one GPU" % bcast)
-        self.sharded = all(f & Q_PARTITIONED for f in flags)
-        self.replica = not self.sharded  # an unpartitioned query: every event, on rank 0 only
+        part = [bool(f & Q_PARTITIONED) for f in flags]
+        streams = self.rt.app_stream_ids()
+        reads = {s: [q for q in range(len(names)) if self.rt.query_reads(q, s)] for s in streams}
+        # a stream that an unpartitioned query reads must reach ONE rank whole (rank 0); if a partitioned query reads
+        # it too, that query's keys would be split between the sharded streams and this one, so at N > 1 the whole app
+        # goes to rank 0 -- said out loud (warning), never silently
+        mixed = sorted(s for s, qs in reads.items() if any(part[q] for q in qs) and not all(part[q] for q in qs))
+        self.sharded = all(part)
+        self.replica = bool(mixed)  # every event, on rank 0 only
+        self.whole_streams = {s for s, qs in reads.items() if qs and not any(part[q] for q in qs)}  # rank 0 only
+        if world > 1 and mixed:
+            import warnings
+            warnings.warn("streams %s are read by partitioned and unpartitioned queries: the app cannot be key-sharded "
+                          "and runs whole on rank 0 of %d" % (mixed, world), RuntimeWarning, stacklevel=2)
         # stream id -> the partition attribute every partitioned query reading it keys it by
         self.key_attr = {}
-        for s in self.rt.app_stream_ids():
+        for s in streams:
             attrs = {self.rt.query_key_attr(q, s) for q in range(len(names))} - {-1}
             if not attrs:
                 continue
@@ -217,9 +228,9 @@ class ShardedAppRuntime:
         if self.replica:
             return self.rank == 0
         ai = self.key_attr.get(stream_id)
-        if ai is None:  # no partitioned query reads the stream
+        if ai is None:  # no partitioned query reads the stream: whole, on rank 0
             return self.rank == 0
-        return owner(row[ai], self.world) == self.rank
+        return route([row[ai]], self.world, self._cache)[0] == self.rank
 
     def send(self, stream_id, ts, row):
         if self.mine(stream_id, row):

@@ -138,6 +138,7 @@ int flush_query(Emu* e, EmuQuery& q, const BatchClock& bc) {
         int key = 0;
         if (P.partitioned && h.key_attr[qpos] == -3) {  // every initialised key, in getPartitionKeys() order
             const std::vector<uint32_t>& o = q.korder.order();
+            if (q.korder.tree_bins()) throw std::runtime_error("broadcast order: a tree bin (not modelled)");
             for (size_t x = 0; x < o.size(); ++x) {
                 rows.push_back(&ev);
                 rkey.push_back((int)o[x]);

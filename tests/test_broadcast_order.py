@@ -71,3 +71,60 @@ def test_jdk_model_presizes_small_table():
     for k in colliding(9):
         m.put(k)
     assert len(m.table) == 128  # tryPresize(32): tableSizeFor(49) = 64 > sizeCtl until the table is 128
+
+
+def same_hash(n):
+    """n distinct strings with one String.hashCode ("Aa" and "BB" hash alike): one bin at every table size"""
+    out = []
+    for i in range(1 << 12):
+        out.append("".join("Aa" if (i >> b) & 1 else "BB" for b in range(12)))
+        if len(out) == n:
+            return out
+    raise AssertionError
+
+
+def test_tree_bin_is_refused_not_misordered(oracle_built, emu_built):
+    """a key set whose map bin the JDK turns into a tree bin (a put walking 8 nodes of a bin in a table of
+    >= 64) has an iteration order neither side models; the oracle and the engine's host code (keyorder.h, through
+    the emulation harness) both refuse the broadcast instead of delivering some order"""
+    from emu_rt import EmuAdapter
+    keys = same_hash(10)  # the 9th put presizes the 16-bin table to 128; the 10th walks 9 nodes there: a TreeBin
+    tr = [("S", 1000 + i, [i, k, 2.0]) for i, k in enumerate(keys)] + [("T", 2000, [99, "x", 0.0])]
+    o = Oracle(APP)
+    try:
+        with pytest.raises(Exception, match="tree bin"):
+            for s, ts, row in tr:
+                o.send(s, ts, row)
+            o.outputs()
+    finally:
+        o.close()
+    e = EmuAdapter(APP)
+    try:
+        with pytest.raises(Exception, match="tree bin"):
+            for s, ts, row in tr:
+                e.send(s, ts, row)
+            e.flush()
+    finally:
+        e.close()
+    # one key fewer (+ a few others): the presized map has no tree bin, the HashSet copy's table (16 or 32 bins)
+    # doubles ONCE when the colliding bin reaches 9, and both sides deliver the same order
+    for extra in range(4):
+        _same_order(keys[:9] + ["z%d" % i for i in range(extra)])
+
+
+def _same_order(keys):
+    from emu_rt import EmuAdapter
+    tr9 = [("S", 1000 + i, [i, k, 2.0]) for i, k in enumerate(keys)] + [("T", 2000, [99, "x", 0.0])]
+    o = Oracle(APP)
+    e = EmuAdapter(APP)
+    try:
+        for s, ts, row in tr9:
+            o.send(s, ts, row)
+            e.send(s, ts, row)
+        e.flush()
+        ref = [r["values"][0][1] for r in o.outputs() if r["kind"] == "query"]
+        got = [r["values"][0][1] for r in e.outputs() if r["kind"] == "query"]
+    finally:
+        o.close()
+        e.close()
+    assert len(ref) == len(keys) and got == ref

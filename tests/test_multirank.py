@@ -127,7 +127,44 @@ def test_sharded_runtime_refuses_absent_states_at_n_gt_1():
     mine = [k for k in keys if s2.mine("StockStream", [0, k, 1.0, 1])]
     assert mine == [k for k in keys if shard.owner(k, 4) == 1]
     r1 = shard.ShardedAppRuntime(w.C1_APP, 1, 2, compile_only=True)
-    assert r1.replica and not r1.mine("StockStream", [0, "IBM", 1.0, 1])
+    assert "StockStream" in r1.whole_streams and not r1.mine("StockStream", [0, "IBM", 1.0, 1])
+
+
+def test_sharded_runtime_mixed_partitioned_and_unpartitioned_queries():
+    """a stream read by both a partitioned and an unpartitioned query cannot be key-sharded; the
+    app then runs whole on rank 0 WITH a warning. Streams only unpartitioned queries read go to rank 0 whole while
+    the partitioned queries' streams stay sharded."""
+    import warnings
+    defs = "define stream S (id long, k string, p double); define stream T (id long, k string, p double); "
+    part = "partition with (k of S) begin @info(name='qp') from every e1=S -> e2=S select e1.id as a insert into O1; end; "
+    mixed = defs + part + "@info(name='qu') from every e1=S -> e2=S select e1.id as a insert into O2;"
+    with pytest.warns(RuntimeWarning, match="cannot be key-sharded"):
+        m = shard.ShardedAppRuntime(mixed, 1, 2, compile_only=True)
+    assert m.replica and not m.mine("S", [0, "a", 1.0]) and not m.mine("S", [0, "b", 1.0])
+    sep = defs + part + "@info(name='qu') from every e1=T -> e2=T select e1.id as a insert into O2;"
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        s0 = shard.ShardedAppRuntime(sep, 0, 2, compile_only=True)
+        s1 = shard.ShardedAppRuntime(sep, 1, 2, compile_only=True)
+    assert not s1.replica and s1.whole_streams == {"T"} and s1.key_attr == {"S": 1}
+    keys = ["x%d" % i for i in range(200)]
+    assert all(s0.mine("S", [0, k, 1.0]) != s1.mine("S", [0, k, 1.0]) for k in keys)  # S sharded
+    assert all(s0.mine("T", [0, k, 1.0]) and not s1.mine("T", [0, k, 1.0]) for k in keys)  # T whole on rank 0
+
+
+def test_route_float32_keys_like_per_row_send():
+    """send() and send_columns() must route a float32 key alike -- the columnar path hashes the numpy
+    scalars (str(np.float32(0.1)) == '0.1'), not Python floats widened to double ('0.10000000149011612')"""
+    import numpy as np
+    defs = "define stream S (id long, k float, p double); "
+    app = defs + "partition with (k of S) begin @info(name='q') from every e1=S -> e2=S select e1.id as a insert into O; end;"
+    r = shard.ShardedAppRuntime(app, 1, 3, compile_only=True)
+    ks = np.round(np.random.default_rng(5).uniform(0, 10, 3000), 2).astype(np.float32)
+    cols = shard.route(ks, 3, {})
+    rows = [1 if r.mine("S", [0, k, 0.0]) else 0 for k in ks]
+    assert [int(x == 1) for x in cols] == rows
+    assert cols.tolist() == [shard.owner(str(k), 3) for k in ks]
+    assert any(shard.owner(str(k), 3) != shard.owner(str(float(k)), 3) for k in ks)  # the old bug would show
 
 
 def test_sharded_runtime_routes_by_the_engines_partition_attribute():

@@ -78,6 +78,18 @@ def test_engine_decoder_refuses_foreign_bytes():
         rt.snapshot_states(b"")
 
 
+def test_engine_decoder_refuses_format_1_snapshots():
+    """blobs of the earlier layout (magic SSDGSNP1, no spilled-key / partition-order sections) get a version error,
+    not a misleading truncation error"""
+    rt = sa.SiddhiAppRuntime(CHAIN, compile_only=True)
+    with open(os.path.join(GOLD, "chain_gt.snap"), "rb") as f:
+        blob = bytearray(f.read())
+    assert bytes(blob[:8]) == b"SSDGSNP2"
+    blob[:8] = b"SSDGSNP1"
+    with pytest.raises(Exception, match="format 1"):
+        rt.snapshot_states(bytes(blob))
+
+
 @pytest.mark.parametrize("name", sorted(state_fixture_cases.CASES))
 def test_committed_snapshot_decodes_to_the_oracle_maps(name, oracle_built):
     """snapshots the GPU engine wrote (scripts/make_state_fixtures.py), decoded here by a compile-only engine of
