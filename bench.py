@@ -769,10 +769,11 @@ def main():
             t = torch.tensor([oel], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             oel = float(t.item())
-        if orecs > 1:  # the last step's export is in delivery order: (emitting position, e1 position) increasing
-            m = orecs // K
-            seq, e1 = o_seq[:m], o_vals[0, :m]
-            okd = bool(((seq[1:] > seq[:-1]) | ((seq[1:] == seq[:-1]) & (e1[1:] > e1[:-1]))).all().item())
+        if orecs > 1:  # the last step's export is in delivery order: (emitting position, e1 position) increasing;
+            m = orecs // K  # ids restart every step, so a partial carried from the step before (e1id > e2id: its e1
+            seq, e1, e2 = o_seq[:m], o_vals[0, :m], o_vals[1, :m]  # lies at the end of the previous batch) ranks first
+            e1k = e1 + (e1 < e2).to(torch.int64) * (1 << 40)
+            okd = bool(((seq[1:] > seq[:-1]) | ((seq[1:] == seq[:-1]) & (e1k[1:] > e1k[:-1]))).all().item())
             if not okd:
                 raise RuntimeError("ordered steps: the export is not in delivery order")
         out["value_ordered"] = n * world * K / oel
