@@ -125,32 +125,43 @@ __global__ __launch_bounds__(256) void unpack_k(ColSet cs, int ncol, const int64
 // events around it (a few coalesced reads of the sorted keys), counts the run's records that precede it by
 // (sub, sorted index) and writes its index at run start + that rank. No thread walks a whole run serially, and no
 // record moves twice (order_runs_k insertion-sorted each run in place, one thread per run: 0.62 ms per 40M records)
+// Each record's sub is read once (the one random read); the run's other subs come from the neighbouring lanes by
+// shuffles (a wave holds 64 consecutive sorted records, and runs are short), from memory only past the wave's edge.
 __global__ __launch_bounds__(256) void order_runs_rank_k(const uint32_t* __restrict__ ek, const uint32_t* __restrict__ ix,
                                                          const int64_t* __restrict__ sub, int64_t n,
                                                          uint32_t* __restrict__ perm, int* __restrict__ long_run) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t e = ek[i];
+    const int lane = threadIdx.x & 63;
+    const bool in = i < n;
+    const uint32_t e = in ? ek[i] : 0u;
     int64_t s = i, t = i + 1;
-    while (s > 0 && i - s <= RUN_MAX && ek[s - 1] == e) --s;
-    while (t < n && t - s <= RUN_MAX && ek[t] == e) ++t;
-    if (t - s > RUN_MAX) {  // (left to the two-sort ordering)
-        atomicOr(long_run, 1);
-        return;
+    if (in) {
+        while (s > 0 && i - s <= RUN_MAX && ek[s - 1] == e) --s;
+        while (t < n && t - s <= RUN_MAX && ek[t] == e) ++t;
     }
-    const uint32_t me = ix[i];
-    if (t - s == 1) {
-        perm[i] = me;
-        return;
-    }
-    const int64_t my = sub[me];
+    const bool lng = in && t - s > RUN_MAX;  // (left to the two-sort ordering)
+    if (lng) atomicOr(long_run, 1);
+    const bool multi = in && !lng && t - s > 1;
+    const uint32_t me = in ? ix[i] : 0u;
+    const int64_t my = multi ? sub[me] : 0;
     int64_t rank = 0;
-    for (int64_t j = s; j < t; ++j) {
-        if (j == i) continue;
-        const int64_t o = sub[ix[j]];
-        rank += o < my || (o == my && j < i);  // stable: equal subs keep the sorted (emission) order
+    // offsets d = 1 .. the wave's longest run: lane + d / lane - d by shuffle when inside the wave
+    int span = multi ? (int)(t - s) : 0;
+    for (int o = 32; o > 0; o >>= 1) span = max(span, __shfl_xor(span, o));
+    for (int d = 1; d < span; ++d) {
+        const int64_t fw = __shfl(my, min(lane + d, 63));
+        const int64_t bw = __shfl(my, max(lane - d, 0));
+        if (!multi) continue;
+        if (i + d < t) {  // a later record of the run: before me only with a smaller sub
+            const int64_t o = lane + d < 64 ? fw : sub[ix[i + d]];
+            rank += o < my;
+        }
+        if (i - d >= s) {  // an earlier one: before me unless its sub is larger (equal subs keep the sorted order)
+            const int64_t o = lane - d >= 0 ? bw : sub[ix[i - d]];
+            rank += o <= my;
+        }
     }
-    perm[s + rank] = me;
+    if (in && !lng) perm[multi ? s + rank : i] = me;
 }
 
 // every column of a record through one index read: dst[c][i] = src[c][perm[i]]. Blocks are mapped XCD-contiguous
@@ -171,13 +182,26 @@ __global__ __launch_bounds__(256) void gather_rows_k(ColSet cs, int ncol, const 
         if (c < ncol) cs.dst[c][i] = x[c];
 }
 
+// the sort by the emitting event: RADIX_BITS per onesweep pass (the flush's positions need ~27 bits: 3 passes of 9
+// instead of 4 of rocPRIM's default 8)
+#ifndef SDG_ORDER_RADIX_BITS
+#define SDG_ORDER_RADIX_BITS 9
+#endif
+using EkSortCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<512, 16>, rocprim::kernel_config<512, 16>,
+                                        SDG_ORDER_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
+
 void temp_sizes(int64_t n, size_t& a, size_t& b) {
     uint64_t* k64 = nullptr;
     uint32_t* k32 = nullptr;
     uint32_t* v = nullptr;
     a = b = 0;
+    size_t c = 0;
     rocprim::radix_sort_pairs(nullptr, a, k64, k64, v, v, (size_t)n, 0, 64);
     rocprim::radix_sort_pairs(nullptr, b, k32, k32, v, v, (size_t)n, 0, 32);
+    rocprim::radix_sort_pairs<EkSortCfg>(nullptr, c, k32, k32, v, v, (size_t)n, 0, 32);
+    b = std::max(b, c);
 }
 
 int bits_for(unsigned long long v) {  // bits to hold 0..v
@@ -226,7 +250,9 @@ void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t e
     if (!full && !two && emit_span > 0) {
         eb = std::max(1, bits_for((unsigned long long)(emit_span - 1)));
         hipLaunchKernelGGL(order_emit_keys_k, dim3(grid), dim3(256), 0, stream, emit, n, emit_base, ek0, ix0);
-        rocprim::radix_sort_pairs(tmp, b, ek0, ek1, ix0, ix1, (size_t)n, 0, eb, stream);
+        static const bool dflt = getenv("SDG_ORDER_DEFAULT_CFG") != nullptr;  // A/B: rocPRIM's default digits
+        if (dflt) rocprim::radix_sort_pairs(tmp, b, ek0, ek1, ix0, ix1, (size_t)n, 0, eb, stream);
+        else rocprim::radix_sort_pairs<EkSortCfg>(tmp, b, ek0, ek1, ix0, ix1, (size_t)n, 0, eb, stream);
         int* flag = (int*)(rng + 3);
         (void)hipMemsetAsync(flag, 0, 4, stream);
         static const bool serial_runs = getenv("SDG_ORDER_SERIAL_RUNS") != nullptr;  // A/B: order_runs_k
