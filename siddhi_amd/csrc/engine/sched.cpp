@@ -120,17 +120,35 @@ void SchedSim::qpop(KS& k) {
     }
 }
 
+void SchedSim::heap_fix(SchedState& S, Heap& H) const {
+    if (H.cap == S.cap) return;
+    size_t w = 0;
+    for (size_t i = 0; i < H.h.size(); ++i) {
+        DueE e = H.h[i];
+        const KS& k = S.ks[e.k.key];
+        if (k.ver != e.ver) continue;  // stale
+        e.k = okey(S, k, e.k.key);
+        H.h[w++] = e;
+    }
+    H.h.resize(w);
+    std::make_heap(H.h.begin(), H.h.end(), std::greater<DueE>());
+    H.cap = S.cap;
+}
+
 void SchedSim::due_add(SchedState& S, uint32_t key, KS& k) {
     const DueE e{okey(S, k, key), ++k.ver};
-    std::vector<DueE>& h = S.due[qfront(k)];
-    h.push_back(e);
-    std::push_heap(h.begin(), h.end(), std::greater<DueE>());
+    Heap& H = S.due[qfront(k)];
+    if (H.h.empty()) H.cap = S.cap;
+    else heap_fix(S, H);
+    H.h.push_back(e);
+    std::push_heap(H.h.begin(), H.h.end(), std::greater<DueE>());
 }
 
 bool SchedSim::due_front(SchedState& S, int64_t& t, OKey& k) {
     while (!S.due.empty()) {
         auto it = S.due.begin();
-        std::vector<DueE>& h = it->second;
+        heap_fix(S, it->second);
+        std::vector<DueE>& h = it->second.h;
         while (!h.empty() && stale(S, h.front())) {
             std::pop_heap(h.begin(), h.end(), std::greater<DueE>());
             h.pop_back();
@@ -155,16 +173,11 @@ void SchedSim::resize(SchedState& S) {  // HashMap.resize(): 16 / 12, then doubl
         S.threshold *= 2;
     }
     S.bin.assign(S.cap, 0);
-    S.due.clear();
     for (size_t key = 0; key < S.kend; ++key) {  // (ks is sized for every key of the batch; only these can be in)
-        KS& k = S.ks[key];
-        if (!k.in_map) continue;
-        S.bin[(uint32_t)k.hash & (S.cap - 1)]++;
-        if (k.n) {  // re-keyed by the new buckets (heaps rebuilt below)
-            S.due[qfront(k)].push_back(DueE{okey(S, k, (uint32_t)key), ++k.ver});
-        }
+        const KS& k = S.ks[key];
+        if (k.in_map) S.bin[(uint32_t)k.hash & (S.cap - 1)]++;
     }
-    for (auto& kv : S.due) std::make_heap(kv.second.begin(), kv.second.end(), std::greater<DueE>());
+    // the due heaps are re-keyed by the new buckets lazily (heap_fix: their cap no longer matches)
 }
 
 void SchedSim::notify(int sch, uint32_t key, int64_t t) {
@@ -525,7 +538,8 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
                     SchedState& S = work_.sc[s];
                     W.clear();
                     for (auto it = S.due.begin(); it != S.due.end() && it->first <= clock;) {
-                        std::vector<DueE>& h = it->second;
+                        heap_fix(S, it->second);
+                        std::vector<DueE>& h = it->second.h;
                         while (!h.empty() && stale(S, h.front())) {
                             std::pop_heap(h.begin(), h.end(), std::greater<DueE>());
                             h.pop_back();
@@ -537,7 +551,15 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
                         W.push_back({it->first, h.front().k.key});
                         ++it;
                     }
-                    for (auto& w : W) fire(s, w.second, (uint32_t)g, clock);
+                    for (size_t wi = 0; wi < W.size(); ++wi) {
+                        if (wi + 4 < W.size()) {  // the keys' cursors and queue entries ahead (random keys)
+                            const uint32_t kf = W[wi + 4].second;
+                            __builtin_prefetch(&kc[kf]);
+                            __builtin_prefetch(&S.ks[kf]);
+                            if (kc[kf].i < logs.size()) __builtin_prefetch(&logs[kc[kf].i]);
+                        }
+                        fire(s, W[wi].second, (uint32_t)g, clock);
+                    }
                     for (auto& w : W) remove_if_empty(s, w.second);  // returnAllStates
                 }
             } else {
@@ -592,6 +614,17 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
         prof.lap(4);
         // 4. the device keys' pushes made by the event at g
         for (; ep < evp.size() && posof(evp[ep]) == g; ++ep) {
+            // the pushes are in position order but the keys' state is scattered: prefetch the log records a few
+            // pushes ahead, and the model entries of the nearer ones (the pass was bound by these cache misses)
+            if (ep + 16 < evp.size()) __builtin_prefetch(&logs[evp[ep + 16]]);
+            if (ep + 8 < evp.size()) {
+                const SchedLog& Lf = logs[evp[ep + 8]];
+                __builtin_prefetch(&kc[Lf.key]);
+                if (Lf.sched < work_.sc.size() && Lf.key < work_.sc[Lf.sched].ks.size()) {
+                    __builtin_prefetch(&work_.sc[Lf.sched].ks[Lf.key]);
+                    if (Lf.key < key_hash.size()) __builtin_prefetch(&key_hash[Lf.key]);
+                }
+            }
             const SchedLog& L = logs[evp[ep]];
             const uint8_t m = kc[L.key].mode;
             if (m != DEV && !(optimistic && m == PENDING)) continue;
@@ -752,9 +785,11 @@ void SchedSim::save(std::vector<uint8_t>& o) const {
     for (const SchedState& S : cur_.sc) {
         put_vec(o, S.ks);
         put<uint64_t>(o, S.due.size());
-        for (const auto& kv : S.due) {
+        for (const auto& kv : S.due) {  // (every heap written keyed for the current capacity)
             put<int64_t>(o, kv.first);
-            put_vec(o, kv.second);
+            Heap H = kv.second;
+            heap_fix(const_cast<SchedState&>(S), H);
+            put_vec(o, H.h);
         }
         put<uint64_t>(o, S.cap);
         put<uint64_t>(o, S.threshold);
@@ -780,9 +815,10 @@ const uint8_t* SchedSim::load(const uint8_t* p, const uint8_t* end) {
         const uint64_t nd = get<uint64_t>(p, end);
         for (uint64_t i = 0; i < nd; ++i) {
             const int64_t t = get<int64_t>(p, end);
-            get_vec(p, end, S.due[t]);
+            get_vec(p, end, S.due[t].h);
         }
         S.cap = get<uint64_t>(p, end);
+        for (auto& kv : S.due) kv.second.cap = S.cap;  // (saved keyed for it)
         S.threshold = get<uint64_t>(p, end);
         S.size = get<uint64_t>(p, end);
         S.stamp = get<uint64_t>(p, end);

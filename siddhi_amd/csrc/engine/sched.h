@@ -216,9 +216,16 @@ class SchedSim {
         uint32_t ver;
         bool operator>(const DueE& o) const { return o.k < k; }
     };
+    // one head time's states: a min-heap by OKey (lazy deletion), its keys computed for the table capacity `cap`.
+    // A HashMap resize changes every state's bucket, so a heap is re-keyed when it is next used (heap_fix), not
+    // every heap at every resize
+    struct Heap {
+        std::vector<DueE> h;
+        uint64_t cap = 0;
+    };
     struct SchedState {
         std::vector<KS> ks;                                 // [dense key id]
-        std::map<int64_t, std::vector<DueE>> due;           // head time -> min-heap of states (lazy deletion)
+        std::map<int64_t, Heap> due;                        // head time -> min-heap of states (lazy deletion)
         uint64_t cap = 0, threshold = 0, size = 0, stamp = 0;
         size_t kend = 0;                                    // keys [0, kend) have ever entered the map (resize scans them)
         std::vector<uint32_t> bin;                          // keys per bucket (treeifyBin on a small table resizes)
@@ -246,6 +253,7 @@ class SchedSim {
     // the earliest due time with a live entry (cleans stale heap tops); false when nothing is due
     bool due_front(SchedState& S, int64_t& t, OKey& k);
     void due_add(SchedState& S, uint32_t key, KS& k);
+    void heap_fix(SchedState& S, Heap& H) const;  // re-key a heap built for an older capacity (drops stale entries)
     void due_del(KS& k) { ++k.ver; }
     void resize(SchedState& S);
     void notify(int sch, uint32_t key, int64_t t);  // Scheduler.notifyAt
