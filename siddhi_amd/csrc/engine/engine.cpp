@@ -267,6 +267,8 @@ struct QueryRt {
     std::vector<std::unique_ptr<KeyRun>> runs;
     // batch staging
     DevBuf st_ts, st_qs, st_key, st_vrank, st_cols[MAX_COLS], st_nulls[MAX_COLS];
+    // broadcast rows expanded on the device (bcast_expand): the expanded view and the expansion's tables
+    DevBuf bx_ts, bx_vpos, bx_qs, bx_key, bx_vrank, bx_cols[MAX_COLS], bx_nulls[MAX_COLS], bx_off, bx_ph, bx_ord;
     DevBuf mv_work, mv_tot, mv_args, kt_vals_in;  // device-side views of mixed pushes
     // sorted view
     DevBuf so_ts, so_qs, so_key, so_orig, so_vrank, so_cols[MAX_COLS], so_nulls[MAX_COLS], seg, kg_counts, kg_gsum;
@@ -1363,13 +1365,33 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         };
         auto bcast_order = [&]() -> const std::vector<uint32_t>& {
             const std::vector<uint32_t>& o = q.korder.order();
-            if (o.size() >= ((size_t)1 << 23))
+            if (o.size() >= ((size_t)1 << 23))  // (the delivery rank sits in bits 40..62 of the record's sub key)
                 throw CompileError(SDG_ERR_CAPACITY, "a broadcast to more than 2^23 partition keys");
             if (q.korder.tree_bins())  // the JDK's tree-bin iteration order is not modelled (keyorder.h)
                 throw CompileError(SDG_ERR_UNSUPPORTED, "query '" + q.hq.name + "': the partition's key set has a "
                                                         "hash bin the JDK would turn into a tree bin; its broadcast "
                                                         "order is not modelled");
             return o;
+        };
+        // Broadcast rows are expanded on the device (bcast_expand, SDG_BCAST_HOST: here, row by row): the view holds one
+        // placeholder row per event of a stream without a partition key (key BX_PLACEHOLDER) and the key order that
+        // event saw, stored once per distinct order (keyorder.h version) -- host work O(events + orders x keys)
+        // instead of O(events x keys)
+        static const bool bc_host = getenv("SDG_BCAST_HOST") != nullptr;
+        const bool bc_dev = q.broadcast && !bc_host;
+        std::vector<uint32_t> bc_row, bc_off, bc_k, bc_ord;  // placeholders: compact row, order start, order length
+        uint64_t bc_ver = ~0ull;
+        auto bc_order_now = [&](uint32_t& off, uint32_t& k) {  // the current order, appended when it changed
+            const std::vector<uint32_t>& o = bcast_order();
+            if (bc_ver != q.korder.version() || bc_ord.empty()) {
+                if (bc_ord.size() + o.size() > ((size_t)1 << 28))
+                    throw CompileError(SDG_ERR_CAPACITY, "query '" + h.name + "': the broadcast key orders of one flush "
+                                                         "exceed 2^28 entries (flush more often)");
+                bc_ver = q.korder.version();
+                bc_ord.insert(bc_ord.end(), o.begin(), o.end());
+            }
+            k = (uint32_t)o.size();
+            off = (uint32_t)(bc_ord.size() - o.size());
         };
         ts.reserve(n);
         vpos.reserve(n);
@@ -1386,6 +1408,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 };
                 std::vector<VRow> vr;
                 vr.reserve((size_t)c->n);
+                std::vector<uint32_t> ph_j, ph_off, ph_k;  // placeholders among vr (their compact row follows below)
                 constexpr int64_t PF = 16;
                 auto pf = [&](int64_t r) {  // the integral key slot of row r, ahead of its lookup
                     const int qp = h.stream_pos(c->rstream[r]);
@@ -1405,6 +1428,15 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                         for (size_t x = 0; x < rs.size(); ++x)
                             if (range_holds(h, rs[x], qpos, *c, r, true)) vr.push_back({r, rs[x].label, (uint32_t)x, (uint8_t)qpos});
                     } else if (partitioned && h.key_attr[qpos] == -3) {  // one view row per initialised key, in order
+                        if (bc_dev) {
+                            uint32_t off = 0, k = 0;
+                            bc_order_now(off, k);
+                            ph_j.push_back((uint32_t)vr.size());
+                            ph_off.push_back(off);
+                            ph_k.push_back(k);
+                            vr.push_back({r, BX_PLACEHOLDER, 0, (uint8_t)qpos});
+                            continue;
+                        }
                         const std::vector<uint32_t>& o = bcast_order();
                         for (size_t x = 0; x < o.size(); ++x) vr.push_back({r, o[x], (uint32_t)x, (uint8_t)qpos});
                     } else if (partitioned) {
@@ -1419,6 +1451,11 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                     }
                 }
                 const size_t base = ts.size(), m = vr.size();
+                for (size_t x = 0; x < ph_j.size(); ++x) {
+                    bc_row.push_back((uint32_t)(base + ph_j[x]));
+                    bc_off.push_back(ph_off[x]);
+                    bc_k.push_back(ph_k[x]);
+                }
                 ts.resize(base + m);
                 vpos.resize(base + m);
                 qs.resize(base + m);
@@ -1466,6 +1503,18 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                             kept.push_back(r);
                             vrank.push_back((uint32_t)x);
                         }
+            } else if (partitioned && h.key_attr[qpos] == -3 && bc_dev) {  // one placeholder per event (one order: no
+                all = false;                                                // keyed row of this chunk changes it)
+                uint32_t off = 0, k = 0;
+                bc_order_now(off, k);
+                for (int64_t r = 0; r < c->n; ++r) {
+                    bc_row.push_back((uint32_t)(base + kept.size()));
+                    bc_off.push_back(off);
+                    bc_k.push_back(k);
+                    keys.push_back(BX_PLACEHOLDER);
+                    kept.push_back(r);
+                    vrank.push_back(0);
+                }
             } else if (partitioned && h.key_attr[qpos] == -3) {  // one view row per initialised key (a chunk of one
                 all = false;                                      // stream: the key set is the same for all its rows)
                 const std::vector<uint32_t>& o = bcast_order();
@@ -1558,6 +1607,78 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 d_nulls[k] = (const uint8_t*)q.st_nulls[k].ensure(cnt);
                 HIPCHECK(hipMemcpyAsync((void*)d_nulls[k], nulls[k].data(), nrows, hipMemcpyHostToDevice, st));
             }
+        }
+        if (!bc_row.empty()) {  // ---- the placeholders expanded on the device (kernels.h bcast_expand)
+            std::vector<uint32_t> off((size_t)nrows + 1);
+            uint64_t o = 0;
+            size_t ph = 0;
+            int64_t kmax = 0;
+            for (int64_t r = 0; r < nrows; ++r) {
+                off[r] = (uint32_t)o;
+                if (ph < bc_row.size() && bc_row[ph] == (uint32_t)r) {
+                    o += bc_k[ph];
+                    kmax = std::max<int64_t>(kmax, bc_k[ph]);
+                    ++ph;
+                } else {
+                    o += 1;
+                }
+                if (o >= (uint64_t)0xFFFFFFF0) throw CompileError(SDG_ERR_CAPACITY, "a flush holds more than 2^32 - 16 view rows");
+            }
+            off[nrows] = (uint32_t)o;
+            if (ph != bc_row.size()) throw DeviceError("broadcast placeholders out of order");
+            const int64_t nx = (int64_t)o;
+            const size_t cx = (size_t)std::max<int64_t>(nx, 1);
+            BcastExpandArgs bx;
+            std::memset(&bx, 0, sizeof bx);
+            bx.n = nrows;
+            uint32_t* d_off = (uint32_t*)q.bx_off.ensure(off.size() * 4);
+            HIPCHECK(hipMemcpyAsync(d_off, off.data(), off.size() * 4, hipMemcpyHostToDevice, st));
+            bx.off = d_off;
+            bx.nph = (int64_t)bc_row.size();
+            uint32_t* d_ph = (uint32_t*)q.bx_ph.ensure(3 * bc_row.size() * 4);
+            HIPCHECK(hipMemcpyAsync(d_ph, bc_row.data(), bc_row.size() * 4, hipMemcpyHostToDevice, st));
+            HIPCHECK(hipMemcpyAsync(d_ph + bc_row.size(), bc_off.data(), bc_row.size() * 4, hipMemcpyHostToDevice, st));
+            HIPCHECK(hipMemcpyAsync(d_ph + 2 * bc_row.size(), bc_k.data(), bc_row.size() * 4, hipMemcpyHostToDevice, st));
+            bx.ph_row = d_ph;
+            bx.ph_ord = d_ph + bc_row.size();
+            bx.ph_k = d_ph + 2 * bc_row.size();
+            uint32_t* d_ord = (uint32_t*)q.bx_ord.ensure(std::max<size_t>(bc_ord.size(), 1) * 4);
+            if (!bc_ord.empty()) HIPCHECK(hipMemcpyAsync(d_ord, bc_ord.data(), bc_ord.size() * 4, hipMemcpyHostToDevice, st));
+            bx.ord = d_ord;
+            if (!d_vpos) {  // (the compact positions were contiguous: upload them anyway, the expansion repeats them)
+                d_vpos = (const uint32_t*)q.d_vpos.ensure(cnt * 4);
+                HIPCHECK(hipMemcpyAsync((void*)d_vpos, vpos.data(), nrows * 4, hipMemcpyHostToDevice, st));
+            }
+            bx.ts = d_ts;
+            bx.vpos = d_vpos;
+            bx.qs = d_qs;
+            bx.key = d_key;
+            bx.vrank = d_vrank;
+            bx.ncols = nc;
+            bx.o_ts = (int64_t*)q.bx_ts.ensure(cx * 8);
+            bx.o_vpos = (uint32_t*)q.bx_vpos.ensure(cx * 4);
+            bx.o_qs = d_qs ? (uint8_t*)q.bx_qs.ensure(cx) : nullptr;
+            bx.o_key = (uint32_t*)q.bx_key.ensure(cx * 4);
+            bx.o_vrank = (uint32_t*)q.bx_vrank.ensure(cx * 4);
+            for (int k = 0; k < nc; ++k) {
+                bx.width[k] = (uint8_t)width_of(P.col_kind[k]);
+                bx.cols[k] = d_cols[k];
+                bx.nulls[k] = d_nulls[k];
+                bx.o_cols[k] = q.bx_cols[k].ensure(cx * bx.width[k]);
+                bx.o_nulls[k] = d_nulls[k] ? (uint8_t*)q.bx_nulls[k].ensure(cx) : nullptr;
+            }
+            bcast_expand(bx, kmax, st);
+            d_ts = bx.o_ts;
+            d_vpos = bx.o_vpos;
+            pos_off = 0;
+            d_qs = bx.o_qs;
+            d_key = bx.o_key;
+            d_vrank = bx.o_vrank;
+            for (int k = 0; k < nc; ++k) {
+                d_cols[k] = bx.o_cols[k];
+                d_nulls[k] = bx.o_nulls[k];
+            }
+            nrows = nx;
         }
         // hipMemcpyAsync from pageable memory: keep the host vectors alive until the copies land
         HIPCHECK(hipStreamSynchronize(st));

@@ -62,8 +62,11 @@ class PartitionKeyOrder {
         }
         if (++count_ >= size_ctl_) grow();
         dirty_ = true;
+        ++ver_;
     }
     int64_t size() const { return count_; }
+    // changes whenever order() may change (a new key, a resize)
+    uint64_t version() const { return ver_; }
     // a tree bin was (or would be) built in the map or its HashSet copy: order() is not the JDK's order then
     bool tree_bins() const { return tree_; }
     // the keys in getPartitionKeys() order (valid until the next add)
@@ -140,6 +143,7 @@ class PartitionKeyOrder {
             }
         }
         dirty_ = true;
+        ++ver_;
     }
 
    private:
@@ -152,6 +156,7 @@ class PartitionKeyOrder {
     int64_t count_ = 0, size_ctl_ = 0;
     std::vector<uint32_t> order_;
     bool dirty_ = true;
+    uint64_t ver_ = 0;
     bool tree_ = false;
     static int64_t pow2_at_least(int64_t c) {
         int64_t n = 1;
@@ -163,6 +168,7 @@ class PartitionKeyOrder {
         const int64_t c = pow2_at_least(3 * (int64_t)bins_.size() + 1);
         while (c > size_ctl_) grow();
         dirty_ = true;
+        ++ver_;
     }
     void grow() {  // ConcurrentHashMap.transfer
         const size_t n = bins_.size();

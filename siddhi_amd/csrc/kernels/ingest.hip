@@ -5,6 +5,8 @@
 // (per-tile counts, one scan, per-tile writes with wave ballot ranks) instead of a per-row host loop.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "kernels.h"
 #include "wave.h"
 
@@ -165,6 +167,55 @@ void mixed_view_write(const MixedViewArgs& a, const MixedViewArgs* d_a, void* wo
     if (nt == 0) return;
     const int64_t* off = (const int64_t*)((uint8_t*)work + ((nt * 4 + 15) & ~15ll));
     hipLaunchKernelGGL(mv_write_k, dim3((unsigned)nt), dim3(256), 0, st, d_a, off);
+}
+
+// ---- broadcast rows (kernels.h BcastExpandArgs) ---------------------------------------------------------------
+namespace {
+__device__ __forceinline__ void bx_copy_cols(const BcastExpandArgs& a, int64_t from, int64_t to) {
+    for (int c = 0; c < a.ncols; ++c) {
+        const int w = a.width[c];
+        if (w == 8) ((int64_t*)a.o_cols[c])[to] = ((const int64_t*)a.cols[c])[from];
+        else if (w == 4) ((uint32_t*)a.o_cols[c])[to] = ((const uint32_t*)a.cols[c])[from];
+        else ((uint8_t*)a.o_cols[c])[to] = ((const uint8_t*)a.cols[c])[from];
+        if (a.o_nulls[c]) a.o_nulls[c][to] = a.nulls[c] ? a.nulls[c][from] : 0;
+    }
+}
+// every compact row moves to off[r]; a placeholder's slot is written by bx_expand_k
+__global__ __launch_bounds__(256) void bx_move_k(BcastExpandArgs a) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= a.n) return;
+    if (a.key[r] == BX_PLACEHOLDER) return;  // a placeholder: bx_expand_k writes its rows
+    const uint32_t o = a.off[r];
+    a.o_ts[o] = a.ts[r];
+    a.o_vpos[o] = a.vpos[r];
+    if (a.o_qs) a.o_qs[o] = a.qs[r];
+    a.o_key[o] = a.key[r];
+    if (a.o_vrank) a.o_vrank[o] = a.vrank ? a.vrank[r] : 0u;
+    bx_copy_cols(a, r, o);
+}
+// placeholder p (grid y, strided) x key x of its order (grid x): the event's row for that key, ranked x
+__global__ __launch_bounds__(256) void bx_expand_k(BcastExpandArgs a) {
+    const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (int64_t p = blockIdx.y; p < a.nph; p += gridDim.y) {
+        const uint32_t k = a.ph_k[p];
+        if (x >= k) continue;
+        const uint32_t r = a.ph_row[p];
+        const int64_t o = (int64_t)a.off[r] + x;
+        a.o_ts[o] = a.ts[r];
+        a.o_vpos[o] = a.vpos[r];
+        if (a.o_qs) a.o_qs[o] = a.qs[r];
+        a.o_key[o] = a.ord[(int64_t)a.ph_ord[p] + x];
+        if (a.o_vrank) a.o_vrank[o] = (uint32_t)x;
+        bx_copy_cols(a, r, o);
+    }
+}
+}  // namespace
+
+void bcast_expand(const BcastExpandArgs& a, int64_t kmax, hipStream_t st) {
+    if (a.n > 0) hipLaunchKernelGGL(bx_move_k, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, st, a);
+    if (a.nph > 0 && kmax > 0)
+        hipLaunchKernelGGL(bx_expand_k, dim3((unsigned)((kmax + 255) / 256), (unsigned)std::min<int64_t>(a.nph, 65535)),
+                           dim3(256), 0, st, a);
 }
 
 }  // namespace sdg

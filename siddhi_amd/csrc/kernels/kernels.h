@@ -488,6 +488,39 @@ void mixed_view_count(const MixedViewArgs& a, const MixedViewArgs* d_a, void* wo
 void mixed_view_write(const MixedViewArgs& a, const MixedViewArgs* d_a, void* work, hipStream_t st);
 void narrow_u32(const int64_t* src, int64_t n, uint32_t* dst, hipStream_t st);
 
+// broadcast rows of a stream without a partition key (ingest.hip; PartitionStreamReceiver.send(ComplexEvent) :274-283):
+// the host view holds ONE placeholder row per such event; this expands it into one row per key of the key order the
+// event saw (getPartitionKeys(), engine/keyorder.h), ranked by its place there, and moves every other row to its
+// place in the expanded view: row r of the compact view lands at off[r] (exclusive prefix of the rows' widths)
+constexpr int BX_MAX_COLS = MAX_COLS;
+constexpr uint32_t BX_PLACEHOLDER = 0xFFFFFFFFu;  // the compact key of a placeholder row
+struct BcastExpandArgs {
+    int64_t n;                       // compact rows
+    const uint32_t* off;             // [n + 1] output row of each compact row (off[n] = expanded rows)
+    int64_t nph;                     // placeholder rows
+    const uint32_t* ph_row;          // [nph] their compact rows
+    const uint32_t* ph_ord;          // [nph] start of the key order they saw in `ord`
+    const uint32_t* ph_k;            // [nph] its length
+    const uint32_t* ord;             // concatenated key orders (dense key ids)
+    const int64_t* ts;
+    const uint32_t* vpos;
+    const uint8_t* qs;               // nullptr: one stream
+    const uint32_t* key;
+    const uint32_t* vrank;           // (ranked view: vrank of the keyed rows; placeholders get their rank)
+    int ncols;
+    uint8_t width[BX_MAX_COLS];
+    const void* cols[BX_MAX_COLS];
+    const uint8_t* nulls[BX_MAX_COLS];  // nullptr: no nulls in the column
+    int64_t* o_ts;
+    uint32_t* o_vpos;
+    uint8_t* o_qs;
+    uint32_t* o_key;
+    uint32_t* o_vrank;
+    void* o_cols[BX_MAX_COLS];
+    uint8_t* o_nulls[BX_MAX_COLS];
+};
+void bcast_expand(const BcastExpandArgs& a, int64_t kmax, hipStream_t st);
+
 // device partition key table for integral partition attributes (keytab.hip): value -> dense key id
 struct KeyTab {
     int64_t* keys;    // [cap + 1]

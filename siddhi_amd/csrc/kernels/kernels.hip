@@ -680,11 +680,23 @@ static int rx_tile() {
     }();
     return t;
 }
+// the fused path's single bucket pass (bucketize): 8192-row tiles, two blocks per CU (r5j: scatter 1.39 -> 1.31 ms
+// per C2 step against 16384-row tiles on the same box; the multi-pass key sort keeps rx_tile()).
+// SDG_RX_TILE_BK=16384 for A/B
+static int rx_tile_bucket() {
+    static const int t = [] {
+        const char* e = getenv("SDG_RX_TILE_BK");
+        return e && atoi(e) == RX_TILE_BIG ? RX_TILE_BIG : RX_TILE;
+    }();
+    return t;
+}
+static int g_tile_override = 0;  // set around bucketize's launches
+static int rx_tile_now() { return g_tile_override ? g_tile_override : rx_tile(); }
 static int64_t rx_ntiles(int64_t n, int tile = RX_TILE) { return n <= 0 ? 1 : (n + tile - 1) / tile; }
 static void launch_rx_hist(int64_t nt, hipStream_t stream, const uint32_t* keys, int64_t n, int shift, uint32_t mask,
                            int nb, uint32_t* counts, uint32_t kcheck, int* kflag, const uint32_t* pre_keys = nullptr,
                            int64_t pre_n = 0, int64_t hole = 0) {
-    if (rx_tile() == RX_TILE_BIG)
+    if (rx_tile_now() == RX_TILE_BIG)
         hipLaunchKernelGGL((rx_hist<RX_TILE_BIG, RX_THREADS_BIG>), dim3((unsigned)nt), dim3(RX_THREADS_BIG), 0, stream,
                            keys, n, shift, mask, nb, counts, kcheck, kflag, pre_keys, pre_n, hole);
     else
@@ -697,12 +709,12 @@ static void launch_rx_scatter(int64_t nt, hipStream_t stream, RxPass rp) {
     rp.xcds = no_xcd ? 1 : g_xcds;
     const int64_t grid = no_xcd ? nt : xcd_round(nt);
     if (rp.pre_n > 0) {  // (the large tile only: prefix rows exist on the sorted-view path alone)
-        if (rx_tile() == RX_TILE_BIG)
+        if (rx_tile_now() == RX_TILE_BIG)
             hipLaunchKernelGGL((rx_scatter<RX_TILE_BIG, RX_THREADS_BIG, true>), dim3((unsigned)grid), dim3(RX_THREADS_BIG),
                                0, stream, rp);
         else
             hipLaunchKernelGGL((rx_scatter<RX_TILE, RX_THREADS, true>), dim3((unsigned)grid), dim3(RX_THREADS), 0, stream, rp);
-    } else if (rx_tile() == RX_TILE_BIG) {
+    } else if (rx_tile_now() == RX_TILE_BIG) {
         hipLaunchKernelGGL((rx_scatter<RX_TILE_BIG, RX_THREADS_BIG, false>), dim3((unsigned)grid), dim3(RX_THREADS_BIG), 0,
                            stream, rp);
     } else {
@@ -847,7 +859,8 @@ void bucketize(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, uint
                int seg_rows, hipStream_t stream, hipEvent_t* marks) {
     const int nb = 1 << bits;
     const uint32_t mask = (uint32_t)nb - 1;
-    const int64_t nt = rx_ntiles(a.n, rx_tile());
+    g_tile_override = rx_tile_bucket();
+    const int64_t nt = rx_ntiles(a.n, g_tile_override);
     const int ng = (int)((nt + KG_GROUP - 1) / KG_GROUP);
     if (marks) (void)hipEventRecord(marks[0], stream);
     launch_rx_hist(nt, stream, a.keys, a.n, 0, mask, nb, a.counts, a.key_flag ? (uint32_t)a.K : 0u, a.key_flag);
@@ -882,6 +895,7 @@ void bucketize(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, uint
     rp.lkey_out = a.lkey_out;
     rp.lkey_shift = bits;
     launch_rx_scatter(nt, stream, rp);
+    g_tile_override = 0;
     if (marks) (void)hipEventRecord(marks[2], stream);
     hipLaunchKernelGGL(bk_plan, dim3(1), dim3(256), 0, stream, a.tot, a.n, nb, seg_rows, bstart, bseg);
     if (marks) (void)hipEventRecord(marks[3], stream);

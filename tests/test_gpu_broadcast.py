@@ -60,3 +60,36 @@ def test_broadcast_key_order_through_resizes(oracle_built):
         finally:
             p.close()
         assert len(ref) > 9_000 and got == ref, batches
+
+
+@pytest.mark.parametrize("batches", [1, 3])
+def test_broadcast_100k_keys_device_expansion(batches, oracle_built):
+    """10^5 initialised keys, each broadcast event expanded into 10^5 view rows ON THE DEVICE
+    (engine bcast_expand: one host placeholder per event plus each distinct key order once), bit-exact vs the oracle.
+    Three T events start a partial in every key; the S events that follow complete them key by key."""
+    import numpy as np
+    keys = ["k%06d" % i for i in range(100_000)]
+    rng = np.random.default_rng(17)
+    rows, eid, ts = [], 0, 1000
+    for k in keys:  # initPartition of every key (price 0: no partial of its own)
+        rows.append(("S", ts, [eid, k, 0.0, 1])); eid += 1
+    ts += 1
+    for p in (95.0, 91.5, 93.0):
+        rows.append(("T", ts, [eid, "ignored", p, 1])); eid += 1
+        ts += 1
+    for i in rng.permutation(len(keys))[:60_000]:
+        rows.append(("S", ts, [eid, keys[i], float(np.round(rng.uniform(85, 100), 2)), 1])); eid += 1
+        if eid % 1000 == 0:
+            ts += 1
+    app = synth.BCAST_APPS["bc_only_t"]
+    o = Oracle(app)
+    try:
+        ref = synth.run(o, rows)
+    finally:
+        o.close()
+    p = ProductAdapter(app)
+    try:
+        got = synth.run(p, rows, batches)
+    finally:
+        p.close()
+    assert len(ref) > 50_000 and got == ref
