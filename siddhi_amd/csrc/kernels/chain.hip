@@ -996,15 +996,13 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
             tot += c;
         }
     }
-    if (t < 256) lend[t] = (uint16_t)tot;
-    __syncthreads();
-    for (int off = 1; off < 256; off <<= 1) {  // inclusive scan of the run lengths (<= FU_ROWS: fits u16)
-        const uint32_t x = (t < 256 && t >= off) ? lend[t - off] : 0u;
-        __syncthreads();
-        if (t < 256) lend[t] = (uint16_t)(lend[t] + x);
-        __syncthreads();
+    {  // inclusive scan of the run lengths (<= FU_ROWS: fits u16)
+        const uint32_t inc = scan256_incl(t < 256 ? tot : 0u, &wcnt[0][0][0]);  // (wcnt is free until the counts)
+        if (t < 256) {
+            lend[t] = (uint16_t)inc;
+            lstart[t] = (uint16_t)(inc - tot);
+        }
     }
-    if (t < 256) lstart[t] = (uint16_t)(lend[t] - tot);
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < FU_PT; ++r) {

@@ -190,6 +190,7 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
     __shared__ uint32_t gbase[1 << RX_MAXBITS];
     __shared__ uint8_t sdig[RX_TILE];  // digit of each staged element: its destination is gbase + rank in the run
     __shared__ uint64_t stage[RX_TILE];
+    __shared__ uint32_t gbase_ws[4];  // scan256_incl's wave totals
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     // XCD-aware tile order (kernels.h xcd_block): virtual tile v gives each XCD a contiguous run of tiles. A digit's
     // runs of consecutive tiles are adjacent in the output, so the cache line where one tile's run ends and the next
@@ -246,17 +247,12 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
                 tot += c;
             }
         }
-        tstart[t] = tot;
     }
-    __syncthreads();
     // exclusive scan of the digit totals (nb <= 256) -> tile-local start of each digit run
-    for (int off = 1; off < 256; off <<= 1) {
-        const uint32_t x = (t < 256 && t >= off) ? tstart[t - off] : 0u;
-        __syncthreads();
-        if (t < 256) tstart[t] += x;
-        __syncthreads();
+    {
+        const uint32_t inc = scan256_incl(t < 256 ? tot : 0u, &gbase_ws[0]);
+        if (t < 256) tstart[t] = inc - tot;
     }
-    if (t < 256) tstart[t] -= tot;
     __syncthreads();
     static_assert(RX_TILE <= 65536, "staged positions packed as u16 pairs");
     uint32_t sp2[R / 2];  // staged position of element r: u16 half (r & 1) of sp2[r / 2] (registers)

@@ -24,6 +24,24 @@ __device__ __forceinline__ int64_t wave_reserve(bool take, unsigned long long* c
     return (int64_t)base + __popcll(m & lanemask_lt());
 }
 
+// inclusive scan of one value per thread over threads 0..255 (waves 0-3: shuffles, then one barrier for the wave
+// totals). Every thread of the block must call it (threads >= 256 pass anything and get garbage); wsum: 4 words of
+// LDS. Replaces the 8-step Hillis-Steele loop over an LDS array (16 block barriers).
+__device__ __forceinline__ uint32_t scan256_incl(uint32_t x, uint32_t* wsum) {
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    if (w < 4 && lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+    if (w < 4)
+        for (int v = 0; v < w; ++v) pre += wsum[v];
+    return x + pre;
+}
+
 // block-wide exclusive scan of two per-thread counts; one atomic per block and counter reserves the block's
 // output ranges (per-wave reservations on one global counter serialise in L2 at ~10^8/s). Every thread of the
 // block must call it.
