@@ -163,10 +163,10 @@ class ShardedAppRuntime:
     on rank 0 (the streams only they read go to rank 0 whole; a stream read by both kinds makes the whole app run on
     rank 0, with a RuntimeWarning). Each stream is routed by the partition attribute the ENGINE compiled for it (sdg_query_key_attr), so
     the router and the queries cannot disagree; a stream keyed by different attributes in different partitions
-    cannot be routed by one key and is refused. Also refused at N > 1, with OperationNotSupportedException:
-      * absent states: the reference's Scheduler collapses the due timers of ALL partition keys into one
-        TreeMultimap per clock advance (Scheduler.java:75-98, only the first state per due time fires), so which
-        fires it delays depends on keys that would live on other GPUs (BASELINE.md C4: 7,857 vs 9,790);
+    cannot be routed by one key and is refused. Queries with absent states run whole on rank 0 (RuntimeWarning): the
+    reference's Scheduler collapses the due timers of ALL partition keys into one TreeMultimap per clock advance
+    (Scheduler.java:75-98, only the first state per due time fires), so which fires it delays depends on keys that
+    would live on other GPUs (7,857 vs 9,790). Refused at N > 1, with OperationNotSupportedException:
       * a stream without a partition key (PartitionStreamReceiver.send(ComplexEvent) :274-283): its events go to
         every key of the partition in ONE global key order that interleaves the ranks' keys;
       * range partitions: an event may belong to several ranges (keys), so it has no single owner.
@@ -182,17 +182,16 @@ class ShardedAppRuntime:
         def refuse(msg):
             self.rt.shutdown()
             raise sa.OperationNotSupportedException(msg)
+        timers = [n for n, f in zip(names, flags) if f & Q_TIMERS]
         if world > 1:
-            timers = [n for n, f in zip(names, flags) if f & Q_TIMERS]
-            if timers:
-                refuse("queries %s have absent states: the reference's scheduler orders timers across all partition "
-                       "keys (Scheduler.java:75-98), so they cannot be key-sharded over %d GPUs; run the app on one GPU"
-                       % (timers, world))
             bcast = [n for n, f in zip(names, flags) if f & Q_BROADCAST]
             if bcast:
                 refuse("queries %s read a stream without a partition key: its events reach every key in one global "
                        "key order (PartitionStreamReceiver.java:274-283); run the app on one GPU" % bcast)
-        part = [bool(f & Q_PARTITIONED) for f in flags]
+        # a query with absent states runs whole on rank 0: the reference's scheduler orders the due timers of ALL its
+        # partition keys in one TreeMultimap per clock advance (Scheduler.java:75-98), so a key shard on another GPU
+        # would change which fires it delays (7,857 vs 9,790 matches under a naive split)
+        part = [bool(f & Q_PARTITIONED) and not (world > 1 and f & Q_TIMERS) for f in flags]
         streams = self.rt.app_stream_ids()
         reads = {s: [q for q in range(len(names)) if self.rt.query_reads(q, s)] for s in streams}
         # a stream that an unpartitioned query reads must reach ONE rank whole (rank 0); if a partitioned query reads
@@ -202,14 +201,18 @@ class ShardedAppRuntime:
         self.sharded = all(part)
         self.replica = bool(mixed)  # every event, on rank 0 only
         self.whole_streams = {s for s, qs in reads.items() if qs and not any(part[q] for q in qs)}  # rank 0 only
-        if world > 1 and mixed:
+        if world > 1 and (mixed or timers):
             import warnings
-            warnings.warn("streams %s are read by partitioned and unpartitioned queries: the app cannot be key-sharded "
-                          "and runs whole on rank 0 of %d" % (mixed, world), RuntimeWarning, stacklevel=2)
+            if timers:
+                warnings.warn("queries %s have absent states (one global timer order, Scheduler.java:75-98): they run "
+                              "whole on rank 0 of %d, not key-sharded" % (timers, world), RuntimeWarning, stacklevel=2)
+            if mixed:
+                warnings.warn("streams %s are read by key-sharded and rank-0-only queries: the app cannot be key-sharded "
+                              "and runs whole on rank 0 of %d" % (mixed, world), RuntimeWarning, stacklevel=2)
         # stream id -> the partition attribute every partitioned query reading it keys it by
         self.key_attr = {}
         for s in streams:
-            attrs = {self.rt.query_key_attr(q, s) for q in range(len(names))} - {-1}
+            attrs = {self.rt.query_key_attr(q, s) for q in range(len(names)) if part[q]} - {-1}
             if not attrs:
                 continue
             if world > 1 and (len(attrs) > 1 or min(attrs) < 0):

@@ -109,17 +109,22 @@ def test_merge_runs_is_a_stable_g_way_merge():
         assert torch.equal(m[c], cat[c][..., order]), c
 
 
-def test_sharded_runtime_refuses_absent_states_at_n_gt_1():
-    """N > 1 semantics for absent queries: refused, because the reference's scheduler collapse is
-    global across keys; the same app on one GPU is accepted"""
+def test_sharded_runtime_runs_absent_states_whole_on_rank_0():
+    """N > 1 semantics for absent queries: the reference's scheduler collapse is global across keys,
+    so such a query is not key-sharded -- its streams go whole to rank 0 (with a warning); on one GPU it is a plain
+    partitioned query"""
     import siddhi_amd as sa
     from siddhi_amd import workloads as w
     flags = sa.SiddhiAppRuntime(w.C4_APP, compile_only=True).query_flags()
     assert flags == [shard.Q_PARTITIONED | shard.Q_TIMERS]
     assert sa.SiddhiAppRuntime(w.C2_APP, compile_only=True).query_flags() == [shard.Q_PARTITIONED]
     assert sa.SiddhiAppRuntime(w.C1_APP, compile_only=True).query_flags() == [0]
-    with pytest.raises(sa.OperationNotSupportedException):
-        shard.ShardedAppRuntime(w.C4_APP, 0, 2, compile_only=True)
+    with pytest.warns(RuntimeWarning, match="absent states"):
+        r1 = shard.ShardedAppRuntime(w.C4_APP, 1, 2, compile_only=True)
+    with pytest.warns(RuntimeWarning, match="absent states"):
+        r0 = shard.ShardedAppRuntime(w.C4_APP, 0, 2, compile_only=True)
+    assert r1.whole_streams == set(w.C4_STREAMS) and not r1.key_attr
+    assert all(r0.mine(s, [0, k, 1.0]) and not r1.mine(s, [0, k, 1.0]) for s in w.C4_STREAMS for k in range(50))
     rt = shard.ShardedAppRuntime(w.C4_APP, 0, 1, compile_only=True)
     assert rt.sharded
     s2 = shard.ShardedAppRuntime(w.C2_APP, 1, 4, compile_only=True, key_attr={"StockStream": 1})
@@ -202,3 +207,60 @@ def test_ordered_gather_checks_its_merge_precondition():
     import torch
     with pytest.raises(ValueError):
         shard.ordered_gather(None, 0, 1, {"a": torch.zeros(3), "b": torch.zeros(3)}, ["a", "b"])
+
+
+def _c4_rank_main(rank, world, port, out_dir, keys):
+    import warnings
+    import numpy as np
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from siddhi_amd import workloads as w
+        from test_c4_host import c4_slots
+        from emu_rt import EmuAdapter
+        c = w.c4_columns(keys, per_tick=keys // 100)
+        end = int(c["ts"][-1]) + 5000
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", RuntimeWarning)
+            router = shard.ShardedAppRuntime(w.C4_APP, rank, world, compile_only=True)
+        streams = np.array(w.C4_STREAMS)[c["stream"]]
+        mine = np.array([router.mine(s, [0, int(k), 0.0]) for s, k in zip(streams, c["key"])])
+        idx = np.nonzero(mine)[0]
+        e = EmuAdapter(w.C4_APP)
+        try:
+            sidx = np.array([e.L.emu_stream_index(e.h, s.encode()) for s in w.C4_STREAMS], dtype=np.int32)[c["stream"][idx]]
+            slots = np.ascontiguousarray(c4_slots(c)[idx])
+            offs = np.arange(len(idx), dtype=np.int64) * 3
+            tsa = np.ascontiguousarray(c["ts"][idx])
+            if len(idx):
+                e.L.emu_send_batch(e.h, len(idx), sidx.ctypes.data, tsa.ctypes.data, offs.ctypes.data, slots.ctypes.data,
+                                   None)
+            e.flush()
+            e.advance(end)  # every rank's clock reaches the end (the batch-boundary watermark)
+            e.flush()
+            recs = [(r["ts"], tuple(v[1] for v in r["values"])) for r in e.outputs() if r["kind"] == "query"]
+        finally:
+            e.close()
+        parts = [None] * world
+        dist.all_gather_object(parts, (int(mine.sum()), recs))
+        if rank == 0:
+            assert parts[1][0] == 0 and not parts[1][1]  # the timer query's streams are not sharded
+            with open(os.path.join(out_dir, "c4.txt"), "w") as f:
+                f.write(repr(parts[0][1]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_absent_app_equals_single_process(tmp_path, oracle_built, emu_built):
+    """the C4 app at 2*10^4 keys on a world-2 run is no longer refused; its streams go
+    whole to rank 0 (shard.ShardedAppRuntime), so the merged output equals the single-process oracle -- the case where
+    a naive key split changes the result (7,857 vs 9,790 matches)"""
+    from siddhi_amd import workloads as w
+    from test_c4_host import oracle_c4
+    keys = 20_000
+    mp.spawn(_c4_rank_main, args=(2, _free_port(), str(tmp_path), keys), nprocs=2, join=True)
+    c = w.c4_columns(keys, per_tick=keys // 100)
+    ots, ovals, _ = oracle_c4(c, int(c["ts"][-1]) + 5000)
+    ref = [(int(t), tuple(int(x) for x in v)) for t, v in zip(ots, ovals)]
+    got = eval((tmp_path / "c4.txt").read_text())
+    assert len(ref) > 1000 and got == ref
