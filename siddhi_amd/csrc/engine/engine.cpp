@@ -4431,7 +4431,26 @@ int export_records(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_t* 
                                                               std::to_string(n) + " records");
         hipStream_t st = e->stream;
         const int na = q.hq.plan.n_user_out;
-        if (n > 0 && ordered) {  // the delivery-order pass of drain(), gathering straight into the caller's buffers
+        bool done = false;
+        static const bool two_pass = getenv("SDG_EXPORT_TWO_PASS") != nullptr;  // A/B: order_records + gather
+        if (n > 0 && ordered && !two_pass) {  // one sort, then ranks + gathers in one kernel (sub compared as int64)
+            const size_t wb = order_workspace(n);
+            void* work = q.ord_ws.ensure(wb + wb / 4);
+            std::vector<const int64_t*> src;
+            std::vector<int64_t*> dst;
+            auto col = [&](const void* from, int64_t* to) {
+                if (!to) return;
+                src.push_back((const int64_t*)from);
+                dst.push_back(to);
+            };
+            col(q.o_ts.p, d_ts);
+            col(q.o_first.p, d_sub);
+            for (int j = 0; j < na && d_vals; ++j) col((const int64_t*)q.o_vals.p + (size_t)j * q.out_cap, d_vals + (size_t)j * cap);
+            done = order_export((const int64_t*)q.o_emit.p, (const int64_t*)q.o_first.p, n, q.emit_base, q.emit_span,
+                                src.data(), dst.data(), (int)src.size(), d_seq, work, st);
+        }
+        if (done) {
+        } else if (n > 0 && ordered) {  // the delivery-order pass of drain(), gathering straight into the caller's buffers
             const size_t wb = order_workspace(n);
             void* work = q.ord_ws.ensure(wb + wb / 4);
             uint32_t* perm = nullptr;

@@ -428,6 +428,12 @@ void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t e
                    int64_t sub_bias, int sub_bits,
                    void* work, size_t work_bytes, uint32_t** perm_out, hipStream_t stream);
 void gather_i64(const int64_t* src, const uint32_t* perm, int64_t n, int64_t* dst, hipStream_t stream);
+// the ordered export in one pass after the sort by emitting event (order.hip): each record's run rank and its columns
+// straight to its slot, the emitting position written from the sorted key (seq_dst, may be nullptr); work =
+// order_workspace(n). false: a run longer than the rank pass handles -- use order_records + gather_cols_i64
+bool order_export(const int64_t* emit, const int64_t* sub, int64_t n, int64_t emit_base, int64_t emit_span,
+                  const int64_t* const* src, int64_t* const* dst, int ncol, int64_t* seq_dst, void* work,
+                  hipStream_t stream);
 // dst[c][i] = src[c][perm[i]] for ncol int64 columns, through a packed row-major copy (work = gather_cols_workspace)
 constexpr int GATHER_MAX_COLS = 16;
 size_t gather_cols_workspace(int64_t n, int ncol);

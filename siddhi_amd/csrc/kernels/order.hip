@@ -164,6 +164,50 @@ __global__ __launch_bounds__(256) void order_runs_rank_k(const uint32_t* __restr
     if (in && !lng) perm[multi ? s + rank : i] = me;
 }
 
+// The export's ordering pass in one kernel (export_ordered): the run rank of order_runs_rank_k, then the record's
+// columns gathered straight to their final slot -- no index array written and read back. The emitting position is
+// not gathered at all: in delivery order it is the sorted key + emit_base (seq_dst).
+__global__ __launch_bounds__(256) void order_runs_gather_k(const uint32_t* __restrict__ ek, const uint32_t* __restrict__ ix,
+                                                           const int64_t* __restrict__ sub, int64_t n, ColSet cs,
+                                                           int ncol, int64_t* __restrict__ seq_dst, int64_t emit_base,
+                                                           int* __restrict__ long_run, uint32_t xcds) {
+    const uint32_t vb = xcd_block(blockIdx.x, gridDim.x, xcds);
+    const int64_t i = (int64_t)vb * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool in = i < n;
+    const uint32_t e = in ? ek[i] : 0u;
+    int64_t s = i, t = i + 1;
+    if (in) {
+        while (s > 0 && i - s <= RUN_MAX && ek[s - 1] == e) --s;
+        while (t < n && t - s <= RUN_MAX && ek[t] == e) ++t;
+    }
+    const bool lng = in && t - s > RUN_MAX;
+    if (lng) atomicOr(long_run, 1);
+    const bool multi = in && !lng && t - s > 1;
+    const uint32_t me = in ? ix[i] : 0u;
+    const int64_t my = multi ? sub[me] : 0;
+    int64_t rank = 0;
+    int span = multi ? (int)(t - s) : 0;
+    for (int o = 32; o > 0; o >>= 1) span = max(span, __shfl_xor(span, o));
+    for (int d = 1; d < span; ++d) {
+        const int64_t fw = __shfl(my, min(lane + d, 63));
+        const int64_t bw = __shfl(my, max(lane - d, 0));
+        if (!multi) continue;
+        if (i + d < t) rank += (lane + d < 64 ? fw : sub[ix[i + d]]) < my;
+        if (i - d >= s) rank += (lane - d >= 0 ? bw : sub[ix[i - d]]) <= my;
+    }
+    if (!in || lng) return;
+    const int64_t f = multi ? s + rank : i;
+    int64_t x[GATHER_MAX_COLS];
+#pragma unroll
+    for (int c = 0; c < GATHER_MAX_COLS; ++c)
+        if (c < ncol) x[c] = cs.src[c][me];
+#pragma unroll
+    for (int c = 0; c < GATHER_MAX_COLS; ++c)
+        if (c < ncol) cs.dst[c][f] = x[c];
+    if (seq_dst) seq_dst[f] = emit_base + (int64_t)e;
+}
+
 // every column of a record through one index read: dst[c][i] = src[c][perm[i]]. Blocks are mapped XCD-contiguous
 // (kernels.h xcd_block): consecutive output records come from a few hundred emission streams (the matcher's blocks),
 // each read forward, so one XCD's slice of the output keeps those streams' lines in its own L2
@@ -295,6 +339,42 @@ void order_records(const int64_t* emit, const int64_t* sub, int64_t n, int64_t e
     hipLaunchKernelGGL(gather_k<uint32_t>, dim3(grid), dim3(256), 0, stream, ek0, perm1, n, ek1);
     rocprim::radix_sort_pairs(tmp, b, ek1, ek0, perm1, ix0, (size_t)n, 0, eb, stream);
     *perm_out = ix0;
+}
+
+bool order_export(const int64_t* emit, const int64_t* sub, int64_t n, int64_t emit_base, int64_t emit_span,
+                  const int64_t* const* src, int64_t* const* dst, int ncol, int64_t* seq_dst, void* work,
+                  hipStream_t stream) {
+    if (n <= 0) return true;
+    if (emit_span <= 0 || ncol > GATHER_MAX_COLS) return false;
+    size_t a = 0, b = 0;
+    temp_sizes(n, a, b);
+    const size_t sort_tmp = ((a > b ? a : b) + 255) & ~size_t(255);
+    uint8_t* p = (uint8_t*)work;
+    void* tmp = p;
+    p += sort_tmp;
+    p += (size_t)n * 16;  // (order_records' 64-bit key buffers: unused here)
+    uint32_t* ek0 = (uint32_t*)p; p += (size_t)n * 4;
+    uint32_t* ek1 = (uint32_t*)p; p += (size_t)n * 4;
+    uint32_t* ix0 = (uint32_t*)p; p += (size_t)n * 4;
+    uint32_t* ix1 = (uint32_t*)p; p += (size_t)n * 4;
+    int* flag = (int*)p;
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    const int eb = std::max(1, bits_for((unsigned long long)(emit_span - 1)));
+    hipLaunchKernelGGL(order_emit_keys_k, dim3(grid), dim3(256), 0, stream, emit, n, emit_base, ek0, ix0);
+    rocprim::radix_sort_pairs<EkSortCfg>(tmp, b, ek0, ek1, ix0, ix1, (size_t)n, 0, eb, stream);
+    (void)hipMemsetAsync(flag, 0, 4, stream);
+    ColSet cs{};
+    for (int c = 0; c < ncol; ++c) {
+        cs.src[c] = src[c];
+        cs.dst[c] = dst[c];
+    }
+    const unsigned g8 = (unsigned)xcd_round(grid);
+    hipLaunchKernelGGL(order_runs_gather_k, dim3(g8), dim3(256), 0, stream, ek1, ix1, sub, n, cs, ncol, seq_dst,
+                       emit_base, flag, (uint32_t)g_xcds);
+    int hf = 0;
+    (void)hipMemcpyAsync(&hf, flag, 4, hipMemcpyDeviceToHost, stream);
+    (void)hipStreamSynchronize(stream);
+    return hf == 0;  // false: a run longer than RUN_MAX (nothing usable written; the caller takes order_records)
 }
 
 size_t gather_cols_workspace(int64_t n, int ncol) { return (size_t)std::max<int64_t>(n, 1) * ncol * 8 + 256; }
