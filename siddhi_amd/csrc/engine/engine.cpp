@@ -223,7 +223,7 @@ struct QueryRt {
     // KC_INT (int / long), KC_F32, KC_F64, KC_BOOL -- or KC_NONE (string keys, mixed classes, range partitions)
     int key_class = 0;
     // device key table (keytab.hip) for device-resident batches of int / long keys: a mirror of keydict's ids
-    DevBuf kt_keys, kt_ids, kt_first, kt_cnt, kt_pairs, kt_vals, kt_slots;
+    DevBuf kt_keys, kt_cnt, kt_pairs, kt_vals, kt_slots;  // kt_keys: the table's KtSlot array
     uint64_t kt_cap = 0;
     size_t kt_synced = 0;                           // keydict ids [0, kt_synced) are in the table
     HostPin kt_ret;
@@ -1128,7 +1128,7 @@ struct HostProf {
 };
 
 KeyTab kt_view(QueryRt& q) {
-    return KeyTab{q.kt_keys.as<int64_t>(), q.kt_ids.as<uint32_t>(), q.kt_first.as<uint32_t>(), q.kt_cap - 1, q.kt_cap};
+    return KeyTab{q.kt_keys.as<KtSlot>(), q.kt_cap - 1, q.kt_cap};
 }
 
 // the host dictionary's ids [kt_synced, K) into the device key table (keys the host path assigned)
@@ -1153,9 +1153,7 @@ void kt_rebuild(sdg_engine* e, QueryRt& q, uint64_t cap) {
     uint64_t c = 1;
     while (c < cap) c <<= 1;
     q.kt_cap = c;
-    q.kt_keys.ensure((size_t)(c + 1) * 8);
-    q.kt_ids.ensure((size_t)(c + 1) * 4);
-    q.kt_first.ensure((size_t)(c + 1) * 4);
+    q.kt_keys.ensure((size_t)(c + 1) * sizeof(KtSlot));
     kt_clear(kt_view(q), e->stream);
     q.kt_synced = 0;
     kt_sync(e, q);

@@ -528,10 +528,15 @@ struct BcastExpandArgs {
 void bcast_expand(const BcastExpandArgs& a, int64_t kmax, hipStream_t st);
 
 // device partition key table for integral partition attributes (keytab.hip): value -> dense key id
+// one slot = 16 B (key, id, first row) so that a probe's key compare and its id read touch one cache line (round 5:
+// the separate key / id arrays cost two dependent random reads per row)
+struct KtSlot {
+    int64_t key;      // KT_EMPTY: free (slot cap holds the value KT_EMPTY itself: key = 1 when used)
+    uint32_t id;      // id + 1 (0: new in this batch)
+    uint32_t first;   // a new key's first row
+};
 struct KeyTab {
-    int64_t* keys;    // [cap + 1]
-    uint32_t* ids;    // [cap + 1] id + 1 (0: new in this batch)
-    uint32_t* first;  // [cap + 1] a new key's first row
+    KtSlot* slots;    // [cap + 1]
     uint64_t mask;    // cap - 1 (cap a power of two)
     uint64_t cap;
 };

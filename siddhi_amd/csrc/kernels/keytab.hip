@@ -6,8 +6,8 @@
 // for the key. Ids are dense and assigned in order of a key's first row, as the host dictionary assigns them
 // (engine.cpp host_key), so a batch maps to the same ids whichever side it was pushed from.
 //
-// Slots: keys[cap] (KT_EMPTY = free; the value KT_EMPTY itself lives in the extra slot keys[cap], used = 1),
-// ids[cap + 1] (id + 1, 0 = new in this batch), first[cap + 1] (smallest row of a new key). Linear probing; a
+// Slots (kernels.h KtSlot, 16 B): key (KT_EMPTY = free; the value KT_EMPTY itself lives in the extra slot cap, key =
+// 1 when used), id (id + 1, 0 = new in this batch), first (smallest row of a new key). Linear probing; a
 // probe sequence longer than KT_MAX_PROBE, or a batch whose new keys would fill the table over half, stops the pass
 // early (flags) and the host grows the table (at least 8x) and probes again.
 #include <hip/hip_runtime.h>
@@ -57,16 +57,16 @@ __device__ __forceinline__ void kt_count_new(unsigned long long* new_count, unsi
 __device__ __forceinline__ int64_t kt_slot(const KeyTab& t, int64_t v, unsigned long long* new_count,
                                            unsigned long long limit, int* flags) {
     if (v == KT_EMPTY) {
-        const unsigned long long was = atomicCAS((unsigned long long*)&t.keys[t.cap], 0ull, 1ull);
+        const unsigned long long was = atomicCAS((unsigned long long*)&t.slots[t.cap].key, 0ull, 1ull);
         if (was == 0ull) kt_count_new(new_count, limit, flags);
         return t.cap;
     }
     uint64_t h = kt_mix((uint64_t)v) & t.mask;
     for (uint32_t i = 0; i < KT_MAX_PROBE && i <= t.mask; ++i) {
         if ((i & 31) == 31 && flags && *(volatile int*)&flags[1]) return -1;
-        int64_t cur = t.keys[h];
+        int64_t cur = t.slots[h].key;
         if (cur == KT_EMPTY) {  // a stale read can only show a slot as still free: the CAS decides
-            cur = (int64_t)atomicCAS((unsigned long long*)&t.keys[h], (unsigned long long)KT_EMPTY, (unsigned long long)v);
+            cur = (int64_t)atomicCAS((unsigned long long*)&t.slots[h].key, (unsigned long long)KT_EMPTY, (unsigned long long)v);
             if (cur == KT_EMPTY) {
                 kt_count_new(new_count, limit, flags);
                 return (int64_t)h;
@@ -81,9 +81,9 @@ __device__ __forceinline__ int64_t kt_slot(const KeyTab& t, int64_t v, unsigned 
 __global__ __launch_bounds__(256) void kt_clear_k(KeyTab t) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i > (int64_t)t.cap) return;
-    t.keys[i] = i == (int64_t)t.cap ? 0 : KT_EMPTY;
-    t.ids[i] = 0;
-    t.first[i] = 0xFFFFFFFFu;
+    t.slots[i].key = i == (int64_t)t.cap ? 0 : KT_EMPTY;
+    t.slots[i].id = 0;
+    t.slots[i].first = 0xFFFFFFFFu;
 }
 
 // known keys (the host dictionary's, id order)
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) void kt_load_k(KeyTab t, const int64_t* __rest
         atomicOr(&flags[0], 1);
         return;
     }
-    t.ids[s] = id0 + (uint32_t)i + 1u;
+    t.slots[s].id = id0 + (uint32_t)i + 1u;
 }
 
 // per row: the key id, or KT_NEW (first sighting in this batch: the row's index competes for the key's first row)
@@ -112,12 +112,12 @@ __global__ __launch_bounds__(256) void kt_probe_k(KeyTab t, const void* __restri
         out[r] = 0;
         return;
     }
-    const uint32_t id = t.ids[s];
+    const uint32_t id = t.slots[s].id;
     if (id) {
         out[r] = id - 1u;
     } else {
         out[r] = KT_NEW;
-        atomicMin(&t.first[s], (uint32_t)r);
+        atomicMin(&t.slots[s].first, (uint32_t)r);
     }
 }
 
@@ -127,18 +127,18 @@ __global__ __launch_bounds__(256) void kt_collect_k(KeyTab t, unsigned long long
                                                     int64_t cap_out) {
     const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (s > (int64_t)t.cap) return;
-    const bool used = s == (int64_t)t.cap ? t.keys[s] != 0 : t.keys[s] != KT_EMPTY;
-    if (!used || t.ids[s] != 0) return;
+    const bool used = s == (int64_t)t.cap ? t.slots[s].key != 0 : t.slots[s].key != KT_EMPTY;
+    if (!used || t.slots[s].id != 0) return;
     const unsigned long long o = atomicAdd(cnt, 1ull);
     if ((int64_t)o >= cap_out) return;  // the host sized pairs by the probe's count
-    pairs[o] = ((unsigned long long)t.first[s] << 32) | (unsigned long long)s;
-    vals[o] = s == (int64_t)t.cap ? KT_EMPTY : t.keys[s];
+    pairs[o] = ((unsigned long long)t.slots[s].first << 32) | (unsigned long long)s;
+    vals[o] = s == (int64_t)t.cap ? KT_EMPTY : t.slots[s].key;
 }
 
 __global__ __launch_bounds__(256) void kt_assign_k(KeyTab t, const uint32_t* __restrict__ slots, uint32_t id0, int64_t m) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= m) return;
-    t.ids[slots[i]] = id0 + (uint32_t)i + 1u;
+    t.slots[slots[i]].id = id0 + (uint32_t)i + 1u;
 }
 
 __global__ __launch_bounds__(256) void kt_fix_k(KeyTab t, const void* __restrict__ col, int kind, int64_t n,
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void kt_fix_k(KeyTab t, const void* __restrict
     const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (r >= n || out[r] != KT_NEW) return;
     const int64_t s = kt_slot(t, kt_value(col, kind, r), nullptr, 0, nullptr);  // present: inserted by the probe
-    out[r] = s >= 0 ? t.ids[s] - 1u : 0u;
+    out[r] = s >= 0 ? t.slots[s].id - 1u : 0u;
 }
 
 dim3 blocks(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
