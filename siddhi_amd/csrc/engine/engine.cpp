@@ -1691,8 +1691,11 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     int kbits = 0;
     while ((1ll << kbits) < (int64_t)K) ++kbits;
     bool try_fused = false;
-    if (P.chain && partitioned && !multi_stream && nrows > 0 && !e->no_fused && P.n_states == 2 && P.has_within &&
-        nc >= 1 && kbits <= 16 && P.fast[0].kind != FP_NONE) {
+    // (round 5: one-key batches -- an unpartitioned chain query, C1 -- take the fused matcher too: the batch is one
+    // bucket of one key, so there is no bucket pass; SDG_FU_NO_ONEKEY keeps them on the lane kernels)
+    static const bool no_onekey = getenv("SDG_FU_NO_ONEKEY") != nullptr;
+    if (P.chain && (partitioned || !no_onekey) && !multi_stream && nrows > 0 && !e->no_fused && P.n_states == 2 &&
+        P.has_within && nc >= 1 && kbits <= 16 && P.fast[0].kind != FP_NONE) {
         ChainArgs pa;
         std::memset(&pa, 0, sizeof pa);
         for (int k = 0; k < nc; ++k) pa.nulls[k] = d_nulls[k];
@@ -1850,6 +1853,19 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         v_segend = (const uint32_t*)q.kg_gsum.ensure((size_t)K * 4);
         HIPCHECK(hipMemsetAsync((void*)v_seg, 0, (size_t)K * 4, st));
         HIPCHECK(hipMemsetAsync((void*)v_segend, 0, (size_t)K * 4, st));
+    } else if (fused && nrows > 0) {  // one key: the batch is one bucket in arrival order; its segment plan here
+        bbits = 0;
+        b_start = (uint32_t*)q.bk_plan.ensure(2 * 257 * 4);
+        b_seg = b_start + 257;
+        uint32_t* hp2 = (uint32_t*)q.h_ret.ensure(64);
+        hp2[0] = 0;
+        hp2[1] = (uint32_t)nrows;
+        hp2[2] = 0;
+        hp2[3] = (uint32_t)((nrows + FU_ROWS / 2 - 1) / (FU_ROWS / 2));
+        HIPCHECK(hipMemcpyAsync(b_start, hp2, 8, hipMemcpyHostToDevice, st));
+        HIPCHECK(hipMemcpyAsync(b_seg, hp2 + 2, 8, hipMemcpyHostToDevice, st));
+        HIPCHECK(hipMemsetAsync(flags, 0, 32, st));
+        HIPCHECK(hipStreamSynchronize(st));  // (hp2 is reused for the run's read-backs)
     }
     hp.mark("keygroup_enqueue");
     ev_record(e->ev[1], st);
@@ -2526,6 +2542,10 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         a.bbits = bbits;
         a.lbits = std::max(0, kbits - bbits);
         a.seg_start = a.seg_end = nullptr;
+        // one key: half the staged rows are halo (its window spans ~all of a batch's rate, C1: 1000 rows per
+        // second), and the staging checks time order itself (no bucket pass did)
+        a.fu_own = partitioned ? FU_OWN : FU_ROWS / 2;
+        a.fu_check_ts = partitioned ? 0 : 1;
     }
     if (sorted) {  // chain_sorted_k: deque / forward scans in LDS blocks, the rest of a cut run in chain_sovf_k
         static const char* skip = getenv("SDG_FU_SKIP");  // A/B: 512 = the deque step's loops; phase timing (results
@@ -2579,7 +2599,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     dbg_sync("chain_carry_k");
     ev_record(e->ev[8], st);
     if (fused) {
-        const int64_t grid = chain_fused_grid(nrows, a.nb);
+        const int64_t grid = chain_fused_grid(nrows, a.nb, a.fu_own);
         static int64_t* trace = nullptr;
         static int64_t trace_n = 0;
         if (dbg) {  // host-mapped progress trace, readable after a device fault
@@ -2649,7 +2669,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     hp.mark("sync_wait");
     if (hf[4]) throw CompileError(SDG_ERR_ARG, "device-resident partition key ids out of range (not from sdg_intern)");
     if (fused && hf[2]) throw DeviceError("fused matcher bounds check failed: bits " + std::to_string(hf[2]));
-    if (fused && hf[3]) {  // batch timestamps not in arrival order (or a block's span over 2^32 ms): radix path
+    if (fused && hf[3]) {  // batch timestamps not in arrival order (or a block's span over 2^32 ms): radix / lane path
         e->stats.fused = 2;
         q.carry_nullable = carry_nullable0;
         return false;

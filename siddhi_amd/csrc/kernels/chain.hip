@@ -41,8 +41,9 @@ __device__ __forceinline__ int64_t vts(const ChainArgs& a, int64_t r) {
 }
 // row r of a bucket view belongs to key kf (the caller scans kf's bucket, so the local key decides)
 __device__ __forceinline__ bool bkey_is(const ChainArgs& a, int64_t r, uint32_t kf) {
-    return a.lkey ? a.lkey[r] == (uint8_t)(kf >> a.bbits) : a.key[r] == kf;
+    return a.lkey ? a.lkey[r] == (uint8_t)(kf >> a.bbits) : (!a.key || a.key[r] == kf);  // (no key: one-key batch)
 }
+__device__ __forceinline__ int64_t orig_of(const ChainArgs& a, int64_t r) { return a.orig ? (int64_t)a.orig[r] : r; }
 __device__ __forceinline__ int64_t ts_row(const ChainArgs& a, const View& v, int64_t r) {
     return in_view(v, r) ? cm_lds[v.ots + (r - v.lo)] : vts(a, r);
 }
@@ -892,7 +893,10 @@ static_assert(FU_ROWS < 65536, "chain_fused_k: u16 rows / run offsets");
 // SAME: the scanned column's kind is the comparison kind (no conversion in the scan loop). W: minimum waves per SIMD
 // the allocator must allow -- 8 = four 512-thread blocks per CU (LDS 4 x 40 KB fits); at 6 it used 104 SGPRs, which
 // admits 6 waves per SIMD = 3 blocks (MI355X_MICROARCH residency rule). 8 costs SGPR / VGPR spills.
-template <int K, bool SAME, int W>
+// ONEK: one-key batches (unpartitioned, C1): a.fu_own rows per segment, the staging's time-order check and the work
+// queue's group summaries. Compile-time, so the many-key build keeps its registers (C2's matcher 2.04 -> 2.26 ms with
+// them present but switched off at run time, r5t/r5u)
+template <int K, bool SAME, int W, bool ONEK = false>
 __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* __restrict__ pa) {
     using C = KT<K>;
     using T = typename C::T;
@@ -906,7 +910,8 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
     __shared__ uint8_t s_lk[FU_ROWS];
     __shared__ uint16_t s_res[FU_ROWS];  // per position: e2 position | R_NONE | R_CARRY | R_OVF
     __shared__ __align__(16) uint16_t wc[NW][256];  // regrouping counters; then the deque chunks' summaries
-    __shared__ uint16_t lstart[256], lend[256];
+    __shared__ __align__(8) uint16_t lstart[256];  // (reused by the work queue: 64 group extremes of 8 bytes)
+    __shared__ uint16_t lend[256];
     __shared__ uint32_t wcnt[3][FU_PT][NW];
     __shared__ unsigned long long bbase[3];
     __shared__ int sb[2];
@@ -925,8 +930,9 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
     FU_TRACE(1);
     if (b < 0) { FU_TRACE(99); return; }  // block-uniform: past the plan
     const int64_t be = a.bstart[b + 1];
-    const int64_t lo = (int64_t)a.bstart[b] + (int64_t)sb[1] * FU_OWN;
-    const int own = (int)min((int64_t)FU_OWN, be - lo);
+    const int fown = ONEK ? a.fu_own : FU_OWN;
+    const int64_t lo = (int64_t)a.bstart[b] + (int64_t)sb[1] * fown;
+    const int own = (int)min((int64_t)fown, be - lo);
     const int nr = (int)min((int64_t)FU_ROWS, be - lo);
     const bool to_end = lo + nr == be;  // the staged rows reach the bucket's (= batch's) end for every key
     const int col = sp.scan_col;
@@ -950,10 +956,21 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
             rkey[r] = (uint32_t)a.lkey[g] << a.bbits;
             rts[r] = tbase + ((int64_t)a.ts32[g] - (int64_t)a.ts32[lo]);
         } else {
-            rkey[r] = a.key[g];
+            rkey[r] = ONEK ? 0u : a.key[g];
             rts[r] = a.ts[g];
         }
         rx[r] = kind == VK_F64 || kind == VK_I64 ? ((const int64_t*)xcol)[g] : load_col(xcol, kind, g);
+    }
+    if (ONEK) {  // one-key batch: arrival order must be time order (the chain path's precondition)
+        bool bad = false;
+#pragma unroll
+        for (int r = 0; r < FU_PT; ++r) {
+            const int row = w * WROWS + r * 64 + lane;
+            int64_t prev = __shfl_up(rts[r], 1);
+            if (lane == 0) prev = lo + row > 0 ? a.ts[lo + row - 1] : INT64_MIN;
+            bad |= row < nr && rts[r] < prev;
+        }
+        if (__ballot(bad) && lane == 0) atomicOr(&a.flags[3], 1);
     }
     FU_TRACE(2);
     if (tlast - tbase > (int64_t)0xFFFFFFFF) {  // staged span does not fit the u32 offsets
@@ -1071,8 +1088,34 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
             if (c) cand[ncand + __popcll(bm & lt)] = (uint16_t)pos;
             ncand += __popcll(bm);
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        // group summaries (stack mode, ordering compares): per 32 consecutive positions the extreme value that could
+        // complete a partial (the max when "x beats y" grows with x, else the min; NaN rows never complete one).
+        // A scan skips a whole group whose extreme cannot beat its partial's e1 value: no row in it completes the
+        // partial, and an expiry inside it shows at the next row scanned (a key's rows are time-ordered). The groups
+        // may mix keys (an upper bound is still an upper bound); they pay for one-key batches (C1), where a high
+        // e1 price scans up to a whole window of rows
+        constexpr int WQ_G = 32;
+        static_assert(FU_ROWS / WQ_G * 8 <= sizeof(lstart), "group summaries fit lstart");
+        const bool wq_mono = ONEK && a.fu_mode == DQ_STACK && (m.gt != m.lt) && !m.ne && !(a.fu_skip & 128);
+        const bool use_max = left == m.gt;
+        T* const s_gx = reinterpret_cast<T*>(&lstart[0]);
+        if (ONEK && wq_mono) {  // (block-uniform; lstart is free after the regrouping)
+            T ext = use_max ? std::numeric_limits<T>::lowest() : std::numeric_limits<T>::max();
+#pragma unroll
+            for (int i = 0; i < FU_ROWS / FU_THREADS; ++i) {
+                const int pos = t * (FU_ROWS / FU_THREADS) + i;
+                const T x = SAME ? C::get(s_x[sw(pos)]) : C::get(cvt(s_x[sw(pos)], kind, (uint8_t)K));
+                if (pos < nr && x == x) ext = use_max ? (x > ext ? x : ext) : (x < ext ? x : ext);
+            }
+            constexpr int LPG = WQ_G / (FU_ROWS / FU_THREADS);  // lanes per group
+#pragma unroll
+            for (int o = 1; o < LPG; o <<= 1) {
+                const T e2 = __shfl_xor(ext, o);
+                ext = use_max ? (e2 > ext ? e2 : ext) : (e2 < ext ? e2 : ext);
+            }
+            if ((t & (LPG - 1)) == 0) s_gx[t / LPG] = ext;
+        }
+        if (ONEK) __syncthreads();
         int p = -1, q = 0, end = 0, head = 0;
         uint32_t t0 = 0;
         T y = kc;
@@ -1102,6 +1145,16 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
                     }
                 }
                 if (__ballot(p >= 0) == 0) break;
+            }
+            if (ONEK && p >= 0 && wq_mono) {  // the rest of q's group, when its extreme cannot beat the partial
+                const int ge = (q & ~(WQ_G - 1)) + WQ_G;
+                if (ge <= end) {
+                    const T g = s_gx[q / WQ_G];
+                    if (!(left ? cmp_m(m, g, y) : cmp_m(m, y, g))) {
+                        q = ge;
+                        continue;
+                    }
+                }
             }
             if (p >= 0) {
                 uint32_t tq[WQ_U];
@@ -1328,7 +1381,7 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
         const uint32_t run = __shfl(inc, 63);
         if (lane == 0) {
             unsigned long long* ctr = ci == 0 ? a.out_count : ci == 1 ? a.carry_count : a.ovf_count;
-            if (a.fu_skip & 32) bbase[ci] = ci == 0 ? (unsigned long long)v * FU_OWN : 0ull;  // phase timing only
+            if (a.fu_skip & 32) bbase[ci] = ci == 0 ? (unsigned long long)v * fown : 0ull;  // phase timing only
             else bbase[ci] = run ? atomicAdd(ctr, (unsigned long long)run) : 0ull;
         }
     }
@@ -1386,8 +1439,8 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
             for (int i = 0; i < FU_EH; ++i) {
                 const int k = h + i;
                 if (slot[k] != NOSLOT) {
-                    op[i] = a.orig[lo + prow[k]];
-                    oq[i] = a.orig[lo + qrow[k]];
+                    op[i] = ONEK ? (uint32_t)orig_of(a, lo + prow[k]) : a.orig[lo + prow[k]];
+                    oq[i] = ONEK ? (uint32_t)orig_of(a, lo + qrow[k]) : a.orig[lo + qrow[k]];
                     if (fast && n_out >= 1) v0[i] = c0p[lo + (in0.a == 0 ? prow[k] : qrow[k])];
                     if (fast && n_out >= 2) v1[i] = c1p[lo + (in1.a == 0 ? prow[k] : qrow[k])];
                 }
@@ -1442,7 +1495,7 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
             const int64_t cs = (int64_t)bbase[1] + wcnt[1][k][w] + __popcll(bc & lt);
             if (cs >= a.carry_cap) atomicOr(&a.flags[0], 1);
             else if (FU_OK(p < a.n, 7))
-                emit_carry(a, View{}, cs, p, ((uint32_t)s_lk[sw(pos)] << a.bbits) | (uint32_t)b, a.seq_base + (int64_t)a.orig[p]);
+                emit_carry(a, View{}, cs, p, ((uint32_t)s_lk[sw(pos)] << a.bbits) | (uint32_t)b, a.seq_base + (ONEK ? orig_of(a, p) : (int64_t)a.orig[p]));
         } else {
             const int64_t os = (int64_t)bbase[2] + wcnt[2][k][w] + __popcll(bo & lt);
             if (FU_OK(os < a.n, 8)) a.ovf_rows[os] = (uint32_t)p;  // os < the batch's rows (capacity n)
@@ -1471,14 +1524,14 @@ __global__ __launch_bounds__(256) void chain_fovf_k(const ChainArgs* __restrict_
                 if ((int64_t)a.bstart[mid] <= p) bl = mid;
                 else bh = mid;
             }
-            key = a.lkey ? (((uint32_t)a.lkey[p] << a.bbits) | (uint32_t)bl) : a.key[p];
+            key = a.lkey ? (((uint32_t)a.lkey[p] << a.bbits) | (uint32_t)bl) : (a.key ? a.key[p] : 0u);
             const int64_t end = a.bstart[bl + 1];
             const int64_t q = chain_scan<false>(a, acc, p + 1, end, vts(a, p), nullptr, 0, key);
             if (q >= 0) { has = true; qhit = q; }
             else if (q == -2) carry = true;
         }
         const int64_t slot = wave_reserve(has, a.out_count);
-        const int64_t seq = p >= 0 ? a.seq_base + (int64_t)a.orig[p] : 0;
+        const int64_t seq = p >= 0 ? a.seq_base + orig_of(a, p) : 0;
         if (has) {
             if (slot >= a.out_cap) atomicOr(&a.flags[0], 1);
             else emit_match<false>(a, acc, slot, qhit, key, seq, nullptr, 0);
@@ -2094,8 +2147,8 @@ void chain_carry(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) {
 #ifndef SDG_FU_W8_DEFAULT
 #define SDG_FU_W8_DEFAULT 1  // r3v: fused 2.52 ms at 8 vs 2.68 ms at 6 waves per SIMD (C2, same box)
 #endif
-int64_t chain_fused_grid(int64_t n, int nb) {
-    return xcd_round((n + FU_OWN - 1) / FU_OWN + nb);
+int64_t chain_fused_grid(int64_t n, int nb, int own) {
+    return xcd_round((n + own - 1) / own + nb);
 }
 
 void chain_fused(const ChainArgs& a, const ChainArgs* d_a, int64_t grid, hipStream_t stream) {
@@ -2106,7 +2159,9 @@ void chain_fused(const ChainArgs& a, const ChainArgs* d_a, int64_t grid, hipStre
     const bool w8 = wv ? atoi(wv) == 8 : SDG_FU_W8_DEFAULT;
 #define FU_LAUNCH(KK)                                                                                    \
     do {                                                                                                 \
-        if (same && w8) hipLaunchKernelGGL((chain_fused_k<KK, true, 8>), g, b, 0, stream, d_a);          \
+        if (a.fu_check_ts && same) hipLaunchKernelGGL((chain_fused_k<KK, true, 8, true>), g, b, 0, stream, d_a); \
+        else if (a.fu_check_ts) hipLaunchKernelGGL((chain_fused_k<KK, false, 8, true>), g, b, 0, stream, d_a); \
+        else if (same && w8) hipLaunchKernelGGL((chain_fused_k<KK, true, 8>), g, b, 0, stream, d_a);     \
         else if (same) hipLaunchKernelGGL((chain_fused_k<KK, true, 6>), g, b, 0, stream, d_a);          \
         else if (w8) hipLaunchKernelGGL((chain_fused_k<KK, false, 8>), g, b, 0, stream, d_a);           \
         else hipLaunchKernelGGL((chain_fused_k<KK, false, 6>), g, b, 0, stream, d_a);                   \

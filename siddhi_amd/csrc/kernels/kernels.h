@@ -206,6 +206,10 @@ struct ChainArgs {
     int32_t fu_mode;                  // chain_fused_k: DQ_STACK / DQ_ALL -> chunked deque pass, DQ_OFF -> forward scans
     int32_t fu_skip;                  // SDG_FU_SKIP (phase timing only, results invalid): 1 scan, 2 emit, 4 stop
                                       // after the loads, 8 stop after the LDS regrouping
+    int32_t fu_own;                   // chain_fused_k: own (candidate) rows per segment (FU_OWN; one-key batches
+                                      // FU_ROWS / 2: a larger halo, as their window spans more rows)
+    int32_t fu_check_ts;              // chain_fused_k: check that the staged rows' ts never decrease (one-key
+                                      // batches, which no bucket pass checked); flags[3] -> the lane kernels
     int32_t fold;                     // chain_sorted_k: the carried partials are rows of the sorted view (orig =
                                       // 0x80000000 | carry index; keygroup's prefix rows), no chain_carry pass
 };
@@ -249,7 +253,7 @@ constexpr int FU_DQ = SDG_FU_DQ;
 constexpr int FU_HALO = 512;  // ~1.3 s of a bucket at C2 (> T)
 constexpr int FU_OWN = FU_ROWS - FU_HALO;            // candidate rows per block
 // grid size for n rows in nb buckets (a multiple of g_xcds: the XCD remap needs it)
-int64_t chain_fused_grid(int64_t n, int nb);
+int64_t chain_fused_grid(int64_t n, int nb, int own = FU_OWN);
 void chain_fused(const ChainArgs& a, const ChainArgs* d_a, int64_t grid, hipStream_t stream);
 // the rows chain_fused_k handed over (ovf_rows / ovf_count): key-filtered bucket scans in HBM, emitted directly
 void chain_fovf(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);

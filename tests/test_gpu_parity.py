@@ -77,11 +77,12 @@ def product_c_rows(app, cols, symbols=None, batches=1, fused=True, expect_fused=
         rt.shutdown()
 
 
+@pytest.mark.parametrize("fused", [True, False])  # the one-key fused matcher (round 5) / the lane deque kernels
 @pytest.mark.parametrize("adversarial", [False, True])
-def test_c1_matches_oracle(adversarial, oracle_built):
+def test_c1_matches_oracle(adversarial, fused, oracle_built):
     cols = w.c1_columns(20_000, adversarial=adversarial)
     ref = oracle_c_rows(w.C1_APP, cols)
-    got = product_c_rows(w.C1_APP, cols)
+    got = product_c_rows(w.C1_APP, cols, batches=3, fused=fused, expect_fused=1 if fused else 0)
     assert len(ref) > 100
     assert got == ref
 
