@@ -275,6 +275,7 @@ struct QueryRt {
     DevBuf so_lkey;                                 // fused path: u8 local keys of the bucket view
     DevBuf sv_tsbase;                               // sorted view: base of its u32 ts offsets (ts_window_base)
     DevBuf bk_plan;                                 // fused path: bstart[257] + bseg[257]
+    DevBuf bk_tm;                                   // fused path: time-major block plan (ChainArgs::tm)
     // carries (double buffered)
     struct Carry {
         DevBuf key, ts, seq, vals, nulls;
@@ -1749,6 +1750,28 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     int bbits = 0;
     uint32_t* b_start = nullptr;
     uint32_t* b_seg = nullptr;
+    uint32_t* b_tm = nullptr;
+    // fused path: columns read only to emit stay in arrival order (the bucket pass does not move them; ChainArgs::
+    // ocols). Not with view positions (orig is then not an arrival row) or nulls; SDG_FU_MOVE_ALL: A/B
+    uint32_t eo_mask = 0;
+    static const bool move_all = getenv("SDG_FU_MOVE_ALL") != nullptr;
+    if (fused && partitioned && !d_vpos && !move_all && !getenv("SDG_FU_WIDE")) {
+        ChainArgs ta;
+        std::memset(&ta, 0, sizeof ta);
+        for (int k = 0; k < nc; ++k) ta.nulls[k] = d_nulls[k];
+        chain_staging(h, ta, q.carry_nullable);
+        auto filt = [&](int k) {
+            for (int i = 0; i < std::min(P.n_states, 2); ++i) {
+                const FastPred& f = P.fast[i];
+                if ((f.kind == FP_CONST || f.kind == FP_SLOT) && f.ca == k) return true;
+                if (f.kind == FP_SLOT && f.cb == k) return true;
+            }
+            return false;
+        };
+        for (int k = 0; k < nc && k < 32 && chain_fused_ocols_ok(ta); ++k)
+            if (!d_nulls[k] && !filt(k) && k != ta.sp.scan_col && !(ta.sp.scan_mode == SCAN_E1 && k == ta.sp.e1_col))
+                eo_mask |= 1u << k;
+    }
     if (partitioned && nrows > 0) {
         KeyGroupArgs a;
         std::memset(&a, 0, sizeof a);
@@ -1770,6 +1793,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         if (d_qs) { a.src[c] = d_qs; a.dst[c] = q.so_qs.ensure(nrows); a.width[c] = 1; v_qs = (const uint8_t*)a.dst[c]; ++c; }
         if (d_vrank) { a.src[c] = d_vrank; a.dst[c] = q.so_vrank.ensure(nrows * 4); a.width[c] = 4; v_vrank = (const uint32_t*)a.dst[c]; ++c; }
         for (int k = 0; k < nc; ++k) {
+            if ((eo_mask >> k) & 1u) continue;  // stays in arrival order (v_cols[k] = d_cols[k])
             if (c >= MAX_COLS + 2) throw CompileError(SDG_ERR_UNSUPPORTED, "too many columns");
             int w = width_of(P.col_kind[k]);
             a.src[c] = d_cols[k]; a.dst[c] = q.so_cols[k].ensure(nv * w); a.width[c] = (uint8_t)w;
@@ -1820,7 +1844,12 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 a.ts_base = d_ts;
                 a.lkey_out = (uint8_t*)q.so_lkey.ensure(nrows);
             }
-            bucketize(a, bbits, 0 /* ts is payload column 0 */, flags + 3, b_start, b_seg, FU_OWN, st, g_no_events ? nullptr : &e->ev[4]);
+            // time-major block order (SDG_FU_BMAJOR: bucket-major, A/B)
+            static const bool bmajor = getenv("SDG_FU_BMAJOR") != nullptr;
+            const int64_t tm_cap = chain_fused_grid(nrows, 1 << bbits) + 2;
+            if (!bmajor && eo_mask) b_tm = (uint32_t*)q.bk_tm.ensure((size_t)tm_cap * 4);
+            bucketize(a, bbits, 0 /* ts is payload column 0 */, flags + 3, b_start, b_seg, FU_OWN, st,
+                      g_no_events ? nullptr : &e->ev[4], b_tm, b_tm ? tm_cap : 0);
             if (!wide) {
                 v_ts32 = (const uint32_t*)a.dst[0];
                 v_lkey = a.lkey_out;
@@ -2489,6 +2518,12 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     a.K = (int32_t)K;
     a.orig = v_orig;
     for (int k = 0; k < nc; ++k) { a.cols[k] = v_cols[k]; a.nulls[k] = v_nulls[k]; }
+    if (fused) {
+        a.ocol_mask = eo_mask;
+        for (int k = 0; k < nc; ++k)
+            if ((eo_mask >> k) & 1u) a.ocols[k] = d_cols[k];
+        a.tm = b_tm;
+    }
     a.seq_base = e->seq + (d_vpos ? 0 : pos_off);  // emission seq = seq_base + orig (view row or position)
     a.s0 = h.stream_pos(P.st[0].stream);
     a.s1 = P.n_states > 1 ? h.stream_pos(P.st[1].stream) : a.s0;

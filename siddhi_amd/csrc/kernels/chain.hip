@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <limits>
+#include <stdexcept>
 
 #include "../engine/eval.h"
 #include "kernels.h"
@@ -44,6 +45,11 @@ __device__ __forceinline__ bool bkey_is(const ChainArgs& a, int64_t r, uint32_t 
     return a.lkey ? a.lkey[r] == (uint8_t)(kf >> a.bbits) : (!a.key || a.key[r] == kf);  // (no key: one-key batch)
 }
 __device__ __forceinline__ int64_t orig_of(const ChainArgs& a, int64_t r) { return a.orig ? (int64_t)a.orig[r] : r; }
+// column `col` of view row r: emission-only columns of the fused path stay in arrival order (ChainArgs::ocols)
+__device__ __forceinline__ int64_t col_at(const ChainArgs& a, int col, uint8_t kind, int64_t r) {
+    if ((a.ocol_mask >> col) & 1u) return load_col(a.ocols[col], kind, orig_of(a, r));
+    return load_col(a.cols[col], kind, r);
+}
 __device__ __forceinline__ int64_t ts_row(const ChainArgs& a, const View& v, int64_t r) {
     return in_view(v, r) ? cm_lds[v.ots + (r - v.lo)] : vts(a, r);
 }
@@ -54,7 +60,7 @@ __device__ __forceinline__ int qs_row(const ChainArgs& a, const View& v, int64_t
 __device__ __forceinline__ int64_t col_row(const ChainArgs& a, const View& v, int col, uint8_t kind, int64_t r) {
     const int s = a.stage_of[col];
     if (s >= 0 && in_view(v, r)) return cm_lds[(s == 0 ? v.oc0 : v.oc1) + (r - v.lo)];
-    return load_col(a.cols[col], kind, r);
+    return col_at(a, col, kind, r);
 }
 __device__ __forceinline__ bool null_row(const ChainArgs& a, int col, int64_t r) {
     return a.nulls[col] ? a.nulls[col][r] != 0 : false;
@@ -284,7 +290,7 @@ __device__ __forceinline__ void emit_carry(const ChainArgs& a, const View& v, in
     a.carry_seq[cs] = seq;
     uint32_t nm = 0;
     for (int c = 0; c < a.sp.n_cols; ++c) {
-        a.carry_vals[(int64_t)c * a.carry_cap + cs] = load_col(a.cols[c], a.sp.col_kind[c], p);
+        a.carry_vals[(int64_t)c * a.carry_cap + cs] = col_at(a, c, a.sp.col_kind[c], p);
         if (null_row(a, c, p)) nm |= 1u << c;
     }
     a.carry_nulls[cs] = nm;
@@ -896,7 +902,9 @@ static_assert(FU_ROWS < 65536, "chain_fused_k: u16 rows / run offsets");
 // ONEK: one-key batches (unpartitioned, C1): a.fu_own rows per segment, the staging's time-order check and the work
 // queue's group summaries. Compile-time, so the many-key build keeps its registers (C2's matcher 2.04 -> 2.26 ms with
 // them present but switched off at run time, r5t/r5u)
-template <int K, bool SAME, int W, bool ONEK = false>
+// OC: some output columns stay in arrival order (ChainArgs::ocols): time-major block order, and the emission reads
+// them through orig (a separate instantiation: the selects cost the others 0.17 ms on C2, r5w)
+template <int K, bool SAME, int W, bool ONEK = false, bool OC = false>
 __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* __restrict__ pa) {
     using C = KT<K>;
     using T = typename C::T;
@@ -920,8 +928,39 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
     // neighbouring segments (which share halo rows) hit one L2
     const uint32_t v = xcd_block(blockIdx.x, gridDim.x, (uint32_t)a.xcds);
     if (t == 0) sb[0] = -1;
-    __syncthreads();
-    if (t < a.nb && a.bseg[t] <= v && v < a.bseg[t + 1]) {
+    const uint32_t tS = (OC && a.tm) ? a.tm[0] : 0u;
+    const uint32_t tmin = OC && tS ? a.tm[1] : 0u;
+    if (OC && tS && v < tmin * (uint32_t)a.nb) {  // time-major, the levels every bucket has: closed form
+        if (t == 0) {
+            sb[0] = (int)(v % (uint32_t)a.nb);
+            sb[1] = (int)(v / (uint32_t)a.nb);
+        }
+    } else if (OC && tS) {  // time-major (bucketize's plan): segment s of every bucket before segment s + 1 of any, so
+                            // the blocks in flight cover one time band (the arrival-order columns stay in cache)
+        __shared__ uint32_t s_sr[2], s_wc[FU_THREADS / 64];
+        if (t == 0) {
+            uint32_t lo_s = tmin, hi_s = tS;  // largest s in [tmin, S] with tm[2 + s] <= v
+            while (lo_s < hi_s) {
+                const uint32_t mid = (lo_s + hi_s + 1) >> 1;
+                if (a.tm[2 + mid] <= v) lo_s = mid;
+                else hi_s = mid - 1;
+            }
+            s_sr[0] = lo_s;
+            s_sr[1] = v - a.tm[2 + lo_s];
+        }
+        __syncthreads();
+        const uint32_t ss = s_sr[0], rr = s_sr[1];
+        const bool has = ss < tS && t < a.nb && a.bseg[t + 1] - a.bseg[t] > ss;
+        const uint64_t bal = __ballot(has);
+        if (lane == 0) s_wc[w] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t before = (uint32_t)__popcll(bal & lanemask_lt());
+        for (int x = 0; x < w; ++x) before += s_wc[x];
+        if (has && before == rr) {
+            sb[0] = t;
+            sb[1] = (int)ss;
+        }
+    } else if (t < a.nb && a.bseg[t] <= v && v < a.bseg[t + 1]) {
         sb[0] = t;
         sb[1] = (int)(v - a.bseg[t]);
     }
@@ -1426,6 +1465,9 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
     {
         const int64_t* c0p = n_out >= 1 ? (const int64_t*)a.cols[in0.b] : nullptr;
         const int64_t* c1p = n_out >= 2 ? (const int64_t*)a.cols[in1.b] : nullptr;
+        // emission-only columns in arrival order: read at the rows' original positions (op / oq)
+        const int64_t* o0 = OC && n_out >= 1 && ((a.ocol_mask >> in0.b) & 1u) ? (const int64_t*)a.ocols[in0.b] : nullptr;
+        const int64_t* o1 = OC && n_out >= 2 && ((a.ocol_mask >> in1.b) & 1u) ? (const int64_t*)a.ocols[in1.b] : nullptr;
         int64_t* const ov0 = a.out_vals;
         int64_t* const ov1 = a.out_vals + a.out_cap;
         // FU_EH rounds at a time: their loads, then their stores. All FU_PT rounds at once needs 24 more VGPRs than
@@ -1441,8 +1483,8 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
                 if (slot[k] != NOSLOT) {
                     op[i] = ONEK ? (uint32_t)orig_of(a, lo + prow[k]) : a.orig[lo + prow[k]];
                     oq[i] = ONEK ? (uint32_t)orig_of(a, lo + qrow[k]) : a.orig[lo + qrow[k]];
-                    if (fast && n_out >= 1) v0[i] = c0p[lo + (in0.a == 0 ? prow[k] : qrow[k])];
-                    if (fast && n_out >= 2) v1[i] = c1p[lo + (in1.a == 0 ? prow[k] : qrow[k])];
+                    if (fast && n_out >= 1) v0[i] = OC && o0 ? o0[in0.a == 0 ? op[i] : oq[i]] : c0p[lo + (in0.a == 0 ? prow[k] : qrow[k])];
+                    if (fast && n_out >= 2) v1[i] = OC && o1 ? o1[in1.a == 0 ? op[i] : oq[i]] : c1p[lo + (in1.a == 0 ? prow[k] : qrow[k])];
                 }
             }
 #pragma unroll
@@ -1464,12 +1506,13 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
     for (int j = jfrom; j < n_out; ++j) {
         const Instr in = load_instr(&sp.out_ins[j]);  // a plain attribute (the fused path has no select bytecode)
         const bool ok = (in.c == 0 || in.c == -1) && in.a < 2;
-        const void* cp = a.cols[in.b];
         const uint8_t* np = a.nulls[in.b];
         int64_t* const ov = a.out_vals + (int64_t)j * a.out_cap;
 #pragma unroll
         for (int k = 0; k < FU_PT; ++k)
-            if (slot[k] != NOSLOT) ov[slot[k]] = ok ? load_col(cp, in.k, lo + (in.a == 0 ? prow[k] : qrow[k])) : 0;
+            if (slot[k] != NOSLOT)
+                ov[slot[k]] = !ok ? 0 : OC ? col_at(a, in.b, in.k, lo + (in.a == 0 ? prow[k] : qrow[k]))
+                                           : load_col(a.cols[in.b], in.k, lo + (in.a == 0 ? prow[k] : qrow[k]));
         if (!ok || np) {
 #pragma unroll
             for (int k = 0; k < FU_PT; ++k)
@@ -2151,15 +2194,23 @@ int64_t chain_fused_grid(int64_t n, int nb, int own) {
     return xcd_round((n + own - 1) / own + nb);
 }
 
+bool chain_fused_ocols_ok(const ChainArgs& a) {  // the OC instantiation: the scan's own kind, 8 waves per SIMD
+    static const char* wv = getenv("SDG_FU_WPS");
+    const bool w8 = wv ? atoi(wv) == 8 : SDG_FU_W8_DEFAULT;
+    return a.sp.scan_col_kind == a.sp.scan_t && w8 && !a.fu_check_ts;
+}
+
 void chain_fused(const ChainArgs& a, const ChainArgs* d_a, int64_t grid, hipStream_t stream) {
     if (a.n <= 0) return;
+    if (a.ocol_mask && !chain_fused_ocols_ok(a)) throw std::runtime_error("chain_fused: arrival-order columns need the OC build");
     const dim3 g((unsigned)grid), b(FU_THREADS);
     const bool same = a.sp.scan_col_kind == a.sp.scan_t;
     static const char* wv = getenv("SDG_FU_WPS");  // A/B: 8 (four blocks per CU) or 6
     const bool w8 = wv ? atoi(wv) == 8 : SDG_FU_W8_DEFAULT;
 #define FU_LAUNCH(KK)                                                                                    \
     do {                                                                                                 \
-        if (a.fu_check_ts && same) hipLaunchKernelGGL((chain_fused_k<KK, true, 8, true>), g, b, 0, stream, d_a); \
+        if (a.ocol_mask) hipLaunchKernelGGL((chain_fused_k<KK, true, 8, false, true>), g, b, 0, stream, d_a); \
+        else if (a.fu_check_ts && same) hipLaunchKernelGGL((chain_fused_k<KK, true, 8, true>), g, b, 0, stream, d_a); \
         else if (a.fu_check_ts) hipLaunchKernelGGL((chain_fused_k<KK, false, 8, true>), g, b, 0, stream, d_a); \
         else if (same && w8) hipLaunchKernelGGL((chain_fused_k<KK, true, 8>), g, b, 0, stream, d_a);     \
         else if (same) hipLaunchKernelGGL((chain_fused_k<KK, true, 6>), g, b, 0, stream, d_a);          \

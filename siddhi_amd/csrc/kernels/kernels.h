@@ -78,8 +78,9 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks = nul
 // the precondition of the fused matcher's per-bucket time order). Outputs bstart[nb + 1] (bucket row ranges)
 // and bseg[nb + 1] (exclusive prefix over buckets of ceil(len / seg_rows): the matcher's block plan).
 // marks (optional, 4 events) as keygroup().
+// tm (optional, tm_cap >= the fused grid + 2 entries): the time-major block plan (ChainArgs::tm)
 void bucketize(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, uint32_t* bstart, uint32_t* bseg,
-               int seg_rows, hipStream_t stream, hipEvent_t* marks = nullptr);
+               int seg_rows, hipStream_t stream, hipEvent_t* marks = nullptr, uint32_t* tm = nullptr, int64_t tm_cap = 0);
 
 // ---- chain matcher: `every e1=S0[c0] -> e2=S1[c1] within T` (independent partials) ---------------------
 // One block per tile of CM_THREADS * CM_EPT sorted events; the block reserves its output range with one atomic.
@@ -212,6 +213,14 @@ struct ChainArgs {
                                       // batches, which no bucket pass checked); flags[3] -> the lane kernels
     int32_t fold;                     // chain_sorted_k: the carried partials are rows of the sorted view (orig =
                                       // 0x80000000 | carry index; keygroup's prefix rows), no chain_carry pass
+    // fused bucket path: columns the matcher reads only to emit (no filter reads them, no nulls) stay in arrival
+    // order -- the bucket pass does not move them; a view row r reads ocols[c][orig[r]] (col_at)
+    uint32_t ocol_mask;
+    const void* ocols[MAX_COLS];
+    // fused bucket path with ocols: time-major block plan (bucketize): tm[0] = S, the most segments of a bucket (0:
+    // bucket-major order), tm[1] = the fewest, tm[2 + s] = blocks of segment index < s over all buckets; block v runs
+    // segment s of the r-th bucket that has more than s segments (v < tm[1] * nb: bucket v % nb, segment v / nb)
+    const uint32_t* tm;
 };
 enum DequeMode : int32_t { DQ_OFF = 0, DQ_STACK = 1, DQ_ALL = 2 };
 constexpr uint32_t MQ_NONE = 0xFFFFFFFFu, MQ_CARRY = 0xFFFFFFFEu, MQ_OVF = 0xFFFFFFFDu;
@@ -255,6 +264,8 @@ constexpr int FU_OWN = FU_ROWS - FU_HALO;            // candidate rows per block
 // grid size for n rows in nb buckets (a multiple of g_xcds: the XCD remap needs it)
 int64_t chain_fused_grid(int64_t n, int nb, int own = FU_OWN);
 void chain_fused(const ChainArgs& a, const ChainArgs* d_a, int64_t grid, hipStream_t stream);
+// whether chain_fused has the arrival-order-column build for this scan (ChainArgs::ocols; sp and fu_check_ts set)
+bool chain_fused_ocols_ok(const ChainArgs& a);
 // the rows chain_fused_k handed over (ovf_rows / ovf_count): key-filtered bucket scans in HBM, emitted directly
 void chain_fovf(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
 

@@ -823,9 +823,12 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
 
 namespace {
 // bucket row ranges and the fused matcher's block plan (one block, nb <= 256)
+// tm: the time-major order (kernels.h ChainArgs::tm), when the buckets are balanced enough that enumerating
+// (segment index, bucket) costs little (S * nb <= 2 * segments + 256) and it fits tm_cap
 __global__ __launch_bounds__(256) void bk_plan(const uint32_t* __restrict__ tot, int64_t n, int nb, int seg_rows,
-                                               uint32_t* __restrict__ bstart, uint32_t* __restrict__ bseg) {
-    __shared__ uint32_t part[256];
+                                               uint32_t* __restrict__ bstart, uint32_t* __restrict__ bseg,
+                                               uint32_t* __restrict__ tm, int64_t tm_cap) {
+    __shared__ uint32_t part[256], sg[256], smax, smin;
     const int d = threadIdx.x;
     uint32_t s0 = 0, len = 0;
     if (d < nb) {
@@ -848,11 +851,33 @@ __global__ __launch_bounds__(256) void bk_plan(const uint32_t* __restrict__ tot,
         bstart[nb] = (uint32_t)n;
         bseg[nb] = part[255];
     }
+    if (!tm) return;
+    sg[d] = segs;
+    if (d == 0) {
+        smax = 0;
+        smin = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    atomicMax(&smax, segs);
+    if (d < nb) atomicMin(&smin, segs);
+    __syncthreads();
+    const uint32_t S = smax, total = part[255];
+    const bool on = S > 0 && (uint64_t)S * (uint64_t)nb <= 2ull * total + 256 && (int64_t)S + 3 <= tm_cap;
+    if (d == 0) {
+        tm[0] = on ? S : 0u;
+        tm[1] = smin;
+    }
+    if (!on) return;
+    for (uint32_t s = d; s <= S; s += 256) {
+        uint32_t acc = 0;
+        for (int b = 0; b < nb; ++b) acc += min(sg[b], s);
+        tm[2 + s] = acc;
+    }
 }
 }  // namespace
 
 void bucketize(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, uint32_t* bstart, uint32_t* bseg,
-               int seg_rows, hipStream_t stream, hipEvent_t* marks) {
+               int seg_rows, hipStream_t stream, hipEvent_t* marks, uint32_t* tm, int64_t tm_cap) {
     const int nb = 1 << bits;
     const uint32_t mask = (uint32_t)nb - 1;
     g_tile_override = rx_tile_bucket();
@@ -893,7 +918,7 @@ void bucketize(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, uint
     launch_rx_scatter(nt, stream, rp);
     g_tile_override = 0;
     if (marks) (void)hipEventRecord(marks[2], stream);
-    hipLaunchKernelGGL(bk_plan, dim3(1), dim3(256), 0, stream, a.tot, a.n, nb, seg_rows, bstart, bseg);
+    hipLaunchKernelGGL(bk_plan, dim3(1), dim3(256), 0, stream, a.tot, a.n, nb, seg_rows, bstart, bseg, tm, tm_cap);
     if (marks) (void)hipEventRecord(marks[3], stream);
 }
 
