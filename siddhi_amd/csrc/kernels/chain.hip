@@ -928,6 +928,7 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
     // neighbouring segments (which share halo rows) hit one L2
     const uint32_t v = xcd_block(blockIdx.x, gridDim.x, (uint32_t)a.xcds);
     if (t == 0) sb[0] = -1;
+    __syncthreads();
     const uint32_t tS = (OC && a.tm) ? a.tm[0] : 0u;
     const uint32_t tmin = OC && tS ? a.tm[1] : 0u;
     if (OC && tS && v < tmin * (uint32_t)a.nb) {  // time-major, the levels every bucket has: closed form
@@ -1154,7 +1155,12 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
             }
             if ((t & (LPG - 1)) == 0) s_gx[t / LPG] = ext;
         }
-        if (ONEK) __syncthreads();
+        if (ONEK) {
+            __syncthreads();
+        } else {  // the candidate list (written by other lanes of this wave) before the queue reads it
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        }
         int p = -1, q = 0, end = 0, head = 0;
         uint32_t t0 = 0;
         T y = kc;

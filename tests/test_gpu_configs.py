@@ -53,9 +53,13 @@ def test_c1_full_config(adversarial):
     check("c1_adv" if adversarial else "c1", ts, vals, nulls, 2)
 
 
-def test_c2_full_step():
-    """C2's bench step: 10^8 device-resident events over 10^4 string keys in one flush on the fused matcher"""
+@pytest.mark.parametrize("ocols", [False, True])
+def test_c2_full_step(ocols, monkeypatch):
+    """C2's bench step: 10^8 device-resident events over 10^4 string keys in one flush on the fused matcher (and with
+    SDG_FU_OCOLS=1: the id column read in arrival order through orig)"""
     import torch
+    if ocols:
+        monkeypatch.setenv("SDG_FU_OCOLS", "1")
     n, keys = 100_000_000, 10_000
     cols = w.c2_columns(n, keys=keys)
     syms = w.symbols(keys)

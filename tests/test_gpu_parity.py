@@ -184,6 +184,28 @@ def test_c2_fused_key_counts(keys, deque, oracle_built, monkeypatch):
     assert got == ref
 
 
+@pytest.mark.parametrize("case", ["k1", "k37", "k700", "k20000", "ovf"])
+def test_c2_fused_arrival_order_columns(case, oracle_built, monkeypatch):
+    """SDG_FU_OCOLS=1: the output-only id column stays in arrival order (the bucket pass does not move it), the
+    emission, the carries (3 batches) and the HBM overflow scans read it through orig; time-major block order"""
+    monkeypatch.setenv("SDG_FU_OCOLS", "1")
+    app = w.C2_APP
+    if case == "ovf":
+        app = w.C2_APP.replace("within 1 sec", "within 100 sec")
+        cols = w.c2_columns(30_000, keys=2, per_ms=1)
+        cols["price"] = np.ascontiguousarray(np.round(np.linspace(30.0, 20.5, len(cols["ts"])) +
+                                                      (np.arange(len(cols["ts"])) % 4001 == 4000) * 5.0, 2))
+        keys = 2
+    else:
+        keys = int(case[1:])
+        cols = w.c2_columns(40_000, keys=keys, per_ms=3)
+    syms = w.symbols(keys)
+    ref = oracle_c_rows(app, cols, syms)
+    got = product_c_rows(app, cols, syms, batches=3, expect_fused=1)
+    assert len(ref) > 100
+    assert got == ref
+
+
 def test_c2_fused_overflow_scans(oracle_built):
     """a long window with few keys: partials outlive the staged halo and finish in the key-filtered HBM scan"""
     app = w.C2_APP.replace("within 1 sec", "within 100 sec")
