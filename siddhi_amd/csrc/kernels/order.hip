@@ -208,6 +208,65 @@ __global__ __launch_bounds__(256) void order_runs_gather_k(const uint32_t* __res
     if (seq_dst) seq_dst[f] = emit_base + (int64_t)e;
 }
 
+// order_runs_gather_k with the run bounds from wave ballots (a record's neighbours by shuffles; only a run that
+// crosses the wave's edge scans HBM) and the column gathers issued right after the index load, so they overlap the
+// run / rank work: two dependent memory waits per record instead of five or more
+__global__ __launch_bounds__(256) void order_runs_gather_w_k(const uint32_t* __restrict__ ek, const uint32_t* __restrict__ ix,
+                                                             const int64_t* __restrict__ sub, int64_t n, ColSet cs,
+                                                             int ncol, int64_t* __restrict__ seq_dst, int64_t emit_base,
+                                                             int* __restrict__ long_run, uint32_t xcds) {
+    const uint32_t vb = xcd_block(blockIdx.x, gridDim.x, xcds);
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)vb * 256 + threadIdx.x;
+    const int64_t i0 = i - lane;  // the wave's first record
+    const bool in = i < n;
+    const uint32_t e = in ? ek[i] : 0xFFFFFFFFu;  // (positions < 2^32 - 1: the sentinel never equals a key)
+    const uint32_t me = in ? ix[i] : 0u;
+    uint32_t edge = 0xFFFFFFFEu;
+    if (lane == 0 && in && i > 0) edge = ek[i - 1];
+    if (lane == 63 && i + 1 < n) edge = ek[i + 1];
+    int64_t x[GATHER_MAX_COLS];
+#pragma unroll
+    for (int c = 0; c < GATHER_MAX_COLS; ++c)
+        if (c < ncol && in) x[c] = cs.src[c][me];
+    uint32_t prev = __shfl_up(e, 1), next = __shfl_down(e, 1);
+    if (lane == 0) prev = edge;
+    if (lane == 63) next = edge;
+    const uint64_t H = __ballot(in && e != prev), T = __ballot(in && e != next);
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);  // lanes 0..lane
+    const uint64_t hm = H & upto, tm = T & ~(upto >> 1);              // heads at or below / tails at or above
+    int64_t s = hm ? i0 + (63 - __clzll(hm)) : -1;
+    int64_t t = tm ? i0 + (__ffsll((unsigned long long)tm) - 1) + 1 : -1;
+    if (in && s < 0) {  // the run began in an earlier wave
+        s = i0;
+        while (s > 0 && i - s <= RUN_MAX && ek[s - 1] == e) --s;
+    }
+    if (in && t < 0) {  // it continues past this wave
+        t = i0 + 64;
+        while (t < n && t - s <= RUN_MAX && ek[t] == e) ++t;
+    }
+    const bool lng = in && t - s > RUN_MAX;
+    if (lng) atomicOr(long_run, 1);
+    const bool multi = in && !lng && t - s > 1;
+    const int64_t my = multi ? sub[me] : 0;
+    int64_t rank = 0;
+    int span = multi ? (int)(t - s) : 0;
+    for (int o = 32; o > 0; o >>= 1) span = max(span, __shfl_xor(span, o));
+    for (int d = 1; d < span; ++d) {
+        const int64_t fw = __shfl(my, min(lane + d, 63));
+        const int64_t bw = __shfl(my, max(lane - d, 0));
+        if (!multi) continue;
+        if (i + d < t) rank += (lane + d < 64 ? fw : sub[ix[i + d]]) < my;
+        if (i - d >= s) rank += (lane - d >= 0 ? bw : sub[ix[i - d]]) <= my;
+    }
+    if (!in || lng) return;
+    const int64_t f = multi ? s + rank : i;
+#pragma unroll
+    for (int c = 0; c < GATHER_MAX_COLS; ++c)
+        if (c < ncol) cs.dst[c][f] = x[c];
+    if (seq_dst) seq_dst[f] = emit_base + (int64_t)e;
+}
+
 // every column of a record through one index read: dst[c][i] = src[c][perm[i]]. Blocks are mapped XCD-contiguous
 // (kernels.h xcd_block): consecutive output records come from a few hundred emission streams (the matcher's blocks),
 // each read forward, so one XCD's slice of the output keeps those streams' lines in its own L2
@@ -369,8 +428,13 @@ bool order_export(const int64_t* emit, const int64_t* sub, int64_t n, int64_t em
         cs.dst[c] = dst[c];
     }
     const unsigned g8 = (unsigned)xcd_round(grid);
-    hipLaunchKernelGGL(order_runs_gather_k, dim3(g8), dim3(256), 0, stream, ek1, ix1, sub, n, cs, ncol, seq_dst,
-                       emit_base, flag, (uint32_t)g_xcds);
+    static const bool scan_runs = getenv("SDG_ORDER_SCAN_RUNS") != nullptr;  // A/B: per-thread HBM run scans
+    if (scan_runs)
+        hipLaunchKernelGGL(order_runs_gather_k, dim3(g8), dim3(256), 0, stream, ek1, ix1, sub, n, cs, ncol, seq_dst,
+                           emit_base, flag, (uint32_t)g_xcds);
+    else
+        hipLaunchKernelGGL(order_runs_gather_w_k, dim3(g8), dim3(256), 0, stream, ek1, ix1, sub, n, cs, ncol, seq_dst,
+                           emit_base, flag, (uint32_t)g_xcds);
     int hf = 0;
     (void)hipMemcpyAsync(&hf, flag, 4, hipMemcpyDeviceToHost, stream);
     (void)hipStreamSynchronize(stream);
