@@ -227,8 +227,8 @@ struct QueryRt {
     uint64_t kt_cap = 0;
     size_t kt_synced = 0;                           // keydict ids [0, kt_synced) are in the table
     HostPin kt_ret;
-    std::unordered_map<std::string, uint32_t> keydict;
-    std::vector<std::string> keystr;                // keydict id -> key text (numeric keys)
+    std::unordered_map<std::string, uint32_t> keydict;  // (not kept for KC_INT queries: intkeys maps their values)
+    std::vector<std::string> keystr;                // key id -> key text (numeric keys)
     // a stream of the query without a partition key (key_attr -3): its events go to every key the partition has
     // initialised, in getPartitionKeys() order (keyorder.h); host batch assembly only
     bool broadcast = false;
@@ -408,6 +408,16 @@ void upload_plan(sdg_engine* e, QueryRt& q) {
     HIPCHECK(hipStreamSynchronize(e->stream));
 }
 
+// a new key of an int / long keyed query (KC_INT): the next id, its text for snapshots and scheduler hashes; the
+// value cache is the dictionary (no string map: a million new keys cost ~0.2 s of string-map inserts, C4 r5h)
+bool new_int_key(QueryRt& q, int64_t iv, uint32_t* key) {
+    *key = (uint32_t)q.keystr.size();
+    q.keystr.push_back(std::to_string(iv));
+    q.intkeys.insert(iv, *key);
+    return true;
+}
+
+
 // key of one host row (ValuePartitionExecutor: toString, null -> dropped)
 bool host_key(sdg_engine* e, QueryRt& q, int qpos, const PushChunk& c, int64_t row, uint32_t* key) {
     int ai = q.hq.key_attr[qpos];
@@ -423,6 +433,7 @@ bool host_key(sdg_engine* e, QueryRt& q, int qpos, const PushChunk& c, int64_t r
     if (integral) {
         iv = kind == VK_I32 ? (int64_t)((const int32_t*)col)[row] : ((const int64_t*)col)[row];
         if (q.intkeys.find(iv, key)) return true;
+        if (q.key_class == KC_INT) return new_int_key(q, iv, key);
     }
     std::string s;
     switch (kind) {
@@ -453,6 +464,7 @@ bool slot_key(sdg_engine* e, QueryRt& q, int qpos, int64_t slot, uint32_t* key) 
     const bool integral = kind == VK_I32 || kind == VK_I64;
     const int64_t iv = kind == VK_I32 ? (int64_t)(int32_t)slot : slot;
     if (integral && q.intkeys.find(iv, key)) return true;
+    if (integral && q.key_class == KC_INT) return new_int_key(q, iv, key);
     std::string s;
     switch (kind) {
         case VK_I32: case VK_I64: s = std::to_string(iv); break;
@@ -1234,14 +1246,15 @@ const uint32_t* device_key_ids(sdg_engine* e, QueryRt& q, const void* col, int k
             order.swap(tmp);
         }
         std::vector<uint32_t> slots(cnt);
-        q.keydict.reserve(K0 + cnt);  // one rehash, not ~log2(cnt) of them
+        if (q.key_class != KC_INT) q.keydict.reserve(K0 + cnt);  // one rehash, not ~log2(cnt) of them
         q.keystr.reserve(K0 + cnt);
         for (uint64_t j = 0; j < cnt; ++j) {
             const uint32_t i = order[j];
             const uint32_t id = (uint32_t)(K0 + j);
             slots[j] = (uint32_t)(pairs[i] & 0xFFFFFFFFull);
             std::string ks = key_string_of_value(q.key_class, vals[i]);
-            if (!q.keydict.emplace(ks, id).second) throw DeviceError("device key table out of step with the dictionary");
+            if (q.key_class != KC_INT && !q.keydict.emplace(ks, id).second)  // (KC_INT: intkeys is the dictionary)
+                throw DeviceError("device key table out of step with the dictionary");
             q.keystr.push_back(std::move(ks));
             if (q.key_class == KC_INT) q.intkeys.insert(vals[i], id);
         }
@@ -1687,7 +1700,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     // sorted positions and original rows are 32-bit on the device
     if (nrows >= (int64_t)0xFFFFFFF0) throw CompileError(SDG_ERR_CAPACITY, "a flush holds more than 2^32 - 16 events");
     uint32_t K = 1;
-    if (partitioned) K = q.string_keys ? (uint32_t)std::max<size_t>(e->strings.strs.size(), 1) : (uint32_t)std::max<size_t>(q.keydict.size(), 1);
+    if (partitioned) K = q.string_keys ? (uint32_t)std::max<size_t>(e->strings.strs.size(), 1) : (uint32_t)std::max<size_t>(q.keystr.size(), 1);
     // fused bucket path (chain.hip chain_fused_k): one radix pass into 2^bbits buckets + per-block regrouping in LDS
     // instead of the full key sort. Shapes it covers: see kernels.h; anything else (or a batch that breaks its
     // time-order precondition) runs the radix path below.
@@ -2638,7 +2651,8 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     // atomically; delivery order comes from the export's sort), so SDG_CARRY_SIDE=1 runs it on a second stream beside
     // it (the stream joins before anything reads the counters). Off by default: C2 step 3.695 -> 3.673 ms, but the
     // matcher's own time grows 2.04 -> 2.10 ms beside it (r5c1)
-    static const bool carry_serial = !(getenv("SDG_CARRY_SIDE") && atoi(getenv("SDG_CARRY_SIDE")) == 1);
+    const char* cside_env = getenv("SDG_CARRY_SIDE");  // (read per flush: the tests switch it)
+    const bool carry_serial = !(cside_env && atoi(cside_env) == 1);
     const bool carry_side = fused && !sorted && a.cin_n > 0 && !carry_serial && !dbg;
     if (carry_side) {
         HIPCHECK(hipEventRecord(e->fork, st));
@@ -3564,7 +3578,8 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
         q.keydict.clear();
         q.kt_cap = 0;  // the device key table is rebuilt from the dictionary on the next device-resident batch
         q.kt_synced = 0;
-        for (size_t i = 0; i < q.keystr.size(); ++i) q.keydict[q.keystr[i]] = (uint32_t)i;
+        if (q.key_class != KC_INT)
+            for (size_t i = 0; i < q.keystr.size(); ++i) q.keydict[q.keystr[i]] = (uint32_t)i;
         q.key_hash = std::move(g.key_hash);
         q.korder = std::move(g.korder);
         q.L = g.L;

@@ -285,15 +285,17 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
     constexpr size_t NONE = ~size_t(0);
     enum : uint8_t { DEV = 0, PENDING = 1, HOST = 2 };  // the key's history so far: its device run / a device fire
                                                       // the scheduler has not made yet / stepped on the host
-    struct KC {
-        size_t i = 0, e = 0;                 // cursor into the key's device records
+    struct KC {                              // 32 bytes: two keys per cache line (the pass is bound by these misses)
+        uint32_t i = 0, e = 0;               // cursor into the key's device records (logs.size() < 2^32)
+        int32_t fh = -1, ft = -1;            // the scheduler's fires of this key so far (list in `fl`)
+        uint32_t nshift = 0;                 // its device fires accepted as shifted
         uint8_t mode = DEV;
         bool reordered = false;              // optimistic pass: the scheduler's order differs from the run's
         bool touched = false;
         KeyRun* run = nullptr;
-        int32_t fh = -1, ft = -1;            // the scheduler's fires of this key so far (list in `fl`)
-        uint32_t nshift = 0;                 // its device fires accepted as shifted
     };
+    static_assert(sizeof(KC) == 32, "KC layout");
+    if (logs.size() >= 0xFFFFFFFFull) throw std::runtime_error("scheduler simulation: more than 2^32 log records");
     struct FN {
         nfa::TimerFire f;
         int32_t next;
@@ -338,8 +340,8 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
         size_t j = i;
         while (j < logs.size() && logs[j].key == logs[i].key) ++j;
         KC& c = K(logs[i].key);
-        c.i = i;
-        c.e = j;
+        c.i = (uint32_t)i;
+        c.e = (uint32_t)j;
         for (size_t x = i; x < j; ++x) {
             if (is_evpush(x)) evp.push_back(x);
             nfire_logs += logs[x].type == nfa::LOG_FIRE;
@@ -471,7 +473,7 @@ void SchedSim::simulate(const BatchClock& bc, const std::vector<nfa::SchedLog>& 
                     ++c.nshift;
                 }
                 out.rank.put(rank_key(logs[f].g, sch, key), Slot{g, rk});
-                c.i = end + 1;
+                c.i = (uint32_t)(end + 1);
                 c.mode = DEV;
                 const size_t nf = next_fire(c);
                 if (nf != NONE) fireq.push({(int64_t)logs[nf].g, key});

@@ -206,6 +206,18 @@ def test_c2_fused_arrival_order_columns(case, oracle_built, monkeypatch):
     assert got == ref
 
 
+@pytest.mark.parametrize("keys", [37, 20_000])
+def test_c2_fused_carry_side_stream(keys, oracle_built, monkeypatch):
+    """SDG_CARRY_SIDE=1: the carried partials' pass runs on a second stream beside the matcher (7 batches)"""
+    monkeypatch.setenv("SDG_CARRY_SIDE", "1")
+    cols = w.c2_columns(40_000, keys=keys, per_ms=3)
+    syms = w.symbols(keys)
+    ref = oracle_c_rows(w.C2_APP, cols, syms)
+    got = product_c_rows(w.C2_APP, cols, syms, batches=7, expect_fused=1)
+    assert len(ref) > 100
+    assert got == ref
+
+
 def test_c2_fused_overflow_scans(oracle_built):
     """a long window with few keys: partials outlive the staged halo and finish in the key-filtered HBM scan"""
     app = w.C2_APP.replace("within 1 sec", "within 100 sec")
