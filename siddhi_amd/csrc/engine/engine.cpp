@@ -2316,8 +2316,13 @@ void flush_query(sdg_engine* e, QueryRt& q) {
                 std::vector<nfa::SchedLog> nl(hc[1]);
                 if (hc[1]) HIPCHECK(hipMemcpy(nl.data(), a.T.log, hc[1] * sizeof(nfa::SchedLog), hipMemcpyDeviceToHost));
                 if (keep_unlisted) {  // the first run's records of the keys that were not rerun
+                    uint32_t km = 0;
+                    for (uint32_t k : q.reordered) km = std::max(km, k);
+                    std::vector<uint8_t> rerun((size_t)km + 1, 0);  // (a flag per key, not a search per record)
+                    for (uint32_t k : q.reordered) rerun[k] = 1;
+                    nl.reserve(nl.size() + logs.size());
                     for (const nfa::SchedLog& r : logs)
-                        if (!std::binary_search(q.reordered.begin(), q.reordered.end(), r.key)) nl.push_back(r);
+                        if (r.key > km || !rerun[r.key]) nl.push_back(r);
                 }
                 // by (key, kseq): a stable counting sort by key (a lane appends its key's records in order); a key
                 // whose records came out of order is sorted by kseq
