@@ -161,16 +161,19 @@ class ShardedAppRuntime:
     """One rank's share of a Siddhi app on an N-GPU node: partitioned queries are key-hash sharded
     (rank r processes the events whose partition key hashes to r, `owner`), unpartitioned queries run as replicas
     on rank 0 (the streams only they read go to rank 0 whole; a stream read by both kinds makes the whole app run on
-    rank 0, with a RuntimeWarning). Each stream is routed by the partition attribute the ENGINE compiled for it (sdg_query_key_attr), so
-    the router and the queries cannot disagree; a stream keyed by different attributes in different partitions
-    cannot be routed by one key and is refused. Queries with absent states run whole on rank 0 (RuntimeWarning): the
-    reference's Scheduler collapses the due timers of ALL partition keys into one TreeMultimap per clock advance
-    (Scheduler.java:75-98, only the first state per due time fires), so which fires it delays depends on keys that
-    would live on other GPUs (7,857 vs 9,790). Refused at N > 1, with OperationNotSupportedException:
+    rank 0, with a RuntimeWarning). Each stream is routed by the partition attribute the ENGINE compiled for it
+    (sdg_query_key_attr), so the router and the queries cannot disagree. At N > 1 these partitioned queries cannot be
+    key-sharded and run whole on rank 0 instead (RuntimeWarning; the same rule as unpartitioned ones, so a stream they
+    share with sharded queries sends the whole app to rank 0):
+      * absent states: the reference's Scheduler collapses the due timers of ALL partition keys into one TreeMultimap
+        per clock advance (Scheduler.java:75-98, only the first state per due time fires), so which fires it delays
+        depends on keys that would live on other GPUs (BASELINE.md C4: 7,857 vs 9,790);
       * a stream without a partition key (PartitionStreamReceiver.send(ComplexEvent) :274-283): its events go to
         every key of the partition in ONE global key order that interleaves the ranks' keys;
-      * range partitions: an event may belong to several ranges (keys), so it has no single owner.
-    Such apps run on one GPU (world 1), where the engine reproduces the reference exactly."""
+      * range partitions: an event may belong to several ranges (keys), so it has no single owner;
+      * a stream that two partitions key by different attributes: no single owner either.
+    Rank 0 then runs them exactly as one GPU does. A caller's key_attr that disagrees with the engine is refused
+    (OperationNotSupportedException)."""
 
     def __init__(self, app_text, rank, world, device=0, key_attr=None, **kw):
         import siddhi_amd as sa
@@ -182,30 +185,39 @@ class ShardedAppRuntime:
         def refuse(msg):
             self.rt.shutdown()
             raise sa.OperationNotSupportedException(msg)
-        timers = [n for n, f in zip(names, flags) if f & Q_TIMERS]
-        if world > 1:
-            bcast = [n for n, f in zip(names, flags) if f & Q_BROADCAST]
-            if bcast:
-                refuse("queries %s read a stream without a partition key: its events reach every key in one global "
-                       "key order (PartitionStreamReceiver.java:274-283); run the app on one GPU" % bcast)
-        # a query with absent states runs whole on rank 0: the reference's scheduler orders the due timers of ALL its
-        # partition keys in one TreeMultimap per clock advance (Scheduler.java:75-98), so a key shard on another GPU
-        # would change which fires it delays (7,857 vs 9,790 matches under a naive split)
-        part = [bool(f & Q_PARTITIONED) and not (world > 1 and f & Q_TIMERS) for f in flags]
         streams = self.rt.app_stream_ids()
         reads = {s: [q for q in range(len(names)) if self.rt.query_reads(q, s)] for s in streams}
-        # a stream that an unpartitioned query reads must reach ONE rank whole (rank 0); if a partitioned query reads
-        # it too, that query's keys would be split between the sharded streams and this one, so at N > 1 the whole app
-        # goes to rank 0 -- said out loud (warning), never silently
+        # partitioned queries that cannot be key-sharded at N > 1 run whole on rank 0 (class docstring)
+        whole = {}
+        if world > 1:
+            for q, f in enumerate(flags):
+                if not f & Q_PARTITIONED:
+                    continue
+                if f & Q_TIMERS:
+                    whole[q] = "absent states (one global timer order, Scheduler.java:75-98)"
+                elif f & Q_BROADCAST:
+                    whole[q] = "a stream without a partition key (one global key order, PartitionStreamReceiver.java:274-283)"
+                elif any(self.rt.query_key_attr(q, s) == -2 for s in streams if q in reads[s]):
+                    whole[q] = "range partitions (an event may belong to several keys)"
+            for s in streams:
+                qs = [q for q in reads[s] if flags[q] & Q_PARTITIONED and q not in whole]
+                if len({self.rt.query_key_attr(q, s) for q in qs} - {-1}) > 1:
+                    for q in qs:
+                        whole[q] = "stream '%s' keyed by different attributes in different partitions" % s
+        part = [bool(f & Q_PARTITIONED) and q not in whole for q, f in enumerate(flags)]
+        # a stream that an unpartitioned (or rank-0-only) query reads must reach ONE rank whole (rank 0); if a sharded
+        # query reads it too, that query's keys would be split between the sharded streams and this one, so at N > 1
+        # the whole app goes to rank 0 -- said out loud (warning), never silently
         mixed = sorted(s for s, qs in reads.items() if any(part[q] for q in qs) and not all(part[q] for q in qs))
         self.sharded = all(part)
         self.replica = bool(mixed)  # every event, on rank 0 only
         self.whole_streams = {s for s, qs in reads.items() if qs and not any(part[q] for q in qs)}  # rank 0 only
-        if world > 1 and (mixed or timers):
+        self.whole_queries = {names[q]: why for q, why in whole.items()}
+        if world > 1 and (mixed or whole):
             import warnings
-            if timers:
-                warnings.warn("queries %s have absent states (one global timer order, Scheduler.java:75-98): they run "
-                              "whole on rank 0 of %d, not key-sharded" % (timers, world), RuntimeWarning, stacklevel=2)
+            for q, why in sorted(whole.items()):
+                warnings.warn("query '%s' has %s: it runs whole on rank 0 of %d, not key-sharded" % (names[q], why, world),
+                              RuntimeWarning, stacklevel=2)
             if mixed:
                 warnings.warn("streams %s are read by key-sharded and rank-0-only queries: the app cannot be key-sharded "
                               "and runs whole on rank 0 of %d" % (mixed, world), RuntimeWarning, stacklevel=2)

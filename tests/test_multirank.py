@@ -174,8 +174,8 @@ def test_route_float32_keys_like_per_row_send():
 
 def test_sharded_runtime_routes_by_the_engines_partition_attribute():
     """the router takes each stream's key attribute from the engine (sdg_query_key_attr), refuses a
-    caller's key_attr that disagrees, a stream keyed by two attributes, range partitions and broadcast streams at
-    N > 1, and routes columnar batches at once (route over the distinct keys)"""
+    caller's key_attr that disagrees, runs a stream keyed by two attributes and broadcast streams whole on rank 0 at
+    N > 1 (warned), and routes columnar batches at once (route over the distinct keys)"""
     import numpy as np
     import siddhi_amd as sa
     import synth
@@ -189,13 +189,26 @@ def test_sharded_runtime_routes_by_the_engines_partition_attribute():
            "from every e1=S -> e2=S select e1.id as x insert into O1; end; partition with (b of S) begin "
            "@info(name='q2') from every e1=S -> e2=S select e1.id as x insert into O2; end;")
     assert shard.ShardedAppRuntime(two, 0, 1, compile_only=True).key_attr  # one GPU: fine
-    with pytest.raises(sa.OperationNotSupportedException):
-        shard.ShardedAppRuntime(two, 0, 2, compile_only=True)
+    # N > 1: no single owner GPU for S's events -> both queries run whole on rank 0 (warned), never refused
+    for rank in (0, 1):
+        with pytest.warns(RuntimeWarning, match="keyed by different attributes"):
+            t = shard.ShardedAppRuntime(two, rank, 2, compile_only=True)
+        assert t.whole_streams == {"S"} and not t.key_attr and set(t.whole_queries) == {"q1", "q2"}
+        assert all(t.mine("S", [0, "a%d" % i, "b%d" % i]) == (rank == 0) for i in range(100))
     bc = synth.BCAST_APPS["bc_pattern"]
     assert sa.SiddhiAppRuntime(bc, compile_only=True).query_flags() == [shard.Q_PARTITIONED | shard.Q_BROADCAST]
     assert sa.SiddhiAppRuntime(bc, compile_only=True).query_key_attr(0, "T") == -3
-    with pytest.raises(sa.OperationNotSupportedException):
-        shard.ShardedAppRuntime(bc, 0, 2, compile_only=True)
+    for rank in (0, 1):
+        with pytest.warns(RuntimeWarning, match="without a partition key"):
+            b = shard.ShardedAppRuntime(bc, rank, 2, compile_only=True)
+        assert not b.key_attr and b.whole_streams and all(b.mine(st, [0, 1, 1.0]) == (rank == 0)
+                                                          for st in b.whole_streams)
+    rg = synth.RANGE_APPS["range_overlap"]
+    for rank in (0, 1):
+        with pytest.warns(RuntimeWarning, match="range partitions"):
+            g = shard.ShardedAppRuntime(rg, rank, 2, compile_only=True)
+        assert g.whole_streams == {"S", "T"} and not g.key_attr
+        assert all(g.mine(st, [0, "k", 50.0, 90]) == (rank == 0) for st in ("S", "T"))
     keys = np.array(["S%05d" % k for k in np.random.default_rng(3).integers(0, 5000, 20000)])
     r = shard.route(keys, 4)
     assert r.tolist() == [shard.owner(k, 4) for k in keys.tolist()]
