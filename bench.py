@@ -651,8 +651,8 @@ def main():
     d_ts0 = torch.from_numpy(cols["ts"]).to(dev)
     span = int(cols["ts"][-1] - cols["ts"][0]) + 1
     nsteps = args.warmup + args.steps
-    ts_steps = [d_ts0 + s * span for s in range(nsteps + 2)]  # consecutive batches of one stream (+2: gather leg;
-                                                              # the ordered steps follow them)
+    ts_steps = [d_ts0 + s * span for s in range(nsteps)]  # consecutive batches of one stream (the ordered steps and
+                                                          # the gather leg continue its time after them)
     torch.cuda.synchronize()
 
     def step(s):
@@ -801,10 +801,15 @@ def main():
         out["cpu_baseline"] = None
     if not args.no_gather:
         log("ordered result gather (one more batch, outside the timed region)")
-        nxt = [nsteps]  # the leg's two batches (a warm-up export, then the timed one) continue the stream's time
+        # the leg's two batches (a warm-up export, then the timed one) continue the stream's time after the ordered
+        # steps (a batch earlier than the last one sends time backwards: the chain query then falls back to the generic
+        # NFA, whose carry replay overflowed at N = 2)
+        t_first = nsteps if args.no_ordered else nsteps + 2 + K + 1
+        leg_ts = [d_ts0 + (t_first + j) * span for j in range(2)]
+        nxt = [0]
 
         def leg_push():
-            rt.push_device("StockStream", n, ts_steps[nxt[0]].data_ptr(),
+            rt.push_device("StockStream", n, leg_ts[nxt[0]].data_ptr(),
                            [d_id.data_ptr(), d_sym.data_ptr(), d_price.data_ptr(), d_vol.data_ptr()])
             nxt[0] += 1
         out["ordered_gather"] = ordered_gather_leg(rt, step_push=leg_push, n=n, dev=dev, dist=dist, rank=rank,
