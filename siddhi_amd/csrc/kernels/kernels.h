@@ -259,7 +259,10 @@ constexpr int FU_ROWS = FU_THREADS * FU_PT;          // 2048 rows in LDS
 // Longer chunks pay a lane's continuation over the key's following rows (~ the window) once per more rows, but
 // lengthen the block's critical path: measured 8 -> 2.85 ms vs 4 -> 2.65 ms (r1ab), so the pass is latency-bound
 constexpr int FU_DQ = SDG_FU_DQ;
-constexpr int FU_HALO = 512;  // ~1.3 s of a bucket at C2 (> T)
+#ifndef SDG_FU_HALO
+#define SDG_FU_HALO 512  // ~1.3 s of a bucket at C2 (> T)
+#endif
+constexpr int FU_HALO = SDG_FU_HALO;
 constexpr int FU_OWN = FU_ROWS - FU_HALO;            // candidate rows per block
 // grid size for n rows in nb buckets (a multiple of g_xcds: the XCD remap needs it)
 int64_t chain_fused_grid(int64_t n, int nb, int own = FU_OWN);
