@@ -211,13 +211,17 @@ __global__ __launch_bounds__(256) void order_runs_gather_k(const uint32_t* __res
 // order_runs_gather_k with the run bounds from wave ballots (a record's neighbours by shuffles; only a run that
 // crosses the wave's edge scans HBM) and the column gathers issued right after the index load, so they overlap the
 // run / rank work: two dependent memory waits per record instead of five or more
-__global__ __launch_bounds__(256) void order_runs_gather_w_k(const uint32_t* __restrict__ ek, const uint32_t* __restrict__ ix,
+#ifndef SDG_OG_THREADS
+#define SDG_OG_THREADS 256
+#endif
+constexpr int OG_T = SDG_OG_THREADS;  // order_runs_gather_w_k block size
+__global__ __launch_bounds__(OG_T) void order_runs_gather_w_k(const uint32_t* __restrict__ ek, const uint32_t* __restrict__ ix,
                                                              const int64_t* __restrict__ sub, int64_t n, ColSet cs,
                                                              int ncol, int64_t* __restrict__ seq_dst, int64_t emit_base,
                                                              int* __restrict__ long_run, uint32_t xcds) {
     const uint32_t vb = xcd_block(blockIdx.x, gridDim.x, xcds);
     const int lane = threadIdx.x & 63;
-    const int64_t i = (int64_t)vb * 256 + threadIdx.x;
+    const int64_t i = (int64_t)vb * OG_T + threadIdx.x;
     const int64_t i0 = i - lane;  // the wave's first record
     const bool in = i < n;
     const uint32_t e = in ? ek[i] : 0xFFFFFFFFu;  // (positions < 2^32 - 1: the sentinel never equals a key)
@@ -442,7 +446,8 @@ bool order_export(const int64_t* emit, const int64_t* sub, int64_t n, int64_t em
         hipLaunchKernelGGL(order_runs_gather_k, dim3(g8), dim3(256), 0, stream, ek1, ix1, sub, n, cs, ncol, seq_dst,
                            emit_base, flag, (uint32_t)g_xcds);
     else
-        hipLaunchKernelGGL(order_runs_gather_w_k, dim3(g8), dim3(256), 0, stream, ek1, ix1, sub, n, cs, ncol, seq_dst,
+        hipLaunchKernelGGL(order_runs_gather_w_k, dim3((unsigned)xcd_round((n + OG_T - 1) / OG_T)), dim3(OG_T), 0, stream,
+                           ek1, ix1, sub, n, cs, ncol, seq_dst,
                            emit_base, flag, (uint32_t)g_xcds);
     int hf = 0;
     (void)hipMemcpyAsync(&hf, flag, 4, hipMemcpyDeviceToHost, stream);
