@@ -902,6 +902,9 @@ static_assert(FU_ROWS < 65536, "chain_fused_k: u16 rows / run offsets");
 // ONEK: one-key batches (unpartitioned, C1): a.fu_own rows per segment, the staging's time-order check and the work
 // queue's group summaries. Compile-time, so the many-key build keeps its registers (C2's matcher 2.04 -> 2.26 ms with
 // them present but switched off at run time, r5t/r5u)
+#ifndef SDG_FU_ROWORDER
+#define SDG_FU_ROWORDER 1  // chain_fused_k emits a block's records in e1-row order (0: regrouped order, A/B)
+#endif
 // OC: some output columns stay in arrival order (ChainArgs::ocols): time-major block order, and the emission reads
 // them through orig (a separate instantiation: the selects cost the others 0.17 ms on C2, r5w)
 template <int K, bool SAME, int W, bool ONEK = false, bool OC = false>
@@ -1392,11 +1395,30 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
         }
     }
     __syncthreads();
-    uint32_t res[FU_PT];
+    // records leave in the order of their e1 ROW (time order within the block), not of the regrouped position: the
+    // delivery-order export then gathers each block's records nearly sequentially (in regrouped order a cache line of
+    // records spanned the whole segment's time: its gather fetched 3.5x the record bytes, r5ox). Position of row r:
+    // s_inv[r], in the values' LDS, free after the matching
+#if SDG_FU_ROWORDER
+    uint16_t* const s_inv = reinterpret_cast<uint16_t*>(&s_x[0]);
 #pragma unroll
     for (int k = 0; k < FU_PT; ++k) {
         const int pos = k * FU_THREADS + t;
-        const uint16_t r16 = pos < nr ? s_res[sw(pos)] : R_NONE;
+        if (pos < nr) s_inv[s_row[sw(pos)]] = (uint16_t)pos;
+    }
+    __syncthreads();
+    auto pos_of = [&](int k) -> int {
+        const int row = k * FU_THREADS + t;
+        return row < nr ? (int)s_inv[row] : row;
+    };
+#else
+    auto pos_of = [&](int k) -> int { return k * FU_THREADS + t; };
+#endif
+    uint32_t res[FU_PT];
+#pragma unroll
+    for (int k = 0; k < FU_PT; ++k) {
+        const int pos = pos_of(k);
+        const uint16_t r16 = k * FU_THREADS + t < nr ? s_res[sw(pos)] : R_NONE;
         const uint32_t out = r16 == R_NONE ? MQ_NONE : r16 == R_CARRY ? MQ_CARRY : r16 == R_OVF ? MQ_OVF : (uint32_t)r16;
         res[k] = out;
         const uint64_t bm = __ballot(out < MQ_OVF), bc = __ballot(out == MQ_CARRY), bo = __ballot(out == MQ_OVF);
@@ -1442,7 +1464,7 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
     for (int k = 0; k < FU_PT; ++k) {
         const uint32_t out = res[k];
         const uint64_t bm = __ballot(out < MQ_OVF);
-        const int pos = k * FU_THREADS + t;
+        const int pos = pos_of(k);
         slot[k] = NOSLOT;
         prow[k] = qrow[k] = 0;
         any_co |= out == MQ_CARRY || out == MQ_OVF;
@@ -1538,7 +1560,7 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
         const uint32_t out = res[k];
         const uint64_t bc = __ballot(out == MQ_CARRY), bo = __ballot(out == MQ_OVF);
         if (out != MQ_CARRY && out != MQ_OVF) continue;
-        const int pos = k * FU_THREADS + t;
+        const int pos = pos_of(k);
         const int64_t p = lo + s_row[sw(pos)];
         if (out == MQ_CARRY) {
             const int64_t cs = (int64_t)bbase[1] + wcnt[1][k][w] + __popcll(bc & lt);
