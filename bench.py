@@ -788,7 +788,10 @@ def main():
         rate, cm, dt = cpu_baseline(cols, syms, cs)
         out["cpu_baseline"] = {"value": rate, "unit": "events/s", "cores": 1, "kind": "port",
                                "sample": "first %d events of %s C2 stream (%.1f s, %d matches), oracle restatement"
-                                         % (cs, "the" if world == 1 else "rank 0's", dt, cm)}
+                                         % (cs, "the" if world == 1 else "rank 0's", dt, cm),
+                               "note": "box-to-box variance: this 1-core figure measured 4.4e5 to 1.05e6 events/s "
+                                       "for the same sample on different pooled boxes (BASELINE.md); compare it "
+                                       "with the GPU figure of the same run only"}
         thr = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
         log("cpu baseline, key-sharded over %d threads" % thr)
         srate, scm, sdt = cpu_baseline_sharded(cols, syms, cs, thr)

@@ -241,6 +241,15 @@ typedef struct sdg_stats {
 } sdg_stats;
 int sdg_last_stats(sdg_engine* e, sdg_stats* out);
 
+/* The ordered result gather's merge on rank 0 (one ordered delivery per input event,
+ * core/query/input/StateMultiProcessStreamReceiver.java:47-68 and core/stream/output/StreamCallback.java:93-129): the
+ * G <= 32 ranks' exports are runs already sorted by their int64 key (sdg_export_ordered), merged on the device into
+ * (key, run, index in run) order -- a stable G-way merge, no re-sort. All pointers are device memory of `device`:
+ * keys[r] (lens[r] records, non-decreasing), cols[r * ncols + c] (ncols <= 16 payload columns of widths[c] = 1, 2, 4
+ * or 8 bytes), out_keys / out_cols[c] (sum of lens records). Synchronous: returns when the outputs are written. */
+int sdg_merge_runs(int32_t device, int32_t G, const int64_t* const* keys, const int64_t* lens, int32_t ncols,
+                   const void* const* cols, const uint8_t* widths, int64_t* out_keys, void* const* out_cols);
+
 #ifdef __cplusplus
 }
 #endif

@@ -152,8 +152,28 @@ def load_library():
     L.sdg_query_key_attr.argtypes = [P, I32, I32]
     L.sdg_query_reads.argtypes = [P, I32, I32]
     L.sdg_last_stats.argtypes = [P, ctypes.POINTER(Stats)]
+    L.sdg_merge_runs.argtypes = [I32, I32, P, P, I32, P, P, P, P]
     _lib = L
     return L
+
+
+def merge_runs_device(keys, cols, out_keys, out_cols):
+    """sdg_merge_runs (merge.hip): stable G-way merge of sorted runs on the GPU. keys: per run a contiguous int64
+    CUDA tensor (non-decreasing); cols: per run a list of contiguous CUDA tensors (1 / 2 / 4 / 8-byte elements, one
+    per record); out_keys / out_cols: preallocated outputs of the total length. Synchronises torch's stream first
+    (the library runs on its own stream and returns when the outputs are written)."""
+    import torch
+    L = load_library()
+    G = len(keys)
+    nc = len(out_cols)
+    torch.cuda.synchronize()
+    kp = (ctypes.c_void_p * G)(*[k.data_ptr() for k in keys])
+    ln = (ctypes.c_int64 * G)(*[k.numel() for k in keys])
+    cp = (ctypes.c_void_p * max(G * nc, 1))(*[c.data_ptr() for r in cols for c in r])
+    wd = (ctypes.c_uint8 * max(nc, 1))(*[c.element_size() for c in out_cols])
+    op = (ctypes.c_void_p * max(nc, 1))(*[c.data_ptr() for c in out_cols])
+    dev = out_keys.device.index if out_keys.device.index is not None else torch.cuda.current_device()
+    _check(L.sdg_merge_runs(dev, G, kp, ln, nc, cp, wd, out_keys.data_ptr(), op))
 
 
 def _check(rc):

@@ -2686,7 +2686,12 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             HIPCHECK(hipMemcpyAsync(d_a, &a, sizeof a, hipMemcpyHostToDevice, st));
         }
         hp.mark("chain_setup+carry");
-        chain_fused(a, d_a, grid, st);
+        try {
+            chain_fused(a, d_a, grid, st);
+        } catch (...) {  // stream2 may still write carry / output buffers: join it before anything reuses them
+            if (carry_side) (void)hipStreamSynchronize(e->stream2);
+            throw;
+        }
         if (carry_side) HIPCHECK(hipStreamWaitEvent(st, e->join, 0));
         hp.mark("fused_enqueue");
         if (dbg) {
@@ -3649,7 +3654,8 @@ void restore(sdg_engine* e, const uint8_t* data, size_t len) {
 //               the next event's updateState() sees it -- NewAndEvery merged into Pending, the start state's seed
 //               with timestamp -1 -- and only for the keys holding partials (a key whose only state is the seed
 //               equals a fresh key);
-//   "registers" the sequence register kernel (seq3.hip): not decoded (SDG_NO_SEQ3 runs the query on the arenas).
+// A query on the sequence register kernel (seq3.hip) is refused with SDG_ERR_UNSUPPORTED (its registers keep
+// e2[0] / e2[last] only; SDG_NO_SEQ3 runs the query on the arenas).
 struct StateJson {
     std::string o;
     void str(const std::string& s) {
@@ -3801,7 +3807,14 @@ void snapshot_states(sdg_engine* e, const SnapParsed& sp, std::string& out) {
         if (qi) J.o += ',';
         J.o += "{\"name\":";
         J.str(h.name);
-        const char* form = q.seq3 ? "registers" : (g.chain || g.cn > 0) ? "chain" : "arena";
+        // the register sequence kernel keeps a partial's e2[0] / e2[last] only, not the reference's count chain
+        // (CountPreStateProcessor.java:206-219 + every pending StateEvent's chain, StreamPreStateProcessor.java:
+        // 450-469): refused rather than decoded into a map that would differ
+        if (q.seq3)
+            throw CompileError(SDG_ERR_UNSUPPORTED, "query '" + h.name + "' runs on the register sequence kernel, whose "
+                               "state keeps e2[0] / e2[last] of a count chain only; its StreamPreState maps cannot be "
+                               "decoded (compile with SDG_NO_SEQ3 to keep the query on the arenas)");
+        const char* form = (g.chain || g.cn > 0) ? "chain" : "arena";
         J.o += std::string(",\"form\":\"") + form + "\",\"states\":{";
         // key ids: the string table's ids for string partition values, else the query's own dictionary
         const int64_t K = !P.partitioned ? 1 : q.string_keys ? (int64_t)S.strs.size() : (int64_t)g.keystr.size();
@@ -4595,6 +4608,27 @@ int sdg_last_stats(sdg_engine* e, sdg_stats* out) {
     if (!e || !out) return fail(SDG_ERR_ARG, "null argument");
     *out = e->stats;
     return SDG_OK;
+}
+
+int sdg_merge_runs(int32_t device, int32_t G, const int64_t* const* keys, const int64_t* lens, int32_t ncols,
+                   const void* const* cols, const uint8_t* widths, int64_t* out_keys, void* const* out_cols) {
+    if (G < 1 || !keys || !lens || !out_keys || (ncols > 0 && (!cols || !widths || !out_cols)))
+        return fail(SDG_ERR_ARG, "null argument");
+    if (G > MG_MAX_RUNS || ncols < 0 || ncols > MG_MAX_COLS) return fail(SDG_ERR_ARG, "too many runs or columns");
+    return guarded([&]() {
+        HIPCHECK(hipSetDevice(device));
+        static hipStream_t st[64] = {};  // one stream per device, the merge's own (synchronous call)
+        if (device < 0 || device >= 64) throw CompileError(SDG_ERR_ARG, "device ordinal out of range");
+        if (!st[device]) HIPCHECK(hipStreamCreateWithFlags(&st[device], hipStreamNonBlocking));
+        try {
+            merge_runs_device(G, keys, lens, ncols, cols, widths, out_keys, out_cols, st[device]);
+        } catch (const std::invalid_argument& x) {
+            throw CompileError(SDG_ERR_ARG, x.what());
+        } catch (const std::runtime_error& x) {
+            throw DeviceError(x.what());
+        }
+        return SDG_OK;
+    });
 }
 
 }  // extern "C"

@@ -1219,7 +1219,10 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
                 for (int u = 0; u < WQ_U; ++u) {
                     if (r >= 0) break;
                     if (q + u >= end) {  // the key's staged rows ended with the partial pending
-                        r = (!to_end && (uint64_t)(tl_off - t0) > within_u) ? R_NONE : ran_off;
+                        // ONEK: a group skip may have jumped straight to `end` over the row that expired the partial
+                        // (its key's last staged row is the block's last, tl_off), so test the window even when the
+                        // rows reach the batch end -- an expired partial must not be carried
+                        r = ((ONEK || !to_end) && (uint64_t)(tl_off - t0) > within_u) ? R_NONE : ran_off;
                     } else if ((uint64_t)(tq[u] - t0) > within_u) {  // isExpired before the row is processed
                         r = R_NONE;
                     } else if (live && (left ? cmp_m(m, xq[u], y) : cmp_m(m, y, xq[u]))) {

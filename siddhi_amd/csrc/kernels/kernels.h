@@ -567,4 +567,12 @@ void kt_collect(const KeyTab& t, unsigned long long* pairs, int64_t* vals, unsig
 void kt_assign(const KeyTab& t, const uint32_t* slots, uint32_t id0, int64_t m, hipStream_t st);
 void kt_fix(const KeyTab& t, const void* col, int kind, int64_t n, uint32_t* out, hipStream_t st);
 
+// G-way merge of sorted runs (merge.hip, the ordered result gather on rank 0): keys[r] (int64, non-decreasing) of
+// lens[r] records; cols[r * ncols + c] their payload columns of widths[c] bytes; the merged keys / columns in
+// (key, run, index) order. Synchronous on `stream` (it reads the runs' end keys back to size the sample sort).
+constexpr int MG_MAX_RUNS = 32;
+constexpr int MG_MAX_COLS = 16;
+void merge_runs_device(int G, const int64_t* const* keys, const int64_t* lens, int ncols, const void* const* cols,
+                       const uint8_t* widths, int64_t* out_keys, void* const* out_cols, hipStream_t stream);
+
 }  // namespace sdg

@@ -1,0 +1,299 @@
+// G-way merge of sorted runs on the device: the ordered result gather's merge on rank 0 (the
+// reference delivers one ordered stream per input event, StateMultiProcessStreamReceiver.java:47-68,
+// StreamCallback.java:93-129). Each rank's export is already a run sorted by its key (sdg_export_ordered), so rank 0
+// merges G runs instead of re-sorting their concatenation.
+//
+// Order: (key, run, index in run) -- equal keys keep run order, then their order inside the run (a stable merge).
+// Regular sampling (PSRS) gives every output bucket a hard size bound, so one workgroup merges one bucket in LDS:
+//  1. samples: every MG_S-th record of every run, in (run, index) order, keys radix-sorted (rocPRIM, stable: ties
+//     stay in (run, index) order = the composite order);
+//  2. splitters: every MG_M-th sorted sample. A splitter's position in each run: its own index in its own run, the
+//     upper bound of its key in earlier runs, the lower bound in later runs (binary searches, one lane per (splitter,
+//     run)). The bucket between two consecutive splitters then holds, from run r, the records between them in the
+//     composite order: at most (c_r + 1) * MG_S where c_r samples of run r lie between them, sum c_r <= MG_M, so a
+//     bucket holds <= (MG_M + G) * MG_S records;
+//  3. one workgroup per bucket: the bucket's key slices into LDS, each record's rank inside the bucket = its index
+//     in its slice + its bounds in the other slices (LDS binary searches), then the records leave in output order:
+//     keys from LDS, payload columns read from the runs (G nearly sequential streams), all stores contiguous.
+// HBM traffic: the keys read once and written once, every payload byte read once and written once, plus the
+// samples (1 / MG_S of the keys) and the splitter bounds (G x 4 B per MG_M x MG_S records).
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "kernels.h"
+
+namespace sdg {
+namespace {
+
+constexpr int MG_S = 128;                              // sample stride (records of one run per sample)
+constexpr int MG_M = 16;                               // samples per bucket
+constexpr int MG_THREADS = 512;
+constexpr int MG_CAP = (MG_M + MG_MAX_RUNS) * MG_S;    // a bucket's records, upper bound (6144 at 32 runs)
+
+struct MergeRuns {
+    const int64_t* keys[MG_MAX_RUNS];
+    const void* cols[MG_MAX_RUNS][MG_MAX_COLS];
+    int64_t len[MG_MAX_RUNS];
+    int64_t sbase[MG_MAX_RUNS + 1];  // first sample id of each run (run-major)
+    void* out_cols[MG_MAX_COLS];
+    int64_t* out_keys;
+    uint8_t width[MG_MAX_COLS];
+    int G;
+    int ncols;
+    int64_t nsamples;
+    int64_t nbuckets;
+    int64_t kmin;                    // samples are sorted as key - kmin (u64, non-negative)
+    int* flag;                       // set if a bucket broke the sampling bound (never expected)
+};
+
+// the runs' first / last keys (they are sorted: the extremes of the whole input)
+__global__ void mg_ends_k(const MergeRuns a, int64_t* __restrict__ ends) {
+    const int r = threadIdx.x;
+    if (r < a.G && a.len[r] > 0) {
+        ends[2 * r] = a.keys[r][0];
+        ends[2 * r + 1] = a.keys[r][a.len[r] - 1];
+    }
+}
+
+// samples: key - kmin and the sample id (run-major ids: the input order of the stable sort)
+__global__ __launch_bounds__(256) void mg_samples_k(const MergeRuns a, uint64_t* __restrict__ skey,
+                                                    uint32_t* __restrict__ sid) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.nsamples) return;
+    int r = 0;
+    while (r + 1 < a.G && a.sbase[r + 1] <= i) ++r;
+    const int64_t idx = (i - a.sbase[r]) * MG_S;
+    skey[i] = (uint64_t)(a.keys[r][idx] - a.kmin);
+    sid[i] = (uint32_t)i;
+}
+
+// records of run `r` with key < k (lower) or <= k (upper)
+__device__ __forceinline__ int64_t mg_bound(const int64_t* __restrict__ keys, int64_t n, int64_t k, bool upper) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        const int64_t v = keys[mid];
+        if (v < k || (upper && v == k)) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// bounds[b * G + r]: the first record of run r in bucket b (b = 0: all zero; b = nbuckets: the run lengths)
+__global__ __launch_bounds__(256) void mg_bounds_k(const MergeRuns a, const uint32_t* __restrict__ sorted_sid,
+                                                   int64_t* __restrict__ bounds) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int G = a.G;
+    if (t >= (a.nbuckets + 1) * G) return;
+    const int64_t b = t / G;
+    const int r = (int)(t - b * G);
+    int64_t v;
+    if (b == 0) {
+        v = 0;
+    } else if (b == a.nbuckets) {
+        v = a.len[r];
+    } else {
+        const uint32_t s = sorted_sid[b * MG_M];  // the splitter: a sample (run rs, index is)
+        int rs = 0;
+        while (rs + 1 < G && a.sbase[rs + 1] <= (int64_t)s) ++rs;
+        const int64_t is = ((int64_t)s - a.sbase[rs]) * MG_S;
+        if (r == rs) v = is;
+        else v = mg_bound(a.keys[r], a.len[r], a.keys[rs][is], r < rs);
+    }
+    bounds[t] = v;
+}
+
+template <int W>
+__device__ __forceinline__ void mg_copy(const void* src, int64_t si, void* dst, int64_t di) {
+    if (W == 8) ((uint64_t*)dst)[di] = ((const uint64_t*)src)[si];
+    else if (W == 4) ((uint32_t*)dst)[di] = ((const uint32_t*)src)[si];
+    else if (W == 2) ((uint16_t*)dst)[di] = ((const uint16_t*)src)[si];
+    else ((uint8_t*)dst)[di] = ((const uint8_t*)src)[si];
+}
+
+__global__ __launch_bounds__(MG_THREADS, 2) void mg_merge_k(const MergeRuns a, const int64_t* __restrict__ bounds) {
+    __shared__ int64_t s_key[MG_CAP];
+    __shared__ uint16_t s_src[MG_CAP];  // output rank -> LDS slot
+    __shared__ uint8_t s_run[MG_CAP];   // LDS slot -> run
+    __shared__ int64_t s_start[MG_MAX_RUNS];
+    __shared__ int s_pre[MG_MAX_RUNS + 1];
+    const int t = threadIdx.x;
+    const int G = a.G;
+    const int64_t b = blockIdx.x;
+    if (t == 0) {
+        int acc = 0;
+        for (int r = 0; r < G; ++r) {
+            const int64_t lo = bounds[b * G + r], hi = bounds[(b + 1) * G + r];
+            s_start[r] = lo;
+            s_pre[r] = acc;
+            acc += (int)(hi - lo);
+        }
+        s_pre[G] = acc;
+    }
+    __syncthreads();
+    const int L = s_pre[G];
+    int64_t off = 0;  // the bucket's first output position: every record below its splitter
+    for (int r = 0; r < G; ++r) off += s_start[r];
+    if (L > MG_CAP) {  // cannot happen (the sampling bound); never write past the LDS
+        if (t == 0) atomicOr(a.flag, 1);
+        return;
+    }
+    // the bucket's key slices into LDS (slice r at s_pre[r])
+    for (int i = t; i < L; i += MG_THREADS) {
+        int r = 0;
+        while (r + 1 < G && s_pre[r + 1] <= i) ++r;
+        s_key[i] = a.keys[r][s_start[r] + (i - s_pre[r])];
+        s_run[i] = (uint8_t)r;
+    }
+    __syncthreads();
+    // each record's rank inside the bucket
+    for (int i = t; i < L; i += MG_THREADS) {
+        const int r = s_run[i];
+        const int64_t k = s_key[i];
+        int rank = i - s_pre[r];
+        for (int r2 = 0; r2 < G; ++r2) {
+            if (r2 == r) continue;
+            int lo = s_pre[r2], hi = s_pre[r2 + 1];
+            const bool upper = r2 < r;  // earlier runs first on equal keys
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                const int64_t v = s_key[mid];
+                if (v < k || (upper && v == k)) lo = mid + 1;
+                else hi = mid;
+            }
+            rank += lo - s_pre[r2];
+        }
+        s_src[rank] = (uint16_t)i;
+    }
+    __syncthreads();
+    // out in output order: contiguous stores, payload gathered from the runs' slices
+    for (int p = t; p < L; p += MG_THREADS) {
+        const int i = s_src[p];
+        const int r = s_run[i];
+        const int64_t si = s_start[r] + (i - s_pre[r]);
+        const int64_t di = off + p;
+        a.out_keys[di] = s_key[i];
+        for (int c = 0; c < a.ncols; ++c) {
+            const void* src = a.cols[r][c];
+            void* dst = a.out_cols[c];
+            switch (a.width[c]) {
+                case 8: mg_copy<8>(src, si, dst, di); break;
+                case 4: mg_copy<4>(src, si, dst, di); break;
+                case 2: mg_copy<2>(src, si, dst, di); break;
+                default: mg_copy<1>(src, si, dst, di); break;
+            }
+        }
+    }
+}
+
+struct MergeWs {
+    void* p = nullptr;
+    size_t n = 0;
+    void* ensure(size_t bytes) {
+        if (bytes <= n) return p;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        if (hipMalloc(&p, bytes) != hipSuccess) throw std::runtime_error("merge workspace: hipMalloc failed");
+        n = bytes;
+        return p;
+    }
+};
+
+}  // namespace
+
+void merge_runs_device(int G, const int64_t* const* keys, const int64_t* lens, int ncols, const void* const* cols,
+                       const uint8_t* widths, int64_t* out_keys, void* const* out_cols, hipStream_t stream) {
+    if (G < 1 || G > MG_MAX_RUNS) throw std::invalid_argument("merge: 1 to " + std::to_string(MG_MAX_RUNS) + " runs");
+    if (ncols < 0 || ncols > MG_MAX_COLS) throw std::invalid_argument("merge: too many columns");
+    MergeRuns a;
+    std::memset(&a, 0, sizeof a);
+    a.G = G;
+    a.ncols = ncols;
+    a.out_keys = out_keys;
+    int64_t total = 0, ns = 0;
+    for (int r = 0; r < G; ++r) {
+        if (lens[r] < 0) throw std::invalid_argument("merge: negative run length");
+        a.keys[r] = keys[r];
+        a.len[r] = lens[r];
+        a.sbase[r] = ns;
+        ns += (lens[r] + MG_S - 1) / MG_S;
+        total += lens[r];
+        for (int c = 0; c < ncols; ++c) a.cols[r][c] = cols[(size_t)r * ncols + c];
+    }
+    a.sbase[G] = ns;
+    for (int c = 0; c < ncols; ++c) {
+        if (widths[c] != 1 && widths[c] != 2 && widths[c] != 4 && widths[c] != 8)
+            throw std::invalid_argument("merge: column widths are 1, 2, 4 or 8 bytes");
+        a.width[c] = widths[c];
+        a.out_cols[c] = out_cols[c];
+    }
+    if (total == 0) return;
+    if (ns >= (int64_t)0xFFFFFFF0) throw std::invalid_argument("merge: too many records");
+    a.nsamples = ns;
+    a.nbuckets = (ns + MG_M - 1) / MG_M;
+    static MergeWs ws;
+    static int64_t* h_ends = nullptr;  // pinned: the runs' end keys, then the bound flag
+    if (!h_ends && hipHostMalloc((void**)&h_ends, (2 * MG_MAX_RUNS + 2) * 8) != hipSuccess)
+        throw std::runtime_error("merge: hipHostMalloc failed");
+    size_t tmp_bytes = 0;  // (sized for 64 key bits: at least what fewer bits need)
+    if (rocprim::radix_sort_pairs(nullptr, tmp_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
+                                  (uint32_t*)nullptr, (size_t)ns, 0, 64, stream) != hipSuccess)
+        throw std::runtime_error("merge: sample sort workspace");
+    const size_t tmp_cap = tmp_bytes;
+    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    const size_t nb1 = (size_t)(a.nbuckets + 1) * G;
+    const size_t need = 1024 + 2 * al((size_t)ns * 8) + 2 * al((size_t)ns * 4) + al(nb1 * 8) + al(tmp_bytes);
+    uint8_t* w = (uint8_t*)ws.ensure(need);
+    int64_t* d_ends = (int64_t*)w;  // 2G end keys + the flag word
+    a.flag = (int*)(d_ends + 2 * MG_MAX_RUNS);
+    w += 1024;
+    // key bits the sample sort needs: keys relative to their minimum (one small read-back)
+    if (hipMemsetAsync(a.flag, 0, 8, stream) != hipSuccess) throw std::runtime_error("merge: memset failed");
+    hipLaunchKernelGGL(mg_ends_k, dim3(1), dim3(64), 0, stream, a, d_ends);
+    if (hipMemcpyAsync(h_ends, d_ends, 2 * G * 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+        throw std::runtime_error("merge: reading the run ends failed");
+    int64_t kmin = INT64_MAX, kmax = INT64_MIN;
+    for (int r = 0; r < G; ++r)
+        if (lens[r] > 0) {
+            kmin = std::min(kmin, h_ends[2 * r]);
+            kmax = std::max(kmax, h_ends[2 * r + 1]);
+        }
+    a.kmin = kmin;
+    const uint64_t span = (uint64_t)kmax - (uint64_t)kmin;
+    int bits = 1;
+    while (bits < 64 && (span >> bits) != 0) ++bits;
+    if (rocprim::radix_sort_pairs(nullptr, tmp_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
+                                  (uint32_t*)nullptr, (size_t)ns, 0, bits, stream) != hipSuccess || tmp_bytes > tmp_cap)
+        throw std::runtime_error("merge: sample sort workspace");
+    uint64_t* sk0 = (uint64_t*)w;
+    w += al((size_t)ns * 8);
+    uint64_t* sk1 = (uint64_t*)w;
+    w += al((size_t)ns * 8);
+    uint32_t* si0 = (uint32_t*)w;
+    w += al((size_t)ns * 4);
+    uint32_t* si1 = (uint32_t*)w;
+    w += al((size_t)ns * 4);
+    int64_t* bounds = (int64_t*)w;
+    w += al(nb1 * 8);
+    void* tmp = w;
+    hipLaunchKernelGGL(mg_samples_k, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, stream, a, sk0, si0);
+    if (rocprim::radix_sort_pairs(tmp, tmp_bytes, sk0, sk1, si0, si1, (size_t)ns, 0, bits, stream) != hipSuccess)
+        throw std::runtime_error("merge: sample sort failed");
+    hipLaunchKernelGGL(mg_bounds_k, dim3((unsigned)((nb1 + 255) / 256)), dim3(256), 0, stream, a, si1, bounds);
+    hipLaunchKernelGGL(mg_merge_k, dim3((unsigned)a.nbuckets), dim3(MG_THREADS), 0, stream, a, bounds);
+    if (hipGetLastError() != hipSuccess) throw std::runtime_error("merge: kernel launch failed");
+    if (hipMemcpyAsync(h_ends + 2 * MG_MAX_RUNS, a.flag, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+        throw std::runtime_error("merge: kernels failed");
+    if (*(int*)(h_ends + 2 * MG_MAX_RUNS)) throw std::runtime_error("merge: a bucket broke the sampling bound");
+}
+
+}  // namespace sdg

@@ -452,7 +452,8 @@ bool order_export(const int64_t* emit, const int64_t* sub, int64_t n, int64_t em
     int hf = 0;
     (void)hipMemcpyAsync(&hf, flag, 4, hipMemcpyDeviceToHost, stream);
     (void)hipStreamSynchronize(stream);
-    return hf == 0;  // false: a run longer than RUN_MAX (nothing usable written; the caller takes order_records)
+    return hf == 0;  // false: a run longer than RUN_MAX. The short runs' records are ALREADY written to dst /
+                     // seq_dst; the caller's fallback (order_records) overwrites all n slots
 }
 
 size_t gather_cols_workspace(int64_t n, int ncol) { return (size_t)std::max<int64_t>(n, 1) * ncol * 8 + 256; }

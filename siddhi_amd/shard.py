@@ -65,15 +65,19 @@ def lexsort(keys):
 
 def merge_runs(runs, key):
     """G-way merge of sorted runs (dicts of torch tensors, records along the last dim) by their 1-D `key` column;
-    equal keys keep run order, then their order inside the run. Large merges: the runs concatenated in run order and
-    ONE stable device radix sort of the key relative to its minimum (32-bit when the span fits: 4 digit passes), so
-    ties keep exactly that order; small ones: each record's slot from binary searches into the other runs."""
+    equal keys keep run order, then their order inside the run. Runs on the GPU go through the device merge
+    (sdg_merge_runs, merge.hip: regular-sampling splitters, one workgroup per bucket merging in LDS, every record
+    read and written once; int64 keys). Runs in host memory (the gloo rehearsals on CPU) are merged on the host: the
+    runs concatenated in run order and one stable sort of the key, or binary searches of each record into the other
+    runs for small inputs."""
     import torch
     runs = [r for r in runs if r[key].numel() > 0]
     if not runs:
         return None
     if len(runs) == 1:
         return runs[0]
+    if runs[0][key].is_cuda and runs[0][key].dtype == torch.int64 and len(runs) <= 32:
+        return _merge_runs_device(runs, key)
     total = sum(int(r[key].numel()) for r in runs)
     if total >= (1 << 20):
         cat = {k: torch.cat([r[k] for r in runs], dim=-1) for k in runs[0]}
@@ -94,6 +98,29 @@ def merge_runs(runs, key):
                 pos += torch.searchsorted(other[key], v, right=r2 < r)
         for k, col in run.items():
             out[k][..., pos] = col
+    return out
+
+
+def _merge_runs_device(runs, key):
+    """merge_runs on the GPU (sdg_merge_runs): each 2-D column [m, n] travels as its m rows"""
+    import torch
+    from siddhi_amd import merge_runs_device
+    names = [k for k in runs[0] if k != key]
+    total = sum(int(r[key].numel()) for r in runs)
+    dev = runs[0][key].device
+    out = {key: torch.empty(total, dtype=torch.int64, device=dev)}
+    out_cols, src = [], [[] for _ in runs]
+    for k in names:
+        v = runs[0][k]
+        out[k] = torch.empty(list(v.shape[:-1]) + [total], dtype=v.dtype, device=dev)
+        rows = [out[k]] if v.dim() == 1 else list(out[k].reshape(-1, total))
+        out_cols += rows
+        for i, r in enumerate(runs):
+            c = r[k].contiguous()
+            src[i] += [c] if c.dim() == 1 else list(c.reshape(-1, c.shape[-1]))
+    if len(out_cols) > 16:
+        raise ValueError("merge_runs: more than 16 payload columns")
+    merge_runs_device([r[key].contiguous() for r in runs], src, out[key], out_cols)
     return out
 
 

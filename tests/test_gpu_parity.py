@@ -87,6 +87,64 @@ def test_c1_matches_oracle(adversarial, fused, oracle_built):
     assert got == ref
 
 
+def _batched_rows(app, cols, bounds, expect):
+    """the product over explicit batch bounds, asserting stats.fused after each flush (None: not checked)"""
+    rt = sa.SiddhiAppRuntime(app)
+    try:
+        h = rt.getInputHandler("StockStream")
+        sym = rt.intern("IBM")
+        rows = []
+        for (s, e), ex in zip(bounds, expect):
+            h.send_columns(cols["ts"][s:e], [cols["id"][s:e], np.full(e - s, sym, np.uint32), cols["price"][s:e],
+                                             cols["volume"][s:e]])
+            rt.flush(deliver=False)
+            if ex is not None:
+                assert rt.stats().fused == ex
+            types, ts, vals, nulls = rt.raw_outputs(0)
+            rows += [(ts[i], (vals[0][i], vals[1][i])) for i in range(len(ts))]
+        return rows
+    finally:
+        rt.shutdown()
+
+
+def test_one_key_skip_to_end_does_not_carry_an_expired_partial(oracle_built):
+    """the one-key work queue skips 32-row groups whose extreme cannot complete a partial; a skip that
+    lands on the staged end must still see that the partial expired inside the skipped rows. A high e1 price 1020
+    rows before a flush's end expires 19 rows before it (the rows after it are all lower), then the next flush's
+    timestamps go back 500 ms with a higher price: the reference already dropped the partial, so nothing matches it
+    (a wrongly carried partial would, the generic path compares |dt|)."""
+    n1 = 4000
+    ts = np.concatenate([w.T0 + np.arange(n1), w.T0 + 2980 + 500 + np.arange(3)]).astype(np.int64)
+    price = np.full(len(ts), 15.0)
+    price[n1 - 1020] = 29.99
+    price[n1:] = [35.0, 12.0, 36.0]
+    cols = {"ts": ts, "id": np.arange(len(ts), dtype=np.int64), "price": price,
+            "volume": np.zeros(len(ts), np.int32)}
+    ref = oracle_c_rows(w.C1_APP, cols)
+    got = _batched_rows(w.C1_APP, cols, [(0, n1), (n1, len(ts))], [1, None])
+    assert got == ref
+    assert ref == [(w.T0 + 3482, (n1, n1 + 2))]  # only the second flush's own partial
+
+
+@pytest.mark.parametrize("carried", [False, True])
+def test_one_key_decreasing_timestamps_fall_back(carried, oracle_built):
+    """an unpartitioned batch whose arrival timestamps decrease locally (once inside a block, once across
+    the block edge at row 1024) fails the one-key fused matcher's time-order check (stats.fused == 2) and reruns on
+    the lane kernels / generic NFA, equal to the oracle; with and without partials carried from an earlier flush"""
+    n0 = 6000 if carried else 0
+    n = n0 + 5000
+    cols = w.c1_columns(n)
+    ts = cols["ts"].copy()
+    for r in (n0 + 300, n0 + 1024, n0 + 3000):
+        ts[r] = ts[r - 1] - 2  # a row earlier than its predecessor
+    cols["ts"] = ts
+    ref = oracle_c_rows(w.C1_APP, cols)
+    bounds = ([(0, n0)] if carried else []) + [(n0, n)]
+    got = _batched_rows(w.C1_APP, cols, bounds, ([1] if carried else []) + [2])
+    assert len(ref) > 100
+    assert got == ref
+
+
 # one-key (unpartitioned) deque shapes: the continuation skips 64-row chunks by their min / max summaries
 # (chain_dq_summ_k), so cover both stack directions, e2 on either side, ties (>= / <=), constant (all-mode) scans, an
 # int column and no `within`, on random and on long descending / ascending runs (partials waiting ~a window)

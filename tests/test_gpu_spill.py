@@ -30,16 +30,19 @@ def _rows(p):
     return [(o["name"], o["ts"], tuple(o["values"])) for o in p.outputs() if o["kind"] == "query" and not o["expired"]]
 
 
-# One device-side case (a key with thousands of open partials runs on one GPU lane until it spills: ~40 s). The other
-# spill shapes -- 4 batches, the unpartitioned and non-reclaiming arenas, host-arena doubling, snapshot across a
-# spilled key, the never-completing-partials case -- run on the CPU through the host build of the same nfa.h code
-# (tests/test_fallbacks.py), which shares spill_keys' arena migration and KeyRunT.
-def test_spilled_key_vs_oracle(oracle_built):
+# Device-side cases (a key with thousands of open partials runs on one GPU lane until it spills: ~40 s each): one and
+# four flushes (the device skipping a spilled key in later flushes), and a snapshot / restore across a spilled key
+# (mark_spilled, the restored device's skip and the device arena growth before the spill run only here).
+# The other shapes -- the unpartitioned and non-reclaiming arenas, host-arena doubling, the never-completing-partials
+# case -- run on the CPU through the host build of the same nfa.h code (tests/test_fallbacks.py), which shares
+# spill_keys' arena migration and KeyRunT.
+@pytest.mark.parametrize("batches", [1, 4])
+def test_spilled_key_vs_oracle(batches, oracle_built):
     tr = spill_trace(depth=4600, keys=("k0", "k1"))
-    ref = oracle_rows(DEEP, tr, 1)
+    ref = oracle_rows(DEEP, tr, batches)
     p = ProductAdapter(DEEP, force_generic=True, max_partials=1024)
     try:
-        _flush_all(p, tr, 1)
+        _flush_all(p, tr, batches)
         got = _rows(p)
         spilled = sum(s.spilled_keys for s in p.stats)
         growths = sum(s.arena_growths for s in p.stats)
@@ -49,4 +52,28 @@ def test_spilled_key_vs_oracle(oracle_built):
     assert len(ref) > 4000 and got == ref
     assert spilled == 2  # k0 and k1 each once (then resident on the host)
     assert growths >= 2  # 1024 -> 4096 on the device first
-    assert host_rows >= 2 * 4600  # both keys' rows of the flush ran on the host (sdg_stats.host_rows)
+    assert host_rows >= (2 * 4600 if batches == 1 else 1)  # the keys' rows ran on the host (sdg_stats.host_rows)
+
+
+def test_spilled_key_survives_snapshot(oracle_built):
+    """snapshot after the key spilled, restore into a fresh runtime, continue over two more flushes: the host arena
+    travels in the snapshot and the restored device still skips the key"""
+    tr = spill_trace(depth=4600, keys=("k0",), seed=8)
+    ref = oracle_rows(DEEP, tr, 1)
+    cut = int(len(tr) * 0.9)  # inside the tail: k0 has spilled with thousands of partials pending
+    a = ProductAdapter(DEEP, force_generic=True, max_partials=4096)
+    try:
+        _flush_all(a, tr[:cut], 1)
+        assert sum(s.spilled_keys for s in a.stats) == 1
+        snap = a.rt.snapshot()
+        first = _rows(a)
+    finally:
+        a.close()
+    b = ProductAdapter(DEEP, force_generic=True, max_partials=4096)
+    try:
+        b.rt.restore(snap)
+        _flush_all(b, tr[cut:], 2)
+        second = _rows(b)
+    finally:
+        b.close()
+    assert len(ref) > 4000 and first + second == ref

@@ -122,3 +122,29 @@ def test_spilled_key_state_maps():
         p.close()
         o.close()
     assert check_maps(ref, got, "arena") > 4000
+
+
+def test_seq3_query_state_maps_are_refused_not_guessed():
+    """the register sequence kernel keeps e2[0] / e2[last] of a count chain only, so its state cannot be
+    decoded into CountPreStateProcessor's maps (CountPreStateProcessor.java:206-219): sdg_snapshot_states refuses
+    with OperationNotSupportedException; the same app on the arenas (seq3=False) decodes"""
+    import numpy as np
+    import siddhi_amd as sa
+    from siddhi_amd import workloads as w
+    cols = w.c3_columns(50, per_key=20)
+    for seq3 in (True, False):
+        rt = sa.SiddhiAppRuntime(w.C3_APP, seq3=seq3)
+        try:
+            rt.getInputHandler("S").send_columns(cols["ts"], [cols["id"], cols["key"], cols["price"],
+                                                              cols["volume"]])
+            rt.flush(deliver=False)
+            if seq3:
+                assert rt.stats().path == 2  # the register kernel ran
+                with pytest.raises(sa.OperationNotSupportedException, match="register sequence kernel"):
+                    rt.snapshot_states()
+            else:
+                maps = rt.snapshot_states()
+                assert maps["query1"]["form"] == "arena" and len(maps["query1"]["states"]) > 0
+        finally:
+            rt.shutdown()
+    assert np.all(np.diff(cols["ts"]) >= 0)
