@@ -238,6 +238,8 @@ typedef struct sdg_stats {
                                   the device arena's 4096 partial matches (they run there from then on) */
     int64_t host_rows;         /* rows of the last flush processed on the host (the engine's NFA code, not the test
                                   oracle): spilled keys' rows plus the scheduler's host replays (sched_host_keys) */
+    int32_t sub_batches;       /* fused chain path: time sub-batches the last flush ran in (0 / 1: the whole batch at once;
+                                  SDG_FU_SUB) */
 } sdg_stats;
 int sdg_last_stats(sdg_engine* e, sdg_stats* out);
 

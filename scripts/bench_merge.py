@@ -4,9 +4,13 @@ records (int64 key + two int64 payload columns, the C5 gather's ts / e1id / e2id
 (concatenate + one stable torch.sort of the key). Prints one JSON line."""
 import argparse
 import json
+import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():

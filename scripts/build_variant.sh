@@ -18,7 +18,7 @@ for S in ${SRC//,/ }; do
 done
 wait
 OBJS=""
-for o in engine compile sched kernels chain order keytab ingest seq3; do
+for o in engine compile sched kernels chain order keytab ingest seq3 merge; do
     if [[ ",$SRC," == *",$o,"* ]]; then OBJS="$OBJS $D/$o.o"; else OBJS="$OBJS _lib/$o.o"; fi
 done
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -Wl,--no-undefined -o $D/libsiddhi_amd.so $OBJS -pthread

@@ -88,7 +88,7 @@ class Stats(ctypes.Structure):
                 ("arena_growths", ctypes.c_int64), ("carry_in", ctypes.c_int64), ("carry_out", ctypes.c_int64),
                 ("arena_slots", ctypes.c_int64), ("sched_exact_passes", ctypes.c_int64),
                 ("sorted_view", ctypes.c_int32), ("spilled_keys", ctypes.c_int32),
-                ("host_rows", ctypes.c_int64)]
+                ("host_rows", ctypes.c_int64), ("sub_batches", ctypes.c_int32)]
 
 
 _lib = None

@@ -216,8 +216,9 @@ struct IntKeyCache {
 struct QueryRt {
     HostQuery hq;
     IntKeyCache intkeys;
-    DevBuf d_plan, d_code, d_consts, d_args, o_mq, o_ovf, o_ovfc, o_dqs;
+    DevBuf d_plan, d_code, d_consts, d_args, o_mq, o_ovf, o_ovfc, o_dqs, d_sub_args;
     HostPin h_args, h_ret;  // chain path: ChainArgs pair; counters (16 B) | flags (16 B) | overflow count (8 B)
+    HostPin h_sub_args;     // fused sub-batches: the two ChainArgs (sub_dead 1 / 0)
     bool string_keys = true;                        // all partition keys are string attributes (ids used as keys)
     // device key table (device-resident batches): the class every partition key attribute of the query shares --
     // KC_INT (int / long), KC_F32, KC_F64, KC_BOOL -- or KC_NONE (string keys, mixed classes, range partitions)
@@ -276,6 +277,9 @@ struct QueryRt {
     DevBuf sv_tsbase;                               // sorted view: base of its u32 ts offsets (ts_window_base)
     DevBuf bk_plan;                                 // fused path: bstart[257] + bseg[257]
     DevBuf bk_tm;                                   // fused path: time-major block plan (ChainArgs::tm)
+    DevBuf bk_own;                                  // fused sub-batches: bown[257] (ChainArgs::bown)
+    bool no_sub = false;                            // fused sub-batches off for good (a halo check failed)
+    std::vector<hipEvent_t> sub_ev;                 // per sub-batch timing marks (4 each)
     // carries (double buffered)
     struct Carry {
         DevBuf key, ts, seq, vals, nulls;
@@ -326,6 +330,15 @@ struct QueryRt {
     std::vector<HostVec<int64_t>> acc_vals;
     std::vector<HostVec<uint8_t>> acc_nulls;
     HostPin h_rb;                                   // pinned read-back staging
+    // pinned delivery (round 6): a flush whose records come out of the device already in delivery order, drained
+    // into an empty backlog, is read back straight into one of two pinned buffers that sdg_poll then hands out (no
+    // host copy into acc_*; the two alternate so the previous poll's arrays stay valid until the next poll)
+    HostPin del_buf[2];
+    int del_cur = 0;                                // the buffer the last sdg_poll handed out
+    int64_t del_n = -1;                             // >= 0: the backlog is these records in del_buf[del_cur ^ 1]
+    int del_nu = 0;                                 // their user-visible columns
+    bool del_nulls = false;                         // their null bytes are in the buffer (else the zero page)
+    std::vector<uint8_t> del_zero[2];               // zeros per buffer: expired flags / null bytes of null-free records
     // host copies for sdg_poll
     HostVec<int64_t> h_ts, h_seq;
     HostVec<uint8_t> h_expired;
@@ -1740,6 +1753,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     }
     e->stats.fused = 0;
     const bool carry_nullable0 = q.carry_nullable;
+    bool sub_retry = false;  // the fused run with sub-batches failed its halo check: once more without them
     // returns false when the fused path found its precondition broken (nothing of the batch is committed then)
     auto run = [&](bool fused) -> bool {
     const bool sorted = !fused && sorted_now && P.chain;
@@ -1770,6 +1784,13 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     // move them; ChainArgs::ocols). Not with view positions (orig is then not an arrival row) or nulls. Off by
     // default: on C2 the scatter gains 0.31 ms and the matcher's dependent gathers cost 0.28 ms (r5x)
     uint32_t eo_mask = 0;
+    // fused sub-batches (round 6; SDG_FU_SUB = own rows per sub-batch, a multiple of the bucket tile, 0 = off): the
+    // flush's bucket pass and matcher run per time sub-batch whose view (own rows + a halo past their window) stays
+    // in the Infinity Cache between the scatter that writes it and the matcher that reads it
+    int64_t sub_S = 0, sub_H = 0, sub_J = 0;
+    KeyGroupArgs sub_kg;
+    std::memset(&sub_kg, 0, sizeof sub_kg);
+    uint32_t* b_own = nullptr;
     const char* oc_env = getenv("SDG_FU_OCOLS");  // (read per flush: the tests switch it)
     const bool move_all = !(oc_env && atoi(oc_env) == 1);
     if (fused && partitioned && !d_vpos && !move_all && !getenv("SDG_FU_WIDE")) {
@@ -1865,8 +1886,37 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             static const bool bmajor = getenv("SDG_FU_BMAJOR") != nullptr;
             const int64_t tm_cap = chain_fused_grid(nrows, 1 << bbits) + 2;
             if (!bmajor && eo_mask) b_tm = (uint32_t*)q.bk_tm.ensure((size_t)tm_cap * 4);
-            bucketize(a, bbits, 0 /* ts is payload column 0 */, flags + 3, b_start, b_seg, FU_OWN, st,
-                      g_no_events ? nullptr : &e->ev[4], b_tm, b_tm ? tm_cap : 0);
+            // sub-batches: the own rows per sub-batch (a multiple of the bucket tile) and a halo sized from the
+            // batch's mean event rate (1.25 x the rows of one window + 2 tiles; checked on the device: a too short
+            // halo reruns the flush without sub-batches)
+            const char* sub_env = getenv("SDG_FU_SUB");  // (read per flush: the tests switch it)
+            const int64_t tile = bucket_tile();
+            int64_t S = sub_env ? atoll(sub_env) : 0;
+            S = S > 0 ? (S + tile - 1) / tile * tile : 0;
+            if (S > 0 && !q.no_sub && !sub_retry && !wide && !eo_mask && !d_vpos && !d_qs && !d_vrank && P.has_within &&
+                nrows >= 2 * S && !sorted) {
+                int64_t te[2];
+                HIPCHECK(hipMemcpyAsync(&te[0], d_ts, 8, hipMemcpyDeviceToHost, st));
+                HIPCHECK(hipMemcpyAsync(&te[1], d_ts + nrows - 1, 8, hipMemcpyDeviceToHost, st));
+                HIPCHECK(hipStreamSynchronize(st));
+                const double span = (double)std::max<int64_t>(te[1] - te[0], 1);
+                const double win_rows = (double)nrows / span * (double)(P.within_ms + 1);
+                int64_t H = (int64_t)(win_rows * 1.25) + 2 * tile;
+                H = (H + tile - 1) / tile * tile;
+                if (te[1] >= te[0] && H <= S / 2) {
+                    sub_S = S;
+                    sub_H = H;
+                    sub_J = (nrows + S - 1) / S;
+                }
+            }
+            if (sub_J > 1) {  // the view holds one sub-batch: S + H rows (the buffers above are reused from row 0)
+                sub_kg = a;
+                b_own = (uint32_t*)q.bk_own.ensure(257 * 4);
+                sub_halo_check(d_ts, nrows, sub_S, sub_H, P.within_ms, flags, st);
+            } else {
+                bucketize(a, bbits, 0 /* ts is payload column 0 */, flags + 3, b_start, b_seg, FU_OWN, st,
+                          g_no_events ? nullptr : &e->ev[4], b_tm, b_tm ? tm_cap : 0);
+            }
             if (!wide) {
                 v_ts32 = (const uint32_t*)a.dst[0];
                 v_lkey = a.lkey_out;
@@ -2658,18 +2708,55 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     // matcher's own time grows 2.04 -> 2.10 ms beside it (r5c1)
     const char* cside_env = getenv("SDG_CARRY_SIDE");  // (read per flush: the tests switch it)
     const bool carry_serial = !(cside_env && atoi(cside_env) == 1);
-    const bool carry_side = fused && !sorted && a.cin_n > 0 && !carry_serial && !dbg;
+    const bool carry_side = fused && !sorted && a.cin_n > 0 && !carry_serial && !dbg && sub_J <= 1;
     if (carry_side) {
         HIPCHECK(hipEventRecord(e->fork, st));
         HIPCHECK(hipStreamWaitEvent(e->stream2, e->fork, 0));
         chain_carry(a, d_a, e->stream2);
         HIPCHECK(hipEventRecord(e->join, e->stream2));
-    } else if (!sorted) {
-        chain_carry(a, d_a, st);  // (sorted: the carried partials are rows of the view)
+    } else if (!sorted && sub_J <= 1) {
+        chain_carry(a, d_a, st);  // (sorted: the carried partials are rows of the view; sub-batches: below)
     }
     dbg_sync("chain_carry_k");
     ev_record(e->ev[8], st);
-    if (fused) {
+    if (fused && sub_J > 1) {
+        // per sub-batch: its bucket pass (view + plan), [the carried partials, on the first view], the matcher and
+        // its HBM scans. Two argument blocks: every sub-batch but the last ends dead (sub_dead), the last carries
+        ChainArgs* d_sub = (ChainArgs*)q.d_sub_args.ensure(2 * sizeof(ChainArgs));
+        ChainArgs* h_sub = (ChainArgs*)q.h_sub_args.ensure(2 * sizeof(ChainArgs));  // pinned
+        h_sub[0] = a;
+        h_sub[0].bown = b_own;
+        h_sub[0].sub_dead = 1;
+        h_sub[1] = h_sub[0];
+        h_sub[1].sub_dead = 0;
+        HIPCHECK(hipMemcpyAsync(d_sub, h_sub, 2 * sizeof(ChainArgs), hipMemcpyHostToDevice, st));
+        const int64_t tile = bucket_tile();
+        if (q.sub_ev.size() < (size_t)(4 * sub_J + 2)) {
+            const size_t old_n = q.sub_ev.size();
+            q.sub_ev.resize((size_t)(4 * sub_J + 2));
+            for (size_t i = old_n; i < q.sub_ev.size(); ++i) HIPCHECK(hipEventCreate(&q.sub_ev[i]));
+        }
+        hp.mark("chain_setup+carry");
+        for (int64_t j = 0; j < sub_J; ++j) {
+            const bool last = j + 1 == sub_J;
+            const int64_t row0 = j * sub_S;
+            const int64_t rows = last ? nrows - row0 : std::min(sub_S + sub_H, nrows - row0);
+            const int64_t own = last ? (rows + tile - 1) / tile * tile : sub_S;
+            ChainArgs* dj = d_sub + (last ? 1 : 0);
+            const ChainArgs& hj = h_sub[last ? 1 : 0];
+            ev_record(q.sub_ev[4 * j], st);
+            bucketize_sub(sub_kg, bbits, 0, flags + 3, row0, rows, own, b_start, b_seg, b_own, FU_OWN, st);
+            ev_record(q.sub_ev[4 * j + 1], st);
+            if (j == 0) chain_carry(hj, dj, st);
+            ev_record(q.sub_ev[4 * j + 2], st);
+            if (j > 0) HIPCHECK(hipMemsetAsync(a.ovf_count, 0, 8, st));  // (the HBM-scan list is per view)
+            chain_fused(hj, dj, chain_fused_grid(rows, a.nb, a.fu_own), st);
+            ev_record(q.sub_ev[4 * j + 3], st);
+            chain_fovf(hj, dj, st);
+            dbg_sync("fused sub-batch");
+        }
+        ev_record(e->ev[9], st);
+    } else if (fused) {
         const int64_t grid = chain_fused_grid(nrows, a.nb, a.fu_own);
         static int64_t* trace = nullptr;
         static int64_t trace_n = 0;
@@ -2746,6 +2833,12 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     hp.mark("sync_wait");
     if (hf[4]) throw CompileError(SDG_ERR_ARG, "device-resident partition key ids out of range (not from sdg_intern)");
     if (fused && hf[2]) throw DeviceError("fused matcher bounds check failed: bits " + std::to_string(hf[2]));
+    if (fused && sub_J > 1 && hf[5]) {  // a sub-batch's halo did not reach past its window: rerun without sub-batches
+        q.no_sub = true;
+        sub_retry = true;
+        q.carry_nullable = carry_nullable0;
+        return false;
+    }
     if (fused && hf[3]) {  // batch timestamps not in arrival order (or a block's span over 2^32 ms): radix / lane path
         e->stats.fused = 2;
         q.carry_nullable = carry_nullable0;
@@ -2765,7 +2858,19 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     e->stats.ms_keygroup += ms_kg;
     e->stats.ms_match += ms_m;
     float t;
-    if (partitioned && nrows > 0) {
+    if (fused && sub_J > 1) {  // sub-batches: bucket passes (hist + prefix + scatter + plan), carry, matcher, HBM scans
+        for (int64_t j = 0; j < sub_J; ++j) {
+            ev_elapsed(&t, q.sub_ev[4 * j], q.sub_ev[4 * j + 1]);
+            e->stats.ms_kg_scatter += t;
+            ev_elapsed(&t, q.sub_ev[4 * j + 1], q.sub_ev[4 * j + 2]);
+            e->stats.ms_chain_carry += t;
+            ev_elapsed(&t, q.sub_ev[4 * j + 2], q.sub_ev[4 * j + 3]);
+            e->stats.ms_chain_match += t;
+            ev_elapsed(&t, q.sub_ev[4 * j + 3], j + 1 < sub_J ? q.sub_ev[4 * j + 4] : e->ev[9]);
+            e->stats.ms_chain_emit += t;
+        }
+        e->stats.sub_batches = (int32_t)sub_J;
+    } else if (partitioned && nrows > 0) {
         // radix: [4]..[5] first hist+prefix, [5]..[6] scatter passes (+ later hist/prefix), [6]..[7] segments
         ev_elapsed(&t, e->ev[4], e->ev[5]);
         e->stats.ms_kg_hist += t;
@@ -2774,14 +2879,16 @@ void flush_query(sdg_engine* e, QueryRt& q) {
         ev_elapsed(&t, e->ev[5], e->ev[6]);
         e->stats.ms_kg_scatter += t;
     }
-    ev_elapsed(&t, e->ev[3], e->ev[8]);
-    e->stats.ms_chain_carry += t;
     e->stats.carry_in += cin.n;
     e->stats.carry_out += (int64_t)hc[1];
-    ev_elapsed(&t, e->ev[8], e->ev[9]);
-    e->stats.ms_chain_match += t;
-    ev_elapsed(&t, e->ev[9], e->ev[2]);
-    e->stats.ms_chain_emit += t;
+    if (!(fused && sub_J > 1)) {
+        ev_elapsed(&t, e->ev[3], e->ev[8]);
+        e->stats.ms_chain_carry += t;
+        ev_elapsed(&t, e->ev[8], e->ev[9]);
+        e->stats.ms_chain_match += t;
+        ev_elapsed(&t, e->ev[9], e->ev[2]);
+        e->stats.ms_chain_emit += t;
+    }
     e->stats.deque = sorted ? a.fu_mode : a.deque_mode;
     e->stats.events += nrows;
     if (hf[0]) {
@@ -2813,16 +2920,44 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     return true;
     };
     // rerun on the radix path (fused precondition broken), or on the generic NFA (chain precondition broken)
-    for (int attempt = 0; !run(try_fused && attempt == 0); ++attempt)
+    for (int attempt = 0; !run(try_fused && (attempt == 0 || (attempt == 1 && sub_retry))); ++attempt)
         if (attempt >= 3) throw DeviceError("query '" + h.name + "': no matcher path accepted the batch");
 }
 
 // read the last flush's match records back (pinned staging) and append them to the query's delivery backlog in
 // the reference's delivery order: by emitting event, then by the partial's position in the pending list
 // (StateMultiProcessStreamReceiver.processAndClear :47-68, QuerySelector.processNoGroupBy :161-205)
+// a pinned delivery batch (QueryRt::del_buf) not polled yet joins the host backlog (acc_*) before more records do
+void del_to_backlog(QueryRt& q) {
+    if (q.del_n < 0) return;
+    const int64_t n = q.del_n;
+    const int nu = q.del_nu;
+    const uint8_t* base = (const uint8_t*)q.del_buf[q.del_cur ^ 1].p;
+    const int64_t* ts = (const int64_t*)base;
+    const int64_t* emit = ts + n;
+    const int64_t* vals = emit + n;
+    const uint8_t* nb = (const uint8_t*)(vals + (size_t)nu * n);
+    const size_t b = q.acc_ts.size();
+    q.acc_ts.resize(b + n);
+    q.acc_seq.resize(b + n);
+    par_memcpy(q.acc_ts.data() + b, ts, (size_t)n * 8);
+    par_memcpy(q.acc_seq.data() + b, emit, (size_t)n * 8);
+    q.acc_vals.resize(nu);
+    q.acc_nulls.resize(nu);
+    for (int j = 0; j < nu; ++j) {
+        q.acc_vals[j].resize(b + n);
+        par_memcpy(q.acc_vals[j].data() + b, vals + (size_t)j * n, (size_t)n * 8);
+        q.acc_nulls[j].resize(b + n);
+        if (q.del_nulls) par_memcpy(q.acc_nulls[j].data() + b, nb + (size_t)j * n, (size_t)n);
+        else std::memset(q.acc_nulls[j].data() + b, 0, (size_t)n);
+    }
+    q.del_n = -1;
+}
+
 void drain(sdg_engine* e, QueryRt& q) {
     if (q.polled) return;
     q.polled = true;
+    del_to_backlog(q);
     const int64_t n = q.out_n;
     // @purge with aggregators: keys purged after their last record restart their aggregator states -- after this
     // flush's records went through the post pass
@@ -2901,6 +3036,38 @@ void drain(sdg_engine* e, QueryRt& q) {
         src_first = nullptr;
         src_vals = gv;
         vstride = n;
+    }
+    // pinned delivery: read the ordered columns straight into the next delivery buffer (layout ts | emit | vals[nu]
+    // | null bytes[nu]); sdg_poll hands it out as it is
+    const int nu_out = q.hq.plan.n_user_out + q.hq.plan.n_list_cols;
+    bool direct = dev_order && !post && q.acc_ts.empty() && nu_out <= na && !getenv("SDG_POLL_COPY");
+    for (int j = 0; j < q.hq.plan.n_user_out && direct; ++j) direct = !q.hq.plan.out_multi[j];
+    if (direct) {
+        const size_t bytes = (size_t)n * (16 + 8 * (size_t)nu_out) + (q.nulls_valid ? (size_t)n * nu_out : 0);
+        uint8_t* db = (uint8_t*)q.del_buf[q.del_cur ^ 1].ensure(bytes + bytes / 8);  // (slack: flush sizes vary)
+        int64_t* dts = (int64_t*)db;
+        int64_t* dem = dts + n;
+        int64_t* dv = dem + n;
+        uint8_t* dnb = (uint8_t*)(dv + (size_t)nu_out * n);
+        HIPCHECK(hipMemcpyAsync(dts, src_ts, n * 8, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(dem, src_emit, n * 8, hipMemcpyDeviceToHost, st));
+        for (int j = 0; j < nu_out; ++j)
+            HIPCHECK(hipMemcpyAsync(dv + (size_t)j * n, src_vals + (size_t)j * vstride, n * 8, hipMemcpyDeviceToHost, st));
+        if (q.nulls_valid) HIPCHECK(hipMemcpyAsync(nulls, src_nulls, n * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        if (q.nulls_valid)
+            for (int j = 0; j < nu_out; ++j) {
+                uint8_t* dn = dnb + (size_t)j * n;
+                par_range(n, 1 << 20, [&](int64_t lo, int64_t hi) {
+                    for (int64_t i = lo; i < hi; ++i) dn[i] = (nulls[i] >> j) & 1u;
+                });
+            }
+        std::vector<uint8_t>& z = q.del_zero[q.del_cur ^ 1];
+        if (z.size() < (size_t)n) z.assign((size_t)n + (size_t)n / 8, 0);
+        q.del_n = n;
+        q.del_nu = nu_out;
+        q.del_nulls = q.nulls_valid;
+        return;
     }
     std::vector<uint32_t> okey;
     std::vector<uint8_t> oround, oflags;
@@ -3171,6 +3338,7 @@ int do_flush(sdg_engine* e) {
     e->stats.sched_fires = e->stats.sched_shifted = e->stats.sched_host_keys = e->stats.sched_rerun_keys = 0;
     e->stats.sched_exact_passes = 0;
     e->stats.sorted_view = 0;
+    e->stats.sub_batches = 0;
     e->stats.spilled_keys = 0;
     e->stats.host_rows = 0;
     // a flush consumes its batch whether or not it succeeds: a failing query must not make the next flush
@@ -4464,6 +4632,32 @@ int sdg_poll(sdg_engine* e, int qi, sdg_out* out) {
         QueryRt& q = *e->qs[qi];
         const int na = q.hq.plan.n_user_out + q.hq.plan.n_list_cols;  // list elements kept for sdg_poll_list
         if (!e->compile_only) drain(e, q);
+        if (q.del_n >= 0 && q.acc_ts.empty()) {  // pinned delivery: hand the buffer out as it is
+            const int64_t n = q.del_n;
+            const int nd = q.del_nu;
+            q.del_cur ^= 1;
+            q.del_n = -1;
+            const uint8_t* base = (const uint8_t*)q.del_buf[q.del_cur].p;
+            const int64_t* ts = (const int64_t*)base;
+            const int64_t* vals = ts + 2 * n;
+            const uint8_t* nb = (const uint8_t*)(vals + (size_t)nd * n);
+            q.h_vptr.assign(na, nullptr);
+            q.h_nptr.assign(na, nullptr);
+            for (int j = 0; j < na && j < nd; ++j) {
+                q.h_vptr[j] = vals + (size_t)j * n;
+                q.h_nptr[j] = q.del_nulls ? nb + (size_t)j * n : q.del_zero[q.del_cur].data();
+            }
+            out->n = n;
+            out->ts = ts;
+            out->expired = q.del_zero[q.del_cur].data();
+            out->n_attrs = q.hq.plan.n_user_out;
+            out->types = e->out_types[qi].data();
+            out->values = q.h_vptr.data();
+            out->nulls = q.h_nptr.data();
+            out->event_seq = ts + n;
+            return (int)SDG_OK;
+        }
+        del_to_backlog(q);
         const int64_t n = (int64_t)q.acc_ts.size();
         q.h_ts.swap(q.acc_ts);
         q.h_seq.swap(q.acc_seq);
@@ -4500,6 +4694,7 @@ int sdg_discard(sdg_engine* e) {
     if (!e) return fail(SDG_ERR_ARG, "null engine");
     for (auto& q : e->qs) {
         q->polled = true;
+        q->del_n = -1;
         q->acc_ts.clear();
         q->acc_seq.clear();
         q->acc_vals.clear();
@@ -4529,7 +4724,8 @@ int export_records(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_t* 
     return guarded([&]() {
         QueryRt& q = *e->qs[qi];
         if (e->compile_only) throw DeviceError("engine was compiled with SDG_COMPILE_ONLY");
-        if (!q.acc_ts.empty()) throw CompileError(SDG_ERR_ARG, "earlier results are still queued on the host: sdg_poll first");
+        if (!q.acc_ts.empty() || q.del_n >= 0)
+            throw CompileError(SDG_ERR_ARG, "earlier results are still queued on the host: sdg_poll first");
         if (q.last_timers) throw CompileError(SDG_ERR_UNSUPPORTED, "device export of timer (absent-state) matches");
         if (!q.spill.empty())
             throw CompileError(SDG_ERR_UNSUPPORTED, "device export of a query with partition keys spilled to the host "

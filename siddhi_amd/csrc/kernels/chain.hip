@@ -672,7 +672,7 @@ __global__ __launch_bounds__(256, 8) void chain_carry_k(const ChainArgs* __restr
         if (!a.bstart && b < e && ts_row(a, v, b) < a.cin_ts[c]) atomicOr(&a.flags[1], 1);
         const int64_t r = chain_scan<true>(a, acc, b, e, a.cin_ts[c], stk, stride, key);
         if (r >= 0) { has = true; qhit = r; }
-        else if (r == -2) carry = true;
+        else if (r == -2 && !a.sub_dead) carry = true;  // (a sub-batch's bucket end: dead)
     }
     const int64_t slot = wave_reserve(has, a.out_count);
     if (has) {
@@ -842,7 +842,7 @@ __global__ __launch_bounds__(256, 8) void chain_carry_wave_k(const ChainArgs* __
     }
     const int64_t c = c_base + lane;
     const bool valid = lane < CW_PER_WAVE && c < a.cin_n;
-    const bool has = valid && mine >= 0, carry = valid && mine == -2;
+    const bool has = valid && mine >= 0, carry = valid && mine == -2 && !a.sub_dead;
     int64_t slot, cs;
     block_reserve2<256>(has, carry, a.out_count, a.carry_count, &slot, &cs);
     if (has) {
@@ -895,6 +895,9 @@ static_assert(FU_ROWS < 65536, "chain_fused_k: u16 rows / run offsets");
 #ifndef SDG_WQ_U
 #define SDG_WQ_U 2  // rows each lane of the work queue tests per iteration
 #endif
+#ifndef SDG_WQ_BF
+#define SDG_WQ_BF 0  // the SOP build's work queue with a branch-free scan step (A/B)
+#endif
 
 // SAME: the scanned column's kind is the comparison kind (no conversion in the scan loop). W: minimum waves per SIMD
 // the allocator must allow -- 8 = four 512-thread blocks per CU (LDS 4 x 40 KB fits); at 6 it used 104 SGPRs, which
@@ -907,10 +910,18 @@ static_assert(FU_ROWS < 65536, "chain_fused_k: u16 rows / run offsets");
 #endif
 // OC: some output columns stay in arrival order (ChainArgs::ocols): time-major block order, and the emission reads
 // them through orig (a separate instantiation: the selects cost the others 0.17 ms on C2, r5w)
-template <int K, bool SAME, int W, bool ONEK = false, bool OC = false>
+// SOP (round 6): -1 the scan's operator is read at run time; else a compile-time ordering operator (CMP_GT / GE / LT
+// / LE) for the common shape `e2.x OP e1.x` on the scan column (SCAN_E1, the e1 operand is the scanned value): x beats
+// the partial's y iff x SOP y, with the host folding e2's side into SOP. Only the work-queue match pass is compiled
+// then (the deque / fixed-scan A/B paths and the run-time operator dispatch drop out: fewer SGPRs, no uniform
+// branches in the scan loop)
+template <int K, bool SAME, int W, bool ONEK = false, bool OC = false, int SOP = -1>
 __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* __restrict__ pa) {
     using C = KT<K>;
     using T = typename C::T;
+    constexpr bool FIX = SOP >= 0;
+    static_assert(!FIX || SOP == CMP_GT || SOP == CMP_GE || SOP == CMP_LT || SOP == CMP_LE, "SOP: an ordering operator");
+    static_assert(!FIX || (SAME && !ONEK && !OC), "SOP: the many-key build of the scan's own kind");
     constexpr int NW = FU_THREADS / 64;
     constexpr int WROWS = FU_ROWS / NW;  // staged rows ranked by one wave (contiguous)
     const ChainArgs& a = *pa;
@@ -975,7 +986,8 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
     const int64_t be = a.bstart[b + 1];
     const int fown = ONEK ? a.fu_own : FU_OWN;
     const int64_t lo = (int64_t)a.bstart[b] + (int64_t)sb[1] * fown;
-    const int own = (int)min((int64_t)fown, be - lo);
+    const int64_t oe = a.bown ? (int64_t)a.bown[b] : be;  // the bucket's own rows end (sub-batches: its halo after)
+    const int own = (int)min((int64_t)fown, oe - lo);
     const int nr = (int)min((int64_t)FU_ROWS, be - lo);
     const bool to_end = lo + nr == be;  // the staged rows reach the bucket's (= batch's) end for every key
     const int col = sp.scan_col;
@@ -1081,10 +1093,18 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
     FU_TRACE(4);
     if (a.fu_skip & 8) return;
     // ---- match: position pos = k * FU_THREADS + t (a run of consecutive positions per round) ---------------
-    const bool stream_e1 = sp.scan_mode == SCAN_E1;
-    const bool e1_is_x = stream_e1 && sp.e1_col == col && sp.e1_col_kind == kind;
+    const bool stream_e1 = FIX || sp.scan_mode == SCAN_E1;
+    const bool e1_is_x = FIX || (stream_e1 && sp.e1_col == col && sp.e1_col_kind == kind);
     const CmpMask m = cmp_mask(sp.scan_mode == SCAN_TRUE ? OP_ALWAYS : sp.scan_op);
     const bool left = sp.scan_e2_left;
+    // x (a later row's value) completes the partial whose e1 operand is y
+    auto beats = [&](T x, T y) -> bool {
+        if constexpr (SOP == CMP_GT) return x > y;
+        else if constexpr (SOP == CMP_GE) return x >= y;
+        else if constexpr (SOP == CMP_LT) return x < y;
+        else if constexpr (SOP == CMP_LE) return x <= y;
+        else return left ? cmp_m(m, x, y) : cmp_m(m, y, x);
+    };
     // bucket rows are time-ordered (bucketize checked it), so a later row's offset is never below the start's
     const uint64_t within_u = sp.has_within ? (uint64_t)sp.within_ms : ~0ull;
     const FastPred& f0 = sp.f0;
@@ -1093,7 +1113,9 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
     const CmpMask m0 = cmp_mask(f0.op);
     const T k0 = C::get(f0.konst);
     const T kc = C::get(sp.scan_konst);
-    const uint16_t ran_off = to_end ? R_CARRY : R_OVF;  // a partial still pending when its key's staged rows end
+    // a partial still pending when its key's staged rows end: carried at the flush's end, dead at a sub-batch's (its
+    // halo reaches past the window), else its key continues past the staged rows (the HBM scan)
+    const uint16_t ran_off = to_end ? (a.sub_dead ? R_NONE : R_CARRY) : R_OVF;
     // ... unless the staged span already reaches past its window: every later row of the bucket (so every later
     // event of its key) has ts >= tlast, where the partial is expired (isExpired) -- dead, no HBM scan needed
     const uint32_t tl_off = (uint32_t)(tlast - tbase);
@@ -1168,6 +1190,48 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
         uint32_t t0 = 0;
         T y = kc;
         bool live = true;  // the e1 operand is not null (a null operand compares false on every row)
+#if SDG_WQ_BF
+        if constexpr (FIX) {
+            // branch-free scan step (SOP build): every lane loads its WQ_U rows (clamped) and resolves them with
+            // selects -- no divergent branches in the loop body; the window test on u32 offsets
+            const uint32_t win32 = within_u > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)within_u;
+            uint16_t rend = R_NONE;  // the candidate's result when its key's staged rows end with it pending
+#pragma unroll 1
+            for (;;) {
+                const uint64_t need = __ballot(p < 0);
+                if (need) {  // wave-uniform
+                    const int idx = head + __popcll(need & lt);
+                    head += __popcll(need);
+                    if (p < 0 && idx < ncand) {
+                        p = cand[idx];
+                        const int sp0 = sw(p);
+                        t0 = s_ts[sp0];
+                        y = C::get(s_x[sp0]);
+                        end = (int)lend[s_lk[sp0]];
+                        if (!FU_OK(end <= nr && end > p, 4)) end = p + 1;
+                        q = p + 1;
+                        rend = (!to_end && tl_off - t0 > win32) ? R_NONE : ran_off;
+                    }
+                    if (__ballot(p >= 0) == 0) break;
+                }
+                int r = -1;  // the first of the WQ_U rows that decides the partial (from the last row back)
+#pragma unroll
+                for (int u = WQ_U - 1; u >= 0; --u) {
+                    const int sq = sw(min(q + u, FU_ROWS - 1));
+                    const uint32_t tq = s_ts[sq];
+                    const T x = C::get(s_x[sq]);
+                    const int d = q + u >= end ? (int)rend : tq - t0 > win32 ? (int)R_NONE : beats(x, y) ? q + u : -1;
+                    r = d >= 0 ? d : r;
+                }
+                if (p >= 0 && r >= 0) {
+                    s_res[sw(p)] = (uint16_t)r;
+                    p = -1;
+                } else {
+                    q += WQ_U;
+                }
+            }
+        } else
+#endif
 #pragma unroll 1
         for (;;) {
             const uint64_t need = __ballot(p < 0);
@@ -1225,7 +1289,7 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
                         r = ((ONEK || !to_end) && (uint64_t)(tl_off - t0) > within_u) ? R_NONE : ran_off;
                     } else if ((uint64_t)(tq[u] - t0) > within_u) {  // isExpired before the row is processed
                         r = R_NONE;
-                    } else if (live && (left ? cmp_m(m, xq[u], y) : cmp_m(m, y, xq[u]))) {
+                    } else if ((FIX || live) && beats(xq[u], y)) {
                         r = q + u;
                     }
                 }
@@ -1237,6 +1301,8 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
                 }
             }
         }
+    } else if constexpr (FIX) {
+        // (the host launches the SOP build for the work queue only)
     } else if (a.fu_mode != DQ_OFF) {
         // ---- monotone-deque pass (chain_deque_k), one lane per FU_DQ consecutive positions: the lane
         // pushes partials from its own positions only and keeps popping over the following positions of the key
@@ -1363,7 +1429,7 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
             }
         }
         for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = ran_res(p0 + __builtin_ctz(pend));
-    } else {
+    } else if constexpr (!FIX) {
         // ---- forward scans: one lane per candidate, its key's run in LDS
 #pragma unroll 1
         for (int k = 0; k < FU_PT; ++k) {
@@ -1602,7 +1668,7 @@ __global__ __launch_bounds__(256) void chain_fovf_k(const ChainArgs* __restrict_
             const int64_t end = a.bstart[bl + 1];
             const int64_t q = chain_scan<false>(a, acc, p + 1, end, vts(a, p), nullptr, 0, key);
             if (q >= 0) { has = true; qhit = q; }
-            else if (q == -2) carry = true;
+            else if (q == -2 && !a.sub_dead) carry = true;  // (a sub-batch's bucket end: dead, its halo)
         }
         const int64_t slot = wave_reserve(has, a.out_count);
         const int64_t seq = p >= 0 ? a.seq_base + orig_of(a, p) : 0;
@@ -2248,6 +2314,31 @@ void chain_fused(const ChainArgs& a, const ChainArgs* d_a, int64_t grid, hipStre
         else if (w8) hipLaunchKernelGGL((chain_fused_k<KK, false, 8>), g, b, 0, stream, d_a);           \
         else hipLaunchKernelGGL((chain_fused_k<KK, false, 6>), g, b, 0, stream, d_a);                   \
     } while (0)
+    // the compile-time operator build (SOP): `e2.x OP e1.x` on the scan column, an ordering OP, the work queue
+    const bool e1_is_x = a.sp.scan_mode == SCAN_E1 && a.sp.e1_col == a.sp.scan_col && a.sp.e1_col_kind == a.sp.scan_col_kind;
+    const uint8_t op = a.sp.scan_op;
+    const bool ord = op == CMP_GT || op == CMP_GE || op == CMP_LT || op == CMP_LE;
+    static const bool no_sop = getenv("SDG_FU_NO_SOP") != nullptr;  // A/B: the run-time operator build
+    if (!no_sop && !a.ocol_mask && !a.fu_check_ts && same && w8 && e1_is_x && ord && !(a.fu_skip & 256) &&
+        (a.sp.scan_t == VK_F64 || a.sp.scan_t == VK_I64 || a.sp.scan_t == VK_I32 || a.sp.scan_t == VK_F32)) {
+        // x beats y: e2 on the left (e2.x OP e1.x) is x OP y, else y OP x = x OP' y (the flipped ordering)
+        const uint8_t sop = a.sp.scan_e2_left ? op : op == CMP_GT ? CMP_LT : op == CMP_GE ? CMP_LE : op == CMP_LT ? CMP_GT : CMP_GE;
+#define FU_SOP(KK)                                                                                                    \
+    do {                                                                                                              \
+        if (sop == CMP_GT) hipLaunchKernelGGL((chain_fused_k<KK, true, 8, false, false, CMP_GT>), g, b, 0, stream, d_a); \
+        else if (sop == CMP_GE) hipLaunchKernelGGL((chain_fused_k<KK, true, 8, false, false, CMP_GE>), g, b, 0, stream, d_a); \
+        else if (sop == CMP_LT) hipLaunchKernelGGL((chain_fused_k<KK, true, 8, false, false, CMP_LT>), g, b, 0, stream, d_a); \
+        else hipLaunchKernelGGL((chain_fused_k<KK, true, 8, false, false, CMP_LE>), g, b, 0, stream, d_a);             \
+    } while (0)
+        switch (a.sp.scan_t) {
+            case VK_I32: FU_SOP(VK_I32); break;
+            case VK_I64: FU_SOP(VK_I64); break;
+            case VK_F32: FU_SOP(VK_F32); break;
+            default: FU_SOP(VK_F64); break;
+        }
+#undef FU_SOP
+        return;
+    }
     switch (a.sp.scan_t) {
         case VK_I32: FU_LAUNCH(VK_I32); break;
         case VK_I64: FU_LAUNCH(VK_I64); break;

@@ -81,6 +81,18 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks = nul
 // tm (optional, tm_cap >= the fused grid + 2 entries): the time-major block plan (ChainArgs::tm)
 void bucketize(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, uint32_t* bstart, uint32_t* bseg,
                int seg_rows, hipStream_t stream, hipEvent_t* marks = nullptr, uint32_t* tm = nullptr, int64_t tm_cap = 0);
+// one time sub-batch of the fused path (round 6): rows [row0, row0 + n) of the batch described by `a` (its src / keys
+// at row 0; a.n ignored), of which the first `own` (a multiple of the bucket tile, bucket_tile()) are the sub-batch's
+// own rows and the rest its halo; writes the view at a.dst / lkey_out / orig_sorted from 0, orig = batch row, and
+// bstart / bseg (segments over own rows only) / bown (ChainArgs::bown). ts_col's arrival order is checked from row0
+// against row0 - 1 as well.
+void bucketize_sub(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, int64_t row0, int64_t n, int64_t own,
+                   uint32_t* bstart, uint32_t* bseg, uint32_t* bown, int seg_rows, hipStream_t stream);
+int bucket_tile();
+// the halo of every sub-batch but the last must reach past the window of its last own row: flags[5] = 1 when row
+// (j + 1) * S + H (if < n) is not later than ts[(j + 1) * S - 1] + within_ms for some j (the host then reruns the flush
+// without sub-batches)
+void sub_halo_check(const int64_t* ts, int64_t n, int64_t S, int64_t H, int64_t within_ms, int* flags, hipStream_t st);
 
 // ---- chain matcher: `every e1=S0[c0] -> e2=S1[c1] within T` (independent partials) ---------------------
 // One block per tile of CM_THREADS * CM_EPT sorted events; the block reserves its output range with one atomic.
@@ -221,6 +233,13 @@ struct ChainArgs {
     // bucket-major order), tm[1] = the fewest, tm[2 + s] = blocks of segment index < s over all buckets; block v runs
     // segment s of the r-th bucket that has more than s segments (v < tm[1] * nb: bucket v % nb, segment v / nb)
     const uint32_t* tm;
+    // fused path over time sub-batches (round 6, bucketize_sub): the view holds one sub-batch's own rows plus a halo of
+    // the following rows that reaches past every own row's window. bown[b]: the end of bucket b's own rows (its
+    // segments cover only those; the halo rows are staged and scanned, never candidates). sub_dead: a partial whose
+    // key's rows end inside this view with it pending is dead (the halo proves the window passed), not carried --
+    // every sub-batch but the flush's last
+    const uint32_t* bown;
+    int32_t sub_dead;
 };
 enum DequeMode : int32_t { DQ_OFF = 0, DQ_STACK = 1, DQ_ALL = 2 };
 constexpr uint32_t MQ_NONE = 0xFFFFFFFFu, MQ_CARRY = 0xFFFFFFFEu, MQ_OVF = 0xFFFFFFFDu;

@@ -171,6 +171,8 @@ struct RxPass {
     const uint32_t* pre_keys; // pre_keys / pre_src (8-byte slots), the others from keys_in / src at i - hole - pre_n;
                               // a prefix row's orig is 0x80000000 | its index
     const void* pre_src[MAX_COLS + 2];
+    int64_t orig_base;        // added to a row's orig when orig_in is nullptr (a sub-batch's first batch row)
+    int32_t mono_prev;        // the mono check compares row 0 with src[-1] too (a sub-batch after the first)
 };
 
 // stable tile scatter. Tile element e = w * 1024 + r * 64 + lane belongs to wave w (16 rounds r), so a wave
@@ -293,7 +295,7 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
         uint32_t o;
         if (PRE && i < pre_end) o = 0x80000000u | (uint32_t)(i - hole);
         else if (a.orig_in) o = i < a.n ? a.orig_in[i - pre_end] : 0u;
-        else o = (uint32_t)(i - pre_end);
+        else o = (uint32_t)(i - pre_end + a.orig_base);
         cur[r] = (uint64_t)kreg[r] | ((uint64_t)o << 32);
     }
     for (int c = -1; c < a.ncols; ++c) {
@@ -308,8 +310,9 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
             for (int r = 0; r < R; ++r) {
                 const int64_t i = wbase + r * 64 + lane;
                 uint64_t prev = __shfl_up(cur[r], 1);
-                if (lane == 0 && i > 0 && i < a.n) prev = src[i - 1];
-                if (i > 0 && i < a.n && (int64_t)cur[r] < (int64_t)prev) *a.mono_flag = 1;
+                const bool has_prev = i > 0 || a.mono_prev;
+                if (lane == 0 && has_prev && i < a.n) prev = src[i - 1];
+                if (has_prev && i < a.n && (int64_t)cur[r] < (int64_t)prev) *a.mono_flag = 1;
             }
         }
         __syncthreads();
@@ -827,7 +830,9 @@ namespace {
 // (segment index, bucket) costs little (S * nb <= 2 * segments + 256) and it fits tm_cap
 __global__ __launch_bounds__(256) void bk_plan(const uint32_t* __restrict__ tot, int64_t n, int nb, int seg_rows,
                                                uint32_t* __restrict__ bstart, uint32_t* __restrict__ bseg,
-                                               uint32_t* __restrict__ tm, int64_t tm_cap) {
+                                               uint32_t* __restrict__ tm, int64_t tm_cap,
+                                               const uint32_t* __restrict__ offs = nullptr, int64_t halo_tile = 0,
+                                               int64_t ntiles = 0, uint32_t* __restrict__ bown = nullptr) {
     __shared__ uint32_t part[256], sg[256], smax, smin;
     const int d = threadIdx.x;
     uint32_t s0 = 0, len = 0;
@@ -836,6 +841,12 @@ __global__ __launch_bounds__(256) void bk_plan(const uint32_t* __restrict__ tot,
         const uint32_t s1 = d + 1 < nb ? tot[d + 1] : (uint32_t)n;
         len = s1 - s0;
         bstart[d] = s0;
+        if (bown) {  // sub-batch: the bucket's own rows end where the first halo tile's run of it starts (the scan's
+                     // rewritten counts are each (tile, digit) run's output offset)
+            const uint32_t oe = halo_tile < ntiles ? offs[halo_tile * nb + d] : s1;
+            bown[d] = oe;
+            len = oe - s0;  // segments over the own rows only
+        }
     }
     const uint32_t segs = (len + (uint32_t)seg_rows - 1) / (uint32_t)seg_rows;
     part[d] = segs;
@@ -920,6 +931,71 @@ void bucketize(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, uint
     if (marks) (void)hipEventRecord(marks[2], stream);
     hipLaunchKernelGGL(bk_plan, dim3(1), dim3(256), 0, stream, a.tot, a.n, nb, seg_rows, bstart, bseg, tm, tm_cap);
     if (marks) (void)hipEventRecord(marks[3], stream);
+}
+
+int bucket_tile() { return rx_tile_bucket(); }
+
+void bucketize_sub(const KeyGroupArgs& a, int bits, int ts_col, int* mono_flag, int64_t row0, int64_t n, int64_t own,
+                   uint32_t* bstart, uint32_t* bseg, uint32_t* bown, int seg_rows, hipStream_t stream) {
+    const int nb = 1 << bits;
+    const uint32_t mask = (uint32_t)nb - 1;
+    g_tile_override = rx_tile_bucket();
+    const int64_t tile = g_tile_override;
+    const int64_t nt = rx_ntiles(n, tile);
+    const int ng = (int)((nt + KG_GROUP - 1) / KG_GROUP);
+    launch_rx_hist(nt, stream, a.keys + row0, n, 0, mask, nb, a.counts, a.key_flag ? (uint32_t)a.K : 0u, a.key_flag);
+    const int64_t gk = (int64_t)ng * nb;
+    hipLaunchKernelGGL(rx_p1, dim3((unsigned)((gk + 255) / 256)), dim3(256), 0, stream, a.counts, (int)nt, nb, a.gsum);
+    hipLaunchKernelGGL(rx_p2, dim3(1), dim3(256), 0, stream, a.gsum, ng, nb, a.tot);
+    hipLaunchKernelGGL(rx_p3, dim3((unsigned)((gk + 255) / 256)), dim3(256), 0, stream, a.counts, a.gsum, a.tot,
+                       (int)nt, nb);
+    RxPass rp;
+    std::memset(&rp, 0, sizeof rp);
+    rp.keys_in = a.keys + row0;
+    rp.keys_out = a.keys_sorted;
+    rp.orig_in = nullptr;
+    rp.orig_out = a.orig_sorted;
+    rp.orig_base = row0;
+    rp.mono_prev = row0 > 0;
+    rp.ncols = a.ncols;
+    for (int c = 0; c < a.ncols; ++c) {
+        rp.src[c] = (const uint8_t*)a.src[c] + row0 * a.width[c];
+        rp.dst[c] = a.dst[c];
+        rp.width[c] = a.width[c];
+    }
+    rp.offsets = a.counts;
+    rp.n = n;
+    rp.shift = 0;
+    rp.mask = mask;
+    rp.nb = nb;
+    rp.bits = bits;
+    rp.mono_col = ts_col;
+    rp.mono_flag = mono_flag;
+    rp.ts32_col = a.ts32_col;
+    rp.ts_base = a.ts_base;
+    rp.lkey_out = a.lkey_out;
+    rp.lkey_shift = bits;
+    launch_rx_scatter(nt, stream, rp);
+    g_tile_override = 0;
+    hipLaunchKernelGGL(bk_plan, dim3(1), dim3(256), 0, stream, a.tot, n, nb, seg_rows, bstart, bseg, (uint32_t*)nullptr,
+                       (int64_t)0, (const uint32_t*)a.counts, own / tile, nt, bown);
+}
+
+namespace {
+__global__ void sub_halo_check_k(const int64_t* __restrict__ ts, int64_t n, int64_t S, int64_t H, int64_t within,
+                                 int64_t J, int* __restrict__ flags) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j + 1 >= J) return;  // the last sub-batch has no halo
+    const int64_t last_own = (j + 1) * S - 1, after = (j + 1) * S + H;
+    if (after < n && !(ts[after] - ts[last_own] > within)) flags[5] = 1;
+}
+}  // namespace
+
+void sub_halo_check(const int64_t* ts, int64_t n, int64_t S, int64_t H, int64_t within_ms, int* flags, hipStream_t st) {
+    const int64_t J = (n + S - 1) / S;
+    if (J <= 1) return;
+    hipLaunchKernelGGL(sub_halo_check_k, dim3((unsigned)((J + 255) / 256)), dim3(256), 0, st, ts, n, S, H, within_ms, J,
+                       flags);
 }
 
 void nfa_migrate(const Plan* plan, const uint8_t* arena, const uint8_t* arena2, const uint8_t* cur,

@@ -300,6 +300,59 @@ def test_c2_fused_overflow_scans(oracle_built):
     assert got == ref
 
 
+def _c2_rows_stats(app, cols, syms, bounds):
+    """the product over explicit batch bounds: (rows, per-flush stats)"""
+    rt = sa.SiddhiAppRuntime(app)
+    try:
+        h = rt.getInputHandler("StockStream")
+        ids = np.array([rt.intern(s) for s in syms], dtype=np.uint32)
+        rows, stats = [], []
+        for s, e in bounds:
+            h.send_columns(cols["ts"][s:e], [cols["id"][s:e], ids[cols["key"][s:e]], cols["price"][s:e],
+                                             cols["volume"][s:e]])
+            rt.flush(deliver=False)
+            stats.append(rt.stats())
+            types, ts, vals, nulls = rt.raw_outputs(0)
+            rows += [(ts[i], (vals[0][i], vals[1][i])) for i in range(len(ts))]
+        return rows, stats
+    finally:
+        rt.shutdown()
+
+
+@pytest.mark.parametrize("case", ["uniform", "keys20k", "bursty", "long_window"])
+def test_c2_fused_sub_batches(case, oracle_built, monkeypatch):
+    """SDG_FU_SUB (round 6): the fused path in time sub-batches -- each sub-batch's bucket view holds its own rows
+    plus a halo reaching past their window, partials pending at a sub-batch's bucket end are dead, the carried
+    partials resolve on the first view, the last sub-batch carries. Two flushes (carries across them). bursty: the
+    event rate changes mid-batch, so the halo sized from the mean rate falls short somewhere -- the device check
+    fails and the flush reruns whole (no sub-batches) -- still equal to the oracle. long_window: partials outlive
+    the staged LDS halo and finish in the per-sub-batch HBM scan."""
+    monkeypatch.setenv("SDG_FU_SUB", "98304")
+    app = w.C2_APP
+    keys = 20_000 if case == "keys20k" else 2 if case == "long_window" else 300
+    n = 260_000
+    cols = w.c2_columns(n, keys=keys, per_ms=5 if case == "long_window" else 20)
+    if case == "bursty":  # 4 events per ms for the first 60% of the rows, then 100 per ms
+        i = np.arange(n)
+        cut = int(n * 0.6)
+        t = np.where(i < cut, i // 4, cut // 4 + (i - cut) // 100)
+        cols["ts"] = np.ascontiguousarray(w.T0 + t)
+    if case == "long_window":
+        app = w.C2_APP.replace("within 1 sec", "within 3 sec")
+        cols["price"] = np.ascontiguousarray(np.round(25.0 + 5.0 * np.sin(np.arange(n) / 7000.0), 2))
+    syms = w.symbols(keys)
+    ref = oracle_c_rows(app, cols, syms)
+    got, st = _c2_rows_stats(app, cols, syms, [(0, n // 2 + 1000), (n // 2 + 1000, n)])
+    assert len(ref) > 1000
+    assert got == ref
+    assert all(s.fused == 1 for s in st)
+    assert st[0].sub_batches >= 2
+    if case == "bursty":  # the second flush's halo (sized from its mean rate) falls short in the dense part: the
+        assert st[1].sub_batches == 0  # device check fails, the flush reruns whole and sub-batches stay off
+    if case == "long_window":
+        assert sum(s.fused_ovf for s in st) > 0
+
+
 def test_c2_fused_falls_back_on_unordered_batch(oracle_built):
     """per-key ordered but globally unordered timestamps: the fused precondition fails, the radix path runs"""
     keys = 50
