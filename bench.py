@@ -703,6 +703,9 @@ def main():
     per_kernel = {k: acc[k] / K for k in keys_k}
     dom = max(per_kernel, key=per_kernel.get)
     step_bytes = n * B_IN + (matches / K) * B_OUT
+    # fused time sub-batches (SDG_FU_SUB): the matcher runs once per sub-batch; per launch = the step's bytes and
+    # time divided by the launches (the same ratio)
+    launches = max(1, int(st.sub_batches)) if dom in ("ms_chain_match", "ms_kg_scatter") else 1
     achieved = step_bytes / (per_kernel[dom] / 1000.0) / 1e9
     kernel_names = {"ms_chain_match": "chain_fused_k" if st.fused == 1 else "chain_deque_k",
                     "ms_kg_scatter": "rx_scatter", "ms_kg_hist": "rx_hist", "ms_chain_carry": "chain_carry_k"}
@@ -711,7 +714,7 @@ def main():
     if os.path.exists(tpath):
         tj = json.load(open(tpath))
         ent = tj.get("kernels", {}).get(kernel_names.get(dom, ""))
-        if ent and tj.get("events_per_launch") == n:
+        if ent and tj.get("events_per_launch") == n and tj.get("launches_per_step", 1) == launches:
             traffic = ent["fetch_bytes"] + ent["write_bytes"]
     out = {
         "metric": "input events/sec matched (node) at 1/2/4/8 MI355X; % HBM roofline",
@@ -734,7 +737,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": kernel_names.get(dom, dom), "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_unit": "bytes per launch (rocprofv3 --pmc, profiles/pmc_traffic.json)",
-                     "algorithmic_bytes_per_launch": step_bytes, "launches_per_step": 1,
+                     "algorithmic_bytes_per_launch": step_bytes / launches, "launches_per_step": launches,
                      "step_frac": step_bytes / (ms_per_step / 1000.0) / 1e9 / HBM_PEAK_GBS,
                      "kernel_ms": per_kernel},
     }

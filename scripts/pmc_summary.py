@@ -29,7 +29,10 @@ for k, cs in acc.items():
 if len(sys.argv) > 3 and sys.argv[3] == "--traffic":
     import json
     events = int(sys.argv[4])
+    launches = int(sys.argv[5]) if len(sys.argv) > 5 else 1  # matcher launches per step (fused sub-batches)
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, gpurun_out/%s" % tag, "events_per_launch": events,
+           "launches_per_step": launches,
+           "note": "events_per_launch: the bench step's events; bytes are per launch (a step runs launches_per_step)",
            "kernels": {}}
     for k, cs in acc.items():
         if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:

@@ -1894,7 +1894,7 @@ void flush_query(sdg_engine* e, QueryRt& q) {
             int64_t S = sub_env ? atoll(sub_env) : 0;
             S = S > 0 ? (S + tile - 1) / tile * tile : 0;
             if (S > 0 && !q.no_sub && !sub_retry && !wide && !eo_mask && !d_vpos && !d_qs && !d_vrank && P.has_within &&
-                nrows >= 2 * S && !sorted) {
+                nrows > S && !sorted) {
                 int64_t te[2];
                 HIPCHECK(hipMemcpyAsync(&te[0], d_ts, 8, hipMemcpyDeviceToHost, st));
                 HIPCHECK(hipMemcpyAsync(&te[1], d_ts + nrows - 1, 8, hipMemcpyDeviceToHost, st));
@@ -2957,7 +2957,9 @@ void del_to_backlog(QueryRt& q) {
 void drain(sdg_engine* e, QueryRt& q) {
     if (q.polled) return;
     q.polled = true;
+    HostProf hp;  // SDG_HOST_PROF: the drain's phases (ordering enqueue, read-back, null bytes)
     del_to_backlog(q);
+    hp.mark("drain_backlog");
     const int64_t n = q.out_n;
     // @purge with aggregators: keys purged after their last record restart their aggregator states -- after this
     // flush's records went through the post pass
@@ -3036,6 +3038,10 @@ void drain(sdg_engine* e, QueryRt& q) {
         src_first = nullptr;
         src_vals = gv;
         vstride = n;
+        if (hp.on) {
+            HIPCHECK(hipStreamSynchronize(st));
+            hp.mark("drain_order");
+        }
     }
     // pinned delivery: read the ordered columns straight into the next delivery buffer (layout ts | emit | vals[nu]
     // | null bytes[nu]); sdg_poll hands it out as it is
@@ -3055,6 +3061,7 @@ void drain(sdg_engine* e, QueryRt& q) {
             HIPCHECK(hipMemcpyAsync(dv + (size_t)j * n, src_vals + (size_t)j * vstride, n * 8, hipMemcpyDeviceToHost, st));
         if (q.nulls_valid) HIPCHECK(hipMemcpyAsync(nulls, src_nulls, n * 4, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
+        hp.mark("drain_d2h_direct");
         if (q.nulls_valid)
             for (int j = 0; j < nu_out; ++j) {
                 uint8_t* dn = dnb + (size_t)j * n;
@@ -3067,6 +3074,7 @@ void drain(sdg_engine* e, QueryRt& q) {
         q.del_n = n;
         q.del_nu = nu_out;
         q.del_nulls = q.nulls_valid;
+        hp.mark("drain_nulls");
         return;
     }
     std::vector<uint32_t> okey;

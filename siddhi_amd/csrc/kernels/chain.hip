@@ -750,7 +750,10 @@ __device__ int64_t wave_scan_typed(const ChainArgs& a, int64_t from, int64_t end
     return -2;
 }
 
-constexpr int CW_PER_WAVE = 16;  // carried partials resolved one after another by one wave
+#ifndef SDG_CW_PER_WAVE
+#define SDG_CW_PER_WAVE 16
+#endif
+constexpr int CW_PER_WAVE = SDG_CW_PER_WAVE;  // carried partials resolved one after another by one wave
 
 // the typed e2 scan of partial (row p / carried c): the e1 operand hoisted as chain_scan does
 __device__ __forceinline__ int64_t wave_scan_partial(const ChainArgs& a, ChainAcc& acc, int64_t b, int64_t e,
@@ -898,6 +901,9 @@ static_assert(FU_ROWS < 65536, "chain_fused_k: u16 rows / run offsets");
 #ifndef SDG_WQ_BF
 #define SDG_WQ_BF 0  // the SOP build's work queue with a branch-free scan step (A/B)
 #endif
+#ifndef SDG_FIX_STAGE
+#define SDG_FIX_STAGE 1  // the SOP build's staging loads without the view / kind dispatch (0: A/B)
+#endif
 
 // SAME: the scanned column's kind is the comparison kind (no conversion in the scan loop). W: minimum waves per SIMD
 // the allocator must allow -- 8 = four 512-thread blocks per CU (LDS 4 x 40 KB fits); at 6 it used 104 SGPRs, which
@@ -1007,14 +1013,17 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
     for (int r = 0; r < FU_PT; ++r) {
         const int row = w * WROWS + r * 64 + lane;
         const int64_t g = lo + min(row, nr - 1);  // clamped: rows past nr are loaded but not staged
-        if (a.lkey) {  // slim view: u8 local key, u32 ts offset
+        if ((FIX && SDG_FIX_STAGE) || a.lkey) {  // slim view: u8 local key, u32 ts offset (the SOP build: always)
             rkey[r] = (uint32_t)a.lkey[g] << a.bbits;
-            rts[r] = tbase + ((int64_t)a.ts32[g] - (int64_t)a.ts32[lo]);
+            rts[r] = tbase + (int64_t)(uint32_t)(a.ts32[g] - a.ts32[lo]);
         } else {
             rkey[r] = ONEK ? 0u : a.key[g];
             rts[r] = a.ts[g];
         }
-        rx[r] = kind == VK_F64 || kind == VK_I64 ? ((const int64_t*)xcol)[g] : load_col(xcol, kind, g);
+        if constexpr (FIX && SDG_FIX_STAGE)  // the scan column's own kind (SAME): its width, no kind dispatch
+            rx[r] = sizeof(T) == 8 ? ((const int64_t*)xcol)[g] : (int64_t)((const int32_t*)xcol)[g];
+        else
+            rx[r] = kind == VK_F64 || kind == VK_I64 ? ((const int64_t*)xcol)[g] : load_col(xcol, kind, g);
     }
     if (ONEK) {  // one-key batch: arrival order must be time order (the chain path's precondition)
         bool bad = false;
@@ -1028,8 +1037,8 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
         if (__ballot(bad) && lane == 0) atomicOr(&a.flags[3], 1);
     }
     FU_TRACE(2);
-    if (tlast - tbase > (int64_t)0xFFFFFFFF) {  // staged span does not fit the u32 offsets
-        if (t == 0) atomicOr(&a.flags[3], 1);     // -> the host reruns the batch on the radix path
+    if (!(FIX && SDG_FIX_STAGE) && tlast - tbase > (int64_t)0xFFFFFFFF) {  // staged span does not fit the u32 offsets (slim view:
+        if (t == 0) atomicOr(&a.flags[3], 1);     // it does) -> the host reruns the batch on the radix path
         return;                                   // block-uniform
     }
     if (a.fu_skip & 4) {
@@ -2319,7 +2328,7 @@ void chain_fused(const ChainArgs& a, const ChainArgs* d_a, int64_t grid, hipStre
     const uint8_t op = a.sp.scan_op;
     const bool ord = op == CMP_GT || op == CMP_GE || op == CMP_LT || op == CMP_LE;
     static const bool no_sop = getenv("SDG_FU_NO_SOP") != nullptr;  // A/B: the run-time operator build
-    if (!no_sop && !a.ocol_mask && !a.fu_check_ts && same && w8 && e1_is_x && ord && !(a.fu_skip & 256) &&
+    if (!no_sop && !a.ocol_mask && !a.fu_check_ts && same && w8 && e1_is_x && ord && !(a.fu_skip & 256) && a.lkey &&
         (a.sp.scan_t == VK_F64 || a.sp.scan_t == VK_I64 || a.sp.scan_t == VK_I32 || a.sp.scan_t == VK_F32)) {
         // x beats y: e2 on the left (e2.x OP e1.x) is x OP y, else y OP x = x OP' y (the flipped ordering)
         const uint8_t sop = a.sp.scan_e2_left ? op : op == CMP_GT ? CMP_LT : op == CMP_GE ? CMP_LE : op == CMP_LT ? CMP_GT : CMP_GE;

@@ -34,7 +34,6 @@ namespace {
 constexpr int MG_S = 128;                              // sample stride (records of one run per sample)
 constexpr int MG_M = 16;                               // samples per bucket
 constexpr int MG_THREADS = 512;
-constexpr int MG_CAP = (MG_M + MG_MAX_RUNS) * MG_S;    // a bucket's records, upper bound (6144 at 32 runs)
 
 struct MergeRuns {
     const int64_t* keys[MG_MAX_RUNS];
@@ -117,30 +116,35 @@ __device__ __forceinline__ void mg_copy(const void* src, int64_t si, void* dst, 
     else ((uint8_t*)dst)[di] = ((const uint8_t*)src)[si];
 }
 
-__global__ __launch_bounds__(MG_THREADS, 2) void mg_merge_k(const MergeRuns a, const int64_t* __restrict__ bounds) {
-    __shared__ int64_t s_key[MG_CAP];
-    __shared__ uint16_t s_src[MG_CAP];  // output rank -> LDS slot
-    __shared__ uint8_t s_run[MG_CAP];   // LDS slot -> run
-    __shared__ int64_t s_start[MG_MAX_RUNS];
-    __shared__ int s_pre[MG_MAX_RUNS + 1];
+// one workgroup per bucket. GMAX: the runs it is compiled for (register pointers), CAP: the bucket bound
+// (MG_M + GMAX) * MG_S records in LDS -- 3072 for up to 8 runs: 33 KB, four workgroups per CU
+template <int GMAX>
+__global__ __launch_bounds__(MG_THREADS) void mg_merge_k(const MergeRuns a, const int64_t* __restrict__ bounds) {
+    constexpr int CAP = (MG_M + GMAX) * MG_S;
+    constexpr int E = 4;  // consecutive records of one slice per chunk: bounds walked forward, not searched again
+    __shared__ int64_t s_key[CAP];
+    __shared__ uint16_t s_src[CAP];  // output rank -> LDS slot
+    __shared__ uint8_t s_run[CAP];   // LDS slot -> run
+    __shared__ int64_t s_start[GMAX];
+    __shared__ int s_pre[GMAX + 1];
     const int t = threadIdx.x;
     const int G = a.G;
     const int64_t b = blockIdx.x;
+    if (t < G) {  // the bucket's slice of each run (one lane per run)
+        const int64_t lo = bounds[b * G + t], hi = bounds[(b + 1) * G + t];
+        s_start[t] = lo;
+        s_pre[t + 1] = (int)(hi - lo);
+    }
+    __syncthreads();
     if (t == 0) {
-        int acc = 0;
-        for (int r = 0; r < G; ++r) {
-            const int64_t lo = bounds[b * G + r], hi = bounds[(b + 1) * G + r];
-            s_start[r] = lo;
-            s_pre[r] = acc;
-            acc += (int)(hi - lo);
-        }
-        s_pre[G] = acc;
+        s_pre[0] = 0;
+        for (int r = 0; r < G; ++r) s_pre[r + 1] += s_pre[r];
     }
     __syncthreads();
     const int L = s_pre[G];
     int64_t off = 0;  // the bucket's first output position: every record below its splitter
     for (int r = 0; r < G; ++r) off += s_start[r];
-    if (L > MG_CAP) {  // cannot happen (the sampling bound); never write past the LDS
+    if (L > CAP) {  // cannot happen (the sampling bound); never write past the LDS
         if (t == 0) atomicOr(a.flag, 1);
         return;
     }
@@ -152,24 +156,46 @@ __global__ __launch_bounds__(MG_THREADS, 2) void mg_merge_k(const MergeRuns a, c
         s_run[i] = (uint8_t)r;
     }
     __syncthreads();
-    // each record's rank inside the bucket
-    for (int i = t; i < L; i += MG_THREADS) {
-        const int r = s_run[i];
-        const int64_t k = s_key[i];
-        int rank = i - s_pre[r];
-        for (int r2 = 0; r2 < G; ++r2) {
-            if (r2 == r) continue;
-            int lo = s_pre[r2], hi = s_pre[r2 + 1];
-            const bool upper = r2 < r;  // earlier runs first on equal keys
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                const int64_t v = s_key[mid];
-                if (v < k || (upper && v == k)) lo = mid + 1;
-                else hi = mid;
+    // each record's rank inside the bucket: its index in its slice + its bound in every other slice (earlier runs
+    // first on equal keys). A chunk of E consecutive records of one slice searches the bounds for its first record
+    // and walks them forward for the next ones (keys ascend inside a slice)
+    for (int c = t; c * E < L; c += MG_THREADS) {
+        const int i0 = c * E, i1 = min(i0 + E, L);
+        int cur = -1;
+        int ptr[GMAX];
+        for (int i = i0; i < i1; ++i) {
+            const int r = s_run[i];
+            const int64_t k = s_key[i];
+            int rank = i - s_pre[r];
+#pragma unroll
+            for (int r2 = 0; r2 < GMAX; ++r2) {
+                if (r2 >= G || r2 == r) continue;
+                const bool upper = r2 < r;
+                const int hi = s_pre[r2 + 1];
+                int lo;
+                if (r != cur) {  // a new slice: binary search
+                    lo = s_pre[r2];
+                    int h = hi;
+                    while (lo < h) {
+                        const int mid = (lo + h) >> 1;
+                        const int64_t v = s_key[mid];
+                        if (v < k || (upper && v == k)) lo = mid + 1;
+                        else h = mid;
+                    }
+                } else {  // the same slice: forward from the previous record's bound
+                    lo = ptr[r2];
+                    while (lo < hi) {
+                        const int64_t v = s_key[lo];
+                        if (!(v < k || (upper && v == k))) break;
+                        ++lo;
+                    }
+                }
+                ptr[r2] = lo;
+                rank += lo - s_pre[r2];
             }
-            rank += lo - s_pre[r2];
+            cur = r;
+            s_src[rank] = (uint16_t)i;
         }
-        s_src[rank] = (uint16_t)i;
     }
     __syncthreads();
     // out in output order: contiguous stores, payload gathered from the runs' slices
@@ -288,7 +314,9 @@ void merge_runs_device(int G, const int64_t* const* keys, const int64_t* lens, i
     if (rocprim::radix_sort_pairs(tmp, tmp_bytes, sk0, sk1, si0, si1, (size_t)ns, 0, bits, stream) != hipSuccess)
         throw std::runtime_error("merge: sample sort failed");
     hipLaunchKernelGGL(mg_bounds_k, dim3((unsigned)((nb1 + 255) / 256)), dim3(256), 0, stream, a, si1, bounds);
-    hipLaunchKernelGGL(mg_merge_k, dim3((unsigned)a.nbuckets), dim3(MG_THREADS), 0, stream, a, bounds);
+    if (G <= 8) hipLaunchKernelGGL(mg_merge_k<8>, dim3((unsigned)a.nbuckets), dim3(MG_THREADS), 0, stream, a, bounds);
+    else if (G <= 16) hipLaunchKernelGGL(mg_merge_k<16>, dim3((unsigned)a.nbuckets), dim3(MG_THREADS), 0, stream, a, bounds);
+    else hipLaunchKernelGGL(mg_merge_k<MG_MAX_RUNS>, dim3((unsigned)a.nbuckets), dim3(MG_THREADS), 0, stream, a, bounds);
     if (hipGetLastError() != hipSuccess) throw std::runtime_error("merge: kernel launch failed");
     if (hipMemcpyAsync(h_ends + 2 * MG_MAX_RUNS, a.flag, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
         hipStreamSynchronize(stream) != hipSuccess)

@@ -327,22 +327,24 @@ def test_c2_fused_sub_batches(case, oracle_built, monkeypatch):
     event rate changes mid-batch, so the halo sized from the mean rate falls short somewhere -- the device check
     fails and the flush reruns whole (no sub-batches) -- still equal to the oracle. long_window: partials outlive
     the staged LDS halo and finish in the per-sub-batch HBM scan."""
-    monkeypatch.setenv("SDG_FU_SUB", "98304")
+    monkeypatch.setenv("SDG_FU_SUB", "131072" if case == "bursty" else "98304")
     app = w.C2_APP
     keys = 20_000 if case == "keys20k" else 2 if case == "long_window" else 300
-    n = 260_000
+    n = 400_000 if case == "bursty" else 260_000
     cols = w.c2_columns(n, keys=keys, per_ms=5 if case == "long_window" else 20)
-    if case == "bursty":  # 4 events per ms for the first 60% of the rows, then 100 per ms
+    bounds = [(0, n // 2 + 1000), (n // 2 + 1000, n)]
+    if case == "bursty":  # 4 events per ms for the first 200k rows, then 100 per ms
         i = np.arange(n)
-        cut = int(n * 0.6)
+        cut = 200_000
         t = np.where(i < cut, i // 4, cut // 4 + (i - cut) // 100)
         cols["ts"] = np.ascontiguousarray(w.T0 + t)
+        bounds = [(0, 170_000), (170_000, n)]  # the second flush's first sub-batch ends in the dense part
     if case == "long_window":
         app = w.C2_APP.replace("within 1 sec", "within 3 sec")
         cols["price"] = np.ascontiguousarray(np.round(25.0 + 5.0 * np.sin(np.arange(n) / 7000.0), 2))
     syms = w.symbols(keys)
     ref = oracle_c_rows(app, cols, syms)
-    got, st = _c2_rows_stats(app, cols, syms, [(0, n // 2 + 1000), (n // 2 + 1000, n)])
+    got, st = _c2_rows_stats(app, cols, syms, bounds)
     assert len(ref) > 1000
     assert got == ref
     assert all(s.fused == 1 for s in st)
