@@ -53,6 +53,9 @@ struct DevBuf {
         return *this;
     }
     ~DevBuf() { if (p) (void)hipFree(p); }
+    // `need` bytes, reallocating (with a quarter of slack) only when they do not fit: a slightly larger flush than the
+    // last must not reallocate GBs (an ensure(need + need / 4) would, whenever need grows at all)
+    void* ensure_slack(size_t need) { return need > cap ? ensure(need + need / 4) : p; }
     void* ensure(size_t bytes) {
         if (bytes == 0) bytes = 8;
         if (bytes > cap) {
@@ -77,6 +80,7 @@ struct HostPin {
     HostPin(const HostPin&) = delete;
     HostPin& operator=(const HostPin&) = delete;
     ~HostPin() { if (p) (void)hipHostFree(p); }
+    void* ensure_slack(size_t need) { return need > cap ? ensure(need + need / 8) : p; }  // (as DevBuf::ensure_slack)
     void* ensure(size_t bytes) {
         if (bytes > cap) {
             if (p) HIPCHECK(hipHostFree(p));
@@ -2999,15 +3003,15 @@ void drain(sdg_engine* e, QueryRt& q) {
     const bool dev_order = !q.last_timers && n > 1 && hruns.empty();
     if (dev_order) {
         const size_t wb = order_workspace(n);
-        void* work = q.ord_ws.ensure(wb + wb / 4);  // (slack: a slightly larger flush must not reallocate -- a
+        void* work = q.ord_ws.ensure_slack(wb);  // (slack: a slightly larger flush must not reallocate -- a
                                                      // hipFree + hipMalloc of GBs costs more than the ordering)
         uint32_t* perm = nullptr;
         order_records((const int64_t*)q.o_emit.p, (const int64_t*)q.o_first.p, n, q.emit_base, q.emit_span,
                       q.sub_is_seq ? q.emit_base - (1ll << 40) : 0, q.sub_bits(), work, wb, &perm, st);
-        const size_t ns = (size_t)(n + n / 4);  // (slack, as the workspaces)
-        int64_t* gts = (int64_t*)q.g_ts.ensure(ns * 8);
-        int64_t* gem = (int64_t*)q.g_emit.ensure(ns * 8);
-        int64_t* gv = (int64_t*)q.g_vals.ensure((size_t)std::max(na, 1) * ns * 8);
+        const size_t ns = (size_t)n;  // (slack: ensure_slack, as the workspaces)
+        int64_t* gts = (int64_t*)q.g_ts.ensure_slack(ns * 8);
+        int64_t* gem = (int64_t*)q.g_emit.ensure_slack(ns * 8);
+        int64_t* gv = (int64_t*)q.g_vals.ensure_slack((size_t)std::max(na, 1) * ns * 8);
         {
             std::vector<const int64_t*> src{(const int64_t*)q.o_ts.p, (const int64_t*)q.o_emit.p};
             std::vector<int64_t*> dst{gts, gem};
@@ -3016,7 +3020,7 @@ void drain(sdg_engine* e, QueryRt& q) {
                 dst.push_back(gv + (size_t)j * n);
             }
             gather_cols_i64(src.data(), dst.data(), (int)src.size(), perm, n,
-                            q.gather_ws.ensure(gather_cols_workspace(n + n / 4, std::min((int)src.size(), GATHER_MAX_COLS))), st);
+                            q.gather_ws.ensure_slack(gather_cols_workspace(n, std::min((int)src.size(), GATHER_MAX_COLS))), st);
         }
         if (q.nulls_valid) {
             uint32_t* gn = (uint32_t*)q.g_nulls.ensure((size_t)n * 4);
@@ -3050,7 +3054,7 @@ void drain(sdg_engine* e, QueryRt& q) {
     for (int j = 0; j < q.hq.plan.n_user_out && direct; ++j) direct = !q.hq.plan.out_multi[j];
     if (direct) {
         const size_t bytes = (size_t)n * (16 + 8 * (size_t)nu_out) + (q.nulls_valid ? (size_t)n * nu_out : 0);
-        uint8_t* db = (uint8_t*)q.del_buf[q.del_cur ^ 1].ensure(bytes + bytes / 8);  // (slack: flush sizes vary)
+        uint8_t* db = (uint8_t*)q.del_buf[q.del_cur ^ 1].ensure_slack(bytes);  // (slack: flush sizes vary)
         int64_t* dts = (int64_t*)db;
         int64_t* dem = dts + n;
         int64_t* dv = dem + n;
@@ -4749,7 +4753,7 @@ int export_records(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_t* 
         static const bool two_pass = getenv("SDG_EXPORT_TWO_PASS") != nullptr;  // A/B: order_records + gather
         if (n > 0 && ordered && !two_pass) {  // one sort, then ranks + gathers in one kernel (sub compared as int64)
             const size_t wb = order_workspace(n);
-            void* work = q.ord_ws.ensure(wb + wb / 4);
+            void* work = q.ord_ws.ensure_slack(wb);
             std::vector<const int64_t*> src;
             std::vector<int64_t*> dst;
             auto col = [&](const void* from, int64_t* to) {
@@ -4766,7 +4770,7 @@ int export_records(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_t* 
         if (done) {
         } else if (n > 0 && ordered) {  // the delivery-order pass of drain(), gathering straight into the caller's buffers
             const size_t wb = order_workspace(n);
-            void* work = q.ord_ws.ensure(wb + wb / 4);
+            void* work = q.ord_ws.ensure_slack(wb);
             uint32_t* perm = nullptr;
             order_records((const int64_t*)q.o_emit.p, (const int64_t*)q.o_first.p, n, q.emit_base, q.emit_span,
                           q.sub_is_seq ? q.emit_base - (1ll << 40) : 0, q.sub_bits(), work, wb, &perm, st);
@@ -4782,7 +4786,7 @@ int export_records(sdg_engine* e, int qi, int64_t cap, int64_t* n_out, int64_t* 
             col(q.o_first.p, d_sub);
             for (int j = 0; j < na && d_vals; ++j) col((const int64_t*)q.o_vals.p + (size_t)j * q.out_cap, d_vals + (size_t)j * cap);
             gather_cols_i64(src.data(), dst.data(), (int)src.size(), perm, n,
-                            q.gather_ws.ensure(gather_cols_workspace(n + n / 4, std::min((int)src.size(), GATHER_MAX_COLS))), st);
+                            q.gather_ws.ensure_slack(gather_cols_workspace(n, std::min((int)src.size(), GATHER_MAX_COLS))), st);
             HIPCHECK(hipStreamSynchronize(st));
         } else if (n > 0) {
             if (d_ts) HIPCHECK(hipMemcpyAsync(d_ts, q.o_ts.p, n * 8, hipMemcpyDeviceToDevice, st));

@@ -23,6 +23,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -108,16 +109,38 @@ __global__ __launch_bounds__(256) void mg_bounds_k(const MergeRuns a, const uint
     bounds[t] = v;
 }
 
-template <int W>
-__device__ __forceinline__ void mg_copy(const void* src, int64_t si, void* dst, int64_t di) {
-    if (W == 8) ((uint64_t*)dst)[di] = ((const uint64_t*)src)[si];
-    else if (W == 4) ((uint32_t*)dst)[di] = ((const uint32_t*)src)[si];
-    else if (W == 2) ((uint16_t*)dst)[di] = ((const uint16_t*)src)[si];
-    else ((uint8_t*)dst)[di] = ((const uint8_t*)src)[si];
+// one workgroup per bucket. GMAX: the runs it is compiled for (register pointers), CAP: the bucket bound
+// (MG_M + GMAX) * MG_S records in LDS -- 3072 for up to 8 runs: 33 KB, four workgroups per CU
+// the payload of a bucket's records in output order, one column (width W) at a time: each lane gathers up to 4 records
+// (issued together, then stored: the loads of one batch never wait for its stores)
+template <int W, int GMAX>
+__device__ __forceinline__ void mg_out_col(const void* const* __restrict__ src, void* __restrict__ dst, int64_t off,
+                                          int L, const uint16_t* s_src, const uint8_t* s_run, const int64_t* s_start,
+                                          const int* s_pre) {
+    using U = typename std::conditional<W == 8, uint64_t, typename std::conditional<W == 4, uint32_t,
+                                        typename std::conditional<W == 2, uint16_t, uint8_t>::type>::type>::type;
+    constexpr int B = 4;
+    for (int p0 = threadIdx.x; p0 < L; p0 += B * MG_THREADS) {
+        U v[B];
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            const int p = p0 + k * MG_THREADS;
+            if (p < L) {
+                const int i = s_src[p];
+                const int r = s_run[i];
+                v[k] = ((const U*)src[r])[s_start[r] + (i - s_pre[r])];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            const int p = p0 + k * MG_THREADS;
+            if (p < L) ((U*)dst)[off + p] = v[k];
+        }
+    }
 }
 
 // one workgroup per bucket. GMAX: the runs it is compiled for (register pointers), CAP: the bucket bound
-// (MG_M + GMAX) * MG_S records in LDS -- 3072 for up to 8 runs: 33 KB, four workgroups per CU
+// (MG_M + GMAX) * MG_S records in LDS -- 3072 for up to 8 runs: ~35 KB, four workgroups per CU
 template <int GMAX>
 __global__ __launch_bounds__(MG_THREADS) void mg_merge_k(const MergeRuns a, const int64_t* __restrict__ bounds) {
     constexpr int CAP = (MG_M + GMAX) * MG_S;
@@ -127,6 +150,7 @@ __global__ __launch_bounds__(MG_THREADS) void mg_merge_k(const MergeRuns a, cons
     __shared__ uint8_t s_run[CAP];   // LDS slot -> run
     __shared__ int64_t s_start[GMAX];
     __shared__ int s_pre[GMAX + 1];
+    __shared__ const void* s_ptr[GMAX];  // the runs' key / column pointers (an LDS read, not a kernel-argument load per lane)
     const int t = threadIdx.x;
     const int G = a.G;
     const int64_t b = blockIdx.x;
@@ -134,6 +158,7 @@ __global__ __launch_bounds__(MG_THREADS) void mg_merge_k(const MergeRuns a, cons
         const int64_t lo = bounds[b * G + t], hi = bounds[(b + 1) * G + t];
         s_start[t] = lo;
         s_pre[t + 1] = (int)(hi - lo);
+        s_ptr[t] = a.keys[t];
     }
     __syncthreads();
     if (t == 0) {
@@ -148,12 +173,25 @@ __global__ __launch_bounds__(MG_THREADS) void mg_merge_k(const MergeRuns a, cons
         if (t == 0) atomicOr(a.flag, 1);
         return;
     }
-    // the bucket's key slices into LDS (slice r at s_pre[r])
-    for (int i = t; i < L; i += MG_THREADS) {
-        int r = 0;
-        while (r + 1 < G && s_pre[r + 1] <= i) ++r;
-        s_key[i] = a.keys[r][s_start[r] + (i - s_pre[r])];
-        s_run[i] = (uint8_t)r;
+    // the bucket's key slices into LDS (slice r at s_pre[r]); all of a lane's loads issued before the stores
+    {
+        constexpr int B = CAP / MG_THREADS;
+        int64_t kv[B];
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            const int i = t + k * MG_THREADS;
+            if (i < L) {
+                int r = 0;
+                while (r + 1 < G && s_pre[r + 1] <= i) ++r;
+                kv[k] = ((const int64_t*)s_ptr[r])[s_start[r] + (i - s_pre[r])];
+                s_run[i] = (uint8_t)r;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            const int i = t + k * MG_THREADS;
+            if (i < L) s_key[i] = kv[k];
+        }
     }
     __syncthreads();
     // each record's rank inside the bucket: its index in its slice + its bound in every other slice (earlier runs
@@ -198,22 +236,18 @@ __global__ __launch_bounds__(MG_THREADS) void mg_merge_k(const MergeRuns a, cons
         }
     }
     __syncthreads();
-    // out in output order: contiguous stores, payload gathered from the runs' slices
-    for (int p = t; p < L; p += MG_THREADS) {
-        const int i = s_src[p];
-        const int r = s_run[i];
-        const int64_t si = s_start[r] + (i - s_pre[r]);
-        const int64_t di = off + p;
-        a.out_keys[di] = s_key[i];
-        for (int c = 0; c < a.ncols; ++c) {
-            const void* src = a.cols[r][c];
-            void* dst = a.out_cols[c];
-            switch (a.width[c]) {
-                case 8: mg_copy<8>(src, si, dst, di); break;
-                case 4: mg_copy<4>(src, si, dst, di); break;
-                case 2: mg_copy<2>(src, si, dst, di); break;
-                default: mg_copy<1>(src, si, dst, di); break;
-            }
+    // keys in output order (contiguous stores)
+    for (int p = t; p < L; p += MG_THREADS) a.out_keys[off + p] = s_key[s_src[p]];
+    // payload columns in output order: one column at a time, its runs' pointers in LDS
+    for (int c = 0; c < a.ncols; ++c) {
+        __syncthreads();  // (s_ptr is rewritten per column)
+        if (t < G) s_ptr[t] = a.cols[t][c];
+        __syncthreads();
+        switch (a.width[c]) {
+            case 8: mg_out_col<8, GMAX>(s_ptr, a.out_cols[c], off, L, s_src, s_run, s_start, s_pre); break;
+            case 4: mg_out_col<4, GMAX>(s_ptr, a.out_cols[c], off, L, s_src, s_run, s_start, s_pre); break;
+            case 2: mg_out_col<2, GMAX>(s_ptr, a.out_cols[c], off, L, s_src, s_run, s_start, s_pre); break;
+            default: mg_out_col<1, GMAX>(s_ptr, a.out_cols[c], off, L, s_src, s_run, s_start, s_pre); break;
         }
     }
 }
