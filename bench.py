@@ -230,7 +230,8 @@ def ordered_gather_leg(rt, step_push, n, dev, dist, rank, world):
     delivery order (sdg_export_ordered: the engine's device ordering pass), sent to rank 0 over RCCL (send/recv) and
     merged there into the single delivery order of the combined stream: (event time, rank, position of the emitting
     event in its rank's stream, ordinal) -- a rank's delivery order is already sorted by event time, so the merge is
-    one stable device sort of the concatenated runs by time. Rank 0 checks the merged order."""
+    a G-way merge of the runs by time (shard.merge_runs: the device merge sdg_merge_runs, no re-sort). Rank 0 checks
+    the merged order."""
     import torch
     from siddhi_amd import shard
     cap = n + n // 4 + 4096
@@ -281,8 +282,8 @@ def ordered_gather_leg(rt, step_push, n, dev, dist, rank, world):
     return {"records": total, "ms": dt * 1000.0, "rank0_ms": {k: v * 1000.0 for k, v in gph.items()},
             "bytes_to_rank0": int((total - cnt) * 8 * 6),
             "key": "(event ts, rank, event position in its rank's stream, ordinal)", "ordered": True,
-            "path": "sdg_export_ordered (per-rank device ordering) -> RCCL send/recv to rank 0 -> stable device "
-                    "sort of the concatenated runs by time (shard.merge_runs)"}
+            "path": "sdg_export_ordered (per-rank device ordering) -> RCCL send/recv to rank 0 -> device G-way "
+                    "merge of the sorted runs by time (shard.merge_runs, sdg_merge_runs)"}
 
 
 def c5_cpu_baseline(sh, nkeys=100_000):
@@ -458,8 +459,8 @@ def run_c5(args, rank, world, local, dist):
             "records_per_rank_step": matches / K,
             "rank0_ms_per_step": {k: v * 1000.0 / K for k, v in gph.items()},
             "key": "(e2id = global position of the emitting event, e1id)",
-            "path": "sdg_export_ordered (device ordering) -> RCCL send/recv to rank 0 -> stable device sort of the "
-                    "concatenated runs on e2id (shard.merge_runs)"},
+            "path": "sdg_export_ordered (device ordering) -> RCCL send/recv to rank 0 -> device G-way merge of the "
+                    "sorted runs on e2id (shard.merge_runs, sdg_merge_runs)"},
         "roofline": {"bound": "hbm", "kernel": names.get(dom, dom), "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "algorithmic_bytes_per_launch": step_bytes,
