@@ -177,11 +177,11 @@ __global__ __launch_bounds__(MG_THREADS) void mg_merge_k(const MergeRuns a, cons
     {
         constexpr int B = CAP / MG_THREADS;
         int64_t kv[B];
+        int r = 0;  // the slice of record i (i grows with k: continue the walk)
 #pragma unroll
         for (int k = 0; k < B; ++k) {
             const int i = t + k * MG_THREADS;
             if (i < L) {
-                int r = 0;
                 while (r + 1 < G && s_pre[r + 1] <= i) ++r;
                 kv[k] = ((const int64_t*)s_ptr[r])[s_start[r] + (i - s_pre[r])];
                 s_run[i] = (uint8_t)r;
