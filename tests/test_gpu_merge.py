@@ -32,11 +32,36 @@ def _expect(runs):
 
 
 @pytest.mark.parametrize("G,n_max,key_range,lo", [(2, 3000, 50, 0), (5, 4000, 300, -1000), (8, 20000, 10 ** 6, 0),
-                                                  (8, 5000, 3, 0), (32, 2000, 700, -5), (17, 9000, 2 ** 40, -2 ** 39)])
-def test_device_merge_is_a_stable_g_way_merge(G, n_max, key_range, lo):
+                                                  (8, 5000, 3, 0), (32, 2000, 700, -5), (17, 9000, 2 ** 40, -2 ** 39),
+                                                  (6, 20000, 2 ** 40, 0), (4, 20000, 2 ** 33, -2 ** 60)])
+@pytest.mark.parametrize("pairwise", ["1", "0"])
+def test_device_merge_is_a_stable_g_way_merge(G, n_max, key_range, lo, pairwise, monkeypatch):
+    """pairwise=1: buckets whose keys span < 2^32 take the pairwise LDS merge paths, the others the rank search;
+    pairwise=0: every bucket ranks (SDG_MG_PAIR)"""
+    monkeypatch.setenv("SDG_MG_PAIR", pairwise)
     runs = _runs(G, seed=G * 7 + n_max, n_max=n_max, key_range=key_range, lo=lo)
     m = shard.merge_runs(runs, "k")
     exp = _expect([r for r in runs if r["k"].numel() > 0])
+    for c in exp:
+        assert torch.equal(m[c].cpu(), exp[c]), c
+
+
+@pytest.mark.parametrize("pairwise", ["1", "0"])
+def test_device_merge_mixed_bucket_spans(pairwise, monkeypatch):
+    """dense keys (buckets spanning < 2^32: pairwise merge) and sparse keys up to 2^62 (wide buckets: rank search)
+    in one merge, with ties between the two populations' runs"""
+    monkeypatch.setenv("SDG_MG_PAIR", pairwise)
+    g = torch.Generator().manual_seed(11)
+    runs = []
+    for r in range(7):
+        dense = torch.randint(0, 5000, (30000,), generator=g, dtype=torch.int64)
+        sparse = torch.randint(0, 2 ** 62, (int(torch.randint(0, 20000, (1,), generator=g)),), generator=g,
+                               dtype=torch.int64)
+        k = torch.sort(torch.cat([dense, sparse, torch.tensor([2 ** 40] * r, dtype=torch.int64)])).values
+        runs.append({"k": k.cuda(), "run": torch.full((len(k),), r, dtype=torch.int32).cuda(),
+                     "i": torch.arange(len(k)).cuda()})
+    m = shard.merge_runs(runs, "k")
+    exp = _expect(runs)
     for c in exp:
         assert torch.equal(m[c].cpu(), exp[c]), c
 
