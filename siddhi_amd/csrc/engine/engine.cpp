@@ -4167,6 +4167,7 @@ int sdg_compile(const char* text, const sdg_opts* opts, sdg_engine** out) {
             if (hipDeviceGetAttribute(&xccs, hipDeviceAttributeNumberOfXccs, e->device) != hipSuccess) xccs = 1;
             if (const char* x = getenv("SDG_XCDS")) xccs = atoi(x);  // override (A/B)
             g_xcds = std::max(1, xccs);
+            g_cus = std::max(1, prop.multiProcessorCount);
             if (getenv("SDG_VERBOSE"))
                 fprintf(stderr, "[sdg] device %d: %s, %d CUs, %d XCDs\n", e->device, prop.gcnArchName,
                         prop.multiProcessorCount, g_xcds);

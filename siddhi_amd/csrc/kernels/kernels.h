@@ -130,6 +130,7 @@ enum ScanMode : int32_t { SCAN_GENERIC = 0, SCAN_TRUE = 1, SCAN_CONST = 2, SCAN_
 // (hipDeviceAttributeNumberOfXccs at engine creation: 8 on MI355X in SPX mode, fewer per device under CPX/DPX
 // partitioning); 1 disables the remap. Grids of remapped kernels are rounded up to a multiple of it (xcd_round).
 extern int g_xcds;
+extern int g_cus;  // the device's CU count (persistent grids)
 __host__ __device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t grid, uint32_t xcds) {
     return xcds > 1 ? (bid % xcds) * (grid / xcds) + bid / xcds : bid;
 }

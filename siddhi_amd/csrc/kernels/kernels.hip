@@ -183,7 +183,9 @@ struct RxPass {
 // Tiles: 8192 rows x 512 threads (2 blocks per CU) or 16384 x 1024 (one block per CU, 154 KB of LDS): both 4
 // waves/SIMD and 16 rows per lane; the larger tile doubles the average bucket run each tile writes (a 256-bucket
 // pass writes runs of 64 rows instead of 32: fewer partial cache lines for the u8 / u32 columns).
-template <int RX_TILE, int RX_THREADS, bool PRE>
+// BITS: the digit width when fixed at compile time (8: every full 256-bucket pass; the ballot-match loop unrolls),
+// 0: a.bits at run time
+template <int RX_TILE, int RX_THREADS, bool PRE, int BITS = 0>
 __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
     constexpr int R = RX_TILE / RX_THREADS;  // 16 elements per lane
     constexpr int NW = RX_THREADS / 64;
@@ -226,10 +228,19 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
         const bool valid = i < a.n && i >= hole;
         const uint32_t d = valid ? digit_of(kreg[r], a.shift, a.mask) : 0u;
         uint64_t peers = __ballot(valid);
-        for (int bit = 0; bit < a.bits; ++bit) {
-            const bool on = (d >> bit) & 1u;
-            const uint64_t b = __ballot(on);
-            peers &= on ? b : ~b;
+        if constexpr (BITS > 0) {
+#pragma unroll
+            for (int bit = 0; bit < BITS; ++bit) {
+                const bool on = (d >> bit) & 1u;
+                const uint64_t b = __ballot(on);
+                peers &= on ? b : ~b;
+            }
+        } else {
+            for (int bit = 0; bit < a.bits; ++bit) {
+                const bool on = (d >> bit) & 1u;
+                const uint64_t b = __ballot(on);
+                peers &= on ? b : ~b;
+            }
         }
         const uint32_t before = valid ? wc[w][d] : 0u;
         rank[r] = before + (uint32_t)__popcll(peers & lt);
@@ -702,23 +713,31 @@ static void launch_rx_hist(int64_t nt, hipStream_t stream, const uint32_t* keys,
         hipLaunchKernelGGL((rx_hist<RX_TILE, RX_THREADS>), dim3((unsigned)nt), dim3(RX_THREADS), 0, stream, keys, n,
                            shift, mask, nb, counts, kcheck, kflag, pre_keys, pre_n, hole);
 }
+template <int BITS>
+static void launch_rx_scatter_b(int64_t grid, hipStream_t stream, const RxPass& rp) {
+    if (rp.pre_n > 0) {  // (prefix rows exist on the sorted-view path alone)
+        if (rx_tile_now() == RX_TILE_BIG)
+            hipLaunchKernelGGL((rx_scatter<RX_TILE_BIG, RX_THREADS_BIG, true, BITS>), dim3((unsigned)grid),
+                               dim3(RX_THREADS_BIG), 0, stream, rp);
+        else
+            hipLaunchKernelGGL((rx_scatter<RX_TILE, RX_THREADS, true, BITS>), dim3((unsigned)grid), dim3(RX_THREADS), 0,
+                               stream, rp);
+    } else if (rx_tile_now() == RX_TILE_BIG) {
+        hipLaunchKernelGGL((rx_scatter<RX_TILE_BIG, RX_THREADS_BIG, false, BITS>), dim3((unsigned)grid),
+                           dim3(RX_THREADS_BIG), 0, stream, rp);
+    } else {
+        hipLaunchKernelGGL((rx_scatter<RX_TILE, RX_THREADS, false, BITS>), dim3((unsigned)grid), dim3(RX_THREADS), 0,
+                           stream, rp);
+    }
+}
 static void launch_rx_scatter(int64_t nt, hipStream_t stream, RxPass rp) {
     static const bool no_xcd = getenv("SDG_RX_NOXCD") != nullptr;  // A/B: tiles in block order
+    static const bool no_b8 = getenv("SDG_RX_NO_B8") != nullptr;    // A/B: the run-time digit width for 8-bit passes
     rp.ntiles = (int)nt;
     rp.xcds = no_xcd ? 1 : g_xcds;
     const int64_t grid = no_xcd ? nt : xcd_round(nt);
-    if (rp.pre_n > 0) {  // (the large tile only: prefix rows exist on the sorted-view path alone)
-        if (rx_tile_now() == RX_TILE_BIG)
-            hipLaunchKernelGGL((rx_scatter<RX_TILE_BIG, RX_THREADS_BIG, true>), dim3((unsigned)grid), dim3(RX_THREADS_BIG),
-                               0, stream, rp);
-        else
-            hipLaunchKernelGGL((rx_scatter<RX_TILE, RX_THREADS, true>), dim3((unsigned)grid), dim3(RX_THREADS), 0, stream, rp);
-    } else if (rx_tile_now() == RX_TILE_BIG) {
-        hipLaunchKernelGGL((rx_scatter<RX_TILE_BIG, RX_THREADS_BIG, false>), dim3((unsigned)grid), dim3(RX_THREADS_BIG), 0,
-                           stream, rp);
-    } else {
-        hipLaunchKernelGGL((rx_scatter<RX_TILE, RX_THREADS, false>), dim3((unsigned)grid), dim3(RX_THREADS), 0, stream, rp);
-    }
+    if (rp.bits == 8 && !no_b8) launch_rx_scatter_b<8>(grid, stream, rp);
+    else launch_rx_scatter_b<0>(grid, stream, rp);
 }
 
 size_t keygroup_workspace(int64_t n, int32_t K, int32_t ncols, const uint8_t* widths) {
@@ -1040,6 +1059,7 @@ void nfa_commit_slots(const SlotPool& sp, uint8_t* cur, uint8_t* ran, int64_t sl
 }
 
 int g_xcds = 8;
+int g_cus = 256;
 
 namespace {
 __global__ void ts_window_base_k(const int64_t* __restrict__ ts, int64_t* __restrict__ out) {
