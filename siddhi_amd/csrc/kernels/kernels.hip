@@ -362,15 +362,34 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
     }
 }
 
-// key segments of the sorted keys
+// key segments of the sorted keys: 4 consecutive rows per thread (one 16-B load; the neighbours come from the
+// adjacent lanes, the wave's edges from two scalar-sized loads)
 __global__ __launch_bounds__(256) void rx_segments(const uint32_t* __restrict__ keys, int64_t n, uint32_t K,
                                                    uint32_t* __restrict__ seg_start, uint32_t* __restrict__ seg_end) {
-    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
-    uint32_t k = keys[p];
-    if (k >= K) return;  // flagged by rx_hist
-    if (p == 0 || keys[p - 1] != k) seg_start[k] = (uint32_t)p;
-    if (p == n - 1 || keys[p + 1] != k) seg_end[k] = (uint32_t)(p + 1);
+    const int64_t p = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    const int lane = threadIdx.x & 63;
+    uint32_t k[4];
+    if (p + 4 <= n) {
+        const uint4 x = *reinterpret_cast<const uint4*>(keys + p);
+        k[0] = x.x; k[1] = x.y; k[2] = x.z; k[3] = x.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) k[j] = p + j < n ? keys[p + j] : 0xFFFFFFFFu;
+    }
+    uint32_t prev = __shfl_up(k[3], 1), next = __shfl_down(k[0], 1);
+    if (lane == 0) prev = p > 0 && p - 1 < n ? keys[p - 1] : 0xFFFFFFFFu;
+    if (lane == 63) next = p + 4 < n ? keys[p + 4] : 0xFFFFFFFFu;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int64_t i = p + j;
+        if (i >= n) break;
+        const uint32_t kk = k[j];
+        if (kk >= K) continue;  // flagged by rx_hist
+        const uint32_t before = j == 0 ? prev : k[j - 1];
+        const uint32_t after = j == 3 ? next : k[j + 1];
+        if (i == 0 || before != kk) seg_start[kk] = (uint32_t)i;
+        if (i == n - 1 || after != kk) seg_end[kk] = (uint32_t)(i + 1);
+    }
 }
 
 // blocks per CU the generic NFA without timers is compiled for. 4 (4 waves/SIMD, <= 128 VGPRs, a few spills) measured
@@ -736,7 +755,9 @@ static void launch_rx_scatter(int64_t nt, hipStream_t stream, RxPass rp) {
     rp.ntiles = (int)nt;
     rp.xcds = no_xcd ? 1 : g_xcds;
     const int64_t grid = no_xcd ? nt : xcd_round(nt);
-    if (rp.bits == 8 && !no_b8) launch_rx_scatter_b<8>(grid, stream, rp);
+    // (the 8192-row tile only: the bucket pass. C2 scatter 1.375 -> 1.350 ms, r6l; the key sort's 16384-row passes
+    // measured no gain)
+    if (rp.bits == 8 && !no_b8 && rx_tile_now() != RX_TILE_BIG) launch_rx_scatter_b<8>(grid, stream, rp);
     else launch_rx_scatter_b<0>(grid, stream, rp);
 }
 
@@ -837,7 +858,7 @@ void keygroup(const KeyGroupArgs& a, hipStream_t stream, hipEvent_t* marks) {
     if (!a.no_segments) {
         (void)hipMemsetAsync(a.seg_start, 0, (size_t)a.K * 4, stream);
         (void)hipMemsetAsync(a.seg_end, 0, (size_t)a.K * 4, stream);
-        hipLaunchKernelGGL(rx_segments, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, stream, a.keys_sorted, a.n,
+        hipLaunchKernelGGL(rx_segments, dim3((unsigned)((a.n + 1023) / 1024)), dim3(256), 0, stream, a.keys_sorted, a.n,
                            (uint32_t)a.K, a.seg_start, a.seg_end);
     }
     if (marks) (void)hipEventRecord(marks[3], stream);

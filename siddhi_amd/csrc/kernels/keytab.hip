@@ -99,25 +99,49 @@ __global__ __launch_bounds__(256) void kt_load_k(KeyTab t, const int64_t* __rest
     t.slots[s].id = id0 + (uint32_t)i + 1u;
 }
 
-// per row: the key id, or KT_NEW (first sighting in this batch: the row's index competes for the key's first row)
+// per row: the key id, or KT_NEW (first sighting in this batch: the row's index competes for the key's first row).
+// KT_RPT rows per thread (a block's rows strided by 256, loads coalesced): the rows' values, the stop flag and then
+// the rows' home slots (16 B: key and id in one load) are all in flight together; a row whose home slot holds its key
+// is done (the common case once the table knows the keys), the others take the probing / inserting walk (kt_slot).
+constexpr int KT_RPT = 4;
 __global__ __launch_bounds__(256) void kt_probe_k(KeyTab t, const void* __restrict__ col, int kind, int64_t n,
                                                   uint32_t* __restrict__ out, unsigned long long* __restrict__ new_count,
                                                   unsigned long long limit, int* __restrict__ flags) {
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= n) return;
-    if (*(volatile int*)&flags[1]) return;  // stopped: the table is being outgrown
-    const int64_t s = kt_slot(t, kt_value(col, kind, r), new_count, limit, flags);
-    if (s < 0) {
-        atomicOr(&flags[0], 1);
-        out[r] = 0;
-        return;
+    const int64_t r0 = (int64_t)blockIdx.x * (256 * KT_RPT) + threadIdx.x;
+    int64_t v[KT_RPT];
+#pragma unroll
+    for (int j = 0; j < KT_RPT; ++j) {
+        const int64_t r = r0 + j * 256;
+        v[j] = r < n ? kt_value(col, kind, r) : KT_EMPTY;
     }
-    const uint32_t id = t.slots[s].id;
-    if (id) {
-        out[r] = id - 1u;
-    } else {
-        out[r] = KT_NEW;
-        atomicMin(&t.slots[s].first, (uint32_t)r);
+    const int stop = *(volatile int*)&flags[1];
+    uint4 home[KT_RPT];
+#pragma unroll
+    for (int j = 0; j < KT_RPT; ++j) {
+        const uint64_t h = kt_mix((uint64_t)v[j]) & t.mask;
+        home[j] = r0 + j * 256 < n && v[j] != KT_EMPTY ? *reinterpret_cast<const uint4*>(&t.slots[h]) : make_uint4(0, 0, 0, 0);
+    }
+    if (stop) return;  // stopped: the table is being outgrown
+#pragma unroll
+    for (int j = 0; j < KT_RPT; ++j) {
+        const int64_t r = r0 + j * 256;
+        if (r >= n) break;
+        const int64_t hk = (int64_t)(((uint64_t)home[j].y << 32) | home[j].x);
+        uint32_t id;
+        if (v[j] != KT_EMPTY && hk == v[j]) {
+            id = home[j].z;
+            if (!id) atomicMin(&t.slots[kt_mix((uint64_t)v[j]) & t.mask].first, (uint32_t)r);
+        } else {
+            const int64_t sl = kt_slot(t, v[j], new_count, limit, flags);
+            if (sl < 0) {
+                atomicOr(&flags[0], 1);
+                out[r] = 0;
+                continue;
+            }
+            id = t.slots[sl].id;
+            if (!id) atomicMin(&t.slots[sl].first, (uint32_t)r);
+        }
+        out[r] = id ? id - 1u : KT_NEW;
     }
 }
 
@@ -159,7 +183,9 @@ void kt_load(const KeyTab& t, const int64_t* vals, uint32_t id0, int64_t n, int*
 }
 void kt_probe(const KeyTab& t, const void* col, int kind, int64_t n, uint32_t* out, unsigned long long* new_count,
               unsigned long long limit, int* flags, hipStream_t st) {
-    if (n > 0) hipLaunchKernelGGL(kt_probe_k, blocks(n), dim3(256), 0, st, t, col, kind, n, out, new_count, limit, flags);
+    if (n > 0)
+        hipLaunchKernelGGL(kt_probe_k, dim3((unsigned)((n + 256 * KT_RPT - 1) / (256 * KT_RPT))), dim3(256), 0, st, t, col,
+                           kind, n, out, new_count, limit, flags);
 }
 void kt_collect(const KeyTab& t, unsigned long long* pairs, int64_t* vals, unsigned long long* cnt, int64_t cap_out,
                 hipStream_t st) {
