@@ -911,6 +911,9 @@ static_assert(FU_ROWS < 65536, "chain_fused_k: u16 rows / run offsets");
 // ONEK: one-key batches (unpartitioned, C1): a.fu_own rows per segment, the staging's time-order check and the work
 // queue's group summaries. Compile-time, so the many-key build keeps its registers (C2's matcher 2.04 -> 2.26 ms with
 // them present but switched off at run time, r5t/r5u)
+#ifndef SDG_FU_W8
+#define SDG_FU_W8 8  // the SOP build's minimum waves per SIMD (A/B builds with more staged rows: 4)
+#endif
 #ifndef SDG_FU_ROWORDER
 #define SDG_FU_ROWORDER 1  // chain_fused_k emits a block's records in e1-row order (0: regrouped order, A/B)
 #endif
@@ -1168,7 +1171,7 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
         // partial, and an expiry inside it shows at the next row scanned (a key's rows are time-ordered). The groups
         // may mix keys (an upper bound is still an upper bound); they pay for one-key batches (C1), where a high
         // e1 price scans up to a whole window of rows
-        constexpr int WQ_G = 32;
+        constexpr int WQ_G = FU_ROWS <= 2048 ? 32 : FU_ROWS / 64;
         static_assert(FU_ROWS / WQ_G * 8 <= sizeof(lstart), "group summaries fit lstart");
         const bool wq_mono = ONEK && a.fu_mode == DQ_STACK && (m.gt != m.lt) && !m.ne && !(a.fu_skip & 128);
         const bool use_max = left == m.gt;
@@ -1726,7 +1729,7 @@ __device__ __forceinline__ int64_t sv_seq(const ChainArgs& a, uint32_t o) {
 // (not events) and NaN rows never complete one. A continuation skips a whole group of its key when the summary cannot
 // beat its deque's top (pops only ever take the top, so the group changes the deque by expiry alone, which the
 // group's last -- latest -- row applies). C5's keys keep partials for ~half a batch: continuations run long there.
-constexpr int SV_GROUP = 8;
+constexpr int SV_GROUP = 2 * FU_DQ;
 static_assert(SV_GROUP == 2 * FU_DQ, "a group summary combines two lanes' chunks");
 
 template <int K, bool SAME>
@@ -2334,10 +2337,10 @@ void chain_fused(const ChainArgs& a, const ChainArgs* d_a, int64_t grid, hipStre
         const uint8_t sop = a.sp.scan_e2_left ? op : op == CMP_GT ? CMP_LT : op == CMP_GE ? CMP_LE : op == CMP_LT ? CMP_GT : CMP_GE;
 #define FU_SOP(KK)                                                                                                    \
     do {                                                                                                              \
-        if (sop == CMP_GT) hipLaunchKernelGGL((chain_fused_k<KK, true, 8, false, false, CMP_GT>), g, b, 0, stream, d_a); \
-        else if (sop == CMP_GE) hipLaunchKernelGGL((chain_fused_k<KK, true, 8, false, false, CMP_GE>), g, b, 0, stream, d_a); \
-        else if (sop == CMP_LT) hipLaunchKernelGGL((chain_fused_k<KK, true, 8, false, false, CMP_LT>), g, b, 0, stream, d_a); \
-        else hipLaunchKernelGGL((chain_fused_k<KK, true, 8, false, false, CMP_LE>), g, b, 0, stream, d_a);             \
+        if (sop == CMP_GT) hipLaunchKernelGGL((chain_fused_k<KK, true, SDG_FU_W8, false, false, CMP_GT>), g, b, 0, stream, d_a); \
+        else if (sop == CMP_GE) hipLaunchKernelGGL((chain_fused_k<KK, true, SDG_FU_W8, false, false, CMP_GE>), g, b, 0, stream, d_a); \
+        else if (sop == CMP_LT) hipLaunchKernelGGL((chain_fused_k<KK, true, SDG_FU_W8, false, false, CMP_LT>), g, b, 0, stream, d_a); \
+        else hipLaunchKernelGGL((chain_fused_k<KK, true, SDG_FU_W8, false, false, CMP_LE>), g, b, 0, stream, d_a);             \
     } while (0)
         switch (a.sp.scan_t) {
             case VK_I32: FU_SOP(VK_I32); break;

@@ -270,7 +270,10 @@ void chain_sovf(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream);
 #define SDG_FU_THREADS 512  // (A/B builds: 1024 -> 4096 staged rows per block, 2 blocks of ~78 KB LDS per CU)
 #endif
 constexpr int FU_THREADS = SDG_FU_THREADS;
-constexpr int FU_PT = 4;                             // staged rows per lane (= the deque chunk)
+#ifndef SDG_FU_PT
+#define SDG_FU_PT 4  // (A/B builds: 8 -> 4096 staged rows per 512-thread block, 2 blocks per CU)
+#endif
+constexpr int FU_PT = SDG_FU_PT;                     // staged rows per lane (= the deque chunk)
 constexpr int FU_ROWS = FU_THREADS * FU_PT;          // 2048 rows in LDS
 #ifndef SDG_FU_DQ
 #define SDG_FU_DQ 4
