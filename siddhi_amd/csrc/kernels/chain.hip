@@ -940,7 +940,8 @@ __global__ __launch_bounds__(FU_THREADS, W) void chain_fused_k(const ChainArgs* 
     __shared__ uint16_t s_row[FU_ROWS];
     __shared__ uint8_t s_lk[FU_ROWS];
     __shared__ uint16_t s_res[FU_ROWS];  // per position: e2 position | R_NONE | R_CARRY | R_OVF
-    __shared__ __align__(16) uint16_t wc[NW][256];  // regrouping counters; then the deque chunks' summaries
+    // regrouping counters; then the deque chunks' summaries, or the work queue's candidate list (up to WROWS a wave)
+    __shared__ __align__(16) uint16_t wc[NW][WROWS > 256 ? WROWS : 256];
     __shared__ __align__(8) uint16_t lstart[256];  // (reused by the work queue: 64 group extremes of 8 bytes)
     __shared__ uint16_t lend[256];
     __shared__ uint32_t wcnt[3][FU_PT][NW];
