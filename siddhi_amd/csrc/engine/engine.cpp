@@ -2661,7 +2661,13 @@ void flush_query(sdg_engine* e, QueryRt& q) {
     if (sorted) {  // chain_sorted_k: deque / forward scans in LDS blocks, the rest of a cut run in chain_sovf_k
         static const char* skip = getenv("SDG_FU_SKIP");  // A/B: 512 = the deque step's loops; phase timing (results
         a.fu_skip = (skip ? atoi(skip) : 0) & (512 | 2 | 8 | 16);  // invalid): 8 staging only, 16 no matching, 2 no emission
-        a.fu_mode = a.deque_mode;
+        // round 6: the wave work queue (C5 shard: matcher 11.16 -> 7.45 ms, flush 28.1 -> 24.4-25.2 ms, r6t).
+        // A/B: SDG_SV_DEQUE=1 the round-4 chunked deque + carried-partial scans, SDG_SV_NODEQUE=1 per-lane forward
+        // scans for every candidate (8.23 ms, r6s)
+        static const bool sv_nodq = getenv("SDG_SV_NODEQUE") != nullptr;
+        static const bool sv_dq = getenv("SDG_SV_DEQUE") != nullptr;
+        if (!sv_dq && !sv_nodq) a.fu_skip |= 1024;
+        a.fu_mode = sv_nodq ? DQ_OFF : a.deque_mode;
         a.deque_mode = DQ_OFF;
         a.seg_start = a.seg_end = nullptr;
     }

@@ -1852,7 +1852,88 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
         return (q < nr || next_key != (k & SV_KEY)) ? R_CARRY : R_OVF;
     };
     const bool no_match = (a.fu_skip & 16) != 0;  // phase timing: everything but the matching
-    if (a.fu_mode != DQ_OFF && !no_match) {
+    const bool wq = (a.fu_skip & 1024) != 0;      // the wave work queue (as chain_fused_k) instead of deque + scans
+    if (wq && !no_match) {
+        // ---- wave work queue: every candidate (an own e1 row passing c0, or a carried partial) is an independent
+        // forward scan over its key's run; a lane that resolves one takes the wave's next. The wave's candidates go
+        // through a 128-entry ring in s_gs (free without the deque's summaries), one round of 64 positions at a time
+        constexpr int WQ_U = SDG_WQ_U;
+        static_assert(sizeof(s_gs) >= NW * 128 * sizeof(uint16_t), "a 128-entry candidate ring per wave fits s_gs");
+        uint16_t* const ring = reinterpret_cast<uint16_t*>(s_gs) + w * 128;
+        uint32_t cm = 0;  // bit r: this lane's position of round r is a candidate
+#pragma unroll
+        for (int r = 0; r < FU_PT; ++r) {
+            const int pos = w * WROWS + r * 64 + lane;
+            if (pos < own) {
+                const bool carried = (s_key[sw(pos)] & SV_CARRIED) != 0;
+                const int64_t xr = s_x[sw(pos)];
+                if (carried || c0_at(pos, xr, xval(xr))) cm |= 1u << r;
+            }
+        }
+        int filled = 0, head = 0, rn = 0;
+        int p = -1, q = 0;
+        uint32_t t0 = 0, kp = 0;
+        T y = kc;
+        CmpMask mm = m;
+#pragma unroll 1
+        for (;;) {
+            const uint64_t need = __ballot(p < 0);
+            if (need) {  // wave-uniform
+                // refill: a round's candidates (<= 64) go in while that cannot overwrite an entry not yet taken
+                while (rn < FU_PT && filled - head <= 64) {
+                    const bool c = (cm >> rn) & 1u;
+                    const uint64_t bm = __ballot(c);
+                    if (c) ring[(filled + __popcll(bm & lanemask_lt())) & 127] = (uint16_t)(w * WROWS + rn * 64 + lane);
+                    filled += __popcll(bm);
+                    ++rn;
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                const int idx = head + __popcll(need & lanemask_lt());
+                head += __popcll(need);
+                if (p < 0 && idx < filled) {
+                    p = ring[idx & 127];
+                    t0 = s_ts[sw(p)];
+                    kp = s_key[sw(p)] & SV_KEY;
+                    q = p + 1;
+                    const int64_t xr = s_x[sw(p)];
+                    mm = m;
+                    if (stream_e1) {
+                        if (e1_is_x) {
+                            y = xval(xr);
+                        } else {
+                            const int64_t g = lo + p;
+                            if (a.nulls[sp.e1_col] && a.nulls[sp.e1_col][g]) mm = CmpMask{false, false, false, false};
+                            y = C::get(cvt(load_col(a.cols[sp.e1_col], sp.e1_col_kind, g), sp.e1_col_kind, (uint8_t)K));
+                        }
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();  // (every take of this round before the next refill writes)
+                if (__ballot(p >= 0) == 0) break;
+            }
+            if (p >= 0) {
+                int r = -1;  // -1 pending, else the s_res value
+#pragma unroll
+                for (int u = 0; u < WQ_U; ++u) {
+                    if (r >= 0) break;
+                    const int qq = q + u;
+                    if (qq >= nr) { r = off_res(nr, kp); break; }  // the staged rows end with the key's run
+                    const uint32_t kq = s_key[sw(qq)];
+                    if ((kq & SV_KEY) != kp) { r = R_CARRY; break; }  // the key's rows of this batch end here
+                    if (kq & SV_CARRIED) continue;                    // another carried partial: not an event
+                    if ((uint64_t)(s_ts[sw(qq)] - t0) > within_u) { r = R_NONE; break; }  // isExpired: dead
+                    const T x = xval(s_x[sw(qq)]);
+                    if (left ? cmp_m(mm, x, y) : cmp_m(mm, y, x)) r = qq;
+                }
+                if (r >= 0) {
+                    s_res[sw(p)] = (uint16_t)r;
+                    p = -1;
+                } else {
+                    q += WQ_U;
+                }
+            }
+        }
+    } else if (a.fu_mode != DQ_OFF && !no_match) {
         // ---- monotone-deque pass: lane t owns positions [FU_DQ t, FU_DQ (t + 1)) ------------------------------
         const bool stack = a.fu_mode == DQ_STACK;
         const int p0 = t * FU_DQ;
@@ -1988,7 +2069,7 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
     }
     // ---- forward scans: carried partials (and every candidate without a deque mode) -------------------------
 #pragma unroll 1
-    for (int k = 0; k < FU_PT && !no_match; ++k) {
+    for (int k = 0; k < FU_PT && !no_match && !wq; ++k) {
         const int pos = k * FU_THREADS + t;
         if (pos >= own) continue;
         const uint32_t kp = s_key[sw(pos)];
