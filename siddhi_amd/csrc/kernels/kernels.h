@@ -13,12 +13,12 @@ namespace sdg {
 // stable tile scatter. Inside a tile (4096 events, 256 threads) ranks are stable (wave ballot match over the
 // digit bits + per-wave prefix in LDS), the tile is staged in LDS in digit order and every column is written
 // out with consecutive lanes on consecutive addresses of one digit run (coalesced), one column at a time.
-constexpr int RX_TILE = 8192;     // 32 rows per bucket run on average at 256 buckets (SDG_RX_TILE=8192, A/B)
+constexpr int RX_TILE = 8192;     // default (round 6): 32 rows per bucket run on average at 256 buckets, two blocks per CU
 constexpr int RX_THREADS = 512;
-constexpr int RX_TILE_BIG = 16384;  // default: 64 rows per run; one 1024-thread block per CU (r3z: C2 scatter -0.14 ms, C5 shard +13%)
-constexpr int RX_THREADS_BIG = 1024;
-#ifndef SDG_RX_TILE_DEFAULT
-#define SDG_RX_TILE_DEFAULT 16384
+constexpr int RX_TILE_BIG = 16384;  // 64 rows per run; one 1024-thread block per CU (SDG_RX_TILE=16384, A/B). r3z had it
+constexpr int RX_THREADS_BIG = 1024;  // ahead; with compile-time 8-bit digits the small tile wins: C5 key sort 14.63 ->
+#ifndef SDG_RX_TILE_DEFAULT           // 13.85 ms per 2^28-row flush (r6u)
+#define SDG_RX_TILE_DEFAULT 8192
 #endif
 constexpr int RX_TILE_DEFAULT = SDG_RX_TILE_DEFAULT;
 constexpr int RX_MAXBITS = 8;
