@@ -173,6 +173,7 @@ struct RxPass {
     const void* pre_src[MAX_COLS + 2];
     int64_t orig_base;        // added to a row's orig when orig_in is nullptr (a sub-batch's first batch row)
     int32_t mono_prev;        // the mono check compares row 0 with src[-1] too (a sub-batch after the first)
+    int32_t tile_off;         // the launch's first tile (ntiles counts from it)
 };
 
 // stable tile scatter. Tile element e = w * 1024 + r * 64 + lane belongs to wave w (16 rounds r), so a wave
@@ -199,16 +200,17 @@ __global__ __launch_bounds__(RX_THREADS, 4) void rx_scatter(RxPass a) {
     // XCD-aware tile order (kernels.h xcd_block): virtual tile v gives each XCD a contiguous run of tiles. A digit's
     // runs of consecutive tiles are adjacent in the output, so the cache line where one tile's run ends and the next
     // one's begins is completed in one XCD's L2 instead of being written back partially by two
-    const uint32_t tile = xcd_block(blockIdx.x, gridDim.x, (uint32_t)a.xcds);
-    if ((int)tile >= a.ntiles) return;  // block-uniform: the rounding of the grid
-    const int64_t base = (int64_t)tile * RX_TILE;
+    const uint32_t vt = xcd_block(blockIdx.x, gridDim.x, (uint32_t)a.xcds);
+    if ((int)vt >= a.ntiles) return;  // block-uniform: the rounding of the grid
+    const int64_t tile = (int64_t)vt + a.tile_off;  // (a launch may cover the pass's tiles from tile_off on)
+    const int64_t base = tile * RX_TILE;
     const int64_t tile_n = min((int64_t)RX_TILE, a.n - base);
     const int64_t hole = PRE ? a.hole : 0;
     const int64_t pre_end = PRE ? a.hole + a.pre_n : 0;
     const int64_t tile_v = tile_n - (base < hole ? hole - base : 0);  // the tile's rows (its staged elements)
     const int64_t wbase = base + w * (R * 64);
     for (int d = t; d < a.nb; d += RX_THREADS) {
-        gbase[d] = a.offsets[(int64_t)tile * a.nb + d];
+        gbase[d] = a.offsets[tile * a.nb + d];
 #pragma unroll
         for (int v = 0; v < NW; ++v) wc[v][d] = 0;
     }
@@ -752,8 +754,35 @@ static void launch_rx_scatter_b(int64_t grid, hipStream_t stream, const RxPass& 
 static void launch_rx_scatter(int64_t nt, hipStream_t stream, RxPass rp) {
     static const bool no_xcd = getenv("SDG_RX_NOXCD") != nullptr;  // A/B: tiles in block order
     static const bool no_b8 = getenv("SDG_RX_NO_B8") != nullptr;    // A/B: the run-time digit width for 8-bit passes
-    rp.ntiles = (int)nt;
+    static const bool no_split = getenv("SDG_RX_NO_SPLIT") != nullptr;  // A/B: one PRE launch over every tile
     rp.xcds = no_xcd ? 1 : g_xcds;
+    if (rp.pre_n > 0 && !no_split) {
+        // the tiles with prefix rows (or the alignment hole) take the PRE build; the ones past them -- nearly all --
+        // the plain build, reading the batch columns through pointers moved back by the prefix (row i of the pass is
+        // batch row i - pre_end there)
+        const int tile = rx_tile_now();
+        const int64_t pre_end = rp.hole + rp.pre_n;
+        const int64_t t1 = std::min<int64_t>(nt, (pre_end + tile - 1) / tile);
+        RxPass b = rp;
+        rp.ntiles = (int)t1;
+        rp.tile_off = 0;
+        if (t1 > 0) launch_rx_scatter_b<0>(no_xcd ? t1 : xcd_round(t1), stream, rp);
+        if (t1 < nt) {
+            b.pre_n = 0;
+            b.hole = 0;
+            b.keys_in = b.keys_in - pre_end;
+            if (b.orig_in) b.orig_in = b.orig_in - pre_end;
+            else b.orig_base -= pre_end;
+            for (int c = 0; c < b.ncols; ++c) b.src[c] = (const uint8_t*)b.src[c] - pre_end * (int64_t)b.width[c];
+            b.ntiles = (int)(nt - t1);
+            b.tile_off = (int32_t)t1;
+            const int64_t g2 = no_xcd ? nt - t1 : xcd_round(nt - t1);
+            if (b.bits == 8 && !no_b8) launch_rx_scatter_b<8>(g2, stream, b);
+            else launch_rx_scatter_b<0>(g2, stream, b);
+        }
+        return;
+    }
+    rp.ntiles = (int)nt;
     const int64_t grid = no_xcd ? nt : xcd_round(nt);
     // (the 8192-row tile only: the bucket pass. C2 scatter 1.375 -> 1.350 ms, r6l; the key sort's 16384-row passes
     // measured no gain)
