@@ -1733,10 +1733,15 @@ __device__ __forceinline__ int64_t sv_seq(const ChainArgs& a, uint32_t o) {
 constexpr int SV_GROUP = 2 * FU_DQ;
 static_assert(SV_GROUP == 2 * FU_DQ, "a group summary combines two lanes' chunks");
 
-template <int K, bool SAME>
+// SOP (round 6): as chain_fused_k's -- a compile-time ordering operator for `e2.x OP e1.x` on the scan column (e2's
+// side folded in on the host); only the work-queue pass is compiled then
+template <int K, bool SAME, int SOP = -1>
 __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs* __restrict__ pa) {
     using C = KT<K>;
     using T = typename C::T;
+    constexpr bool FIX = SOP >= 0;
+    static_assert(!FIX || SOP == CMP_GT || SOP == CMP_GE || SOP == CMP_LT || SOP == CMP_LE, "SOP: an ordering operator");
+    static_assert(!FIX || SAME, "SOP: the scan's own kind");
     constexpr int NW = FU_THREADS / 64;
     constexpr int WROWS = FU_ROWS / NW;
     const ChainArgs& a = *pa;
@@ -1852,7 +1857,14 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
         return (q < nr || next_key != (k & SV_KEY)) ? R_CARRY : R_OVF;
     };
     const bool no_match = (a.fu_skip & 16) != 0;  // phase timing: everything but the matching
-    const bool wq = (a.fu_skip & 1024) != 0;      // the wave work queue (as chain_fused_k) instead of deque + scans
+    const bool wq = FIX || (a.fu_skip & 1024) != 0;  // the wave work queue (as chain_fused_k) instead of deque + scans
+    auto beats = [&](T x, T y, const CmpMask& mm) -> bool {  // x (a later row's value) completes the partial of y
+        if constexpr (SOP == CMP_GT) return x > y;
+        else if constexpr (SOP == CMP_GE) return x >= y;
+        else if constexpr (SOP == CMP_LT) return x < y;
+        else if constexpr (SOP == CMP_LE) return x <= y;
+        else return left ? cmp_m(mm, x, y) : cmp_m(mm, y, x);
+    };
     if (wq && !no_match) {
         // ---- wave work queue: every candidate (an own e1 row passing c0, or a carried partial) is an independent
         // forward scan over its key's run; a lane that resolves one takes the wave's next. The wave's candidates go
@@ -1923,7 +1935,7 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
                     if (kq & SV_CARRIED) continue;                    // another carried partial: not an event
                     if ((uint64_t)(s_ts[sw(qq)] - t0) > within_u) { r = R_NONE; break; }  // isExpired: dead
                     const T x = xval(s_x[sw(qq)]);
-                    if (left ? cmp_m(mm, x, y) : cmp_m(mm, y, x)) r = qq;
+                    if (beats(x, y, mm)) r = qq;
                 }
                 if (r >= 0) {
                     s_res[sw(p)] = (uint16_t)r;
@@ -1933,7 +1945,8 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
                 }
             }
         }
-    } else if (a.fu_mode != DQ_OFF && !no_match) {
+    } else if constexpr (!FIX) {
+      if (a.fu_mode != DQ_OFF && !no_match) {
         // ---- monotone-deque pass: lane t owns positions [FU_DQ t, FU_DQ (t + 1)) ------------------------------
         const bool stack = a.fu_mode == DQ_STACK;
         const int p0 = t * FU_DQ;
@@ -2066,6 +2079,7 @@ __global__ __launch_bounds__(FU_THREADS, 8) void chain_sorted_k(const ChainArgs*
             const uint16_t rr = off_res(q, cur);
             for (; pend; pend &= pend - 1) s_res[sw(p0 + __builtin_ctz(pend))] = rr;
         }
+      }
     }
     // ---- forward scans: carried partials (and every candidate without a deque mode) -------------------------
 #pragma unroll 1
@@ -2449,6 +2463,31 @@ void chain_sorted(const ChainArgs& a, const ChainArgs* d_a, hipStream_t stream) 
     const int64_t grid = xcd_round((a.n + FU_OWN - 1) / FU_OWN);  // rounded for the XCD remap
     const dim3 g((unsigned)grid), b(FU_THREADS);
     const bool same = a.sp.scan_col_kind == a.sp.scan_t;
+    {  // the compile-time operator build (SOP), work-queue mode only
+        const bool e1_is_x = a.sp.scan_mode == SCAN_E1 && a.sp.e1_col == a.sp.scan_col && a.sp.e1_col_kind == a.sp.scan_col_kind;
+        const uint8_t op = a.sp.scan_op;
+        const bool ord = op == CMP_GT || op == CMP_GE || op == CMP_LT || op == CMP_LE;
+        static const bool no_sop = getenv("SDG_SV_NO_SOP") != nullptr;  // A/B: the run-time operator build
+        if (!no_sop && (a.fu_skip & 1024) && same && e1_is_x && ord &&
+            (a.sp.scan_t == VK_F64 || a.sp.scan_t == VK_I64 || a.sp.scan_t == VK_I32 || a.sp.scan_t == VK_F32)) {
+            const uint8_t sop = a.sp.scan_e2_left ? op : op == CMP_GT ? CMP_LT : op == CMP_GE ? CMP_LE : op == CMP_LT ? CMP_GT : CMP_GE;
+#define SV_SOP(KK)                                                                                        \
+    do {                                                                                                  \
+        if (sop == CMP_GT) hipLaunchKernelGGL((chain_sorted_k<KK, true, CMP_GT>), g, b, 0, stream, d_a);      \
+        else if (sop == CMP_GE) hipLaunchKernelGGL((chain_sorted_k<KK, true, CMP_GE>), g, b, 0, stream, d_a); \
+        else if (sop == CMP_LT) hipLaunchKernelGGL((chain_sorted_k<KK, true, CMP_LT>), g, b, 0, stream, d_a); \
+        else hipLaunchKernelGGL((chain_sorted_k<KK, true, CMP_LE>), g, b, 0, stream, d_a);                    \
+    } while (0)
+            switch (a.sp.scan_t) {
+                case VK_I32: SV_SOP(VK_I32); break;
+                case VK_I64: SV_SOP(VK_I64); break;
+                case VK_F32: SV_SOP(VK_F32); break;
+                default: SV_SOP(VK_F64); break;
+            }
+#undef SV_SOP
+            return;
+        }
+    }
 #define SV_LAUNCH(KK)                                                                    \
     do {                                                                                 \
         if (same) hipLaunchKernelGGL((chain_sorted_k<KK, true>), g, b, 0, stream, d_a);  \
